@@ -1,0 +1,94 @@
+/*
+ * rst.h — C ABI of the MI355X-native realtime style-transfer hot path (librst.so).
+ *
+ * Plain C: pointers, sizes and ints only (no torch / TF / HIP types), so ctypes, cgo,
+ * JNI or N-API can bind it. Streams are passed as `void*` and interpreted as
+ * `hipStream_t`. All tensor pointers are DEVICE pointers owned by the caller, fp32,
+ * NHWC (channels last), densely packed. Every call is asynchronous on the given
+ * stream, allocates nothing and never synchronises, so it can be captured into a
+ * hipGraph. Errors: every entry point returns an rst_status; rst_last_error() gives a
+ * thread-local message for the last failing call on this thread.
+ *
+ * Reference interfaces each entry point replaces (realtime_style_transfer @ /root/reference):
+ *   rst_create / rst_destroy     create_style_transfer_model(input_shape, output_shape,
+ *                                bottleneck_res_y, bottleneck_num_filters, num_styles)
+ *                                -> (tf.keras.Model, P)          models/styleTransfer.py:213-214,332
+ *                                plus Model.set_weights/load_weights (predict_using_checkpoint.py:84)
+ *   rst_num_style_params         the returned P                  models/styleTransfer.py:278-279,332
+ *   rst_forward                  Model.__call__ / predict({'content','style_params'[,'style_weights']})
+ *                                                                 models/styleTransfer.py:281-331,
+ *                                                                 predict_video_using_checkpoint.py:96
+ *   rst_gram                     gram_matrix / get_gram_matrix_model  models/styleLoss.py:11-37
+ *   rst_instance_norm            ConditionalInstanceNormalization.call models/styleTransfer.py:57-71
+ *   rst_copy_activation          (debug) per-block outputs of the Keras sub-models
+ */
+#ifndef RST_H_
+#define RST_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum rst_status {
+    RST_OK = 0,
+    RST_ERR_INVALID = 1,      /* bad argument / shape mismatch (reference: Python assert / ValueError) */
+    RST_ERR_UNSUPPORTED = 2,  /* configuration this build does not implement */
+    RST_ERR_HIP = 3,          /* HIP runtime error */
+    RST_ERR_ALLOC = 4         /* device allocation failed (only in rst_create) */
+} rst_status;
+
+/* Network geometry — the arguments of create_style_transfer_model (styleTransfer.py:213). */
+typedef struct rst_shape {
+    int in_h, in_w, in_c;        /* content input (H, W, C)                      */
+    int out_h, out_w;            /* stylised output (H, W); always 3 channels    */
+    int bottleneck_res_y;        /* ShapeConfig.bottleneck_res_y                 */
+    int bottleneck_num_filters;  /* ShapeConfig.bottleneck_num_filters           */
+    int num_styles;              /* ShapeConfig.num_styles (this build: 1)       */
+    int max_batch;               /* largest batch rst_forward will be called with */
+} rst_shape;
+
+typedef struct rst_handle rst_handle;
+
+/* Build the network on the current HIP device: derive the block plan exactly as the
+ * reference does, upload the weights (HOST pointer, Keras get_weights() order, see
+ * realtime_style_transfer_amd/plan.py) into device layouts, allocate the activation /
+ * statistics workspace for max_batch. num_weights must equal the plan's total. */
+int rst_create(const rst_shape* shape, const float* weights_host, size_t num_weights, rst_handle** out);
+void rst_destroy(rst_handle* h);
+
+/* Number of style parameters P per style (2662 for rst-960-120-128-17). */
+int rst_num_style_params(const rst_handle* h);
+/* Total weight count expected by rst_create for this shape (no device work). */
+size_t rst_num_weights_for_shape(const rst_shape* shape);
+
+/* out (B, out_h, out_w, 3) = transfer(content (B, in_h, in_w, in_c), style_params (B, S, P)).
+ * style_weights must be NULL when num_styles == 1. */
+int rst_forward(rst_handle* h, const float* content, const float* style_params, const float* style_weights,
+                float* out, int batch, void* stream);
+
+/* Debug: number of conv layers, and a copy of layer idx's most recent output
+ * (post-normalisation/activation as the reference block emits it) into dst. */
+int rst_num_layers(const rst_handle* h);
+int rst_layer_output_shape(const rst_handle* h, int idx, int batch, int* hwc3);
+int rst_copy_activation(rst_handle* h, int idx, float* dst, size_t count, int batch, void* stream);
+
+/* Gram matrices: out[b][c][d] = sum_p feat[b][p][c] * feat[b][p][d] / hw.
+ * feat (B, hw, C) fp32; out (B, C, C). workspace: rst_gram_workspace_size() bytes. */
+size_t rst_gram_workspace_size(int batch, int hw, int channels);
+int rst_gram(const float* feat, int batch, int hw, int channels, float* out, void* workspace, void* stream);
+
+/* Conditional instance norm: y = bias + scale * (x - mean) * rsqrt(var + eps) per (b, c)
+ * over H*W, optional ReLU. scale/bias (B, C). workspace: rst_instance_norm_workspace_size(). */
+size_t rst_instance_norm_workspace_size(int batch, int hw, int channels);
+int rst_instance_norm(const float* x, int batch, int hw, int channels, const float* scale, const float* bias,
+                      float eps, int relu, float* y, void* workspace, void* stream);
+
+const char* rst_last_error(void);
+const char* rst_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RST_H_ */

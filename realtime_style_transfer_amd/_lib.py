@@ -1,0 +1,107 @@
+"""ctypes binding of librst.so (the C ABI in include/rst.h).
+
+The product path has no fallback: if librst.so is missing or cannot be loaded, every
+entry point raises. ``torch`` is imported first so that librst resolves
+``libamdhip64.so.7`` to the HIP runtime torch already loaded (one runtime per process,
+so torch's hipStream_t handles are valid inside librst).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede loading librst, see module docstring)
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "librst.so"
+
+RST_OK, RST_ERR_INVALID, RST_ERR_UNSUPPORTED, RST_ERR_HIP, RST_ERR_ALLOC = range(5)
+
+# Symbols declared in include/rst.h — tests check that the library exports all of them.
+EXPORTED_SYMBOLS = [
+    "rst_create", "rst_destroy", "rst_num_style_params", "rst_num_weights_for_shape", "rst_forward",
+    "rst_num_layers", "rst_layer_output_shape", "rst_copy_activation", "rst_gram_workspace_size", "rst_gram",
+    "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_last_error", "rst_version",
+]
+
+
+class RstShape(ctypes.Structure):
+    _fields_ = [("in_h", ctypes.c_int), ("in_w", ctypes.c_int), ("in_c", ctypes.c_int),
+                ("out_h", ctypes.c_int), ("out_w", ctypes.c_int),
+                ("bottleneck_res_y", ctypes.c_int), ("bottleneck_num_filters", ctypes.c_int),
+                ("num_styles", ctypes.c_int), ("max_batch", ctypes.c_int)]
+
+
+class RstError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"librst error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = os.environ.get("RST_LIB", str(LIB_PATH))
+    if not Path(path).exists():
+        raise RuntimeError(f"librst.so not found at {path}: build it with "
+                           f"`python -m realtime_style_transfer_amd.build` (there is no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    vp, i, sz, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_float
+    lib.rst_create.argtypes = [ctypes.POINTER(RstShape), vp, sz, ctypes.POINTER(vp)]
+    lib.rst_create.restype = i
+    lib.rst_destroy.argtypes = [vp]
+    lib.rst_destroy.restype = None
+    lib.rst_num_style_params.argtypes = [vp]
+    lib.rst_num_style_params.restype = i
+    lib.rst_num_weights_for_shape.argtypes = [ctypes.POINTER(RstShape)]
+    lib.rst_num_weights_for_shape.restype = sz
+    lib.rst_forward.argtypes = [vp, vp, vp, vp, vp, i, vp]
+    lib.rst_forward.restype = i
+    lib.rst_num_layers.argtypes = [vp]
+    lib.rst_num_layers.restype = i
+    lib.rst_layer_output_shape.argtypes = [vp, i, i, ctypes.POINTER(ctypes.c_int)]
+    lib.rst_layer_output_shape.restype = i
+    lib.rst_copy_activation.argtypes = [vp, i, vp, sz, i, vp]
+    lib.rst_copy_activation.restype = i
+    lib.rst_gram_workspace_size.argtypes = [i, i, i]
+    lib.rst_gram_workspace_size.restype = sz
+    lib.rst_gram.argtypes = [vp, i, i, i, vp, vp, vp]
+    lib.rst_gram.restype = i
+    lib.rst_instance_norm_workspace_size.argtypes = [i, i, i]
+    lib.rst_instance_norm_workspace_size.restype = sz
+    lib.rst_instance_norm.argtypes = [vp, i, i, i, vp, vp, fp, i, vp, vp, vp]
+    lib.rst_instance_norm.restype = i
+    lib.rst_last_error.argtypes = []
+    lib.rst_last_error.restype = ctypes.c_char_p
+    lib.rst_version.argtypes = []
+    lib.rst_version.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def check(code: int):
+    if code != RST_OK:
+        msg = load().rst_last_error().decode(errors="replace")
+        if code == RST_ERR_INVALID:
+            raise ValueError(f"librst: {msg}")
+        raise RstError(code, msg)
+
+
+def stream_ptr(stream=None) -> int:
+    s = torch.cuda.current_stream() if stream is None else stream
+    return int(s.cuda_stream)
+
+
+def dev_ptr(t: torch.Tensor) -> int:
+    if not t.is_cuda:
+        raise ValueError("librst operates on device tensors; got a CPU tensor")
+    if t.dtype != torch.float32:
+        raise ValueError(f"librst expects float32 tensors, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError("librst expects contiguous (NHWC) tensors")
+    return int(t.data_ptr())

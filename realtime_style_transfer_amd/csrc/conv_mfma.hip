@@ -1,0 +1,406 @@
+// conv_mfma.hip — implicit-GEMM convolution on gfx950 f32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// One kernel template serves every conv of the transfer network
+// (realtime_style_transfer/models/styleTransfer.py:95-205):
+//   * Conv2D 'same' (contract 9x9 s1, 3x3 s2; residual 3x3 s1)       styleTransfer.py:170,194
+//   * Conv2DTranspose 3x3 s2 'same' rewritten as a 2x2 stride-1 conv with N = 4 phases x Cout
+//     and a pixel-shuffle store (no zero insertion)                    styleTransfer.py:115-119
+// with the neighbouring element-wise work fused:
+//   prologue (applied while the input halo is staged to LDS):
+//     PRO_AFF_RELU  y = relu(a[c]*x + b[c])          CIN-apply + ReLU   (:173-182)
+//     PRO_AFF       y = a[c]*x + b[c]                CIN-apply (block output of residual_block 0)
+//     PRO_AFF_RES   y = r + a[c]*x + b[c]            CIN-apply + residual Add (:184)
+//     (PRO_AFF / PRO_AFF_RES can also materialise y for the next skip connection)
+//   epilogue:
+//     EPI_RELU_BN    relu -> BatchNorm(inference) -> relu              contract (:194-203)
+//     EPI_RELU_STATS relu, store, per-(tile, channel) {sum, M2, n}      residual conv (:170)
+//     EPI_STATS      store, {sum, M2, n}                               expand conv (no act, :118)
+//
+// Numerics: exact f32 — every product is a single-rounding fmaf in the MFMA (no xf32 on
+// gfx950), accumulation f32, tile statistics by two-pass (mean, M2) merged in f64 later.
+//
+// Data layout: activations NHWC fp32 in HBM. Per workgroup: an output tile of TH x TW
+// pixels x NT channels. Input halo for one Cin chunk (CK channels) is staged in LDS as
+// [halo pixel][CS] (CS = CK + pad, odd 16-B slot count -> conflict-free b128 column reads);
+// the weight stage (TPS taps x CK x NT) is pre-packed on the host in exactly the LDS image
+// order [tap][k-group][lane-half][n][VEC] so staging is a contiguous float4 copy.
+// K order inside a tap pairs channel s (lane half 0) with channel s + CK/2 (lane half 1),
+// so one ds_read_b128 feeds 4 consecutive MFMA k-steps for both operands.
+#include <hip/hip_runtime.h>
+#include "kernels.h"
+
+namespace rst {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+template <int VEC>
+struct vec_t;
+template <>
+struct vec_t<1> { typedef float type; };
+template <>
+struct vec_t<4> { typedef float4 type; };
+
+__device__ __forceinline__ float vget(float v, int) { return v; }
+__device__ __forceinline__ float vget(const float4& v, int q) {
+    return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
+}
+
+__device__ __forceinline__ float apply_pro(int mode, float x, float2 ab, float r) {
+    float y = fmaf(ab.x, x, ab.y);
+    if (mode == PRO_AFF_RELU) y = fmaxf(y, 0.f);
+    else if (mode == PRO_AFF_RES) y = r + y;
+    return y;
+}
+
+template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+struct ConvCfg {
+    static constexpr int VEC = ((CK / 2) % 4 == 0) ? 4 : 1;
+    static constexpr int CS = (VEC == 4) ? (CK + 4) : (((CK + 1) & 1) ? CK + 1 : CK + 2);  // odd for VEC=1
+    static constexpr int HH = (TH - 1) * S + KH;
+    static constexpr int HWD = (TW - 1) * S + KW;
+    static constexpr int HP = HH * HWD;
+    static constexpr int MT = TH * TW / 32;
+    static constexpr int MW = MT / WM;
+    static constexpr int NTILES = NT / 32;
+    static constexpr int NW = NTILES / WN;
+    static constexpr int KSTEPS = CK / 2;
+    static constexpr int SG = KSTEPS / VEC;
+    static constexpr int WSTAGE = TPS * CK * NT;
+    static constexpr int NTAPS = KH * KW;
+    static constexpr int NGROUPS = NTAPS / TPS;
+    static constexpr int HALO_FLOATS = ((HP * CS + 3) / 4) * 4;
+    static constexpr int MAX_CIN = 256;
+    static constexpr size_t LDS_BYTES = (size_t)(HALO_FLOATS + WSTAGE) * 4 + MAX_CIN * 8;
+    static_assert(WM * WN == 4, "4 waves per workgroup");
+    static_assert(MT % WM == 0 && NTILES % WN == 0, "wave tiling");
+    static_assert((TH * TW) % 32 == 0, "M tile = 32 pixels");
+    static_assert(NTAPS % TPS == 0, "taps per stage");
+    static_assert(KSTEPS % VEC == 0, "vector k-steps");
+};
+
+template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+    using C = ConvCfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    constexpr int VEC = C::VEC, CS = C::CS, HWD = C::HWD, HP = C::HP;
+    constexpr int MW = C::MW, NW = C::NW, SG = C::SG, KSTEPS = C::KSTEPS;
+    typedef typename vec_t<VEC>::type vT;
+
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* halo = smem;
+    float* wts = smem + C::HALO_FLOATS;
+    float2* pab = reinterpret_cast<float2*>(wts + C::WSTAGE);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int li = lane & 31, lh = lane >> 5;
+
+    int bid = blockIdx.x;
+    const int nb = bid % a.n_blocks;
+    bid /= a.n_blocks;
+    const int tx = bid % a.tiles_x;
+    bid /= a.tiles_x;
+    const int ty = bid % a.tiles_y;
+    const int b = bid / a.tiles_y;
+    const int y0 = ty * TH, x0 = tx * TW;
+    const int iy0 = y0 * S - a.pad_t, ix0 = x0 * S - a.pad_l;
+    const int Cin = a.cin;
+
+    int pixoff[MW];
+#pragma unroll
+    for (int m = 0; m < MW; ++m) {
+        const int p = (wm * MW + m) * 32 + li;
+        const int pr = p / TW, pc = p % TW;
+        pixoff[m] = ((pr * S) * HWD + pc * S) * CS + lh * KSTEPS;
+    }
+    int woff[NW];
+#pragma unroll
+    for (int n = 0; n < NW; ++n) woff[n] = (lh * NT + (wn * NW + n) * 32 + li) * VEC;
+
+    floatx16 acc[MW][NW];
+#pragma unroll
+    for (int m = 0; m < MW; ++m)
+#pragma unroll
+        for (int n = 0; n < NW; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+
+    const int pro = a.pro_mode;
+    if (pro != PRO_NONE) {
+        for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[b * Cin + c];
+    }
+    const bool do_mat = (a.mat != nullptr) && nb == 0;
+    const size_t img_base = (size_t)b * a.H * a.W;
+
+    for (int chunk = 0; chunk < a.nchunks; ++chunk) {
+        // ---------------- stage the input halo for this Cin chunk (prologue fused) -------------
+        __syncthreads();
+        if ((Cin & 3) == 0 && (CK & 3) == 0) {
+            constexpr int Q = CK / 4;
+            for (int it = tid; it < HP * Q; it += 256) {
+                const int hp = it / Q, q = it - (it / Q) * Q;
+                const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
+                const int iy = iy0 + hy, ix = ix0 + hx;
+                const int c = chunk * CK + q * 4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c < Cin) {
+                    const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
+                    v = *reinterpret_cast<const float4*>(a.in + gi);
+                    if (pro != PRO_NONE) {
+                        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (pro == PRO_AFF_RES) r = *reinterpret_cast<const float4*>(a.res + gi);
+                        v.x = apply_pro(pro, v.x, pab[c + 0], r.x);
+                        v.y = apply_pro(pro, v.y, pab[c + 1], r.y);
+                        v.z = apply_pro(pro, v.z, pab[c + 2], r.z);
+                        v.w = apply_pro(pro, v.w, pab[c + 3], r.w);
+                        if (do_mat && iy >= y0 && iy < y0 + TH && ix >= x0 && ix < x0 + TW)
+                            *reinterpret_cast<float4*>(a.mat + gi) = v;
+                    }
+                }
+                float* dst = halo + hp * CS + q * 4;
+                if constexpr (VEC == 4) {
+                    *reinterpret_cast<float4*>(dst) = v;
+                } else {
+                    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+                }
+            }
+        } else {
+            for (int it = tid; it < HP * CK; it += 256) {
+                const int hp = it / CK, q = it - (it / CK) * CK;
+                const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
+                const int iy = iy0 + hy, ix = ix0 + hx;
+                const int c = chunk * CK + q;
+                float v = 0.f;
+                if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c < Cin) {
+                    const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
+                    v = a.in[gi];
+                    if (pro != PRO_NONE) {
+                        const float r = (pro == PRO_AFF_RES) ? a.res[gi] : 0.f;
+                        v = apply_pro(pro, v, pab[c], r);
+                        if (do_mat && iy >= y0 && iy < y0 + TH && ix >= x0 && ix < x0 + TW) a.mat[gi] = v;
+                    }
+                }
+                halo[hp * CS + q] = v;
+            }
+        }
+
+        for (int g = 0; g < C::NGROUPS; ++g) {
+            // ---------------- stage weights for TPS taps of this chunk ---------------------------
+            if (g > 0) __syncthreads();
+            {
+                const float4* src = reinterpret_cast<const float4*>(
+                    a.wpk + ((size_t)(nb * a.nchunks + chunk) * C::NGROUPS + g) * C::WSTAGE);
+                float4* dst = reinterpret_cast<float4*>(wts);
+                for (int it = tid; it < C::WSTAGE / 4; it += 256) dst[it] = src[it];
+            }
+            __syncthreads();
+            // ---------------- MFMA main loop over the stage -------------------------------------
+#pragma unroll
+            for (int t = 0; t < TPS; ++t) {
+                const int tap = g * TPS + t;
+                const int ky = tap / KW, kx = tap - (tap / KW) * KW;
+                const int tap_off = (ky * HWD + kx) * CS;
+#pragma unroll
+                for (int sg = 0; sg < SG; ++sg) {
+                    vT av[MW], bv[NW];
+#pragma unroll
+                    for (int m = 0; m < MW; ++m)
+                        av[m] = *reinterpret_cast<const vT*>(halo + pixoff[m] + tap_off + sg * VEC);
+#pragma unroll
+                    for (int n = 0; n < NW; ++n)
+                        bv[n] = *reinterpret_cast<const vT*>(wts + (t * SG + sg) * 2 * NT * VEC + woff[n]);
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q)
+#pragma unroll
+                        for (int m = 0; m < MW; ++m)
+#pragma unroll
+                            for (int n = 0; n < NW; ++n)
+                                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget(av[m], q), vget(bv[n], q),
+                                                                                 acc[m][n], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    // ---------------- epilogue ---------------------------------------------------------------
+    const int epi = a.epi_mode;
+    const int n_mtiles = a.tiles_y * a.tiles_x * C::MT;
+#pragma unroll
+    for (int n = 0; n < NW; ++n) {
+        const int ng = nb * NT + (wn * NW + n) * 32 + li;
+        const bool nvalid = ng < a.ntot;
+        const float bias = nvalid ? a.bias[ng] : 0.f;
+        float2 bn = make_float2(1.f, 0.f);
+        if (epi == EPI_RELU_BN && nvalid) bn = a.bn_ab[ng];
+        int co = ng, py = 0, px = 0;
+        if (a.shuffle) {
+            const int ph = ng / a.cout;
+            co = ng - ph * a.cout;
+            py = ph >> 1;
+            px = ph & 1;
+        }
+#pragma unroll
+        for (int m = 0; m < MW; ++m) {
+            const int mt = wm * MW + m;
+            float s = 0.f, cnt = 0.f;
+            float vals[16];
+            bool ok[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int p = mt * 32 + row;
+                const int oy = y0 + p / TW, ox = x0 + p % TW;
+                const bool valid = nvalid && oy < a.Ho && ox < a.Wo;
+                float v = acc[m][n][r] + bias;
+                if (epi == EPI_RELU_BN) {
+                    v = fmaxf(v, 0.f);
+                    v = fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                } else if (epi == EPI_RELU_STATS) {
+                    v = fmaxf(v, 0.f);
+                }
+                vals[r] = v;
+                ok[r] = valid;
+                if (valid) {
+                    size_t oi;
+                    if (a.shuffle)
+                        oi = (((size_t)b * (2 * a.Ho) + 2 * oy + py) * (2 * a.Wo) + 2 * ox + px) * a.cout + co;
+                    else
+                        oi = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ng;
+                    a.out[oi] = v;
+                    s += v;
+                    cnt += 1.f;
+                }
+            }
+            if (a.part != nullptr) {
+                // two-pass tile statistics: lanes l and l^32 hold the two row halves of column ng
+                s += __shfl_xor(s, 32);
+                cnt += __shfl_xor(cnt, 32);
+                const float mean = cnt > 0.f ? s / cnt : 0.f;
+                float m2 = 0.f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float d = vals[r] - mean;
+                    if (ok[r]) m2 = fmaf(d, d, m2);
+                }
+                m2 += __shfl_xor(m2, 32);
+                if (lh == 0 && nvalid) {
+                    const int mtg = (ty * a.tiles_x + tx) * C::MT + mt;
+                    a.part[((size_t)b * a.ntot + ng) * n_mtiles + mtg] = make_float4(s, m2, cnt, 0.f);
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side dispatch over the instantiated configurations
+// ------------------------------------------------------------------------------------------
+template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+static hipError_t launch_cfg(const ConvArgs& a, hipStream_t st) {
+    using C = ConvCfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    auto kern = conv_mfma_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x * a.n_blocks);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), C::LDS_BYTES, st, a);
+    return hipGetLastError();
+}
+
+template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+static hipError_t prepare_cfg() {
+    using C = ConvCfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    auto kern = conv_mfma_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES);
+}
+
+template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+static ConvTile tile_of() {
+    using C = ConvCfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    ConvTile t;
+    t.kh = KH; t.kw = KW; t.stride = S; t.ck = CK; t.nt = NT; t.th = TH; t.tw = TW; t.tps = TPS;
+    t.vec = C::VEC; t.mt = C::MT; t.ngroups = C::NGROUPS; t.wstage = C::WSTAGE;
+    t.lds_bytes = (int)C::LDS_BYTES;
+    t.id = 0;
+    return t;
+}
+
+// The configuration table. Each row: (KH,KW,S,CK,NT,TH,TW,WM,WN,TPS).
+#define RST_CONV_CONFIGS(X)                       \
+    X(1, 9, 9, 1, 18, 32, 8, 16, 4, 1, 9)         \
+    X(2, 9, 9, 1, 4, 32, 8, 16, 4, 1, 9)          \
+    X(3, 3, 3, 2, 16, 32, 8, 16, 4, 1, 9)         \
+    X(4, 3, 3, 2, 8, 32, 8, 16, 4, 1, 9)          \
+    X(5, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1)        \
+    X(6, 3, 3, 1, 32, 32, 8, 16, 4, 1, 9)         \
+    X(7, 3, 3, 1, 8, 32, 8, 16, 4, 1, 9)          \
+    X(8, 2, 2, 1, 32, 128, 4, 16, 2, 2, 1)        \
+    X(9, 2, 2, 1, 32, 64, 8, 16, 2, 2, 4)         \
+    X(10, 2, 2, 1, 32, 32, 8, 16, 4, 1, 4)        \
+    X(11, 2, 2, 1, 16, 32, 8, 16, 4, 1, 4)        \
+    X(12, 2, 2, 1, 8, 32, 8, 16, 4, 1, 4)         \
+    X(13, 3, 3, 1, 16, 32, 8, 16, 4, 1, 9)        \
+    X(14, 3, 3, 2, 4, 32, 8, 16, 4, 1, 9)         \
+    X(15, 3, 3, 1, 4, 32, 8, 16, 4, 1, 9)         \
+    X(16, 2, 2, 1, 4, 32, 8, 16, 4, 1, 4)         \
+    X(17, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1)
+
+bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
+    // pick CK (Cin chunk) and NT (output columns per workgroup)
+    int ck;
+    if (cin <= 4) ck = 4;
+    else if (cin <= 8) ck = 8;
+    else if (cin <= 16) ck = 16;
+    else if (cin <= 18) ck = 18;
+    else if (cin % 32 == 0) ck = 32;
+    else return false;
+    if (kh == 3 && stride == 2 && ck == 32) ck = 16;   // keep the stride-2 halo within LDS budget
+    int nt = ntot > 64 ? 128 : (ntot > 32 ? 64 : 32);
+    if (ntot > 128 && ntot % 128 != 0) return false;
+    if (kh == 9 || (kh == 3 && stride == 2)) nt = 32;  // these variants exist only with NT=32
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS)                       \
+    if (kh == KH && stride == S && ck == CK && nt == NT) {                   \
+        *out = tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>();           \
+        out->id = ID;                                                        \
+        return true;                                                         \
+    }
+    RST_CONV_CONFIGS(X)
+#undef X
+    // fall back to NT=32 variants (more N blocks)
+    if (nt != 32) {
+        nt = 32;
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS)                       \
+    if (kh == KH && stride == S && ck == CK && nt == NT) {                   \
+        *out = tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>();           \
+        out->id = ID;                                                        \
+        return true;                                                         \
+    }
+        RST_CONV_CONFIGS(X)
+#undef X
+    }
+    return false;
+}
+
+hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
+    switch (t.id) {
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS) \
+    case ID:                                          \
+        return launch_cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>(a, st);
+        RST_CONV_CONFIGS(X)
+#undef X
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
+hipError_t conv_prepare(const ConvTile& t) {
+    switch (t.id) {
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS) \
+    case ID:                                          \
+        return prepare_cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>();
+        RST_CONV_CONFIGS(X)
+#undef X
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace rst

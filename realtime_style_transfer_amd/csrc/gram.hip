@@ -1,0 +1,126 @@
+// gram.hip — Gram matrices of VGG feature maps on f32 MFMA.
+//
+// gram_matrix (realtime_style_transfer/models/styleLoss.py:21-37):
+//   G[b,c,d] = einsum('bijc,bijd->bcd', F, F) / (H*W)
+// A tall-skinny Fᵀ·F: M = N = C (64..512), K = H*W (up to 460 800 px at 480x960). The K
+// dimension is split across workgroups (split-K) so every CU has work even for C = 64;
+// each workgroup stages 64 pixels x (64 + 64) channels of F in LDS and its 4 waves each own
+// one 32x32 block of a 64x64 G tile (v_mfma_f32_32x32x2_f32: exact f32 products). Partial
+// tiles go to a slab [b][split][C][C]; a second kernel sums the splits in fixed order
+// (bitwise reproducible, no float atomics) and scales by 1/(H*W).
+#include <hip/hip_runtime.h>
+#include "kernels.h"
+
+namespace rst {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace gram {
+constexpr int KP = 64;        // pixels per LDS stage
+constexpr int TILE = 64;      // G tile edge per workgroup
+constexpr int LS = TILE + 1;  // padded LDS row
+}  // namespace gram
+
+static int gram_splits(int batch, int hw, int channels) {
+    const int tiles = (channels / gram::TILE) * (channels / gram::TILE);
+    int ns = 2048 / (batch * tiles);
+    const int max_ns = (hw + 255) / 256;
+    if (ns > max_ns) ns = max_ns;
+    if (ns < 1) ns = 1;
+    return ns;
+}
+
+size_t gram_workspace_bytes(int batch, int hw, int channels) {
+    return (size_t)batch * gram_splits(batch, hw, channels) * channels * channels * sizeof(float);
+}
+
+__global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restrict__ feat, float* __restrict__ slab,
+                                                           int hw, int C, int nsplit, int span) {
+    using namespace gram;
+    __shared__ float la[KP * LS];
+    __shared__ float lb[KP * LS];
+    const int ntile = C / TILE;
+    int bid = blockIdx.x;
+    const int split = bid % nsplit;
+    bid /= nsplit;
+    const int tj = bid % ntile;
+    bid /= ntile;
+    const int ti = bid % ntile;
+    const int b = bid / ntile;
+    const int c0 = ti * TILE, d0 = tj * TILE;
+    const int p_begin = split * span;
+    const int p_end = min(hw, p_begin + span);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wi = wave >> 1, wj = wave & 1;
+    const int li = lane & 31, lh = lane >> 5;
+    const float* fb = feat + (size_t)b * hw * C;
+
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+    for (int p0 = p_begin; p0 < p_end; p0 += KP) {
+        __syncthreads();
+        // stage KP pixels x 64 channels for both operands (float4 loads, 16 per pixel row)
+        for (int it = tid; it < KP * (TILE / 4); it += 256) {
+            const int pp = it / (TILE / 4), q = it % (TILE / 4);
+            const int p = p0 + pp;
+            float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+            if (p < p_end) {
+                va = *reinterpret_cast<const float4*>(fb + (size_t)p * C + c0 + 4 * q);
+                vb = *reinterpret_cast<const float4*>(fb + (size_t)p * C + d0 + 4 * q);
+            }
+            float* da = la + pp * LS + 4 * q;
+            float* db = lb + pp * LS + 4 * q;
+            da[0] = va.x; da[1] = va.y; da[2] = va.z; da[3] = va.w;
+            db[0] = vb.x; db[1] = vb.y; db[2] = vb.z; db[3] = vb.w;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int s = 0; s < KP / 2; ++s) {
+            const int p = 2 * s + lh;
+            const float av = la[p * LS + wi * 32 + li];
+            const float bv = lb[p * LS + wj * 32 + li];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        }
+    }
+    float* out = slab + ((size_t)b * nsplit + split) * C * C;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        out[(size_t)(c0 + wi * 32 + row) * C + d0 + wj * 32 + li] = acc[r];
+    }
+}
+
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                          int C, int nsplit, float inv_hw, int batch) {
+    const size_t cc = (size_t)C * C;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < (size_t)batch * cc; i += (size_t)gridDim.x * 256) {
+        const size_t b = i / cc, e = i % cc;
+        const float* s = slab + b * nsplit * cc + e;
+        float acc = 0.f;
+        for (int k = 0; k < nsplit; ++k) acc += s[(size_t)k * cc];
+        out[i] = acc * inv_hw;
+    }
+}
+
+hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st) {
+    if (channels % gram::TILE != 0) return hipErrorInvalidValue;
+    const int ns = gram_splits(batch, hw, channels);
+    int span = (hw + ns - 1) / ns;
+    span = ((span + gram::KP - 1) / gram::KP) * gram::KP;
+    const int ntile = channels / gram::TILE;
+    const unsigned grid = (unsigned)(batch * ntile * ntile * ns);
+    float* slab = static_cast<float*>(ws);
+    hipLaunchKernelGGL(gram_partial_kernel, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns, span);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t total = (size_t)batch * channels * channels;
+    unsigned rb = (unsigned)((total + 255) / 256);
+    if (rb > 4096) rb = 4096;
+    hipLaunchKernelGGL(gram_reduce_kernel, dim3(rb), dim3(256), 0, st, slab, out, channels, ns, 1.0f / (float)hw,
+                       batch);
+    return hipGetLastError();
+}
+
+}  // namespace rst

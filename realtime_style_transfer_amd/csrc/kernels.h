@@ -1,0 +1,82 @@
+// kernels.h — internal kernel interfaces of librst (not part of the public C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+
+namespace rst {
+
+enum ProMode { PRO_NONE = 0, PRO_AFF_RELU = 1, PRO_AFF = 2, PRO_AFF_RES = 3 };
+enum EpiMode { EPI_NONE = 0, EPI_RELU_BN = 1, EPI_RELU_STATS = 2, EPI_STATS = 3 };
+
+// Arguments of the implicit-GEMM MFMA conv kernel (conv_mfma.hip).
+struct ConvArgs {
+    const float* in;        // NHWC [B][H][W][cin] raw producer output
+    const float* res;       // residual source (PRO_AFF_RES), same shape as in
+    float* mat;             // materialise transformed input here (or null)
+    const float2* pro_ab;   // [B][cin] prologue affine (a, b)
+    const float* wpk;       // packed weights [n_blocks][nchunks][ngroups][wstage]
+    const float* bias;      // [ntot]
+    const float2* bn_ab;    // [ntot] BatchNorm affine (EPI_RELU_BN)
+    float* out;             // NHWC output
+    float4* part;           // [B][ntot][n_mtiles] {sum, M2, n} or null
+    int batch, H, W, cin;
+    int Ho, Wo;             // GEMM-space output dims (convT: input dims, shuffle doubles them)
+    int ntot;               // GEMM N
+    int cout;               // stored channels (convT: per phase)
+    int pad_t, pad_l;
+    int tiles_y, tiles_x, n_blocks, nchunks;
+    int pro_mode, epi_mode, shuffle;
+};
+
+// A compiled tile configuration of conv_mfma_kernel.
+struct ConvTile {
+    int id;
+    int kh, kw, stride, ck, nt, th, tw, tps, vec, mt, ngroups, wstage, lds_bytes;
+};
+
+bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out);
+hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st);
+// one-time per-configuration setup (dynamic LDS > 64 KB); call outside graph capture
+hipError_t conv_prepare(const ConvTile& t);
+
+// Final 9x9 transposed conv with Cout = 3 on the VALU (conv_small.hip).
+struct SmallConvArgs {
+    const float* in;        // [B][H][W][cin]
+    const float2* pro_ab;   // [B][cin] prologue affine + ReLU (or null: identity)
+    const float* w;         // packed [ky][ci][kx][3]
+    const float* bias;      // [3]
+    float* out;             // [B][H][W][3] raw conv output
+    float4* part;           // [B][3][n_tiles]
+    int batch, H, W, cin;
+    int tiles_y, tiles_x;
+};
+hipError_t small_conv_launch(const SmallConvArgs& a, hipStream_t st);
+int small_conv_tiles_y(int H);
+int small_conv_tiles_x(int W);
+
+// CIN statistics finalize: merge per-tile {sum, M2, n} (Chan, f64) -> per-(b,c) affine.
+struct FinalizeArgs {
+    const float4* part;      // [B][ntot][n_part]
+    const float* style;      // style params base (B, S, P) or null (then scale=1, bias=0)
+    const float* scale;      // alternative explicit scale [B][C] (or null)
+    const float* bias;       // alternative explicit bias [B][C] (or null)
+    float2* ab;              // out [B][C]
+    int batch, C, ntot, n_part, phases;
+    int style_stride;        // S*P
+    int style_offset;        // offset of scale in the style vector; bias at +C
+    float eps;
+};
+hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st);
+
+// y = act(a*x + b [+ res]) element-wise, act: 0 none, 1 relu, 2 sigmoid.  x,res,y [B][HW][C]
+hipError_t affine_act_launch(const float* x, const float2* ab, const float* res, float* y, int batch, long hw, int C,
+                             int act, hipStream_t st);
+
+// Per-tile statistics of an NHWC tensor (standalone instance norm).
+hipError_t tile_stats_launch(const float* x, float4* part, int batch, long hw, int C, int tile, hipStream_t st);
+
+// Gram matrices (gram.hip)
+size_t gram_workspace_bytes(int batch, int hw, int channels);
+hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st);
+
+}  // namespace rst

@@ -1,0 +1,127 @@
+// norm.hip — conditional-instance-norm statistics and element-wise apply kernels.
+//
+// ConditionalInstanceNormalization.call (realtime_style_transfer/models/styleTransfer.py:57-71):
+//   mean, var = tf.nn.moments(x, axes=[1,2])        (biased variance, per (b, c))
+//   x = x * rsqrt(var + eps) + (-mean * rsqrt(var + eps));  x = bias + x * scale
+// The producing conv writes per-tile {sum, M2, n} (two-pass inside the tile). finalize merges
+// them with Chan's parallel formula in f64 — deterministic (no atomics, fixed order) and
+// immune to the E[x^2]-E[x]^2 cancellation that ReLU'd, positive-weight residual convs
+// (mean/std ~ 20) would suffer — and folds scale/bias/rsqrt into one affine (a, b) per
+// (b, c) that the consumer applies in its prologue: y = a*x + b.
+#include <hip/hip_runtime.h>
+#include "kernels.h"
+
+namespace rst {
+
+template <typename T>
+__device__ __forceinline__ T block_sum256(T v, T* scratch) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) scratch[wave] = v;
+    __syncthreads();
+    T t = scratch[0] + scratch[1] + scratch[2] + scratch[3];
+    return t;
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
+    __shared__ double scratch[4];
+    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    double s = 0.0, n = 0.0;
+    for (int ph = 0; ph < a.phases; ++ph) {
+        const float4* p = a.part + ((size_t)b * a.ntot + ph * a.C + c) * a.n_part;
+        for (int t = tid; t < a.n_part; t += 256) {
+            const float4 v = p[t];
+            s += (double)v.x;
+            n += (double)v.z;
+        }
+    }
+    s = block_sum256(s, scratch);
+    n = block_sum256(n, scratch);
+    const double mean = n > 0.0 ? s / n : 0.0;
+    double m2 = 0.0;
+    for (int ph = 0; ph < a.phases; ++ph) {
+        const float4* p = a.part + ((size_t)b * a.ntot + ph * a.C + c) * a.n_part;
+        for (int t = tid; t < a.n_part; t += 256) {
+            const float4 v = p[t];
+            if (v.z > 0.f) {
+                const double d = (double)v.x / (double)v.z - mean;
+                m2 += (double)v.y + (double)v.z * d * d;
+            }
+        }
+    }
+    m2 = block_sum256(m2, scratch);
+    if (tid == 0) {
+        const double var = n > 0.0 ? m2 / n : 0.0;
+        const float rstd = (float)(1.0 / sqrt(var + (double)a.eps));
+        float scale = 1.f, bias = 0.f;
+        if (a.style != nullptr) {
+            const float* sp = a.style + (size_t)b * a.style_stride + a.style_offset;
+            scale = sp[c];
+            bias = sp[a.C + c];
+        } else if (a.scale != nullptr) {
+            scale = a.scale[b * a.C + c];
+            bias = a.bias[b * a.C + c];
+        }
+        const float aa = scale * rstd;
+        a.ab[b * a.C + c] = make_float2(aa, bias - (float)mean * aa);
+    }
+}
+
+hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(a.C, a.batch), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void affine_act_kernel(const float* __restrict__ x, const float2* __restrict__ ab,
+                                                         const float* __restrict__ res, float* __restrict__ y,
+                                                         long total, long hwc, int C, int act) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+        const int b = (int)(i / hwc);
+        const int c = (int)(i % C);
+        const float2 p = ab[b * C + c];
+        float v = fmaf(p.x, x[i], p.y);
+        if (res != nullptr) v += res[i];
+        if (act == 1) v = fmaxf(v, 0.f);
+        else if (act == 2) v = 1.f / (1.f + __expf(-v));
+        y[i] = v;
+    }
+}
+
+hipError_t affine_act_launch(const float* x, const float2* ab, const float* res, float* y, int batch, long hw, int C,
+                             int act, hipStream_t st) {
+    const long total = (long)batch * hw * C;
+    long blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(affine_act_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, ab, res, y, total, hw * C, C, act);
+    return hipGetLastError();
+}
+
+// Per-tile {sum, M2, n} of x [B][hw][C] over tiles of `tile` pixels; part [B][C][n_tiles].
+__global__ __launch_bounds__(256) void tile_stats_kernel(const float* __restrict__ x, float4* __restrict__ part,
+                                                         long hw, int C, int tile, int n_tiles) {
+    const int t = blockIdx.x, b = blockIdx.y;
+    const long p0 = (long)t * tile;
+    const long p1 = (p0 + tile < hw) ? p0 + tile : hw;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float s = 0.f;
+        for (long p = p0; p < p1; ++p) s += x[((size_t)b * hw + p) * C + c];
+        const float cnt = (float)(p1 - p0);
+        const float mean = s / cnt;
+        float m2 = 0.f;
+        for (long p = p0; p < p1; ++p) {
+            const float d = x[((size_t)b * hw + p) * C + c] - mean;
+            m2 = fmaf(d, d, m2);
+        }
+        part[((size_t)b * C + c) * n_tiles + t] = make_float4(s, m2, cnt, 0.f);
+    }
+}
+
+hipError_t tile_stats_launch(const float* x, float4* part, int batch, long hw, int C, int tile, hipStream_t st) {
+    const int n_tiles = (int)((hw + tile - 1) / tile);
+    hipLaunchKernelGGL(tile_stats_kernel, dim3(n_tiles, batch), dim3(256), 0, st, x, part, hw, C, tile, n_tiles);
+    return hipGetLastError();
+}
+
+}  // namespace rst

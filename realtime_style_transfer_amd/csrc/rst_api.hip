@@ -1,0 +1,529 @@
+// rst_api.hip — host side of the librst C ABI (include/rst.h).
+//
+// rst_create restates create_style_transfer_model's block derivation
+// (realtime_style_transfer/models/styleTransfer.py:213-332), uploads the Keras-ordered weights
+// into the device layouts the kernels stage from, and allocates every activation / statistics
+// buffer once (sized for max_batch; HBM is plentiful — 288 GB — so every layer keeps its own
+// output buffer and nothing is allocated or freed in the hot path).
+//
+// rst_forward launches, in order, one kernel per conv (+ one CIN-finalize per normalised conv)
+// on the caller's stream. Fusion across the layer boundary:
+//   contract:  conv + bias + ReLU + BN + ReLU in one epilogue                 (:194-203)
+//   residual:  conv + ReLU + tile stats;  CIN-apply (+ReLU | +skip Add) is done by the NEXT
+//              conv while it stages its input halo, which also materialises the block output
+//              needed by the next skip connection                              (:144-185)
+//   expand:    2x2 phase conv (pixel-shuffle store) + tile stats; CIN-apply + ReLU in the
+//              next conv's prologue                                            (:95-141)
+//   last:      VALU 9x9 conv (CIN-apply+ReLU prologue) + stats -> finalize -> sigmoid(CIN) (:269-276)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rst.h"
+#include "kernels.h"
+
+using namespace rst;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return fail(RST_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+const int CONTRACT_FILTERS[4] = {16, 32, 32, 32};                // styleTransfer.py:218-223
+const int EXPAND_FILTERS[8] = {32, 16, 8, 4, 3, 3, 3, 3};        // styleTransfer.py:247-256
+
+enum LayerKind { K_CONV = 0, K_CONVT2 = 1, K_SMALL = 2 };
+enum Norm { N_BN = 0, N_CIN = 1 };
+enum Post { P_RELU = 0, P_NONE = 1, P_SIGMOID = 2 };
+
+struct LayerSpec {
+    std::string name;
+    int keras_kind;      // 0 Conv2D, 1 Conv2DTranspose
+    int k, stride, cin, cout;
+    int H, W, Ho, Wo;    // input / output spatial dims
+    int norm, post;
+    bool conv_relu;
+    int style_offset;
+    int res_block;       // residual block index or -1
+    int res_conv;        // 0/1 within the residual block
+};
+
+struct LayerExec {
+    LayerSpec s;
+    int kind = K_CONV;
+    ConvTile tile{};
+    int ntot = 0, gHo = 0, gWo = 0, pad_t = 0, pad_l = 0;
+    int tiles_y = 0, tiles_x = 0, n_blocks = 1, nchunks = 1;
+    int n_part = 0;
+    float* d_w = nullptr;
+    float* d_bias = nullptr;
+    float2* d_bn = nullptr;
+    float* d_out = nullptr;       // raw (CIN) or final (BN) output [max_batch][Ho][Wo][cout]
+    float4* d_part = nullptr;
+    float2* d_ab = nullptr;       // CIN affine of this layer's output [max_batch][cout]
+    float* d_mat = nullptr;       // block input materialised by this layer's prologue (or null)
+    // prologue (how this layer reads its input)
+    int pro = PRO_NONE;
+    int pro_src = -1;             // layer whose d_ab/d_out feed the prologue (-1: network input)
+    const float* pro_res = nullptr;
+    // debug "emitted" tensor of this layer = act(a*raw + b) [+ res]
+    const float* emit_res = nullptr;
+};
+
+size_t layer_weight_count(const LayerSpec& s) {
+    size_t n = (size_t)s.k * s.k * s.cin * s.cout + s.cout;
+    if (s.norm == N_BN) n += 4 * (size_t)s.cout;
+    return n;
+}
+
+int build_plan(const rst_shape* sh, std::vector<LayerSpec>& L, int* P) {
+    if (sh->in_h <= 0 || sh->in_w <= 0 || sh->in_c <= 0 || sh->out_h <= 0 || sh->out_w <= 0 ||
+        sh->bottleneck_res_y <= 0 || sh->bottleneck_num_filters <= 0 || sh->num_styles <= 0)
+        return fail(RST_ERR_INVALID, "rst_shape: all dimensions must be positive");
+    const int n_c = (int)std::ceil(std::log2((double)sh->in_h) - std::log2((double)sh->bottleneck_res_y));
+    if (n_c < 0 || n_c > 4) return fail(RST_ERR_UNSUPPORTED, "number of contract blocks must be in [0, 4]");
+    int H = sh->in_h, W = sh->in_w, cin = sh->in_c;
+    L.clear();
+    L.push_back({"contract_start", 0, 9, 1, cin, 32, H, W, H, W, N_BN, P_RELU, true, -1, -1, -1});
+    cin = 32;
+    for (int i = 0; i < n_c; ++i) {
+        const int f = CONTRACT_FILTERS[i];
+        const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+        L.push_back({"contract_" + std::to_string(i), 0, 3, 2, cin, f, H, W, Ho, Wo, N_BN, P_RELU, true, -1, -1, -1});
+        H = Ho; W = Wo; cin = f;
+    }
+    const int F = sh->bottleneck_num_filters;
+    int off = 0;
+    for (int r = 0; r < 5; ++r)
+        for (int j = 0; j < 2; ++j) {
+            L.push_back({"residual_block_" + std::to_string(r) + "_conv" + std::to_string(j), 0, 3, 1, cin, F, H, W, H,
+                         W, N_CIN, j == 0 ? P_RELU : P_NONE, true, off, r, j});
+            off += 2 * F;
+            cin = F;
+        }
+    const int n_e = (int)std::ceil(std::log2((double)sh->out_h) - std::log2((double)H));
+    if (n_e < 0 || n_e > 8) return fail(RST_ERR_UNSUPPORTED, "number of expand blocks must be in [0, 8]");
+    for (int i = 0; i < n_e; ++i) {
+        const int f = EXPAND_FILTERS[i];
+        L.push_back({"expand_" + std::to_string(i), 1, 3, 2, cin, f, H, W, 2 * H, 2 * W, N_CIN, P_RELU, false, off,
+                     -1, -1});
+        off += 2 * f;
+        H *= 2; W *= 2; cin = f;
+    }
+    L.push_back({"expand_last", 1, 9, 1, cin, 3, H, W, H, W, N_CIN, P_SIGMOID, false, off, -1, -1});
+    off += 6;
+    if (H != sh->out_h || W != sh->out_w)
+        return fail(RST_ERR_INVALID, "plan output " + std::to_string(H) + "x" + std::to_string(W) +
+                                         " does not match out_h x out_w");
+    *P = off;
+    return RST_OK;
+}
+
+// Pack a GEMM-form kernel Wg[tap][ci][n] (taps = kh*kw, row-major) into the LDS stage image
+// [nb][chunk][g][t][sg][h][n][v] of conv_mfma_kernel.
+std::vector<float> pack_tiles(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t) {
+    const int ck = t.ck, nt = t.nt, tps = t.tps, vec = t.vec;
+    const int ksteps = ck / 2, sg_n = ksteps / vec;
+    const int nchunks = (cin + ck - 1) / ck, nblocks = (ntot + nt - 1) / nt, ngroups = taps / tps;
+    std::vector<float> out((size_t)nblocks * nchunks * ngroups * t.wstage, 0.f);
+    size_t idx = 0;
+    for (int nb = 0; nb < nblocks; ++nb)
+        for (int c = 0; c < nchunks; ++c)
+            for (int g = 0; g < ngroups; ++g)
+                for (int tt = 0; tt < tps; ++tt)
+                    for (int sg = 0; sg < sg_n; ++sg)
+                        for (int h = 0; h < 2; ++h)
+                            for (int n = 0; n < nt; ++n)
+                                for (int v = 0; v < vec; ++v) {
+                                    const int tap = g * tps + tt;
+                                    const int ci = c * ck + h * ksteps + sg * vec + v;
+                                    const int ng = nb * nt + n;
+                                    float val = 0.f;
+                                    if (ci < cin && ng < ntot) val = Wg[((size_t)tap * cin + ci) * ntot + ng];
+                                    out[idx++] = val;
+                                }
+    return out;
+}
+
+template <typename T>
+int upload(T** dst, const void* src, size_t bytes) {
+    if (hipMalloc((void**)dst, bytes) != hipSuccess) return fail(RST_ERR_ALLOC, "hipMalloc failed");
+    if (src != nullptr && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(RST_ERR_HIP, "hipMemcpy failed");
+    return RST_OK;
+}
+
+}  // namespace
+
+struct rst_handle {
+    rst_shape shape;
+    int P = 0;
+    std::vector<LayerExec> layers;
+    std::vector<void*> allocs;
+    ~rst_handle() {
+        for (void* p : allocs) hipFree(p);
+    }
+    template <typename T>
+    int alloc(T** p, size_t bytes, const void* src = nullptr) {
+        int st = upload(p, src, bytes);
+        if (*p) allocs.push_back((void*)*p);
+        return st;
+    }
+};
+
+extern "C" {
+
+const char* rst_last_error(void) { return g_last_error.c_str(); }
+const char* rst_version(void) { return "rst-mi355x 0.1 (gfx950, f32 MFMA)"; }
+
+size_t rst_num_weights_for_shape(const rst_shape* shape) {
+    std::vector<LayerSpec> L;
+    int P = 0;
+    if (shape == nullptr || build_plan(shape, L, &P) != RST_OK) return 0;
+    size_t n = 0;
+    for (auto& s : L) n += layer_weight_count(s);
+    return n;
+}
+
+int rst_num_style_params(const rst_handle* h) { return h ? h->P : -1; }
+int rst_num_layers(const rst_handle* h) { return h ? (int)h->layers.size() : -1; }
+
+int rst_create(const rst_shape* shape, const float* weights_host, size_t num_weights, rst_handle** out) {
+    if (shape == nullptr || out == nullptr || weights_host == nullptr)
+        return fail(RST_ERR_INVALID, "rst_create: null argument");
+    *out = nullptr;
+    if (shape->num_styles != 1)
+        return fail(RST_ERR_UNSUPPORTED, "rst_create: num_styles > 1 (style_weights blending) not implemented yet");
+    if (shape->max_batch <= 0) return fail(RST_ERR_INVALID, "rst_create: max_batch must be positive");
+    std::vector<LayerSpec> specs;
+    int P = 0;
+    int st = build_plan(shape, specs, &P);
+    if (st != RST_OK) return st;
+    size_t expect = 0;
+    for (auto& s : specs) expect += layer_weight_count(s);
+    if (expect != num_weights)
+        return fail(RST_ERR_INVALID, "rst_create: expected " + std::to_string(expect) + " weights, got " +
+                                         std::to_string(num_weights));
+
+    rst_handle* h = new rst_handle();
+    h->shape = *shape;
+    h->P = P;
+    const int B = shape->max_batch;
+    const float* wp = weights_host;
+    h->layers.resize(specs.size());
+    for (size_t li = 0; li < specs.size(); ++li) {
+        LayerExec& e = h->layers[li];
+        const LayerSpec& s = specs[li];
+        e.s = s;
+        const size_t kcount = (size_t)s.k * s.k * s.cin * s.cout;
+        const float* kern = wp;
+        const float* bias = wp + kcount;
+        wp += kcount + s.cout;
+        std::vector<float> bias_n;
+        if (s.keras_kind == 1 && s.k == 9 && s.stride == 1) {
+            // ---- final 9x9 transposed conv: flip -> correlation, pack [ky][ci][kx][co]
+            if (s.cout != 3) { delete h; return fail(RST_ERR_UNSUPPORTED, "last layer must have 3 channels"); }
+            e.kind = K_SMALL;
+            std::vector<float> w((size_t)81 * s.cin * 3);
+            for (int ky = 0; ky < 9; ++ky)
+                for (int kx = 0; kx < 9; ++kx)
+                    for (int ci = 0; ci < s.cin; ++ci)
+                        for (int co = 0; co < 3; ++co)
+                            w[(((size_t)ky * s.cin + ci) * 9 + kx) * 3 + co] =
+                                kern[(((size_t)(8 - ky) * 9 + (8 - kx)) * 3 + co) * s.cin + ci];
+            if ((st = h->alloc(&e.d_w, w.size() * 4, w.data())) != RST_OK) { delete h; return st; }
+            bias_n.assign(bias, bias + 3);
+            e.ntot = 3;
+            e.tiles_y = small_conv_tiles_y(s.Ho);
+            e.tiles_x = small_conv_tiles_x(s.Wo);
+            e.n_part = e.tiles_y * e.tiles_x;
+        } else {
+            int taps, ntot, kh;
+            std::vector<float> Wg;
+            if (s.keras_kind == 0) {
+                kh = s.k;
+                taps = s.k * s.k;
+                ntot = s.cout;
+                Wg.assign(kern, kern + kcount);   // HWIO already == [tap][ci][co]
+                e.kind = K_CONV;
+                const int pt = std::max((s.Ho - 1) * s.stride + s.k - s.H, 0);
+                const int pl = std::max((s.Wo - 1) * s.stride + s.k - s.W, 0);
+                e.pad_t = pt / 2;
+                e.pad_l = pl / 2;
+                e.gHo = s.Ho;
+                e.gWo = s.Wo;
+                bias_n.assign(bias, bias + s.cout);
+            } else {
+                if (!(s.k == 3 && s.stride == 2)) {
+                    delete h;
+                    return fail(RST_ERR_UNSUPPORTED, "Conv2DTranspose other than 3x3/s2 and 9x9/s1");
+                }
+                // 3x3 s2 SAME transposed conv == 2x2 conv (pad 1) with 4 output phases:
+                // out[2p+py][2q+px][co] = sum_{ty,tx} in[p+ty-1][q+tx-1] . w[py+2(1-ty)][px+2(1-tx)][co]
+                kh = 2;
+                taps = 4;
+                ntot = 4 * s.cout;
+                e.kind = K_CONVT2;
+                Wg.assign((size_t)4 * s.cin * ntot, 0.f);
+                for (int ty = 0; ty < 2; ++ty)
+                    for (int tx = 0; tx < 2; ++tx)
+                        for (int py = 0; py < 2; ++py)
+                            for (int px = 0; px < 2; ++px) {
+                                const int ky = py + 2 * (1 - ty), kx = px + 2 * (1 - tx);
+                                if (ky > 2 || kx > 2) continue;
+                                for (int ci = 0; ci < s.cin; ++ci)
+                                    for (int co = 0; co < s.cout; ++co)
+                                        Wg[((size_t)(ty * 2 + tx) * s.cin + ci) * ntot + (py * 2 + px) * s.cout + co] =
+                                            kern[(((size_t)ky * 3 + kx) * s.cout + co) * s.cin + ci];
+                            }
+                e.pad_t = e.pad_l = 1;
+                e.gHo = s.H;
+                e.gWo = s.W;
+                for (int n = 0; n < ntot; ++n) bias_n.push_back(bias[n % s.cout]);
+            }
+            if (!conv_select(kh, s.keras_kind == 0 ? s.stride : 1, s.cin, ntot, &e.tile)) {
+                delete h;
+                return fail(RST_ERR_UNSUPPORTED, "no conv tile configuration for layer " + s.name);
+            }
+            e.ntot = ntot;
+            e.tiles_y = (e.gHo + e.tile.th - 1) / e.tile.th;
+            e.tiles_x = (e.gWo + e.tile.tw - 1) / e.tile.tw;
+            e.n_blocks = (ntot + e.tile.nt - 1) / e.tile.nt;
+            e.nchunks = (s.cin + e.tile.ck - 1) / e.tile.ck;
+            e.n_part = e.tiles_y * e.tiles_x * e.tile.mt;
+            std::vector<float> pk = pack_tiles(Wg, taps, s.cin, ntot, e.tile);
+            if ((st = h->alloc(&e.d_w, pk.size() * 4, pk.data())) != RST_OK) { delete h; return st; }
+        }
+        if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
+        if (s.norm == N_BN) {
+            const float* gamma = wp;
+            const float* beta = wp + s.cout;
+            const float* mm = wp + 2 * s.cout;
+            const float* mv = wp + 3 * s.cout;
+            wp += 4 * s.cout;
+            std::vector<float2> ab(s.cout);
+            for (int c = 0; c < s.cout; ++c) {
+                const double inv = (double)gamma[c] / std::sqrt((double)mv[c] + 1e-3);
+                ab[c] = make_float2((float)inv, (float)((double)beta[c] - (double)mm[c] * inv));
+            }
+            if ((st = h->alloc(&e.d_bn, ab.size() * sizeof(float2), ab.data())) != RST_OK) { delete h; return st; }
+        } else {
+            if ((st = h->alloc(&e.d_part, (size_t)B * e.ntot * e.n_part * sizeof(float4))) != RST_OK) { delete h; return st; }
+            if ((st = h->alloc(&e.d_ab, (size_t)B * s.cout * sizeof(float2))) != RST_OK) { delete h; return st; }
+        }
+        if ((st = h->alloc(&e.d_out, (size_t)B * s.Ho * s.Wo * s.cout * 4)) != RST_OK) { delete h; return st; }
+    }
+
+    // ---- wire prologues: how each layer consumes its predecessor (see file header)
+    const float* block_input = nullptr;   // materialised input of the current residual block
+    for (size_t li = 0; li < h->layers.size(); ++li) {
+        LayerExec& e = h->layers[li];
+        if (li == 0) { e.pro = PRO_NONE; e.pro_src = -1; continue; }
+        LayerExec& p = h->layers[li - 1];
+        e.pro_src = (int)li - 1;
+        if (p.s.norm == N_BN) {
+            e.pro = PRO_NONE;
+        } else if (p.s.post == P_RELU) {
+            e.pro = PRO_AFF_RELU;
+        } else {
+            // predecessor is the second conv of residual block r: block output = [x_r +] CIN(h)
+            const bool first = p.s.res_block == 0;
+            e.pro = first ? PRO_AFF : PRO_AFF_RES;
+            e.pro_res = first ? nullptr : block_input;
+            p.emit_res = e.pro_res;
+            if (e.s.res_block > 0 && e.s.res_conv == 0) {
+                // this conv opens residual block r>0: materialise its input for the skip add
+                if ((st = h->alloc(&e.d_mat, (size_t)B * e.s.H * e.s.W * e.s.cin * 4)) != RST_OK) { delete h; return st; }
+            }
+        }
+        if (e.s.res_block >= 1 && e.s.res_conv == 0) block_input = e.d_mat;
+    }
+    // kernels with > 64 KB of dynamic LDS need the attribute before any (graph-captured) launch
+    for (auto& e : h->layers) {
+        if (e.kind == K_SMALL) continue;
+        hipError_t pe = conv_prepare(e.tile);
+        if (pe != hipSuccess) {
+            delete h;
+            return fail(RST_ERR_HIP, std::string("conv_prepare: ") + hipGetErrorString(pe));
+        }
+    }
+    *out = h;
+    return RST_OK;
+}
+
+void rst_destroy(rst_handle* h) { delete h; }
+
+static int launch_layer(rst_handle* h, size_t li, const float* content, const float* style, int B, hipStream_t st) {
+    LayerExec& e = h->layers[li];
+    const float* in = (e.pro_src < 0) ? content : h->layers[e.pro_src].d_out;
+    const float2* pro_ab = (e.pro_src >= 0 && e.pro != PRO_NONE) ? h->layers[e.pro_src].d_ab : nullptr;
+    if (e.kind == K_SMALL) {
+        SmallConvArgs a{};
+        a.in = in;
+        a.pro_ab = pro_ab;
+        a.w = e.d_w;
+        a.bias = e.d_bias;
+        a.out = e.d_out;
+        a.part = e.d_part;
+        a.batch = B;
+        a.H = e.s.H;
+        a.W = e.s.W;
+        a.cin = e.s.cin;
+        a.tiles_y = e.tiles_y;
+        a.tiles_x = e.tiles_x;
+        if (e.pro != PRO_AFF_RELU && e.pro != PRO_NONE)
+            return fail(RST_ERR_UNSUPPORTED, "last layer prologue must be CIN+ReLU");
+        HIP_TRY(small_conv_launch(a, st));
+    } else {
+        ConvArgs a{};
+        a.in = in;
+        a.res = e.pro_res;
+        a.mat = e.d_mat;
+        a.pro_ab = pro_ab;
+        a.wpk = e.d_w;
+        a.bias = e.d_bias;
+        a.bn_ab = e.d_bn;
+        a.out = e.d_out;
+        a.part = e.d_part;
+        a.batch = B;
+        a.H = e.s.H;
+        a.W = e.s.W;
+        a.cin = e.s.cin;
+        a.Ho = e.gHo;
+        a.Wo = e.gWo;
+        a.ntot = e.ntot;
+        a.cout = e.s.cout;
+        a.pad_t = e.pad_t;
+        a.pad_l = e.pad_l;
+        a.tiles_y = e.tiles_y;
+        a.tiles_x = e.tiles_x;
+        a.n_blocks = e.n_blocks;
+        a.nchunks = e.nchunks;
+        a.pro_mode = e.pro;
+        a.epi_mode = e.s.norm == N_BN ? EPI_RELU_BN : (e.s.conv_relu ? EPI_RELU_STATS : EPI_STATS);
+        a.shuffle = e.kind == K_CONVT2 ? 1 : 0;
+        HIP_TRY(conv_launch(e.tile, a, st));
+    }
+    if (e.s.norm == N_CIN) {
+        FinalizeArgs f{};
+        f.part = e.d_part;
+        f.style = style;
+        f.ab = e.d_ab;
+        f.batch = B;
+        f.C = e.s.cout;
+        f.ntot = e.ntot;
+        f.n_part = e.n_part;
+        f.phases = e.kind == K_CONVT2 ? 4 : 1;
+        f.style_stride = h->shape.num_styles * h->P;
+        f.style_offset = e.s.style_offset;
+        f.eps = 1e-5f;
+        HIP_TRY(finalize_launch(f, st));
+    }
+    return RST_OK;
+}
+
+int rst_forward(rst_handle* h, const float* content, const float* style_params, const float* style_weights,
+                float* out, int batch, void* stream) {
+    if (h == nullptr || content == nullptr || style_params == nullptr || out == nullptr)
+        return fail(RST_ERR_INVALID, "rst_forward: null argument");
+    if (batch <= 0 || batch > h->shape.max_batch)
+        return fail(RST_ERR_INVALID, "rst_forward: batch " + std::to_string(batch) + " outside [1, max_batch=" +
+                                         std::to_string(h->shape.max_batch) + "]");
+    if (style_weights != nullptr && h->shape.num_styles == 1)
+        return fail(RST_ERR_INVALID, "rst_forward: style_weights given but num_styles == 1");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    for (size_t li = 0; li < h->layers.size(); ++li) {
+        int r = launch_layer(h, li, content, style_params, batch, st);
+        if (r != RST_OK) return r;
+    }
+    const LayerExec& last = h->layers.back();
+    HIP_TRY(affine_act_launch(last.d_out, last.d_ab, nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
+    return RST_OK;
+}
+
+int rst_layer_output_shape(const rst_handle* h, int idx, int batch, int* hwc3) {
+    if (h == nullptr || idx < 0 || idx >= (int)h->layers.size() || hwc3 == nullptr)
+        return fail(RST_ERR_INVALID, "rst_layer_output_shape: bad argument");
+    const LayerSpec& s = h->layers[idx].s;
+    hwc3[0] = s.Ho;
+    hwc3[1] = s.Wo;
+    hwc3[2] = s.cout;
+    (void)batch;
+    return RST_OK;
+}
+
+int rst_copy_activation(rst_handle* h, int idx, float* dst, size_t count, int batch, void* stream) {
+    if (h == nullptr || idx < 0 || idx >= (int)h->layers.size() || dst == nullptr)
+        return fail(RST_ERR_INVALID, "rst_copy_activation: bad argument");
+    const LayerExec& e = h->layers[idx];
+    const size_t n = (size_t)batch * e.s.Ho * e.s.Wo * e.s.cout;
+    if (count != n) return fail(RST_ERR_INVALID, "rst_copy_activation: count mismatch, expected " + std::to_string(n));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (e.s.norm == N_BN) {
+        HIP_TRY(hipMemcpyAsync(dst, e.d_out, n * 4, hipMemcpyDeviceToDevice, st));
+    } else {
+        const int act = e.s.post == P_RELU ? 1 : (e.s.post == P_SIGMOID ? 2 : 0);
+        HIP_TRY(affine_act_launch(e.d_out, e.d_ab, e.emit_res, dst, batch, (long)e.s.Ho * e.s.Wo, e.s.cout, act, st));
+    }
+    return RST_OK;
+}
+
+size_t rst_gram_workspace_size(int batch, int hw, int channels) { return gram_workspace_bytes(batch, hw, channels); }
+
+int rst_gram(const float* feat, int batch, int hw, int channels, float* out, void* workspace, void* stream) {
+    if (feat == nullptr || out == nullptr || workspace == nullptr || batch <= 0 || hw <= 0 || channels <= 0)
+        return fail(RST_ERR_INVALID, "rst_gram: bad argument");
+    if (channels % 64 != 0) return fail(RST_ERR_UNSUPPORTED, "rst_gram: channels must be a multiple of 64");
+    HIP_TRY(gram_launch(feat, batch, hw, channels, out, workspace, static_cast<hipStream_t>(stream)));
+    return RST_OK;
+}
+
+static const int IN_TILE = 256;
+
+size_t rst_instance_norm_workspace_size(int batch, int hw, int channels) {
+    const size_t n_tiles = (size_t)(hw + IN_TILE - 1) / IN_TILE;
+    return (size_t)batch * channels * n_tiles * sizeof(float4) + (size_t)batch * channels * sizeof(float2);
+}
+
+int rst_instance_norm(const float* x, int batch, int hw, int channels, const float* scale, const float* bias,
+                      float eps, int relu, float* y, void* workspace, void* stream) {
+    if (x == nullptr || y == nullptr || workspace == nullptr || scale == nullptr || bias == nullptr || batch <= 0 ||
+        hw <= 0 || channels <= 0)
+        return fail(RST_ERR_INVALID, "rst_instance_norm: bad argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int n_tiles = (hw + IN_TILE - 1) / IN_TILE;
+    float4* part = static_cast<float4*>(workspace);
+    float2* ab = reinterpret_cast<float2*>(part + (size_t)batch * channels * n_tiles);
+    HIP_TRY(tile_stats_launch(x, part, batch, hw, channels, IN_TILE, st));
+    FinalizeArgs f{};
+    f.part = part;
+    f.scale = scale;
+    f.bias = bias;
+    f.ab = ab;
+    f.batch = batch;
+    f.C = channels;
+    f.ntot = channels;
+    f.n_part = n_tiles;
+    f.phases = 1;
+    f.eps = eps;
+    HIP_TRY(finalize_launch(f, st));
+    HIP_TRY(affine_act_launch(x, ab, nullptr, y, batch, hw, channels, relu ? 1 : 0, st));
+    return RST_OK;
+}
+
+}  // extern "C"

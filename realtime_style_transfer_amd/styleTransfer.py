@@ -1,0 +1,168 @@
+"""Host mirror of ``realtime_style_transfer/models/styleTransfer.py`` on librst (MI355X).
+
+``create_style_transfer_model(input_shape, output_shape, bottleneck_res_y,
+bottleneck_num_filters, num_styles, name)`` keeps the reference signature
+(styleTransfer.py:213-214) and return value ``(model, num_style_parameters)`` (:332).
+The model is called like the Keras model: ``model({'content': (B,H,W,C),
+'style_params': (B,S,P)[, 'style_weights': ...]})`` -> ``(B,Ho,Wo,3)`` float32 in (0, 1),
+NHWC, on the GPU. All compute runs in hand-written gfx950 kernels behind the C ABI
+(include/rst.h); there is no CPU fallback.
+
+Weights: ``get_weights()/set_weights()`` use the Keras ``model.get_weights()`` order of the
+reference graph (see plan.py); the default is the seeded initialisation that mirrors the
+reference initialisers (styleTransfer.py:97,146,190).
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .plan import CIN_EPS, Plan, init_weights, network_plan
+
+log = logging.getLogger(__name__)
+
+
+class StyleTransferModel:
+    """A built transfer network resident on one GPU (one librst handle)."""
+
+    def __init__(self, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, num_styles=1,
+                 name="StyleTransferModel", weights: Optional[Sequence[np.ndarray]] = None, seed: int = 2,
+                 max_batch: int = 8, device=None):
+        self.name = name
+        self.plan: Plan = network_plan(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
+                                       num_styles)
+        self.input_shape = tuple(int(v) for v in input_shape)
+        self.output_shape = tuple(int(v) for v in output_shape)
+        self.num_styles = int(num_styles)
+        self.num_style_parameters = self.plan.num_style_params
+        self.max_batch = int(max_batch)
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self._handle = None
+        self._weights = [np.ascontiguousarray(w, np.float32) for w in
+                         (weights if weights is not None else init_weights(self.plan, seed))]
+        self._build()
+
+    # ------------------------------------------------------------------ lifecycle
+    def _shape_struct(self) -> _lib.RstShape:
+        H, W, C = self.input_shape
+        return _lib.RstShape(H, W, C, self.output_shape[0], self.output_shape[1], self.plan.bottleneck_res_y,
+                             self.plan.bottleneck_num_filters, self.num_styles, self.max_batch)
+
+    def _build(self):
+        lib = _lib.load()
+        shapes = self.plan.weight_shapes()
+        if len(self._weights) != len(shapes) or any(tuple(w.shape) != tuple(s) for w, s in zip(self._weights, shapes)):
+            raise ValueError("weights do not match the network plan: expected shapes "
+                             f"{shapes}, got {[w.shape for w in self._weights]}")
+        flat = np.concatenate([w.reshape(-1) for w in self._weights]).astype(np.float32)
+        shape = self._shape_struct()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(lib.rst_create(ctypes.byref(shape), flat.ctypes.data, flat.size, ctypes.byref(h)))
+        self._release()
+        self._handle = h
+        P = lib.rst_num_style_params(h)
+        if P != self.num_style_parameters:
+            raise RuntimeError(f"librst plan P={P} disagrees with host plan P={self.num_style_parameters}")
+
+    def _release(self):
+        if self._handle is not None:
+            _lib.load().rst_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ Keras-like API
+    def get_weights(self) -> List[np.ndarray]:
+        return [w.copy() for w in self._weights]
+
+    def set_weights(self, weights: Sequence[np.ndarray]):
+        self._weights = [np.ascontiguousarray(w, np.float32) for w in weights]
+        self._build()
+
+    @property
+    def input(self) -> Dict[str, tuple]:
+        spec = {'content': (None,) + self.input_shape, 'style_params': (None, self.num_styles,
+                                                                           self.num_style_parameters)}
+        if self.num_styles > 1:
+            spec['style_weights'] = (None, self.output_shape[0], self.output_shape[1], self.num_styles - 1)
+        return spec
+
+    def _check_inputs(self, content: torch.Tensor, style_params: torch.Tensor):
+        if content.dim() != 4 or tuple(content.shape[1:]) != self.input_shape:
+            raise ValueError(f"content must be (B,{','.join(map(str, self.input_shape))}), got {tuple(content.shape)}")
+        B = content.shape[0]
+        if style_params.dim() == 2:
+            style_params = style_params.unsqueeze(1)
+        if tuple(style_params.shape) != (B, self.num_styles, self.num_style_parameters):
+            raise ValueError(f"style_params must be (B,{self.num_styles},{self.num_style_parameters}), "
+                             f"got {tuple(style_params.shape)}")
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} exceeds max_batch={self.max_batch} chosen at build time")
+        return style_params
+
+    def __call__(self, inputs: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None,
+                 stream=None) -> torch.Tensor:
+        content = inputs['content']
+        style_params = self._check_inputs(content, inputs['style_params'])
+        if 'style_weights' in inputs and self.num_styles == 1:
+            raise ValueError("style_weights given but num_styles == 1")
+        content = content.contiguous()
+        style_params = style_params.contiguous()
+        B = content.shape[0]
+        if out is None:
+            out = torch.empty((B,) + self.output_shape, dtype=torch.float32, device=content.device)
+        _lib.check(_lib.load().rst_forward(self._handle, _lib.dev_ptr(content), _lib.dev_ptr(style_params), None,
+                                           _lib.dev_ptr(out), B, _lib.stream_ptr(stream)))
+        return out
+
+    predict = __call__
+
+    # ------------------------------------------------------------------ debugging
+    def num_layers(self) -> int:
+        return _lib.load().rst_num_layers(self._handle)
+
+    def layer_output(self, idx: int, batch: int) -> torch.Tensor:
+        """Most recent output of conv layer ``idx`` as its reference block emits it."""
+        lib = _lib.load()
+        hwc = (ctypes.c_int * 3)()
+        _lib.check(lib.rst_layer_output_shape(self._handle, idx, batch, hwc))
+        t = torch.empty((batch, hwc[0], hwc[1], hwc[2]), dtype=torch.float32, device=self.device)
+        _lib.check(lib.rst_copy_activation(self._handle, idx, _lib.dev_ptr(t), t.numel(), batch, _lib.stream_ptr()))
+        return t
+
+
+def create_style_transfer_model(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, num_styles,
+                                name="StyleTransferModel", **kwargs):
+    """Drop-in for styleTransfer.create_style_transfer_model (styleTransfer.py:213-332)."""
+    log.info(f"Using {num_styles} styles")
+    model = StyleTransferModel(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, num_styles,
+                               name=name, **kwargs)
+    return model, model.num_style_parameters
+
+
+def instance_norm(x: torch.Tensor, scale: torch.Tensor, bias: torch.Tensor, eps: float = CIN_EPS,
+                  relu: bool = False) -> torch.Tensor:
+    """ConditionalInstanceNormalization.call (styleTransfer.py:57-71) for S=1 on librst.
+
+    x (B,H,W,C); scale/bias (B,C)."""
+    lib = _lib.load()
+    B, H, W, C = x.shape
+    x = x.contiguous()
+    scale = scale.reshape(B, C).contiguous()
+    bias = bias.reshape(B, C).contiguous()
+    ws = torch.empty(lib.rst_instance_norm_workspace_size(B, H * W, C), dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(x)
+    _lib.check(lib.rst_instance_norm(_lib.dev_ptr(x), B, H * W, C, _lib.dev_ptr(scale), _lib.dev_ptr(bias),
+                                     float(eps), int(relu), _lib.dev_ptr(y), int(ws.data_ptr()), _lib.stream_ptr()))
+    return y
+

@@ -1,0 +1,91 @@
+"""Generate the golden fixtures under tests/golden/ from the CPU oracle.
+
+Run: ``python tests/golden/make_golden.py`` (CPU only, a few seconds).
+
+Fixtures (all float32 inputs/weights, float64 expected outputs, npz):
+* transfer_small.npz — config (i) of SURVEY §8c: 32x64x17 -> 32x64x3, bottleneck 8 rows,
+  8 filters (2 contract + 2 expand blocks), B=2, S=1.
+* transfer_up.npz — config (ii): the reference training-test geometry
+  (styleTransferTrainingModelTest.py:15-20: 240x480x3 -> 480x960x3, bottleneck 30 rows x 4
+  filters) scaled by 1/10: 24x48x3 -> 48x96x3, bottleneck 3 rows, 4 filters
+  (3 contract + 4 expand blocks, SDR content), B=2.
+* apply_style_weights_kat.npz — the reference's only numeric known-answer test,
+  models/styleTransferTest.py:12-49, recomputed from its formula.
+* gram_loss.npz — gram matrices / mean_l2 / total_variation of seeded tensors.
+Each transfer fixture also stores ``stats`` in the metrics.get_stats format
+(realtime_style_transfer/metrics.py:4-12: mean/var/min/max).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import numpy_ref as R  # noqa: E402
+from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params  # noqa: E402
+
+
+def stats(t):
+    return np.array([np.mean(t), np.var(t), np.min(t), np.max(t)])
+
+
+def transfer_fixture(name, ins, outs, bres, bf, batch=2):
+    plan = network_plan(ins, outs, bres, bf)
+    w = init_weights(plan, seed=2)
+    sp = synthetic_style_params(batch, 1, plan.num_style_params, plan, seed=1)
+    x = np.random.default_rng(0).random((batch,) + tuple(ins)).astype(np.float32)
+    y, inter = R.transfer_forward(x, sp, w, ins, outs, bres, bf, return_intermediates=True)
+    arrays = {'content': x, 'style_params': sp, 'output': y, 'stats': stats(y),
+              'shape': np.array(list(ins) + list(outs) + [bres, bf])}
+    for i, wi in enumerate(w):
+        arrays[f'w{i:02d}'] = wi
+    np.savez_compressed(os.path.join(HERE, name), **arrays)
+
+
+def vertical_gradient(min_max, shape):
+    """_generate_vertical_gradient_tensor (styleTransferTest.py:12-24), including its use of
+    shape[0] (the batch) as the divisor."""
+    out = []
+    for b in range(shape[0]):
+        for i in range(shape[1]):
+            out.append([min_max[0] + (i / shape[0]) * (min_max[1] - min_max[0]) for _ in range(shape[2])])
+    return np.array(out, np.float32).reshape(shape)
+
+
+def kat_fixture():
+    sw = np.stack([vertical_gradient((0, 1), (2, 10, 20)), vertical_gradient((1, 0), (2, 10, 20))], axis=-1)
+    sp = np.array([[[[10, 20, 30, 40, 50, 60], [70, 80, 90, 100, 110, 120]]]] * 2, np.float32).reshape(2, 1, 2, 6)
+    expected = np.zeros((2, 10, 20, 6))
+    for b in range(2):
+        for x in range(10):
+            for y in range(20):
+                for c in range(6):
+                    expected[b, x, y, c] = sw[b, x, y, 0] * sp[b, 0, 0, c] + sw[b, x, y, 1] * sp[b, 0, 1, c]
+    np.savez_compressed(os.path.join(HERE, 'apply_style_weights_kat.npz'), style_weights=sw, style_params=sp,
+                        expected=expected)
+
+
+def gram_fixture():
+    rng = np.random.default_rng(5)
+    f = {f'f{c}': rng.random((2, 4, 6, c)).astype(np.float32) for c in (64, 128)}
+    arrays = dict(f)
+    for k, v in f.items():
+        arrays['gram_' + k] = R.gram_matrix(v)
+    img = rng.random((2, 12, 16, 3)).astype(np.float32)
+    arrays['img'] = img
+    arrays['tv'] = R.total_variation(img)
+    arrays['l2'] = R.mean_l2_loss_on_batch(img - 0.5)
+    np.savez_compressed(os.path.join(HERE, 'gram_loss.npz'), **arrays)
+
+
+if __name__ == '__main__':
+    transfer_fixture('transfer_small.npz', (32, 64, 17), (32, 64, 3), 8, 8)
+    transfer_fixture('transfer_up.npz', (24, 48, 3), (48, 96, 3), 3, 4)
+    kat_fixture()
+    gram_fixture()
+    print('golden fixtures written to', HERE)
