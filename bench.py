@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""Benchmark: stylised frames/s of the rst-960-120-128-17 transfer network on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched
+by torch.distributed.run (one rank per GPU, RCCL). One "step" = one forward of the transfer
+network over one batch of synthetic 480x960x17 G-buffer frames (BASELINE config 2:
+single-frame fp32 inference, B=1, unless --batch). Frames shard across ranks with no
+data-path collective (weak scaling); the timed region is bracketed by barrier + device sync,
+and the max time over ranks is used. Rank 0 prints ONE JSON line.
+
+Extra fields: ``roofline`` (dominant kernel, HIP-event timed inside the timed region),
+``cpu_baseline`` (torch-CPU f32 restatement of the same graph on the host cores — TF-CPU is not
+installed; a bounded sample), ``max_abs_delta_vs_oracle`` (same frame, GPU vs that restatement),
+and the batch-8 hipGraph stream throughput (BASELINE config 3).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params  # noqa: E402
+from realtime_style_transfer_amd.shape_config import ShapeConfig  # noqa: E402
+
+SPEC = "rst-960-120-128-17"
+METRIC = "stylized FPS/GPU at 960p×17ch (rst-960-120-128-17); max-abs Δ vs TF ref"
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: Peak FP32 (matrix) = vector peak
+HBM_PEAK_GBS = 8000.0
+
+
+def layer_flops(layer) -> float:
+    """Algorithmic FLOPs (2 x MAC) of one conv layer for one image (SURVEY §8d convention)."""
+    if layer.kind == 'conv':
+        return 2.0 * layer.out_hw[0] * layer.out_hw[1] * layer.k * layer.k * layer.cin * layer.cout
+    # transposed conv: counted as H_in * W_in * k^2 * Cin * Cout MACs
+    return 2.0 * layer.in_hw[0] * layer.in_hw[1] * layer.k * layer.k * layer.cin * layer.cout
+
+
+KERNEL_NAMES = {
+    1: "conv_mfma<9x9 s1 CK18 NT32>", 2: "conv_mfma<9x9 s1 CK4 NT32>", 3: "conv_mfma<3x3 s2 CK16 NT32>",
+    4: "conv_mfma<3x3 s2 CK8 NT32>", 5: "conv_mfma<3x3 s1 CK32 NT128>", 6: "conv_mfma<3x3 s1 CK32 NT32>",
+    7: "conv_mfma<3x3 s1 CK8 NT32>", 8: "conv_mfma<2x2 phase CK32 NT128>", 9: "conv_mfma<2x2 phase CK32 NT64>",
+    10: "conv_mfma<2x2 phase CK32 NT32>", 11: "conv_mfma<2x2 phase CK16 NT32>", 12: "conv_mfma<2x2 phase CK8 NT32>",
+    13: "conv_mfma<3x3 s1 CK16 NT32>", 14: "conv_mfma<3x3 s2 CK4 NT32>", 15: "conv_mfma<3x3 s1 CK4 NT32>",
+    16: "conv_mfma<2x2 phase CK4 NT32>", 17: "conv_mfma<3x3 s1 CK32 NT64>", 100: "small_conv_kernel<9x9 Cout3 VALU>",
+}
+
+
+def cpu_threads() -> int:
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env))) if env else aff
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1, help="frames per step per GPU (config 2: 1)")
+    ap.add_argument("--stream-batch", type=int, default=8, help="config 3 (hipGraph stream) batch; 0 to skip")
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0, help="bounded CPU-baseline sample (seconds)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device(f"cuda:{torch.cuda.current_device()}")
+
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+
+    cfg = ShapeConfig.from_spec(SPEC)
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    weights = init_weights(plan, seed=2)
+    B = args.batch
+    max_b = max(B, args.stream_batch)
+    model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                           weights=weights, max_batch=max_b, device=dev)
+    # synthetic frames (distinct per rank), resident in HBM before the timed region
+    rng = np.random.default_rng(1000 + rank)
+    content = torch.from_numpy(rng.random((B,) + ins, dtype=np.float32)).to(dev)
+    sp_np = synthetic_style_params(B, 1, P, plan, seed=1)
+    style = torch.from_numpy(sp_np).to(dev)
+    out = torch.empty((B,) + outs, dtype=torch.float32, device=dev)
+    inputs = {'content': content, 'style_params': style}
+
+    for _ in range(args.warmup):
+        model(inputs, out=out)
+    torch.cuda.synchronize()
+
+    # ---------------- timed region (per-layer HIP events recorded on the forward's stream) -----
+    model.profile_begin(args.steps)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model(inputs, out=out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    conv_ms, layer_ms, nsteps = model.profile_end()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    frames = world * B * args.steps
+    fps = frames / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # ---------------- dominant kernel roofline (from the timed region's events) ----------------
+    flops = [layer_flops(l) * B for l in plan.layers]
+    groups = {}
+    for i, l in enumerate(plan.layers):
+        kid = model.layer_kernel_id(i)
+        g = groups.setdefault(kid, {"ms": 0.0, "flops": 0.0, "launches": 0})
+        g["ms"] += conv_ms[i]
+        g["flops"] += flops[i] * nsteps
+        g["launches"] += nsteps
+    dom_id = max(groups, key=lambda k: groups[k]["ms"])
+    dom = groups[dom_id]
+    avg_ms = dom["ms"] / dom["launches"]
+    flops_per_launch = dom["flops"] / dom["launches"]
+    achieved_tf = flops_per_launch / (avg_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            traffic = tj.get("per_launch_bytes", {}).get(KERNEL_NAMES.get(dom_id, ""), None)
+        except Exception:
+            traffic = None
+    total_flops = sum(flops) / B
+    conv_ms_per_frame = sum(conv_ms) / max(nsteps, 1) / B
+    layer_table = [{"layer": l.name, "kernel": KERNEL_NAMES.get(model.layer_kernel_id(i), "?"),
+                    "ms": round(conv_ms[i] / max(nsteps, 1), 4),
+                    "tflops": round(flops[i] / (conv_ms[i] / max(nsteps, 1) * 1e-3) / 1e12, 2) if conv_ms[i] > 0 else None}
+                   for i, l in enumerate(plan.layers)]
+
+    # ---------------- config 3: batch-8 stream, hipGraph steady state -------------------------
+    stream_fps = None
+    if args.stream_batch > 0:
+        SB = args.stream_batch
+        rng2 = np.random.default_rng(2000 + rank)
+        c8 = torch.from_numpy(rng2.random((SB,) + ins, dtype=np.float32)).to(dev)
+        s8 = torch.from_numpy(synthetic_style_params(SB, 1, P, plan, seed=1)).to(dev)
+        o8 = torch.empty((SB,) + outs, dtype=torch.float32, device=dev)
+        in8 = {'content': c8, 'style_params': s8}
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                model(in8, out=o8)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            model(in8, out=o8)
+        for _ in range(5):
+            g.replay()
+        torch.cuda.synchronize()
+        reps = 20
+        if world > 1:
+            dist.barrier()
+        ts = time.perf_counter()
+        for _ in range(reps):
+            g.replay()
+        torch.cuda.synchronize()
+        te = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([te], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            te = float(t.item())
+        stream_fps = world * SB * reps / te
+
+    # ---------------- parity + CPU baseline (rank 0 only, bounded sample) -----------------------
+    max_abs = None
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle.torch_ref import TorchTransfer
+        threads = cpu_threads()
+        torch.set_num_threads(threads)
+        ref = TorchTransfer(weights, ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+        x0 = content[:1].cpu().numpy()
+        ts = time.perf_counter()
+        y_ref = ref(x0, sp_np[:1])
+        first = time.perf_counter() - ts
+        model({'content': content[:1].contiguous(), 'style_params': style[:1].contiguous()}, out=out[:1])
+        torch.cuda.synchronize()
+        max_abs = float(np.abs(out[:1].cpu().numpy() - y_ref).max())
+        n, tsum = 0, 0.0
+        while tsum < args.cpu_budget_s and n < 20:
+            ts = time.perf_counter()
+            ref(x0, sp_np[:1])
+            tsum += time.perf_counter() - ts
+            n += 1
+            if first > args.cpu_budget_s:
+                break
+        cpu = {"value": round(n / tsum, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+               "sample": f"{n} frames of 480x960x17 (B=1) after 1 warm-up frame; torch-CPU f32 restatement of the "
+                         f"same graph (oracle/torch_ref.py; TF-CPU not installed), {n} x {tsum / n:.3f} s"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(fps, 3),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (U[0,1) 480x960x17 G-buffer frames, seeded weights; no checkpoints offline)",
+            "config": {"workload": f"{SPEC} single-frame transfer inference (BASELINE config 2)", "spec": SPEC,
+                       "frames_per_step_per_gpu": B, "input": list(ins), "output": list(outs),
+                       "parallelism": f"frame-sharded x{world}, no data-path collective"},
+            "fps_per_gpu": round(fps / world, 3),
+            "max_abs_delta_vs_oracle": max_abs,
+            "roofline": {
+                "bound": "mfma",
+                "kernel": KERNEL_NAMES.get(dom_id, str(dom_id)),
+                "achieved": round(achieved_tf, 3),
+                "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": traffic,
+                "avg_launch_ms": round(avg_ms, 5),
+                "flops_per_launch": flops_per_launch,
+                "launches": dom["launches"],
+            },
+            "network_roofline": {
+                "gflop_per_frame": round(total_flops / 1e9, 3),
+                "conv_kernel_ms_per_frame": round(conv_ms_per_frame, 4),
+                "achieved_tflops_conv_kernels": round(total_flops / (conv_ms_per_frame * 1e-3) / 1e12, 3),
+                "achieved_tflops_end_to_end": round(total_flops * fps / world / 1e12, 3),
+                "frac_end_to_end": round(total_flops * fps / world / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+            },
+            "stream_graph_fps": None if stream_fps is None else round(stream_fps, 3),
+            "stream_graph_batch": args.stream_batch,
+            "layers": layer_table,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

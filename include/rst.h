@@ -74,6 +74,15 @@ int rst_num_layers(const rst_handle* h);
 int rst_layer_output_shape(const rst_handle* h, int idx, int batch, int* hwc3);
 int rst_copy_activation(rst_handle* h, int idx, float* dst, size_t count, int batch, void* stream);
 
+/* Per-layer timing with HIP events recorded on the forward's stream (for bench roofline):
+ * rst_profile_begin allocates 3 events per layer for up to max_steps forwards (call outside
+ * graph capture); rst_profile_end waits for the last event and returns, per conv layer, the
+ * summed conv-kernel time and conv+CIN-finalize time (ms) over the recorded steps. */
+int rst_profile_begin(rst_handle* h, int max_steps);
+int rst_profile_end(rst_handle* h, float* conv_ms, float* layer_ms, int* steps);
+/* Which compiled kernel configuration runs layer idx (100 = VALU 9x9 Cout=3 kernel). */
+int rst_layer_kernel_id(const rst_handle* h, int idx);
+
 /* Gram matrices: out[b][c][d] = sum_p feat[b][p][c] * feat[b][p][d] / hw.
  * feat (B, hw, C) fp32; out (B, C, C). workspace: rst_gram_workspace_size() bytes. */
 size_t rst_gram_workspace_size(int batch, int hw, int channels);

@@ -23,6 +23,7 @@ EXPORTED_SYMBOLS = [
     "rst_create", "rst_destroy", "rst_num_style_params", "rst_num_weights_for_shape", "rst_forward",
     "rst_num_layers", "rst_layer_output_shape", "rst_copy_activation", "rst_gram_workspace_size", "rst_gram",
     "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_last_error", "rst_version",
+    "rst_profile_begin", "rst_profile_end", "rst_layer_kernel_id",
 ]
 
 
@@ -76,6 +77,12 @@ def load() -> ctypes.CDLL:
     lib.rst_instance_norm_workspace_size.restype = sz
     lib.rst_instance_norm.argtypes = [vp, i, i, i, vp, vp, fp, i, vp, vp, vp]
     lib.rst_instance_norm.restype = i
+    lib.rst_profile_begin.argtypes = [vp, i]
+    lib.rst_profile_begin.restype = i
+    lib.rst_profile_end.argtypes = [vp, ctypes.POINTER(fp), ctypes.POINTER(fp), ctypes.POINTER(i)]
+    lib.rst_profile_end.restype = i
+    lib.rst_layer_kernel_id.argtypes = [vp, i]
+    lib.rst_layer_kernel_id.restype = i
     lib.rst_last_error.argtypes = []
     lib.rst_last_error.restype = ctypes.c_char_p
     lib.rst_version.argtypes = []

@@ -175,7 +175,18 @@ struct rst_handle {
     int P = 0;
     std::vector<LayerExec> layers;
     std::vector<void*> allocs;
+    // optional per-layer timing: 3 events per layer per step (before conv, after conv, after finalize)
+    std::vector<hipEvent_t> prof_events;
+    int prof_max_steps = 0, prof_step = 0;
+    bool prof_on = false;
+    void prof_free() {
+        for (hipEvent_t e : prof_events) hipEventDestroy(e);
+        prof_events.clear();
+        prof_on = false;
+        prof_max_steps = prof_step = 0;
+    }
     ~rst_handle() {
+        prof_free();
         for (void* p : allocs) hipFree(p);
     }
     template <typename T>
@@ -370,6 +381,10 @@ void rst_destroy(rst_handle* h) { delete h; }
 
 static int launch_layer(rst_handle* h, size_t li, const float* content, const float* style, int B, hipStream_t st) {
     LayerExec& e = h->layers[li];
+    hipEvent_t* ev = nullptr;
+    if (h->prof_on && h->prof_step < h->prof_max_steps)
+        ev = &h->prof_events[((size_t)h->prof_step * h->layers.size() + li) * 3];
+    if (ev) HIP_TRY(hipEventRecord(ev[0], st));
     const float* in = (e.pro_src < 0) ? content : h->layers[e.pro_src].d_out;
     const float2* pro_ab = (e.pro_src >= 0 && e.pro != PRO_NONE) ? h->layers[e.pro_src].d_ab : nullptr;
     if (e.kind == K_SMALL) {
@@ -419,6 +434,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.shuffle = e.kind == K_CONVT2 ? 1 : 0;
         HIP_TRY(conv_launch(e.tile, a, st));
     }
+    if (ev) HIP_TRY(hipEventRecord(ev[1], st));
     if (e.s.norm == N_CIN) {
         FinalizeArgs f{};
         f.part = e.d_part;
@@ -434,6 +450,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         f.eps = 1e-5f;
         HIP_TRY(finalize_launch(f, st));
     }
+    if (ev) HIP_TRY(hipEventRecord(ev[2], st));
     return RST_OK;
 }
 
@@ -453,7 +470,45 @@ int rst_forward(rst_handle* h, const float* content, const float* style_params, 
     }
     const LayerExec& last = h->layers.back();
     HIP_TRY(affine_act_launch(last.d_out, last.d_ab, nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
+    if (h->prof_on && h->prof_step < h->prof_max_steps) h->prof_step++;
     return RST_OK;
+}
+
+int rst_profile_begin(rst_handle* h, int max_steps) {
+    if (h == nullptr || max_steps <= 0) return fail(RST_ERR_INVALID, "rst_profile_begin: bad argument");
+    h->prof_free();
+    h->prof_events.resize((size_t)max_steps * h->layers.size() * 3);
+    for (auto& e : h->prof_events) HIP_TRY(hipEventCreate(&e));
+    h->prof_max_steps = max_steps;
+    h->prof_step = 0;
+    h->prof_on = true;
+    return RST_OK;
+}
+
+int rst_profile_end(rst_handle* h, float* conv_ms, float* layer_ms, int* steps) {
+    if (h == nullptr || conv_ms == nullptr || layer_ms == nullptr || steps == nullptr)
+        return fail(RST_ERR_INVALID, "rst_profile_end: bad argument");
+    const size_t L = h->layers.size();
+    for (size_t i = 0; i < L; ++i) conv_ms[i] = layer_ms[i] = 0.f;
+    *steps = h->prof_step;
+    if (h->prof_step > 0) HIP_TRY(hipEventSynchronize(h->prof_events[((size_t)(h->prof_step - 1) * L + L - 1) * 3 + 2]));
+    for (int s = 0; s < h->prof_step; ++s)
+        for (size_t i = 0; i < L; ++i) {
+            hipEvent_t* ev = &h->prof_events[((size_t)s * L + i) * 3];
+            float a = 0.f, b = 0.f;
+            HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+            HIP_TRY(hipEventElapsedTime(&b, ev[0], ev[2]));
+            conv_ms[i] += a;
+            layer_ms[i] += b;
+        }
+    h->prof_free();
+    return RST_OK;
+}
+
+int rst_layer_kernel_id(const rst_handle* h, int idx) {
+    if (h == nullptr || idx < 0 || idx >= (int)h->layers.size()) return -1;
+    const LayerExec& e = h->layers[idx];
+    return e.kind == K_SMALL ? 100 : e.tile.id;
 }
 
 int rst_layer_output_shape(const rst_handle* h, int idx, int batch, int* hwc3) {

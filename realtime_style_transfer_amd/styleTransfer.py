@@ -127,6 +127,23 @@ class StyleTransferModel:
 
     predict = __call__
 
+    # ------------------------------------------------------------------ profiling
+    def profile_begin(self, max_steps: int):
+        _lib.check(_lib.load().rst_profile_begin(self._handle, int(max_steps)))
+
+    def profile_end(self):
+        """-> (conv_ms[L], layer_ms[L], steps): summed per-layer HIP-event times."""
+        lib = _lib.load()
+        L = self.num_layers()
+        conv = (ctypes.c_float * L)()
+        lay = (ctypes.c_float * L)()
+        steps = ctypes.c_int()
+        _lib.check(lib.rst_profile_end(self._handle, conv, lay, ctypes.byref(steps)))
+        return list(conv), list(lay), steps.value
+
+    def layer_kernel_id(self, idx: int) -> int:
+        return _lib.load().rst_layer_kernel_id(self._handle, idx)
+
     # ------------------------------------------------------------------ debugging
     def num_layers(self) -> int:
         return _lib.load().rst_num_layers(self._handle)
