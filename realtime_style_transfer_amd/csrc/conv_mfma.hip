@@ -23,15 +23,23 @@
 // pixels x NT channels. Input halo for one Cin chunk (CK channels) is staged in LDS as
 // [halo pixel][CS] (CS = CK + pad, odd 16-B slot count -> conflict-free b128 column reads);
 // the weight stage (TPS taps x CK x NT) is pre-packed on the host in exactly the LDS image
-// order [tap][k-group][lane-half][n][VEC] so staging is a contiguous float4 copy.
+// order [tap][k-group][lane-half][n][VEC] so staging is a lane-linear copy.
+//
+// Pipeline (one barrier per stage): weights of stage s+1 are issued as global_load_lds
+// (LDS-DMA, no VGPRs) into the other half of a double-buffered weight image while stage s
+// computes; with HB = 2 the next Cin chunk's halo is prefetched into registers during the
+// last stage of a chunk and written (CIN-apply fused) into the other halo buffer after it.
 // K order inside a tap pairs channel s (lane half 0) with channel s + CK/2 (lane half 1),
 // so one ds_read_b128 feeds 4 consecutive MFMA k-steps for both operands.
 #include <hip/hip_runtime.h>
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace rst {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));   // native vector (HIP float4 is a struct)
 
 template <int VEC>
 struct vec_t;
@@ -52,7 +60,10 @@ __device__ __forceinline__ float apply_pro(int mode, float x, float2 ab, float r
     return y;
 }
 
-template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+#define RST_TP int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS, int HB
+#define RST_TA KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB
+
+template <RST_TP>
 struct ConvCfg {
     static constexpr int VEC = ((CK / 2) % 4 == 0) ? 4 : 1;
     static constexpr int CS = (VEC == 4) ? (CK + 4) : (((CK + 1) & 1) ? CK + 1 : CK + 2);  // odd for VEC=1
@@ -70,25 +81,73 @@ struct ConvCfg {
     static constexpr int NGROUPS = NTAPS / TPS;
     static constexpr int HALO_FLOATS = ((HP * CS + 3) / 4) * 4;
     static constexpr int MAX_CIN = 256;
-    static constexpr size_t LDS_BYTES = (size_t)(HALO_FLOATS + WSTAGE) * 4 + MAX_CIN * 8;
+    static constexpr int HQ = CK / 4;                         // float4 per halo pixel (vector path)
+    static constexpr int HREG = (HP * HQ + 255) / 256;        // halo prefetch registers (float4) per thread
+    static constexpr int WCOPY = WSTAGE / 4;                  // float4 per weight stage
+    static constexpr size_t LDS_BYTES = (size_t)(HB * HALO_FLOATS + 2 * WSTAGE) * 4 + MAX_CIN * 8;
     static_assert(WM * WN == 4, "4 waves per workgroup");
     static_assert(MT % WM == 0 && NTILES % WN == 0, "wave tiling");
     static_assert((TH * TW) % 32 == 0, "M tile = 32 pixels");
     static_assert(NTAPS % TPS == 0, "taps per stage");
     static_assert(KSTEPS % VEC == 0, "vector k-steps");
+    static_assert(WSTAGE % 4 == 0, "weight stage is a float4 copy");
+    static_assert(HB == 1 || (CK % 4) == 0, "halo prefetch needs the float4 path");
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+// Weight stages are staged through registers: global_load_dwordx4 issued at the start of a
+// stage, ds_write_b128 after its MFMAs. (LDS-DMA would need no VGPRs, but hipcc orders every
+// ds_read behind all pending LDS-DMA with s_waitcnt vmcnt(0), which would drain the prefetch at
+// the first operand read of the stage.)
+// Compile-time loop: the index is a constant expression from the front end on, so arrays
+// indexed by it are promoted to registers (a #pragma-unrolled runtime index left the weight
+// prefetch registers in scratch).
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+template <int WCOPY>
+struct WeightRegs {
+    static constexpr int N = (WCOPY + 255) / 256;
+    f32x4 r[N];
+    __device__ __forceinline__ void load(const float* __restrict__ src, int tid) {
+        static_for<0, N>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int idx = k * 256 + tid;
+            if (WCOPY % 256 == 0 || (k + 1) * 256 <= WCOPY || idx < WCOPY)
+                r[k] = reinterpret_cast<const f32x4*>(src)[idx];
+        });
+    }
+    __device__ __forceinline__ void store(float* dst, int tid) const {
+        static_for<0, N>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int idx = k * 256 + tid;
+            if (WCOPY % 256 == 0 || (k + 1) * 256 <= WCOPY || idx < WCOPY)
+                reinterpret_cast<f32x4*>(dst)[idx] = r[k];
+        });
+    }
+};
+
+// OPT: experiment bits for tools/conv_bench (production uses RST_CONV_OPT):
+//   bit0  pin LDS read-ahead before the MFMAs with sched_barrier
+#ifndef RST_CONV_OPT
+#define RST_CONV_OPT 1
+#endif
+template <RST_TP, int OPT = RST_CONV_OPT>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
-    using C = ConvCfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    using C = ConvCfg<RST_TA>;
     constexpr int VEC = C::VEC, CS = C::CS, HWD = C::HWD, HP = C::HP;
-    constexpr int MW = C::MW, NW = C::NW, SG = C::SG, KSTEPS = C::KSTEPS;
+    constexpr int MW = C::MW, NW = C::NW, SG = C::SG, KSTEPS = C::KSTEPS, HQ = C::HQ;
     typedef typename vec_t<VEC>::type vT;
 
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* halo = smem;
-    float* wts = smem + C::HALO_FLOATS;
-    float2* pab = reinterpret_cast<float2*>(wts + C::WSTAGE);
+    float* halo0 = smem;
+    float* wts0 = smem + HB * C::HALO_FLOATS;
+    float2* pab = reinterpret_cast<float2*>(wts0 + 2 * C::WSTAGE);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -106,6 +165,12 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     const int y0 = ty * TH, x0 = tx * TW;
     const int iy0 = y0 * S - a.pad_t, ix0 = x0 * S - a.pad_l;
     const int Cin = a.cin;
+    const int pro = a.pro_mode;
+    const bool do_mat = (a.mat != nullptr) && nb == 0;
+    const size_t img_base = (size_t)b * a.H * a.W;
+    const bool vec_in = ((Cin & 3) == 0) && ((CK & 3) == 0);
+    const float* wsrc = a.wpk + (size_t)nb * a.nchunks * C::NGROUPS * C::WSTAGE;
+    const int n_stages = a.nchunks * C::NGROUPS;
 
     int pixoff[MW];
 #pragma unroll
@@ -126,53 +191,56 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
-    const int pro = a.pro_mode;
-    if (pro != PRO_NONE) {
-        for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[b * Cin + c];
-    }
-    const bool do_mat = (a.mat != nullptr) && nb == 0;
-    const size_t img_base = (size_t)b * a.H * a.W;
-
-    for (int chunk = 0; chunk < a.nchunks; ++chunk) {
-        // ---------------- stage the input halo for this Cin chunk (prologue fused) -------------
-        __syncthreads();
-        if ((Cin & 3) == 0 && (CK & 3) == 0) {
-            constexpr int Q = CK / 4;
-            for (int it = tid; it < HP * Q; it += 256) {
-                const int hp = it / Q, q = it - (it / Q) * Q;
-                const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
-                const int iy = iy0 + hy, ix = ix0 + hx;
+    // ---- halo helpers -------------------------------------------------------------------------
+    auto pixel_of = [&](int hp, int& iy, int& ix) __attribute__((always_inline)) {
+        const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
+        iy = iy0 + hy;
+        ix = ix0 + hx;
+        return iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    };
+    auto transform4 = [&](float4 v, float4 r, int c, size_t gi, int iy, int ix) __attribute__((always_inline)) {
+        if (pro != PRO_NONE) {
+            v.x = apply_pro(pro, v.x, pab[c + 0], r.x);
+            v.y = apply_pro(pro, v.y, pab[c + 1], r.y);
+            v.z = apply_pro(pro, v.z, pab[c + 2], r.z);
+            v.w = apply_pro(pro, v.w, pab[c + 3], r.w);
+            if (do_mat && iy >= y0 && iy < y0 + TH && ix >= x0 && ix < x0 + TW)
+                *reinterpret_cast<float4*>(a.mat + gi) = v;
+        }
+        return v;
+    };
+    auto write_halo4 = [&](float* hbuf, int hp, int q, float4 v) __attribute__((always_inline)) {
+        float* dst = hbuf + hp * CS + q * 4;
+        if constexpr (VEC == 4) {
+            *reinterpret_cast<float4*>(dst) = v;
+        } else {
+            dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+        }
+    };
+    // synchronous staging of one Cin chunk (prologue, and chunk changes when HB == 1)
+    auto stage_halo_sync = [&](int chunk, float* hbuf) __attribute__((always_inline)) {
+        if (vec_in) {
+            for (int it = tid; it < HP * HQ; it += 256) {
+                const int hp = it / HQ, q = it - (it / HQ) * HQ;
+                int iy, ix;
                 const int c = chunk * CK + q * 4;
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c < Cin) {
+                if (pixel_of(hp, iy, ix) && c < Cin) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
                     v = *reinterpret_cast<const float4*>(a.in + gi);
-                    if (pro != PRO_NONE) {
-                        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-                        if (pro == PRO_AFF_RES) r = *reinterpret_cast<const float4*>(a.res + gi);
-                        v.x = apply_pro(pro, v.x, pab[c + 0], r.x);
-                        v.y = apply_pro(pro, v.y, pab[c + 1], r.y);
-                        v.z = apply_pro(pro, v.z, pab[c + 2], r.z);
-                        v.w = apply_pro(pro, v.w, pab[c + 3], r.w);
-                        if (do_mat && iy >= y0 && iy < y0 + TH && ix >= x0 && ix < x0 + TW)
-                            *reinterpret_cast<float4*>(a.mat + gi) = v;
-                    }
+                    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (pro == PRO_AFF_RES) r = *reinterpret_cast<const float4*>(a.res + gi);
+                    v = transform4(v, r, c, gi, iy, ix);
                 }
-                float* dst = halo + hp * CS + q * 4;
-                if constexpr (VEC == 4) {
-                    *reinterpret_cast<float4*>(dst) = v;
-                } else {
-                    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
-                }
+                write_halo4(hbuf, hp, q, v);
             }
         } else {
             for (int it = tid; it < HP * CK; it += 256) {
                 const int hp = it / CK, q = it - (it / CK) * CK;
-                const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
-                const int iy = iy0 + hy, ix = ix0 + hx;
+                int iy, ix;
                 const int c = chunk * CK + q;
                 float v = 0.f;
-                if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c < Cin) {
+                if (pixel_of(hp, iy, ix) && c < Cin) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
                     v = a.in[gi];
                     if (pro != PRO_NONE) {
@@ -181,44 +249,118 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                         if (do_mat && iy >= y0 && iy < y0 + TH && ix >= x0 && ix < x0 + TW) a.mat[gi] = v;
                     }
                 }
-                halo[hp * CS + q] = v;
+                hbuf[hp * CS + q] = v;
             }
         }
+    };
 
-        for (int g = 0; g < C::NGROUPS; ++g) {
-            // ---------------- stage weights for TPS taps of this chunk ---------------------------
-            if (g > 0) __syncthreads();
-            {
-                const float4* src = reinterpret_cast<const float4*>(
-                    a.wpk + ((size_t)(nb * a.nchunks + chunk) * C::NGROUPS + g) * C::WSTAGE);
-                float4* dst = reinterpret_cast<float4*>(wts);
-                for (int it = tid; it < C::WSTAGE / 4; it += 256) dst[it] = src[it];
-            }
-            __syncthreads();
-            // ---------------- MFMA main loop over the stage -------------------------------------
-#pragma unroll
-            for (int t = 0; t < TPS; ++t) {
+    // ---- prologue -----------------------------------------------------------------------------
+    if (pro != PRO_NONE) {
+        for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[b * Cin + c];
+        __syncthreads();
+    }
+    {
+        WeightRegs<C::WCOPY> w0;
+        w0.load(wsrc, tid);
+        stage_halo_sync(0, halo0);
+        w0.store(wts0, tid);
+    }
+    __syncthreads();
+
+    const float* res_src = (pro == PRO_AFF_RES) ? a.res : a.in;
+
+    // Uniform pipeline stage (one body, so the accumulators keep their registers): prefetch the
+    // weights of stage s+1 and slice g of the next chunk's halo (HB == 2), MFMAs of stage s from
+    // LDS, then write the prefetched data into the other LDS buffers. All prefetch loads are
+    // unconditional (addresses clamped into the tensor, dummy re-reads on the last stage/chunk)
+    // so no register copies of in-flight loads are generated; validity is applied at the write.
+    constexpr int HIT = HP * HQ;                                    // halo items per chunk
+    constexpr int HSL = (HIT + C::NGROUPS - 1) / C::NGROUPS;        // items per stage slice
+    constexpr int HSR = (HSL + 255) / 256;                          // registers per thread
+    for (int s = 0; s < n_stages; ++s) {
+        const int chunk = s / C::NGROUPS;
+        const int g = s - chunk * C::NGROUPS;
+        const int s_next = (s + 1 < n_stages) ? s + 1 : s;
+        const bool has_next_chunk = chunk + 1 < a.nchunks;
+        const float* halo = halo0 + (HB == 2 ? (chunk & 1) * C::HALO_FLOATS : 0);
+        const float* wts = wts0 + (s & 1) * C::WSTAGE;
+        WeightRegs<C::WCOPY> wnext;
+        wnext.load(wsrc + (size_t)s_next * C::WSTAGE, tid);
+        f32x4 hreg[HB == 2 ? HSR : 1], rreg[HB == 2 ? HSR : 1];
+        if constexpr (HB == 2) {
+            const int cn = has_next_chunk ? chunk + 1 : chunk;
+            static_for<0, HSR>([&](auto K) __attribute__((always_inline)) {
+                constexpr int k = decltype(K)::value;
+                int it = g * HSL + k * 256 + tid;
+                it = it < HIT ? it : HIT - 1;
+                const int hp = it / HQ, q = it - (it / HQ) * HQ;
+                const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
+                const int iy = min(max(iy0 + hy, 0), a.H - 1), ix = min(max(ix0 + hx, 0), a.W - 1);
+                const int c = min(cn * CK + q * 4, Cin - 4);
+                const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
+                hreg[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
+                rreg[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
+            });
+        }
+        // ---------------- MFMA main loop over the stage -------------------------------------
+        // operand fragments for step u+1 are read from LDS before the MFMAs of step u
+        {
+            constexpr int U = TPS * SG;
+            vT av[2][MW], bv[2][NW];
+            auto read_step = [&](int u, vT* A, vT* Bv) __attribute__((always_inline)) {
+                const int t = u / SG, sg = u - (u / SG) * SG;
                 const int tap = g * TPS + t;
                 const int ky = tap / KW, kx = tap - (tap / KW) * KW;
-                const int tap_off = (ky * HWD + kx) * CS;
+                const int off = (ky * HWD + kx) * CS + sg * VEC;
 #pragma unroll
-                for (int sg = 0; sg < SG; ++sg) {
-                    vT av[MW], bv[NW];
+                for (int m = 0; m < MW; ++m) A[m] = *reinterpret_cast<const vT*>(halo + pixoff[m] + off);
+#pragma unroll
+                for (int n = 0; n < NW; ++n) Bv[n] = *reinterpret_cast<const vT*>(wts + u * 2 * NT * VEC + woff[n]);
+            };
+            read_step(0, av[0], bv[0]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (u + 1 < U) read_step(u + 1, av[(u + 1) & 1], bv[(u + 1) & 1]);
+                if constexpr (OPT & 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < VEC; ++q)
 #pragma unroll
                     for (int m = 0; m < MW; ++m)
-                        av[m] = *reinterpret_cast<const vT*>(halo + pixoff[m] + tap_off + sg * VEC);
 #pragma unroll
-                    for (int n = 0; n < NW; ++n)
-                        bv[n] = *reinterpret_cast<const vT*>(wts + (t * SG + sg) * 2 * NT * VEC + woff[n]);
-#pragma unroll
-                    for (int q = 0; q < VEC; ++q)
-#pragma unroll
-                        for (int m = 0; m < MW; ++m)
-#pragma unroll
-                            for (int n = 0; n < NW; ++n)
-                                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget(av[m], q), vget(bv[n], q),
-                                                                                 acc[m][n], 0, 0, 0);
-                }
+                        for (int n = 0; n < NW; ++n)
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget(av[u & 1][m], q),
+                                                                             vget(bv[u & 1][n], q), acc[m][n], 0, 0, 0);
+                if constexpr (OPT & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        wnext.store(wts0 + ((s + 1) & 1) * C::WSTAGE, tid);
+        if constexpr (HB == 2) {
+            if (has_next_chunk) {
+                float* hn = halo0 + ((chunk + 1) & 1) * C::HALO_FLOATS;
+                static_for<0, HSR>([&](auto K) __attribute__((always_inline)) {
+                    constexpr int k = decltype(K)::value;
+                    const int it = g * HSL + k * 256 + tid;
+                    if ((k * 256 < HSL) && (k * 256 + tid < HSL) && it < HIT) {
+                        const int hp = it / HQ, q = it - (it / HQ) * HQ;
+                        int iy, ix;
+                        const int c = (chunk + 1) * CK + q * 4;
+                        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (pixel_of(hp, iy, ix) && c < Cin) {
+                            const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
+                            const f32x4 h4 = hreg[k], r4 = rreg[k];
+                            v = transform4(make_float4(h4.x, h4.y, h4.z, h4.w), make_float4(r4.x, r4.y, r4.z, r4.w),
+                                           c, gi, iy, ix);
+                        }
+                        write_halo4(hn, hp, q, v);
+                    }
+                });
+            }
+        }
+        __syncthreads();   // next weight stage / halo slice visible; this stage's buffers free
+        if constexpr (HB == 1) {
+            if (g == C::NGROUPS - 1 && has_next_chunk) {
+                stage_halo_sync(chunk + 1, halo0);
+                __syncthreads();
             }
         }
     }
@@ -296,52 +438,52 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 // ------------------------------------------------------------------------------------------
 // host-side dispatch over the instantiated configurations
 // ------------------------------------------------------------------------------------------
-template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+template <RST_TP>
 static hipError_t launch_cfg(const ConvArgs& a, hipStream_t st) {
-    using C = ConvCfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
-    auto kern = conv_mfma_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    using C = ConvCfg<RST_TA>;
+    auto kern = conv_mfma_kernel<RST_TA>;
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x * a.n_blocks);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), C::LDS_BYTES, st, a);
     return hipGetLastError();
 }
 
-template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+template <RST_TP>
 static hipError_t prepare_cfg() {
-    using C = ConvCfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
-    auto kern = conv_mfma_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    using C = ConvCfg<RST_TA>;
+    auto kern = conv_mfma_kernel<RST_TA>;
     return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES);
 }
 
-template <int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS>
+template <RST_TP>
 static ConvTile tile_of() {
-    using C = ConvCfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>;
+    using C = ConvCfg<RST_TA>;
     ConvTile t;
-    t.kh = KH; t.kw = KW; t.stride = S; t.ck = CK; t.nt = NT; t.th = TH; t.tw = TW; t.tps = TPS;
+    t.kh = KH; t.kw = KW; t.stride = S; t.ck = CK; t.nt = NT; t.th = TH; t.tw = TW; t.tps = TPS; t.hb = HB;
     t.vec = C::VEC; t.mt = C::MT; t.ngroups = C::NGROUPS; t.wstage = C::WSTAGE;
     t.lds_bytes = (int)C::LDS_BYTES;
     t.id = 0;
     return t;
 }
 
-// The configuration table. Each row: (KH,KW,S,CK,NT,TH,TW,WM,WN,TPS).
+// The configuration table. Each row: (ID, KH,KW,S,CK,NT,TH,TW,WM,WN,TPS,HB).
 #define RST_CONV_CONFIGS(X)                       \
-    X(1, 9, 9, 1, 18, 32, 8, 16, 4, 1, 9)         \
-    X(2, 9, 9, 1, 4, 32, 8, 16, 4, 1, 9)          \
-    X(3, 3, 3, 2, 16, 32, 8, 16, 4, 1, 9)         \
-    X(4, 3, 3, 2, 8, 32, 8, 16, 4, 1, 9)          \
-    X(5, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1)        \
-    X(6, 3, 3, 1, 32, 32, 8, 16, 4, 1, 9)         \
-    X(7, 3, 3, 1, 8, 32, 8, 16, 4, 1, 9)          \
-    X(8, 2, 2, 1, 32, 128, 4, 16, 2, 2, 1)        \
-    X(9, 2, 2, 1, 32, 64, 8, 16, 2, 2, 4)         \
-    X(10, 2, 2, 1, 32, 32, 8, 16, 4, 1, 4)        \
-    X(11, 2, 2, 1, 16, 32, 8, 16, 4, 1, 4)        \
-    X(12, 2, 2, 1, 8, 32, 8, 16, 4, 1, 4)         \
-    X(13, 3, 3, 1, 16, 32, 8, 16, 4, 1, 9)        \
-    X(14, 3, 3, 2, 4, 32, 8, 16, 4, 1, 9)         \
-    X(15, 3, 3, 1, 4, 32, 8, 16, 4, 1, 9)         \
-    X(16, 2, 2, 1, 4, 32, 8, 16, 4, 1, 4)         \
-    X(17, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1)
+    X(1, 9, 9, 1, 18, 32, 8, 16, 4, 1, 3, 1)         \
+    X(2, 9, 9, 1, 4, 32, 8, 16, 4, 1, 3, 1)          \
+    X(3, 3, 3, 2, 16, 32, 8, 16, 4, 1, 3, 1)         \
+    X(4, 3, 3, 2, 8, 32, 8, 16, 4, 1, 3, 1)          \
+    X(5, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 1)        \
+    X(6, 3, 3, 1, 32, 32, 8, 16, 4, 1, 3, 1)         \
+    X(7, 3, 3, 1, 8, 32, 8, 16, 4, 1, 9, 1)          \
+    X(8, 2, 2, 1, 32, 128, 4, 16, 2, 2, 1, 1)        \
+    X(9, 2, 2, 1, 32, 64, 8, 16, 2, 2, 1, 1)         \
+    X(10, 2, 2, 1, 32, 32, 8, 16, 4, 1, 4, 1)        \
+    X(11, 2, 2, 1, 16, 32, 8, 16, 4, 1, 4, 1)        \
+    X(12, 2, 2, 1, 8, 32, 8, 16, 4, 1, 4, 1)         \
+    X(13, 3, 3, 1, 16, 32, 8, 16, 4, 1, 9, 1)        \
+    X(14, 3, 3, 2, 4, 32, 8, 16, 4, 1, 9, 1)         \
+    X(15, 3, 3, 1, 4, 32, 8, 16, 4, 1, 9, 1)         \
+    X(16, 2, 2, 1, 4, 32, 8, 16, 4, 1, 4, 1)         \
+    X(17, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 1)
 
 bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
     // pick CK (Cin chunk) and NT (output columns per workgroup)
@@ -356,9 +498,9 @@ bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
     int nt = ntot > 64 ? 128 : (ntot > 32 ? 64 : 32);
     if (ntot > 128 && ntot % 128 != 0) return false;
     if (kh == 9 || (kh == 3 && stride == 2)) nt = 32;  // these variants exist only with NT=32
-#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS)                       \
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB)                       \
     if (kh == KH && stride == S && ck == CK && nt == NT) {                   \
-        *out = tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>();           \
+        *out = tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB>();           \
         out->id = ID;                                                        \
         return true;                                                         \
     }
@@ -367,9 +509,9 @@ bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
     // fall back to NT=32 variants (more N blocks)
     if (nt != 32) {
         nt = 32;
-#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS)                       \
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB)                       \
     if (kh == KH && stride == S && ck == CK && nt == NT) {                   \
-        *out = tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>();           \
+        *out = tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB>();           \
         out->id = ID;                                                        \
         return true;                                                         \
     }
@@ -381,9 +523,9 @@ bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
 
 hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
     switch (t.id) {
-#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS) \
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB) \
     case ID:                                          \
-        return launch_cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>(a, st);
+        return launch_cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB>(a, st);
         RST_CONV_CONFIGS(X)
 #undef X
         default:
@@ -393,9 +535,9 @@ hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
 
 hipError_t conv_prepare(const ConvTile& t) {
     switch (t.id) {
-#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS) \
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB) \
     case ID:                                          \
-        return prepare_cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS>();
+        return prepare_cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB>();
         RST_CONV_CONFIGS(X)
 #undef X
         default:

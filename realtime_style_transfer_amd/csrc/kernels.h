@@ -31,7 +31,7 @@ struct ConvArgs {
 // A compiled tile configuration of conv_mfma_kernel.
 struct ConvTile {
     int id;
-    int kh, kw, stride, ck, nt, th, tw, tps, vec, mt, ngroups, wstage, lds_bytes;
+    int kh, kw, stride, ck, nt, th, tw, tps, hb, vec, mt, ngroups, wstage, lds_bytes;
 };
 
 bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out);

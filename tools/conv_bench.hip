@@ -1,0 +1,117 @@
+// conv_bench.hip — standalone timing harness for conv_mfma_kernel variants (no torch).
+// Times kernel variants interleaved in one process (cdna_hip_programming.md §5.4 rule 24) on
+// the residual-block conv of rst-960-120-128-17 (B x 120 x 240 x 128 -> 128, 3x3 s1) and the
+// start conv (480 x 960 x 17 -> 32, 9x9). Build: see tools/build_conv_bench.sh.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <functional>
+#include "../realtime_style_transfer_amd/csrc/conv_mfma.hip"
+
+using namespace rst;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+template <typename F>
+static float time_ms(F&& launch, int iters) {
+    hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < iters; ++i) launch();
+    CK(hipEventRecord(b, 0)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    return ms / iters;
+}
+
+static float* dev_rand(size_t n, float lo, float hi, unsigned seed) {
+    std::vector<float> h(n); srand(seed);
+    for (auto& v : h) v = lo + (hi - lo) * (rand() / (float)RAND_MAX);
+    float* d; CK(hipMalloc(&d, n * 4)); CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+    return d;
+}
+
+struct Layer { int H, W, Cin, Ntot, kh, s, pad; double flops; };
+
+template <RST_TP, int OPT>
+static ConvArgs make_args(const Layer& L, int B, float* in, float* w, float* bias, float2* ab, float* out, float4* part) {
+    using C = ConvCfg<RST_TA>;
+    ConvArgs a{};
+    a.in = in; a.res = in; a.mat = nullptr; a.pro_ab = ab; a.wpk = w; a.bias = bias; a.bn_ab = ab; a.out = out; a.part = part;
+    a.batch = B; a.H = L.H; a.W = L.W; a.cin = L.Cin;
+    a.Ho = (L.H + L.s - 1) / L.s; a.Wo = (L.W + L.s - 1) / L.s; a.ntot = L.Ntot; a.cout = L.Ntot;
+    a.pad_t = L.pad; a.pad_l = L.pad;
+    a.tiles_y = (a.Ho + TH - 1) / TH; a.tiles_x = (a.Wo + TW - 1) / TW;
+    a.n_blocks = (L.Ntot + NT - 1) / NT; a.nchunks = (L.Cin + CK - 1) / CK;
+    a.pro_mode = L.Cin % 4 == 0 ? PRO_AFF_RELU : PRO_NONE; a.epi_mode = L.Cin % 4 == 0 ? EPI_RELU_STATS : EPI_RELU_BN;
+    a.shuffle = 0;
+    return a;
+}
+
+template <RST_TP, int OPT>
+struct Variant {
+    const char* name;
+    ConvArgs a;
+    unsigned grid;
+    void setup(const char* n, const Layer& L, int B, float* in, float* w, float* bias, float2* ab, float* out, float4* part) {
+        using C = ConvCfg<RST_TA>;
+        name = n;
+        a = make_args<RST_TA, OPT>(L, B, in, w, bias, ab, out, part);
+        grid = (unsigned)(B * a.tiles_y * a.tiles_x * a.n_blocks);
+        CK(hipFuncSetAttribute((const void*)conv_mfma_kernel<RST_TA, OPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)C::LDS_BYTES));
+    }
+    void launch() {
+        using C = ConvCfg<RST_TA>;
+        hipLaunchKernelGGL((conv_mfma_kernel<RST_TA, OPT>), dim3(grid), dim3(256), C::LDS_BYTES, 0, a);
+    }
+};
+
+int main(int argc, char** argv) {
+    int B = argc > 1 ? atoi(argv[1]) : 1;
+    const int iters = 20, rounds = 7;
+    Layer res{120, 240, 128, 128, 3, 1, 1, 2.0 * 120 * 240 * 9 * 128 * 128};
+    float* in = dev_rand((size_t)B * 120 * 240 * 128, 0.f, 1.f, 1);
+    float* w = dev_rand((size_t)9 * 128 * 128 * 2, -0.05f, 0.05f, 2);
+    float* bias = dev_rand(256, -0.1f, 0.1f, 3);
+    float2* ab = (float2*)dev_rand(2 * 128 * B, 0.5f, 1.5f, 4);
+    float* out; CK(hipMalloc(&out, (size_t)B * 120 * 240 * 128 * 4));
+    float4* part; CK(hipMalloc(&part, (size_t)B * 128 * 4096 * 16));
+
+    Layer start{480, 960, 17, 32, 9, 1, 4, 2.0 * 480 * 960 * 81 * 17 * 32};
+    float* in_s = dev_rand((size_t)B * 480 * 960 * 17, 0.f, 1.f, 5);
+    float* out_s; CK(hipMalloc(&out_s, (size_t)B * 480 * 960 * 32 * 4));
+    float* w_s = dev_rand((size_t)81 * 18 * 32, -0.05f, 0.05f, 6);
+#define VARIANTS(X)                                                   \
+    X(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 1, 1, "res CK32 NT128 4x16 HB1 (prod)", res, in, w, out)  \
+    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 9, 1, 1, "start TPS9 8x16 (prod)", start, in_s, w_s, out_s)  \
+    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 9, 1, 0, "start TPS9 8x16 nosb", start, in_s, w_s, out_s)  \
+    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 3, 1, 1, "start TPS3 8x16", start, in_s, w_s, out_s)  \
+    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 1, 1, 1, "start TPS1 8x16", start, in_s, w_s, out_s)  \
+    X(9, 9, 1, 18, 32, 16, 16, 4, 1, 9, 1, 1, "start TPS9 16x16 2M/wave", start, in_s, w_s, out_s)  \
+    X(9, 9, 1, 18, 32, 8, 32, 4, 1, 9, 1, 1, "start TPS9 8x32 2M/wave", start, in_s, w_s, out_s)
+    int nv = 0;
+    std::vector<std::function<void()>> launches;
+    std::vector<const char*> names;
+    std::vector<double> flops;
+#define X(KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, HB, OPT, NAME, LAY, IN, WW, OUT)      \
+    {                                                                                     \
+        auto* v = new Variant<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, HB, OPT>();         \
+        v->setup(NAME, LAY, B, IN, WW, bias, ab, OUT, part);                              \
+        flops.push_back(LAY.flops);                                                       \
+        launches.push_back([v] { v->launch(); });                                         \
+        names.push_back(NAME);                                                            \
+        ++nv;                                                                             \
+    }
+    VARIANTS(X)
+#undef X
+    std::vector<std::vector<float>> t(nv);
+    for (int r = 0; r < rounds; ++r)
+        for (int i = 0; i < nv; ++i) t[i].push_back(time_ms(launches[i], iters));
+    for (int i = 0; i < nv; ++i) {
+        std::sort(t[i].begin(), t[i].end());
+        const float med = t[i][rounds / 2];
+        printf("%-40s B=%d  median %8.2f us  min %8.2f us  %7.2f TF/s\n", names[i], B, med * 1e3, t[i][0] * 1e3,
+               flops[i] * B / (med * 1e-3) / 1e12);
+    }
+    return 0;
+}

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of each kernel from rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE).
+
+Collected in two separate passes (MI355X_MICROARCH.md §rocprofv3 PMC slots: FETCH_SIZE costs 3 TCC
+slots and WRITE_SIZE 2, they cannot share a pass):
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d <dir_f> -o r01 -- python bench.py ...
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d <dir_w> -o r01 -- python bench.py ...
+Units are KiB. gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports exactly half of
+the bytes of wide (16 B/lane) coalesced reads, which is how every conv kernel here stages its
+halo and weights, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B stores
+(our stores are 4-B/lane, 128-B contiguous per half-wave: treated as exact, uncalibrated).
+Infinity-Cache hits are counted too (the counters sit at the L2's memory side).
+
+Usage: python tools/pmc_traffic.py <fetch_csv> <write_csv> <out_json>
+"""
+import collections
+import csv
+import json
+import re
+import sys
+
+CONFIG_NAMES = {
+    (9, 9, 1, 18, 32): "conv_mfma<9x9 s1 CK18 NT32>", (9, 9, 1, 4, 32): "conv_mfma<9x9 s1 CK4 NT32>",
+    (3, 3, 2, 16, 32): "conv_mfma<3x3 s2 CK16 NT32>", (3, 3, 2, 8, 32): "conv_mfma<3x3 s2 CK8 NT32>",
+    (3, 3, 1, 32, 128): "conv_mfma<3x3 s1 CK32 NT128>", (3, 3, 1, 32, 32): "conv_mfma<3x3 s1 CK32 NT32>",
+    (2, 2, 1, 32, 128): "conv_mfma<2x2 phase CK32 NT128>", (2, 2, 1, 32, 64): "conv_mfma<2x2 phase CK32 NT64>",
+}
+
+
+def short_name(k: str) -> str:
+    m = re.search(r"conv_mfma_kernel<([^>]*)>", k)
+    if m:
+        args = tuple(int(v) for v in m.group(1).split(","))
+        return CONFIG_NAMES.get(args[:5], "conv_mfma<" + ",".join(map(str, args)) + ">")
+    if "small_conv_kernel" in k:
+        return "small_conv_kernel<9x9 Cout3 VALU>"
+    return k.split("(")[0]
+
+
+def load(path, counter):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return d
+
+
+def main():
+    fetch = load(sys.argv[1], "FETCH_SIZE")
+    write = load(sys.argv[2], "WRITE_SIZE")
+    out = {"note": __doc__.split("\n\n")[1], "per_launch_bytes": {}, "raw": {}}
+    for k, fv in fetch.items():
+        wv = write.get(k, [0.0])
+        f_mean = sum(fv) / len(fv)
+        w_mean = sum(wv) / len(wv)
+        b = 2.0 * f_mean * 1024 + w_mean * 1024
+        name = short_name(k)
+        out["per_launch_bytes"][name] = round(b)
+        out["raw"][name] = {"launches": len(fv), "fetch_kib_mean": f_mean, "write_kib_mean": w_mean,
+                            "read_bytes_corrected": 2.0 * f_mean * 1024, "write_bytes": w_mean * 1024}
+    json.dump(out, open(sys.argv[3], "w"), indent=1)
+    for n, v in sorted(out["per_launch_bytes"].items(), key=lambda t: -t[1]):
+        print(f"{v / 1e6:10.2f} MB/launch  {n}")
+
+
+if __name__ == "__main__":
+    main()
