@@ -4,11 +4,16 @@
 // A SAME 9x9 s1 transposed conv is a 9x9 correlation with the spatially flipped kernel and
 // pad 4 (adjoint of the SAME forward conv). With N = 3 an MFMA tile would idle 29/32 (32x32)
 // or 13/16 (16x16) of its columns, so this layer runs on the f32 VALU (same 64 FLOP/clk/SIMD
-// peak as f32 MFMA on gfx950): each thread owns RX=4 consecutive pixels x 3 channels, the
-// input halo is staged channel-planar in LDS (fused CIN-apply + ReLU of expand_1), the 27
-// weights of each (ky, ci) are wave-uniform and come in through the scalar cache, and each
-// 12-float input row segment (3 x ds_read_b128) feeds 108 FMAs. The epilogue writes the raw
-// conv output plus per-tile {sum, M2, n} for the final CIN (sigmoid is applied after finalize).
+// peak as f32 MFMA on gfx950):
+//   * each thread owns RX=4 consecutive pixels x 3 channels (12 accumulators);
+//   * the input halo is staged channel-planar in LDS, CC=4 channels at a time, double-buffered:
+//     the next chunk is prefetched into registers while the current one is consumed, and the
+//     CIN-apply + ReLU of expand_1 is fused into that LDS write;
+//   * the 27 weights of each (ky, ci) are wave-uniform; they are staged in LDS once per
+//     workgroup and read as broadcast ds_read_b128 (measured 67 us vs 79 us for the s_load
+//     variant at B=1, tools/conv_bench; equal at B=8) — SOPT selects the variant;
+//   * each 12-float input row segment (3 x ds_read_b128) feeds 108 FMAs.
+// The epilogue writes the raw conv output plus per-tile {sum, M2, n} for the final CIN.
 #include <hip/hip_runtime.h>
 #include "kernels.h"
 
@@ -19,11 +24,27 @@ constexpr int K = 9, PAD = 4, RX = 4, TH = 32, TW = 32, CC = 4;
 constexpr int HH = TH + K - 1, HWD = TW + K - 1;   // 40 x 40
 constexpr int RS = HWD + 4;                          // padded row stride (floats), 16-B multiple
 constexpr int SEGS = TW / RX;                        // 8 segments per row
+constexpr int PLANE = HH * RS;                       // floats per channel plane
+constexpr int CHUNK_FLOATS = CC * PLANE;
+constexpr int ITEMS = HH * HWD;                      // halo pixels per chunk (one float4 each)
+constexpr int PREG = (ITEMS + 255) / 256;            // prefetch registers (float4) per thread
+constexpr int WS = 28;                               // 27 weights per (ky, ci), padded
 }  // namespace small
 
-__global__ __launch_bounds__(256) void small_conv_kernel(SmallConvArgs a) {
+typedef float sf32x4 __attribute__((ext_vector_type(4)));
+
+// SOPT bit0: unroll the 4 channels of a chunk (lets hipcc hoist the next channel's weight s_loads)
+//      bit1: weights staged in LDS once and read as broadcast ds_read_b128 (instead of s_load)
+#ifndef RST_SMALL_OPT
+#define RST_SMALL_OPT 2
+#endif
+template <int SOPT>
+__global__ __launch_bounds__(256, 2) void small_conv_kernel(SmallConvArgs a, const float* __restrict__ w,
+                                                            const float* __restrict__ in) {
     using namespace small;
-    __shared__ __attribute__((aligned(16))) float halo[CC * HH * RS];
+    constexpr bool WLDS = (SOPT & 2) != 0;
+    __shared__ __attribute__((aligned(16))) float halo[2 * CHUNK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float wl[WLDS ? 9 * 16 * WS : 4];
     __shared__ float2 pab[256];
     __shared__ float red[4][8];
 
@@ -34,66 +55,128 @@ __global__ __launch_bounds__(256) void small_conv_kernel(SmallConvArgs a) {
     const int y0 = ty * TH, x0 = tx * TW;
     const int r = tid / SEGS, seg = tid % SEGS;
     const int Cin = a.cin;
-    const float* __restrict__ w = a.w;
+    const bool pro = a.pro_ab != nullptr;
+    const size_t img = (size_t)b * a.H * a.W;
 
-    if (a.pro_ab != nullptr)
+    if (pro)
         for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[b * Cin + c];
+    if constexpr (WLDS)
+        for (int i = tid; i < 9 * Cin * WS; i += 256) wl[i] = w[i];
+    __syncthreads();
+
+    auto item_src = [&](int it, int& hy, int& hx, bool& valid) __attribute__((always_inline)) {
+        hy = it / HWD;
+        hx = it - hy * HWD;
+        const int iy = y0 - PAD + hy, ix = x0 - PAD + hx;
+        valid = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        const int cy = min(max(iy, 0), a.H - 1), cx = min(max(ix, 0), a.W - 1);
+        return (img + (size_t)cy * a.W + cx) * Cin;
+    };
+    auto write_item = [&](float* buf, int hy, int hx, bool valid, sf32x4 v, int c0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < CC; ++q) {
+            float x = valid && (c0 + q < Cin) ? v[q] : 0.f;
+            if (pro && valid && c0 + q < Cin) {
+                const float2 p = pab[c0 + q];
+                x = fmaxf(fmaf(p.x, x, p.y), 0.f);
+            }
+            buf[q * PLANE + hy * RS + hx] = x;
+        }
+    };
+    const bool vec = (Cin % CC) == 0;
+    // synchronous staging of one chunk (prologue; also the whole path when Cin % 4 != 0)
+    auto stage_sync = [&](int c0, float* buf) __attribute__((always_inline)) {
+        for (int it = tid; it < ITEMS; it += 256) {
+            int hy, hx;
+            bool valid;
+            const size_t gi = item_src(it, hy, hx, valid) + c0;
+            sf32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (vec) {
+                v = *reinterpret_cast<const sf32x4*>(in + gi);
+            } else {
+#pragma unroll
+                for (int q = 0; q < CC; ++q) v[q] = (c0 + q < Cin) ? in[gi + q] : 0.f;
+            }
+            write_item(buf, hy, hx, valid, v, c0);
+        }
+    };
 
     float acc[RX][3];
 #pragma unroll
     for (int i = 0; i < RX; ++i) acc[i][0] = acc[i][1] = acc[i][2] = 0.f;
 
-    for (int c0 = 0; c0 < Cin; c0 += CC) {
-        __syncthreads();
-        for (int it = tid; it < HH * HWD; it += 256) {
-            const int hy = it / HWD, hx = it % HWD;
-            const int iy = y0 - PAD + hy, ix = x0 - PAD + hx;
-            float v[CC];
+    stage_sync(0, halo);
+    __syncthreads();
+    const int nchunks = (Cin + CC - 1) / CC;
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int c0 = ch * CC;
+        const bool has_next = ch + 1 < nchunks;
+        const float* cur = halo + (ch & 1) * CHUNK_FLOATS;
+        sf32x4 pre[PREG];
+        if (vec) {
+            const int cn = has_next ? c0 + CC : c0;
 #pragma unroll
-            for (int q = 0; q < CC; ++q) v[q] = 0.f;
-            if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
-                const float* src = a.in + (((size_t)b * a.H + iy) * a.W + ix) * Cin + c0;
-#pragma unroll
-                for (int q = 0; q < CC; ++q) {
-                    if (c0 + q < Cin) {
-                        float x = src[q];
-                        if (a.pro_ab != nullptr) {
-                            const float2 p = pab[c0 + q];
-                            x = fmaxf(fmaf(p.x, x, p.y), 0.f);
-                        }
-                        v[q] = x;
-                    }
-                }
+            for (int k = 0; k < PREG; ++k) {
+                const int it = min(k * 256 + tid, ITEMS - 1);
+                int hy, hx;
+                bool valid;
+                pre[k] = *reinterpret_cast<const sf32x4*>(in + item_src(it, hy, hx, valid) + cn);
             }
-#pragma unroll
-            for (int q = 0; q < CC; ++q) halo[(q * HH + hy) * RS + hx] = v[q];
         }
-        __syncthreads();
+#pragma unroll((SOPT & 1) ? CC : 1)
         for (int q = 0; q < CC; ++q) {
             const int ci = c0 + q;
             if (ci >= Cin) break;
+#pragma unroll
             for (int ky = 0; ky < K; ++ky) {
-                const float* row = halo + (q * HH + r + ky) * RS + seg * RX;
-                float in[12];
-                const float4 i0 = *reinterpret_cast<const float4*>(row);
-                const float4 i1 = *reinterpret_cast<const float4*>(row + 4);
-                const float4 i2 = *reinterpret_cast<const float4*>(row + 8);
-                in[0] = i0.x; in[1] = i0.y; in[2] = i0.z; in[3] = i0.w;
-                in[4] = i1.x; in[5] = i1.y; in[6] = i1.z; in[7] = i1.w;
-                in[8] = i2.x; in[9] = i2.y; in[10] = i2.z; in[11] = i2.w;
-                const float* wk = w + ((size_t)ky * Cin + ci) * (K * 3);
+                const float* row = cur + q * PLANE + (r + ky) * RS + seg * RX;
+                const sf32x4 i0 = *reinterpret_cast<const sf32x4*>(row);
+                const sf32x4 i1 = *reinterpret_cast<const sf32x4*>(row + 4);
+                const sf32x4 i2 = *reinterpret_cast<const sf32x4*>(row + 8);
+                const float x[12] = {i0[0], i0[1], i0[2], i0[3], i1[0], i1[1], i1[2], i1[3], i2[0], i2[1], i2[2], i2[3]};
+                float wv[WS];
+                if constexpr (WLDS) {
+                    const float* wk = wl + (ky * Cin + ci) * WS;
+#pragma unroll
+                    for (int j = 0; j < WS / 4; ++j) {
+                        const sf32x4 t = *reinterpret_cast<const sf32x4*>(wk + 4 * j);
+                        wv[4 * j] = t[0]; wv[4 * j + 1] = t[1]; wv[4 * j + 2] = t[2]; wv[4 * j + 3] = t[3];
+                    }
+                } else {
+                    const float* wk = w + ((size_t)ky * Cin + ci) * WS;
+#pragma unroll
+                    for (int j = 0; j < WS; ++j) wv[j] = wk[j];
+                }
 #pragma unroll
                 for (int kx = 0; kx < K; ++kx) {
-                    const float w0 = wk[kx * 3 + 0], w1 = wk[kx * 3 + 1], w2 = wk[kx * 3 + 2];
+                    const float w0 = wv[kx * 3 + 0], w1 = wv[kx * 3 + 1], w2 = wv[kx * 3 + 2];
 #pragma unroll
                     for (int i = 0; i < RX; ++i) {
-                        acc[i][0] = fmaf(in[i + kx], w0, acc[i][0]);
-                        acc[i][1] = fmaf(in[i + kx], w1, acc[i][1]);
-                        acc[i][2] = fmaf(in[i + kx], w2, acc[i][2]);
+                        acc[i][0] = fmaf(x[i + kx], w0, acc[i][0]);
+                        acc[i][1] = fmaf(x[i + kx], w1, acc[i][1]);
+                        acc[i][2] = fmaf(x[i + kx], w2, acc[i][2]);
                     }
                 }
             }
         }
+        if (has_next) {
+            float* nxt = halo + ((ch + 1) & 1) * CHUNK_FLOATS;
+            if (vec) {
+#pragma unroll
+                for (int k = 0; k < PREG; ++k) {
+                    const int it = k * 256 + tid;
+                    if (it < ITEMS) {
+                        int hy, hx;
+                        bool valid;
+                        item_src(it, hy, hx, valid);
+                        write_item(nxt, hy, hx, valid, pre[k], c0 + CC);
+                    }
+                }
+            } else {
+                stage_sync(c0 + CC, nxt);
+            }
+        }
+        __syncthreads();
     }
 
     // epilogue: bias, raw store, per-tile statistics per channel
@@ -124,7 +207,6 @@ __global__ __launch_bounds__(256) void small_conv_kernel(SmallConvArgs a) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) tot[k] += __shfl_xor(tot[k], o);
     }
-    __syncthreads();
     if (lane == 0)
         for (int k = 0; k < 4; ++k) red[wave][k] = tot[k];
     __syncthreads();
@@ -161,11 +243,12 @@ __global__ __launch_bounds__(256) void small_conv_kernel(SmallConvArgs a) {
 
 int small_conv_tiles_y(int H) { return (H + small::TH - 1) / small::TH; }
 int small_conv_tiles_x(int W) { return (W + small::TW - 1) / small::TW; }
+int small_conv_weight_stride() { return small::WS; }
 
 hipError_t small_conv_launch(const SmallConvArgs& a, hipStream_t st) {
-    if (a.cin > 256) return hipErrorInvalidValue;
+    if (a.cin > 256 || ((RST_SMALL_OPT & 2) && a.cin > 16)) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
-    hipLaunchKernelGGL(small_conv_kernel, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(small_conv_kernel<RST_SMALL_OPT>, dim3(grid), dim3(256), 0, st, a, a.w, a.in);
     return hipGetLastError();
 }
 

@@ -43,7 +43,7 @@ hipError_t conv_prepare(const ConvTile& t);
 struct SmallConvArgs {
     const float* in;        // [B][H][W][cin]
     const float2* pro_ab;   // [B][cin] prologue affine + ReLU (or null: identity)
-    const float* w;         // packed [ky][ci][kx][3]
+    const float* w;         // packed [ky][ci][28] ([kx][3] + 1 pad)
     const float* bias;      // [3]
     float* out;             // [B][H][W][3] raw conv output
     float4* part;           // [B][3][n_tiles]
@@ -53,6 +53,7 @@ struct SmallConvArgs {
 hipError_t small_conv_launch(const SmallConvArgs& a, hipStream_t st);
 int small_conv_tiles_y(int H);
 int small_conv_tiles_x(int W);
+int small_conv_weight_stride();
 
 // CIN statistics finalize: merge per-tile {sum, M2, n} (Chan, f64) -> per-(b,c) affine.
 struct FinalizeArgs {

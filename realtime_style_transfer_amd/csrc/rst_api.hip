@@ -250,12 +250,13 @@ int rst_create(const rst_shape* shape, const float* weights_host, size_t num_wei
             // ---- final 9x9 transposed conv: flip -> correlation, pack [ky][ci][kx][co]
             if (s.cout != 3) { delete h; return fail(RST_ERR_UNSUPPORTED, "last layer must have 3 channels"); }
             e.kind = K_SMALL;
-            std::vector<float> w((size_t)81 * s.cin * 3);
+            const int ws = small_conv_weight_stride();
+            std::vector<float> w((size_t)9 * s.cin * ws, 0.f);
             for (int ky = 0; ky < 9; ++ky)
                 for (int kx = 0; kx < 9; ++kx)
                     for (int ci = 0; ci < s.cin; ++ci)
                         for (int co = 0; co < 3; ++co)
-                            w[(((size_t)ky * s.cin + ci) * 9 + kx) * 3 + co] =
+                            w[((size_t)ky * s.cin + ci) * ws + kx * 3 + co] =
                                 kern[(((size_t)(8 - ky) * 9 + (8 - kx)) * 3 + co) * s.cin + ci];
             if ((st = h->alloc(&e.d_w, w.size() * 4, w.data())) != RST_OK) { delete h; return st; }
             bias_n.assign(bias, bias + 3);

@@ -9,6 +9,7 @@
 #include <vector>
 #include <functional>
 #include "../realtime_style_transfer_amd/csrc/conv_mfma.hip"
+#include "../realtime_style_transfer_amd/csrc/conv_small.hip"
 
 using namespace rst;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -82,13 +83,7 @@ int main(int argc, char** argv) {
     float* out_s; CK(hipMalloc(&out_s, (size_t)B * 480 * 960 * 32 * 4));
     float* w_s = dev_rand((size_t)81 * 18 * 32, -0.05f, 0.05f, 6);
 #define VARIANTS(X)                                                   \
-    X(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 1, 1, "res CK32 NT128 4x16 HB1 (prod)", res, in, w, out)  \
-    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 9, 1, 1, "start TPS9 8x16 (prod)", start, in_s, w_s, out_s)  \
-    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 9, 1, 0, "start TPS9 8x16 nosb", start, in_s, w_s, out_s)  \
-    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 3, 1, 1, "start TPS3 8x16", start, in_s, w_s, out_s)  \
-    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 1, 1, 1, "start TPS1 8x16", start, in_s, w_s, out_s)  \
-    X(9, 9, 1, 18, 32, 16, 16, 4, 1, 9, 1, 1, "start TPS9 16x16 2M/wave", start, in_s, w_s, out_s)  \
-    X(9, 9, 1, 18, 32, 8, 32, 4, 1, 9, 1, 1, "start TPS9 8x32 2M/wave", start, in_s, w_s, out_s)
+    X(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 1, 1, "res CK32 NT128 4x16 HB1 (prod)", res, in, w, out)
     int nv = 0;
     std::vector<std::function<void()>> launches;
     std::vector<const char*> names;
@@ -104,6 +99,22 @@ int main(int argc, char** argv) {
     }
     VARIANTS(X)
 #undef X
+    // final 9x9 -> 3 channel layer (VALU kernel), 480 x 960 x 16
+    float* in_l = dev_rand((size_t)B * 480 * 960 * 16, 0.f, 1.f, 7);
+    float* w_l = dev_rand((size_t)9 * 16 * 28, -0.05f, 0.05f, 8);
+    float* out_l; CK(hipMalloc(&out_l, (size_t)B * 480 * 960 * 3 * 4));
+    SmallConvArgs sa{};
+    sa.in = in_l; sa.pro_ab = ab; sa.w = w_l; sa.bias = bias; sa.out = out_l; sa.part = part;
+    sa.batch = B; sa.H = 480; sa.W = 960; sa.cin = 16; sa.tiles_y = small_conv_tiles_y(480); sa.tiles_x = small_conv_tiles_x(960);
+    const unsigned sgrid = (unsigned)(B * sa.tiles_y * sa.tiles_x);
+    const double sflops = 2.0 * 480 * 960 * 81 * 16 * 3;
+#define SV(OPTV, NAME)                                                                                  \
+    launches.push_back([=] { hipLaunchKernelGGL(small_conv_kernel<OPTV>, dim3(sgrid), dim3(256), 0, 0, sa, w_l, in_l); }); \
+    names.push_back(NAME); flops.push_back(sflops); ++nv;
+    SV(0, "small opt0 (s_load, q loop)")
+    SV(1, "small opt1 (s_load, q unrolled)")
+    SV(2, "small opt2 (LDS weights)")
+    SV(3, "small opt3 (LDS weights, q unrolled)")
     std::vector<std::vector<float>> t(nv);
     for (int r = 0; r < rounds; ++r)
         for (int i = 0; i < nv; ++i) t[i].push_back(time_ms(launches[i], iters));
