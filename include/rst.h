@@ -21,6 +21,8 @@
  *   rst_gram                     gram_matrix / get_gram_matrix_model  models/styleLoss.py:11-37
  *   rst_instance_norm            ConditionalInstanceNormalization.call models/styleTransfer.py:57-71
  *   rst_copy_activation          (debug) per-block outputs of the Keras sub-models
+ *   rst_loss_create / _forward   StyleLossModelVGG + make_style_loss_function(..., with_depth_loss=False)
+ *                                -> compute_loss(y_pred, y_true) dict      models/styleLoss.py:69-109,295-369
  */
 #ifndef RST_H_
 #define RST_H_
@@ -93,6 +95,28 @@ int rst_gram(const float* feat, int batch, int hw, int channels, float* out, voi
 size_t rst_instance_norm_workspace_size(int batch, int hw, int channels);
 int rst_instance_norm(const float* x, int batch, int hw, int channels, const float* scale, const float* bias,
                       float eps, int relu, float* y, void* workspace, void* stream);
+
+/* ---- VGG16 / Gram style loss (StyleLossModelVGG + make_style_loss_function, no depth term) ---- */
+typedef struct rst_loss_shape {
+    int h, w;                 /* prediction / content / style image size (multiples of 16)        */
+    int max_batch;
+    float content_factor;     /* StyleLossModelVGG: 1e4   (styleLoss.py:101)                      */
+    float style_factor;       /*                    1e-3  (styleLoss.py:102)                      */
+    float tv_factor;          /*                    1e-1  (styleLoss.py:103)                      */
+} rst_loss_shape;
+typedef struct rst_loss_handle rst_loss_handle;
+
+/* Number of VGG16 trunk weights (13 x [kernel (3,3,cin,cout), bias]) in Keras order. */
+size_t rst_loss_num_weights(void);
+int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, size_t num_weights,
+                    rst_loss_handle** out);
+void rst_loss_destroy(rst_loss_handle* h);
+/* prediction, gt_content: (B, h, w, 3); gt_style: (B, 1, h, w, 3) == (B, h, w, 3), all in [0, 1].
+ * losses (device, B x 4): [loss, feature_loss, style_loss, total_variation_loss] per image. */
+int rst_loss_forward(rst_loss_handle* h, const float* prediction, const float* gt_content, const float* gt_style,
+                     int batch, float* losses, void* stream);
+/* Debug: VGG16 conv layer (0..12) output of the most recent run (the prediction). */
+int rst_loss_copy_feature(rst_loss_handle* h, int layer, float* dst, size_t count, int batch, void* stream);
 
 const char* rst_last_error(void);
 const char* rst_version(void);

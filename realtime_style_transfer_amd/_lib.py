@@ -24,6 +24,7 @@ EXPORTED_SYMBOLS = [
     "rst_num_layers", "rst_layer_output_shape", "rst_copy_activation", "rst_gram_workspace_size", "rst_gram",
     "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_last_error", "rst_version",
     "rst_profile_begin", "rst_profile_end", "rst_layer_kernel_id",
+    "rst_loss_num_weights", "rst_loss_create", "rst_loss_destroy", "rst_loss_forward", "rst_loss_copy_feature",
 ]
 
 
@@ -32,6 +33,11 @@ class RstShape(ctypes.Structure):
                 ("out_h", ctypes.c_int), ("out_w", ctypes.c_int),
                 ("bottleneck_res_y", ctypes.c_int), ("bottleneck_num_filters", ctypes.c_int),
                 ("num_styles", ctypes.c_int), ("max_batch", ctypes.c_int)]
+
+
+class RstLossShape(ctypes.Structure):
+    _fields_ = [("h", ctypes.c_int), ("w", ctypes.c_int), ("max_batch", ctypes.c_int),
+                ("content_factor", ctypes.c_float), ("style_factor", ctypes.c_float), ("tv_factor", ctypes.c_float)]
 
 
 class RstError(RuntimeError):
@@ -83,6 +89,16 @@ def load() -> ctypes.CDLL:
     lib.rst_profile_end.restype = i
     lib.rst_layer_kernel_id.argtypes = [vp, i]
     lib.rst_layer_kernel_id.restype = i
+    lib.rst_loss_num_weights.argtypes = []
+    lib.rst_loss_num_weights.restype = sz
+    lib.rst_loss_create.argtypes = [ctypes.POINTER(RstLossShape), vp, sz, ctypes.POINTER(vp)]
+    lib.rst_loss_create.restype = i
+    lib.rst_loss_destroy.argtypes = [vp]
+    lib.rst_loss_destroy.restype = None
+    lib.rst_loss_forward.argtypes = [vp, vp, vp, vp, i, vp, vp]
+    lib.rst_loss_forward.restype = i
+    lib.rst_loss_copy_feature.argtypes = [vp, i, vp, sz, i, vp]
+    lib.rst_loss_copy_feature.restype = i
     lib.rst_last_error.argtypes = []
     lib.rst_last_error.restype = ctypes.c_char_p
     lib.rst_version.argtypes = []

@@ -1,0 +1,23 @@
+// common.h — host helpers shared by the C-ABI translation units of librst.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace rst {
+
+// Record the thread-local error message returned by rst_last_error(); returns code.
+int set_error(int code, const std::string& msg);
+
+// Pack a GEMM-form conv kernel Wg[tap][ci][n] (taps = kh*kw, row-major) into the LDS stage image
+// [n_block][cin_chunk][tap_group][tap][kgroup][lane_half][n][VEC] that conv_mfma_kernel stages.
+std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t);
+
+}  // namespace rst
+
+#define RST_HIP_TRY(expr)                                                                         \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess) return rst::set_error(3, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)

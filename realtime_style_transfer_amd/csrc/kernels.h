@@ -80,4 +80,13 @@ hipError_t tile_stats_launch(const float* x, float4* part, int batch, long hw, i
 size_t gram_workspace_bytes(int batch, int hw, int channels);
 hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st);
 
+// Loss kernels (loss.hip)
+hipError_t maxpool2_launch(const float* x, float* y, int B, int H, int W, int C, hipStream_t st);
+int loss_partial_blocks(long n);
+hipError_t sqdiff_loss_launch(const float* a, const float* c, int B, long n, float* partial, double scale, float* out,
+                              int out_stride, int out_col, int accumulate, hipStream_t st);
+hipError_t tv_loss_launch(const float* x, int B, int H, int W, int C, float* partial, double scale, float* out,
+                          int out_stride, int out_col, hipStream_t st);
+hipError_t loss_combine_launch(float* table, int B, hipStream_t st);
+
 }  // namespace rst

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/rst.h"
+#include "common.h"
 #include "kernels.h"
 
 using namespace rst;
@@ -134,9 +135,24 @@ int build_plan(const rst_shape* sh, std::vector<LayerSpec>& L, int* P) {
     return RST_OK;
 }
 
-// Pack a GEMM-form kernel Wg[tap][ci][n] (taps = kh*kw, row-major) into the LDS stage image
-// [nb][chunk][g][t][sg][h][n][v] of conv_mfma_kernel.
 std::vector<float> pack_tiles(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t) {
+    return pack_conv_tiles(Wg, taps, cin, ntot, t);
+}
+
+template <typename T>
+int upload(T** dst, const void* src, size_t bytes) {
+    if (hipMalloc((void**)dst, bytes) != hipSuccess) return fail(RST_ERR_ALLOC, "hipMalloc failed");
+    if (src != nullptr && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(RST_ERR_HIP, "hipMemcpy failed");
+    return RST_OK;
+}
+
+}  // namespace
+
+namespace rst {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t) {
     const int ck = t.ck, nt = t.nt, tps = t.tps, vec = t.vec;
     const int ksteps = ck / 2, sg_n = ksteps / vec;
     const int nchunks = (cin + ck - 1) / ck, nblocks = (ntot + nt - 1) / nt, ngroups = taps / tps;
@@ -159,16 +175,7 @@ std::vector<float> pack_tiles(const std::vector<float>& Wg, int taps, int cin, i
                                 }
     return out;
 }
-
-template <typename T>
-int upload(T** dst, const void* src, size_t bytes) {
-    if (hipMalloc((void**)dst, bytes) != hipSuccess) return fail(RST_ERR_ALLOC, "hipMalloc failed");
-    if (src != nullptr && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
-        return fail(RST_ERR_HIP, "hipMemcpy failed");
-    return RST_OK;
-}
-
-}  // namespace
+}  // namespace rst
 
 struct rst_handle {
     rst_shape shape;
