@@ -54,6 +54,7 @@ __device__ __forceinline__ float vget(const float4& v, int q) {
 }
 
 __device__ __forceinline__ float apply_pro(int mode, float x, float2 ab, float r) {
+    if (mode == PRO_MASK) return r > 0.f ? x : 0.f;   // ReLU backward: gradient masked by the forward output
     float y = fmaf(ab.x, x, ab.y);
     if (mode == PRO_AFF_RELU) y = fmaxf(y, 0.f);
     else if (mode == PRO_AFF_RES) y = r + y;
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
             v.y = apply_pro(pro, v.y, pab[c + 1], r.y);
             v.z = apply_pro(pro, v.z, pab[c + 2], r.z);
             v.w = apply_pro(pro, v.w, pab[c + 3], r.w);
-            if (do_mat && iy >= y0 && iy < y0 + TH && ix >= x0 && ix < x0 + TW)
+            if (do_mat && iy >= y0 * S && iy < (y0 + TH) * S && ix >= x0 * S && ix < (x0 + TW) * S)
                 *reinterpret_cast<float4*>(a.mat + gi) = v;
         }
         return v;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
                     v = *reinterpret_cast<const float4*>(a.in + gi);
                     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (pro == PRO_AFF_RES) r = *reinterpret_cast<const float4*>(a.res + gi);
+                    if (pro == PRO_AFF_RES || pro == PRO_MASK) r = *reinterpret_cast<const float4*>(a.res + gi);
                     v = transform4(v, r, c, gi, iy, ix);
                 }
                 write_halo4(hbuf, hp, q, v);
@@ -244,9 +245,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
                     v = a.in[gi];
                     if (pro != PRO_NONE) {
-                        const float r = (pro == PRO_AFF_RES) ? a.res[gi] : 0.f;
+                        const float r = (pro == PRO_AFF_RES || pro == PRO_MASK) ? a.res[gi] : 0.f;
                         v = apply_pro(pro, v, pab[c], r);
-                        if (do_mat && iy >= y0 && iy < y0 + TH && ix >= x0 && ix < x0 + TW) a.mat[gi] = v;
+                        if (do_mat && iy >= y0 * S && iy < (y0 + TH) * S && ix >= x0 * S && ix < (x0 + TW) * S) a.mat[gi] = v;
                     }
                 }
                 hbuf[hp * CS + q] = v;
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     };
 
     // ---- prologue -----------------------------------------------------------------------------
-    if (pro != PRO_NONE) {
+    if (pro != PRO_NONE && a.pro_ab != nullptr) {
         for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[b * Cin + c];
         __syncthreads();
     }
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     }
     __syncthreads();
 
-    const float* res_src = (pro == PRO_AFF_RES) ? a.res : a.in;
+    const float* res_src = (pro == PRO_AFF_RES || pro == PRO_MASK) ? a.res : a.in;
 
     // Uniform pipeline stage (one body, so the accumulators keep their registers): prefetch the
     // weights of stage s+1 and slice g of the next chunk's halo (HB == 2), MFMAs of stage s from
@@ -483,7 +484,9 @@ static ConvTile tile_of() {
     X(14, 3, 3, 2, 4, 32, 8, 16, 4, 1, 9, 1)         \
     X(15, 3, 3, 1, 4, 32, 8, 16, 4, 1, 9, 1)         \
     X(16, 2, 2, 1, 4, 32, 8, 16, 4, 1, 4, 1)         \
-    X(17, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 1)
+    X(17, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 1)         \
+    X(18, 1, 1, 1, 32, 64, 8, 16, 2, 2, 1, 1)         \
+    X(19, 1, 1, 1, 32, 128, 4, 16, 2, 2, 1, 1)
 
 bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
     // pick CK (Cin chunk) and NT (output columns per workgroup)
@@ -498,6 +501,7 @@ bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
     int nt = ntot > 64 ? 128 : (ntot > 32 ? 64 : 32);
     if (ntot > 128 && ntot % 128 != 0) return false;
     if (kh == 9 || (kh == 3 && stride == 2)) nt = 32;  // these variants exist only with NT=32
+    if (kh == 1 && ck != 32) return false;             // 1x1 (Gram backward GEMM): Cin multiple of 32
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB)                       \
     if (kh == KH && stride == S && ck == CK && nt == NT) {                   \
         *out = tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB>();           \

@@ -5,7 +5,7 @@
 
 namespace rst {
 
-enum ProMode { PRO_NONE = 0, PRO_AFF_RELU = 1, PRO_AFF = 2, PRO_AFF_RES = 3 };
+enum ProMode { PRO_NONE = 0, PRO_AFF_RELU = 1, PRO_AFF = 2, PRO_AFF_RES = 3, PRO_MASK = 4 };
 enum EpiMode { EPI_NONE = 0, EPI_RELU_BN = 1, EPI_RELU_STATS = 2, EPI_STATS = 3 };
 
 // Arguments of the implicit-GEMM MFMA conv kernel (conv_mfma.hip).
@@ -62,6 +62,12 @@ struct FinalizeArgs {
     const float* scale;      // alternative explicit scale [B][C] (or null)
     const float* bias;       // alternative explicit bias [B][C] (or null)
     float2* ab;              // out [B][C]
+    float2* mr;              // optional out [B][C] (mean, rstd) for the backward pass
+    int affine_bstride;      // image stride of scale/bias (C per image; 0 = per-channel, BatchNorm)
+    int merge_images;        // BatchNorm (training): statistics over the whole batch
+    float* moving_mean;      // optional BatchNorm moving statistics update (Keras momentum)
+    float* moving_var;
+    float momentum;
     int batch, C, ntot, n_part, phases;
     int style_stride;        // S*P
     int style_offset;        // offset of scale in the style vector; bias at +C

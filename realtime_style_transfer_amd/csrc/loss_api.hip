@@ -22,55 +22,12 @@
 #include "../../include/rst.h"
 #include "common.h"
 #include "kernels.h"
+#include "lossnet.h"
 
 using namespace rst;
 
-namespace {
-
-struct VggConv {
-    int cin, cout, H, W;     // input dims (output H, W equal: SAME, stride 1)
-    bool pool_after;
-    ConvTile tile;
-    int tiles_y, tiles_x, n_blocks, nchunks;
-    float* d_w = nullptr;
-    float* d_b = nullptr;
-    float* d_out = nullptr;  // [B][H][W][cout]
-    float* d_pool = nullptr; // [B][H/2][W/2][cout] when pool_after
-};
-
-const int VGG_CH[13] = {64, 64, 128, 128, 256, 256, 256, 512, 512, 512, 512, 512, 512};
-const bool VGG_POOL[13] = {false, true, false, true, false, false, true, false, false, true, false, false, false};
-const int STYLE_IDX[4] = {1, 3, 6, 9};   // block1_conv2, block2_conv2, block3_conv3, block4_conv3
-const int CONTENT_IDX = 12;              // block5_conv3
-const double VGG_MEAN_BGR[3] = {103.939, 116.779, 123.68};
-
-}  // namespace
-
-struct rst_loss_handle {
-    rst_loss_shape shape;
-    std::vector<VggConv> convs;
-    std::vector<void*> allocs;
-    float2* d_pre = nullptr;              // preprocess affine [max_batch][3]
-    float* d_content_feat = nullptr;      // F5(gt_content)
-    float* d_gram_style[4] = {nullptr, nullptr, nullptr, nullptr};
-    float* d_gram_pred[4] = {nullptr, nullptr, nullptr, nullptr};
-    void* d_gram_ws = nullptr;
-    float* d_partial = nullptr;
-    size_t gram_ws_bytes = 0;
-    ~rst_loss_handle() {
-        for (void* p : allocs) hipFree(p);
-    }
-    template <typename T>
-    int alloc(T** p, size_t bytes, const void* src = nullptr) {
-        if (hipMalloc((void**)p, bytes) != hipSuccess) return set_error(RST_ERR_ALLOC, "hipMalloc failed");
-        allocs.push_back((void*)*p);
-        if (src && hipMemcpy(*p, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
-            return set_error(RST_ERR_HIP, "hipMemcpy failed");
-        return RST_OK;
-    }
-};
-
-static int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t st) {
+namespace rst {
+int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t st) {
     const float* in = img;
     for (int i = 0; i <= last; ++i) {
         VggConv& c = h->convs[i];
@@ -106,6 +63,8 @@ static int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStr
     return RST_OK;
 }
 
+}  // namespace rst
+
 extern "C" {
 
 size_t rst_loss_num_weights(void) {
@@ -130,6 +89,7 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
                                               " VGG16 weights, got " + std::to_string(num_weights));
     rst_loss_handle* h = new rst_loss_handle();
     h->shape = *shape;
+    h->host_w.assign(vgg_weights_host, vgg_weights_host + num_weights);
     const int B = shape->max_batch;
     int H = shape->h, W = shape->w, cin = 3;
     const float* wp = vgg_weights_host;

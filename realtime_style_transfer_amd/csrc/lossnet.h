@@ -1,0 +1,60 @@
+// lossnet.h — VGG16 loss network internals shared by loss_api.hip and train_api.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../../include/rst.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace rst {
+struct VggConv {
+    int cin, cout, H, W;     // input dims (output H, W equal: SAME, stride 1)
+    bool pool_after;
+    ConvTile tile;
+    int tiles_y, tiles_x, n_blocks, nchunks;
+    float* d_w = nullptr;
+    float* d_b = nullptr;
+    float* d_out = nullptr;  // [B][H][W][cout]
+    float* d_pool = nullptr; // [B][H/2][W/2][cout] when pool_after
+};
+
+const int VGG_CH[13] = {64, 64, 128, 128, 256, 256, 256, 512, 512, 512, 512, 512, 512};
+const bool VGG_POOL[13] = {false, true, false, true, false, false, true, false, false, true, false, false, false};
+const int STYLE_IDX[4] = {1, 3, 6, 9};   // block1_conv2, block2_conv2, block3_conv3, block4_conv3
+const int CONTENT_IDX = 12;              // block5_conv3
+const double VGG_MEAN_BGR[3] = {103.939, 116.779, 123.68};
+
+}  // namespace rst
+
+struct rst_loss_handle {
+    rst_loss_shape shape;
+    std::vector<rst::VggConv> convs;
+    std::vector<void*> allocs;
+    float2* d_pre = nullptr;              // preprocess affine [max_batch][3]
+    float* d_content_feat = nullptr;      // F5(gt_content)
+    float* d_gram_style[4] = {nullptr, nullptr, nullptr, nullptr};
+    float* d_gram_pred[4] = {nullptr, nullptr, nullptr, nullptr};
+    void* d_gram_ws = nullptr;
+    float* d_partial = nullptr;
+    size_t gram_ws_bytes = 0;
+    std::vector<float> host_w;            // VGG16 weights as given (Keras order), for the backward packing
+    ~rst_loss_handle() {
+        for (void* p : allocs) (void)hipFree(p);
+    }
+    template <typename T>
+    int alloc(T** p, size_t bytes, const void* src = nullptr) {
+        if (hipMalloc((void**)p, bytes) != hipSuccess) return rst::set_error(RST_ERR_ALLOC, "hipMalloc failed");
+        allocs.push_back((void*)*p);
+        if (src && hipMemcpy(*p, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
+            return rst::set_error(RST_ERR_HIP, "hipMemcpy failed");
+        return RST_OK;
+    }
+};
+
+namespace rst {
+// Run the VGG16 trunk on B images up to (and including) conv `last`; conv outputs land in convs[i].d_out.
+int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t st);
+}  // namespace rst
+

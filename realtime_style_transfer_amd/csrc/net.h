@@ -1,0 +1,98 @@
+// net.h — the transfer network's host-side description, shared by the inference (rst_api.hip)
+// and training (train_api.hip) translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rst.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace rst {
+
+const int CONTRACT_FILTERS[4] = {16, 32, 32, 32};                // styleTransfer.py:218-223
+const int EXPAND_FILTERS[8] = {32, 16, 8, 4, 3, 3, 3, 3};        // styleTransfer.py:247-256
+
+enum LayerKind { K_CONV = 0, K_CONVT2 = 1, K_SMALL = 2 };
+enum Norm { N_BN = 0, N_CIN = 1 };
+enum Post { P_RELU = 0, P_NONE = 1, P_SIGMOID = 2 };
+
+struct LayerSpec {
+    std::string name;
+    int keras_kind;      // 0 Conv2D, 1 Conv2DTranspose
+    int k, stride, cin, cout;
+    int H, W, Ho, Wo;    // input / output spatial dims
+    int norm, post;
+    bool conv_relu;
+    int style_offset;
+    int res_block;       // residual block index or -1
+    int res_conv;        // 0/1 within the residual block
+};
+
+struct LayerExec {
+    LayerSpec s;
+    int kind = K_CONV;
+    ConvTile tile{};
+    int ntot = 0, gHo = 0, gWo = 0, pad_t = 0, pad_l = 0;
+    int tiles_y = 0, tiles_x = 0, n_blocks = 1, nchunks = 1;
+    int n_part = 0;
+    float* d_w = nullptr;
+    float* d_bias = nullptr;
+    float2* d_bn = nullptr;
+    float* d_out = nullptr;       // raw (CIN) or final (BN) output [max_batch][Ho][Wo][cout]
+    float4* d_part = nullptr;
+    float2* d_ab = nullptr;       // CIN affine of this layer's output [max_batch][cout]
+    float* d_mat = nullptr;       // block input materialised by this layer's prologue (or null)
+    // prologue (how this layer reads its input)
+    int pro = PRO_NONE;
+    int pro_src = -1;             // layer whose d_ab/d_out feed the prologue (-1: network input)
+    const float* pro_res = nullptr;
+    // debug "emitted" tensor of this layer = act(a*raw + b) [+ res]
+    const float* emit_res = nullptr;
+};
+
+size_t layer_weight_count(const LayerSpec& s);
+int build_plan(const rst_shape* sh, std::vector<LayerSpec>& L, int* P);
+int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const float* bias, std::vector<float>& packed,
+                  std::vector<float>& bias_n);
+
+template <typename T>
+int upload(T** dst, const void* src, size_t bytes) {
+    if (hipMalloc((void**)dst, bytes) != hipSuccess) return set_error(RST_ERR_ALLOC, "hipMalloc failed");
+    if (src != nullptr && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
+        return set_error(RST_ERR_HIP, "hipMemcpy failed");
+    return RST_OK;
+}
+
+}  // namespace rst
+
+struct rst_handle {
+    using LayerExec = rst::LayerExec;
+    rst_shape shape;
+    int P = 0;
+    std::vector<LayerExec> layers;
+    std::vector<void*> allocs;
+    // optional per-layer timing: 3 events per layer per step (before conv, after conv, after finalize)
+    std::vector<hipEvent_t> prof_events;
+    int prof_max_steps = 0, prof_step = 0;
+    bool prof_on = false;
+    void prof_free() {
+        for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
+        prof_events.clear();
+        prof_on = false;
+        prof_max_steps = prof_step = 0;
+    }
+    ~rst_handle() {
+        prof_free();
+        for (void* p : allocs) (void)hipFree(p);
+    }
+    template <typename T>
+    int alloc(T** p, size_t bytes, const void* src = nullptr) {
+        int st = rst::upload(p, src, bytes);
+        if (*p) allocs.push_back((void*)*p);
+        return st;
+    }
+};
+

@@ -28,29 +28,32 @@ __device__ __forceinline__ T block_sum256(T v, T* scratch) {
 __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
     __shared__ double scratch[4];
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int b0 = a.merge_images ? 0 : b, b1 = a.merge_images ? a.batch : b + 1;
     double s = 0.0, n = 0.0;
-    for (int ph = 0; ph < a.phases; ++ph) {
-        const float4* p = a.part + ((size_t)b * a.ntot + ph * a.C + c) * a.n_part;
-        for (int t = tid; t < a.n_part; t += 256) {
-            const float4 v = p[t];
-            s += (double)v.x;
-            n += (double)v.z;
+    for (int bb = b0; bb < b1; ++bb)
+        for (int ph = 0; ph < a.phases; ++ph) {
+            const float4* p = a.part + ((size_t)bb * a.ntot + ph * a.C + c) * a.n_part;
+            for (int t = tid; t < a.n_part; t += 256) {
+                const float4 v = p[t];
+                s += (double)v.x;
+                n += (double)v.z;
+            }
         }
-    }
     s = block_sum256(s, scratch);
     n = block_sum256(n, scratch);
     const double mean = n > 0.0 ? s / n : 0.0;
     double m2 = 0.0;
-    for (int ph = 0; ph < a.phases; ++ph) {
-        const float4* p = a.part + ((size_t)b * a.ntot + ph * a.C + c) * a.n_part;
-        for (int t = tid; t < a.n_part; t += 256) {
-            const float4 v = p[t];
-            if (v.z > 0.f) {
-                const double d = (double)v.x / (double)v.z - mean;
-                m2 += (double)v.y + (double)v.z * d * d;
+    for (int bb = b0; bb < b1; ++bb)
+        for (int ph = 0; ph < a.phases; ++ph) {
+            const float4* p = a.part + ((size_t)bb * a.ntot + ph * a.C + c) * a.n_part;
+            for (int t = tid; t < a.n_part; t += 256) {
+                const float4 v = p[t];
+                if (v.z > 0.f) {
+                    const double d = (double)v.x / (double)v.z - mean;
+                    m2 += (double)v.y + (double)v.z * d * d;
+                }
             }
         }
-    }
     m2 = block_sum256(m2, scratch);
     if (tid == 0) {
         const double var = n > 0.0 ? m2 / n : 0.0;
@@ -61,11 +64,17 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
             scale = sp[c];
             bias = sp[a.C + c];
         } else if (a.scale != nullptr) {
-            scale = a.scale[b * a.C + c];
-            bias = a.bias[b * a.C + c];
+            scale = a.scale[b * a.affine_bstride + c];
+            bias = a.bias[b * a.affine_bstride + c];
         }
         const float aa = scale * rstd;
         a.ab[b * a.C + c] = make_float2(aa, bias - (float)mean * aa);
+        if (a.mr != nullptr) a.mr[b * a.C + c] = make_float2((float)mean, rstd);
+        if (a.moving_mean != nullptr && b == 0) {
+            const double unbiased = n > 1.0 ? m2 / (n - 1.0) : var;
+            a.moving_mean[c] = (float)(a.momentum * a.moving_mean[c] + (1.0 - a.momentum) * mean);
+            a.moving_var[c] = (float)(a.momentum * a.moving_var[c] + (1.0 - a.momentum) * unbiased);
+        }
     }
 }
 

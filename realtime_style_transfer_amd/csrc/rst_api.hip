@@ -26,6 +26,7 @@
 #include "../../include/rst.h"
 #include "common.h"
 #include "kernels.h"
+#include "net.h"
 
 using namespace rst;
 
@@ -45,47 +46,9 @@ int fail(int code, const std::string& msg) {
             return fail(RST_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
     } while (0)
 
-const int CONTRACT_FILTERS[4] = {16, 32, 32, 32};                // styleTransfer.py:218-223
-const int EXPAND_FILTERS[8] = {32, 16, 8, 4, 3, 3, 3, 3};        // styleTransfer.py:247-256
+}  // namespace
 
-enum LayerKind { K_CONV = 0, K_CONVT2 = 1, K_SMALL = 2 };
-enum Norm { N_BN = 0, N_CIN = 1 };
-enum Post { P_RELU = 0, P_NONE = 1, P_SIGMOID = 2 };
-
-struct LayerSpec {
-    std::string name;
-    int keras_kind;      // 0 Conv2D, 1 Conv2DTranspose
-    int k, stride, cin, cout;
-    int H, W, Ho, Wo;    // input / output spatial dims
-    int norm, post;
-    bool conv_relu;
-    int style_offset;
-    int res_block;       // residual block index or -1
-    int res_conv;        // 0/1 within the residual block
-};
-
-struct LayerExec {
-    LayerSpec s;
-    int kind = K_CONV;
-    ConvTile tile{};
-    int ntot = 0, gHo = 0, gWo = 0, pad_t = 0, pad_l = 0;
-    int tiles_y = 0, tiles_x = 0, n_blocks = 1, nchunks = 1;
-    int n_part = 0;
-    float* d_w = nullptr;
-    float* d_bias = nullptr;
-    float2* d_bn = nullptr;
-    float* d_out = nullptr;       // raw (CIN) or final (BN) output [max_batch][Ho][Wo][cout]
-    float4* d_part = nullptr;
-    float2* d_ab = nullptr;       // CIN affine of this layer's output [max_batch][cout]
-    float* d_mat = nullptr;       // block input materialised by this layer's prologue (or null)
-    // prologue (how this layer reads its input)
-    int pro = PRO_NONE;
-    int pro_src = -1;             // layer whose d_ab/d_out feed the prologue (-1: network input)
-    const float* pro_res = nullptr;
-    // debug "emitted" tensor of this layer = act(a*raw + b) [+ res]
-    const float* emit_res = nullptr;
-};
-
+namespace rst {
 size_t layer_weight_count(const LayerSpec& s) {
     size_t n = (size_t)s.k * s.k * s.cin * s.cout + s.cout;
     if (s.norm == N_BN) n += 4 * (size_t)s.cout;
@@ -139,17 +102,6 @@ std::vector<float> pack_tiles(const std::vector<float>& Wg, int taps, int cin, i
     return pack_conv_tiles(Wg, taps, cin, ntot, t);
 }
 
-template <typename T>
-int upload(T** dst, const void* src, size_t bytes) {
-    if (hipMalloc((void**)dst, bytes) != hipSuccess) return fail(RST_ERR_ALLOC, "hipMalloc failed");
-    if (src != nullptr && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
-        return fail(RST_ERR_HIP, "hipMemcpy failed");
-    return RST_OK;
-}
-
-}  // namespace
-
-namespace rst {
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 
 std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t) {
@@ -177,32 +129,87 @@ std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int c
 }
 }  // namespace rst
 
-struct rst_handle {
-    rst_shape shape;
-    int P = 0;
-    std::vector<LayerExec> layers;
-    std::vector<void*> allocs;
-    // optional per-layer timing: 3 events per layer per step (before conv, after conv, after finalize)
-    std::vector<hipEvent_t> prof_events;
-    int prof_max_steps = 0, prof_step = 0;
-    bool prof_on = false;
-    void prof_free() {
-        for (hipEvent_t e : prof_events) hipEventDestroy(e);
-        prof_events.clear();
-        prof_on = false;
-        prof_max_steps = prof_step = 0;
+namespace rst {
+// Geometry, kernel choice and device weight image of one layer (no device work). `kern`/`bias`
+// point at the layer's Keras weights; passing an array of (index + 1) values instead yields the
+// gather map from canonical weights to the packed image (training re-packs after each update).
+int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const float* bias, std::vector<float>& packed,
+                  std::vector<float>& bias_n) {
+    const size_t kcount = (size_t)s.k * s.k * s.cin * s.cout;
+    (void)kcount;
+    if (s.keras_kind == 1 && s.k == 9 && s.stride == 1) {
+        // ---- final 9x9 transposed conv: flip -> correlation, pack [ky][ci][kx][co]
+        if (s.cout != 3) return fail(RST_ERR_UNSUPPORTED, "last layer must have 3 channels");
+        e.kind = K_SMALL;
+        const int ws = small_conv_weight_stride();
+        std::vector<float> w((size_t)9 * s.cin * ws, 0.f);
+        for (int ky = 0; ky < 9; ++ky)
+            for (int kx = 0; kx < 9; ++kx)
+                for (int ci = 0; ci < s.cin; ++ci)
+                    for (int co = 0; co < 3; ++co)
+                        w[((size_t)ky * s.cin + ci) * ws + kx * 3 + co] =
+                            kern[(((size_t)(8 - ky) * 9 + (8 - kx)) * 3 + co) * s.cin + ci];
+        packed.swap(w);
+        bias_n.assign(bias, bias + 3);
+        e.ntot = 3;
+        e.tiles_y = small_conv_tiles_y(s.Ho);
+        e.tiles_x = small_conv_tiles_x(s.Wo);
+        e.n_part = e.tiles_y * e.tiles_x;
+    } else {
+        int taps, ntot, kh;
+        std::vector<float> Wg;
+        if (s.keras_kind == 0) {
+            kh = s.k;
+            taps = s.k * s.k;
+            ntot = s.cout;
+            Wg.assign(kern, kern + kcount);   // HWIO already == [tap][ci][co]
+            e.kind = K_CONV;
+            const int pt = std::max((s.Ho - 1) * s.stride + s.k - s.H, 0);
+            const int pl = std::max((s.Wo - 1) * s.stride + s.k - s.W, 0);
+            e.pad_t = pt / 2;
+            e.pad_l = pl / 2;
+            e.gHo = s.Ho;
+            e.gWo = s.Wo;
+            bias_n.assign(bias, bias + s.cout);
+        } else {
+            if (!(s.k == 3 && s.stride == 2))
+                return fail(RST_ERR_UNSUPPORTED, "Conv2DTranspose other than 3x3/s2 and 9x9/s1");
+            // 3x3 s2 SAME transposed conv == 2x2 conv (pad 1) with 4 output phases:
+            // out[2p+py][2q+px][co] = sum_{ty,tx} in[p+ty-1][q+tx-1] . w[py+2(1-ty)][px+2(1-tx)][co]
+            kh = 2;
+            taps = 4;
+            ntot = 4 * s.cout;
+            e.kind = K_CONVT2;
+            Wg.assign((size_t)4 * s.cin * ntot, 0.f);
+            for (int ty = 0; ty < 2; ++ty)
+                for (int tx = 0; tx < 2; ++tx)
+                    for (int py = 0; py < 2; ++py)
+                        for (int px = 0; px < 2; ++px) {
+                            const int ky = py + 2 * (1 - ty), kx = px + 2 * (1 - tx);
+                            if (ky > 2 || kx > 2) continue;
+                            for (int ci = 0; ci < s.cin; ++ci)
+                                for (int co = 0; co < s.cout; ++co)
+                                    Wg[((size_t)(ty * 2 + tx) * s.cin + ci) * ntot + (py * 2 + px) * s.cout + co] =
+                                        kern[(((size_t)ky * 3 + kx) * s.cout + co) * s.cin + ci];
+                        }
+            e.pad_t = e.pad_l = 1;
+            e.gHo = s.H;
+            e.gWo = s.W;
+            for (int n = 0; n < ntot; ++n) bias_n.push_back(bias[n % s.cout]);
+        }
+        if (!conv_select(kh, s.keras_kind == 0 ? s.stride : 1, s.cin, ntot, &e.tile))
+            return fail(RST_ERR_UNSUPPORTED, "no conv tile configuration for layer " + s.name);
+        e.ntot = ntot;
+        e.tiles_y = (e.gHo + e.tile.th - 1) / e.tile.th;
+        e.tiles_x = (e.gWo + e.tile.tw - 1) / e.tile.tw;
+        e.n_blocks = (ntot + e.tile.nt - 1) / e.tile.nt;
+        e.nchunks = (s.cin + e.tile.ck - 1) / e.tile.ck;
+        e.n_part = e.tiles_y * e.tiles_x * e.tile.mt;
+        packed = pack_tiles(Wg, taps, s.cin, ntot, e.tile);
     }
-    ~rst_handle() {
-        prof_free();
-        for (void* p : allocs) hipFree(p);
-    }
-    template <typename T>
-    int alloc(T** p, size_t bytes, const void* src = nullptr) {
-        int st = upload(p, src, bytes);
-        if (*p) allocs.push_back((void*)*p);
-        return st;
-    }
-};
+    return RST_OK;
+}
+}  // namespace rst
 
 extern "C" {
 
@@ -252,82 +259,9 @@ int rst_create(const rst_shape* shape, const float* weights_host, size_t num_wei
         const float* kern = wp;
         const float* bias = wp + kcount;
         wp += kcount + s.cout;
-        std::vector<float> bias_n;
-        if (s.keras_kind == 1 && s.k == 9 && s.stride == 1) {
-            // ---- final 9x9 transposed conv: flip -> correlation, pack [ky][ci][kx][co]
-            if (s.cout != 3) { delete h; return fail(RST_ERR_UNSUPPORTED, "last layer must have 3 channels"); }
-            e.kind = K_SMALL;
-            const int ws = small_conv_weight_stride();
-            std::vector<float> w((size_t)9 * s.cin * ws, 0.f);
-            for (int ky = 0; ky < 9; ++ky)
-                for (int kx = 0; kx < 9; ++kx)
-                    for (int ci = 0; ci < s.cin; ++ci)
-                        for (int co = 0; co < 3; ++co)
-                            w[((size_t)ky * s.cin + ci) * ws + kx * 3 + co] =
-                                kern[(((size_t)(8 - ky) * 9 + (8 - kx)) * 3 + co) * s.cin + ci];
-            if ((st = h->alloc(&e.d_w, w.size() * 4, w.data())) != RST_OK) { delete h; return st; }
-            bias_n.assign(bias, bias + 3);
-            e.ntot = 3;
-            e.tiles_y = small_conv_tiles_y(s.Ho);
-            e.tiles_x = small_conv_tiles_x(s.Wo);
-            e.n_part = e.tiles_y * e.tiles_x;
-        } else {
-            int taps, ntot, kh;
-            std::vector<float> Wg;
-            if (s.keras_kind == 0) {
-                kh = s.k;
-                taps = s.k * s.k;
-                ntot = s.cout;
-                Wg.assign(kern, kern + kcount);   // HWIO already == [tap][ci][co]
-                e.kind = K_CONV;
-                const int pt = std::max((s.Ho - 1) * s.stride + s.k - s.H, 0);
-                const int pl = std::max((s.Wo - 1) * s.stride + s.k - s.W, 0);
-                e.pad_t = pt / 2;
-                e.pad_l = pl / 2;
-                e.gHo = s.Ho;
-                e.gWo = s.Wo;
-                bias_n.assign(bias, bias + s.cout);
-            } else {
-                if (!(s.k == 3 && s.stride == 2)) {
-                    delete h;
-                    return fail(RST_ERR_UNSUPPORTED, "Conv2DTranspose other than 3x3/s2 and 9x9/s1");
-                }
-                // 3x3 s2 SAME transposed conv == 2x2 conv (pad 1) with 4 output phases:
-                // out[2p+py][2q+px][co] = sum_{ty,tx} in[p+ty-1][q+tx-1] . w[py+2(1-ty)][px+2(1-tx)][co]
-                kh = 2;
-                taps = 4;
-                ntot = 4 * s.cout;
-                e.kind = K_CONVT2;
-                Wg.assign((size_t)4 * s.cin * ntot, 0.f);
-                for (int ty = 0; ty < 2; ++ty)
-                    for (int tx = 0; tx < 2; ++tx)
-                        for (int py = 0; py < 2; ++py)
-                            for (int px = 0; px < 2; ++px) {
-                                const int ky = py + 2 * (1 - ty), kx = px + 2 * (1 - tx);
-                                if (ky > 2 || kx > 2) continue;
-                                for (int ci = 0; ci < s.cin; ++ci)
-                                    for (int co = 0; co < s.cout; ++co)
-                                        Wg[((size_t)(ty * 2 + tx) * s.cin + ci) * ntot + (py * 2 + px) * s.cout + co] =
-                                            kern[(((size_t)ky * 3 + kx) * s.cout + co) * s.cin + ci];
-                            }
-                e.pad_t = e.pad_l = 1;
-                e.gHo = s.H;
-                e.gWo = s.W;
-                for (int n = 0; n < ntot; ++n) bias_n.push_back(bias[n % s.cout]);
-            }
-            if (!conv_select(kh, s.keras_kind == 0 ? s.stride : 1, s.cin, ntot, &e.tile)) {
-                delete h;
-                return fail(RST_ERR_UNSUPPORTED, "no conv tile configuration for layer " + s.name);
-            }
-            e.ntot = ntot;
-            e.tiles_y = (e.gHo + e.tile.th - 1) / e.tile.th;
-            e.tiles_x = (e.gWo + e.tile.tw - 1) / e.tile.tw;
-            e.n_blocks = (ntot + e.tile.nt - 1) / e.tile.nt;
-            e.nchunks = (s.cin + e.tile.ck - 1) / e.tile.ck;
-            e.n_part = e.tiles_y * e.tiles_x * e.tile.mt;
-            std::vector<float> pk = pack_tiles(Wg, taps, s.cin, ntot, e.tile);
-            if ((st = h->alloc(&e.d_w, pk.size() * 4, pk.data())) != RST_OK) { delete h; return st; }
-        }
+        std::vector<float> bias_n, packed;
+        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n)) != RST_OK) { delete h; return st; }
+        if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
         if (s.norm == N_BN) {
             const float* gamma = wp;
@@ -583,6 +517,7 @@ int rst_instance_norm(const float* x, int batch, int hw, int channels, const flo
     f.ntot = channels;
     f.n_part = n_tiles;
     f.phases = 1;
+    f.affine_bstride = channels;
     f.eps = eps;
     HIP_TRY(finalize_launch(f, st));
     HIP_TRY(affine_act_launch(x, ab, nullptr, y, batch, hw, channels, relu ? 1 : 0, st));

@@ -1,0 +1,482 @@
+// train.hip — backward-pass and optimizer kernels of the training step (BASELINE config 4,
+// train_network.py:102-138: Keras fit with RMSprop; loss styleLoss.py:295-369).
+//
+// Norm backward (CIN styleTransfer.py:57-71, BatchNorm training mode styleTransfer.py:201):
+//   n = a z + b (a = scale*rstd, b = bias - mean*a), x^ = (z - mean) rstd, post in {relu, none, sigmoid}
+//   dn = post'(G)                      (G = gradient w.r.t. the post-activation output)
+//   S1 = sum dn, S2 = sum dn x^        (over HW per (image, channel); over B*HW for BN)
+//   d bias = S1, d scale = S2          (style-parameter / beta, gamma gradients)
+//   dz = a (dn - S1/N - x^ S2/N) [z > 0 when the conv carries a built-in ReLU]
+// reduce -> finalize (f64, fixed order) -> apply, no atomics.
+//
+// Weight gradients: split-K f32 MFMA (v_mfma_f32_32x32x2_f32) over pixels,
+//   conv : dW[tap][ci][co] = sum_{b,q} X[b][q*s + tap - pad][ci] * Dz[b][q][co]
+//   convT: dW[tap][co][ci] = sum_{b,i} X[b][i][ci] * Dz[b][i*s + tap - pad][co]
+// per-split slabs, reduced in fixed order (bitwise reproducible).
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+#include "train.h"
+
+namespace rst {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float post_grad(int post, float g, float z, float2 ab) {
+    const float n = fmaf(ab.x, z, ab.y);
+    if (post == 0) return n > 0.f ? g : 0.f;                      // relu
+    if (post == 2) {                                               // sigmoid
+        const float s = 1.f / (1.f + __expf(-n));
+        return g * s * (1.f - s);
+    }
+    return g;                                                      // none
+}
+
+// ---------------------------------------------------------------------------------------------
+// norm backward: per-tile partial {S1, S2}; layout [b][c][tile]
+__global__ __launch_bounds__(256) void norm_bwd_reduce_kernel(NormBwdArgs a) {
+    __shared__ float2 red[256];
+    const int tile = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int C = a.C;
+    const int R = 256 / C;                 // pixel lanes per channel
+    const int c = tid % C, r = tid / C;
+    float s1 = 0.f, s2 = 0.f;
+    if (r < R) {
+        const float2 ab = a.ab[b * C + c];
+        const float2 mr = a.mr[b * C + c];
+        const long p0 = (long)tile * a.tile, p1 = min((long)a.hw, p0 + a.tile);
+        for (long p = p0 + r; p < p1; p += R) {
+            const size_t i = ((size_t)b * a.hw + p) * C + c;
+            const float z = a.z[i];
+            const float dn = post_grad(a.post, a.g[i], z, ab);
+            s1 += dn;
+            s2 = fmaf(dn, (z - mr.x) * mr.y, s2);
+        }
+    }
+    red[tid] = make_float2(s1, s2);
+    __syncthreads();
+    if (tid < C) {
+        float t1 = 0.f, t2 = 0.f;
+        for (int k = 0; k < R; ++k) {
+            t1 += red[k * C + tid].x;
+            t2 += red[k * C + tid].y;
+        }
+        a.part[((size_t)b * C + tid) * a.n_tiles + tile] = make_float2(t1, t2);
+    }
+}
+
+// per (b, c) [per c when merge_images]: S1, S2 in f64 -> consts (S1/N, S2/N), and the parameter grads
+__global__ __launch_bounds__(64) void norm_bwd_finalize_kernel(NormBwdArgs a) {
+    const int c = blockIdx.x, b = blockIdx.y;
+    double s1 = 0.0, s2 = 0.0;
+    const int b0 = a.merge_images ? 0 : b, b1 = a.merge_images ? a.batch : b + 1;
+    for (int bb = b0; bb < b1; ++bb) {
+        const float2* p = a.part + ((size_t)bb * a.C + c) * a.n_tiles;
+        for (int t = threadIdx.x; t < a.n_tiles; t += 64) {
+            s1 += (double)p[t].x;
+            s2 += (double)p[t].y;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+    }
+    if (threadIdx.x == 0) {
+        const double n = (double)a.hw * (a.merge_images ? a.batch : 1);
+        a.consts[b * a.C + c] = make_float2((float)(s1 / n), (float)(s2 / n));
+        if (a.dscale != nullptr && (!a.merge_images || b == 0)) {
+            // CIN: style-param grads per image; BN: gamma/beta grads (accumulated once)
+            const size_t o = a.merge_images ? (size_t)c : (size_t)b * a.dstride + c;
+            a.dscale[o] = (float)s2;
+            a.dbias[o] = (float)s1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void norm_bwd_apply_kernel(NormBwdArgs a) {
+    const size_t total = (size_t)a.batch * a.hw * a.C;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+        const int c = (int)(i % a.C);
+        const int b = (int)(i / ((size_t)a.hw * a.C));
+        const float2 ab = a.ab[b * a.C + c];
+        const float2 mr = a.mr[b * a.C + c];
+        const float2 k = a.consts[b * a.C + c];
+        const float z = a.z[i];
+        const float dn = post_grad(a.post, a.g[i], z, ab);
+        const float xh = (z - mr.x) * mr.y;
+        float dz = ab.x * (dn - k.x - xh * k.y);
+        if (a.conv_relu && !(z > 0.f)) dz = 0.f;
+        a.dz[i] = dz;
+    }
+}
+
+hipError_t norm_bwd_launch(const NormBwdArgs& a0, hipStream_t st) {
+    NormBwdArgs a = a0;
+    if (a.C > 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(norm_bwd_reduce_kernel, dim3(a.n_tiles, a.batch), dim3(256), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3(a.C, a.batch), dim3(64), 0, st, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const size_t total = (size_t)a.batch * a.hw * a.C;
+    unsigned blocks = (unsigned)((total + 255) / 256);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// y = x1 + x2 (skip-connection gradient chains)
+__global__ __launch_bounds__(256) void add_kernel(const float* __restrict__ x1, const float* __restrict__ x2,
+                                                  float* __restrict__ y, size_t n) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = x1[i] + x2[i];
+}
+
+hipError_t add_launch(const float* x1, const float* x2, float* y, size_t n, hipStream_t st) {
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(add_kernel, dim3(blocks), dim3(256), 0, st, x1, x2, y, n);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight gradients (split-K MFMA): dW[r][c] = sum_q S(q, r) U(q, c), where r = (tap, channel of the
+// shifted operand) and q runs over the unshifted operand's pixels (and images):
+//   conv : S = X at q*s + tap - pad (r = (tap, ci)), U = D at q   -> dW (kh, kw, ci, co)
+//   convT: S = D at q*s + tap - pad (r = (tap, co)), U = X at q   -> dW (kh, kw, co, ci)
+// i.e. both land in the canonical Keras kernel layout. WG: 64 rows x 64 cols x one pixel split.
+namespace wg {
+constexpr int KP = 64;       // pixels per LDS stage
+constexpr int T = 64;        // row / col tile edge
+constexpr int LS = T + 1;
+}  // namespace wg
+
+__global__ __launch_bounds__(256) void wgrad_partial_kernel(WgradArgs a) {
+    using namespace wg;
+    __shared__ float la[KP * LS];
+    __shared__ float lb[KP * LS];
+    const bool tr = a.transposed != 0;
+    const int Cs = tr ? a.C2 : a.C1;                 // channels of the shifted operand
+    const int Cu = tr ? a.C1 : a.C2;                 // channels of the unshifted operand
+    const int R = a.kh * a.kw * Cs;
+    const int nr = (R + T - 1) / T, nc = (Cu + T - 1) / T;
+    const float* S = tr ? a.D : a.X;
+    const float* U = tr ? a.X : a.D;
+    const int SH = tr ? a.DH : a.XH, SW = tr ? a.DW : a.XW;
+    int bid = blockIdx.x;
+    const int split = bid % a.nsplit;
+    bid /= a.nsplit;
+    const int tc = bid % nc;
+    const int tr_ = bid / nc;
+    const int r0 = tr_ * T, c0 = tc * T;
+    const long qhw = (long)a.Qh * a.Qw;
+    const long total = (long)a.batch * qhw;
+    const long q_begin = (long)split * a.span;
+    const long q_end = min(total, q_begin + a.span);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wi = wave >> 1, wj = wave & 1;
+    const int li = lane & 31, lh = lane >> 5;
+
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+    for (long q0 = q_begin; q0 < q_end; q0 += KP) {
+        __syncthreads();
+        for (int it = tid; it < KP * T; it += 256) {
+            const int pp = it / T, cc = it % T;
+            const long q = q0 + pp;
+            float vs = 0.f, vu = 0.f;
+            if (q < q_end) {
+                const int b = (int)(q / qhw);
+                const int qr = (int)(q % qhw);
+                const int qy = qr / a.Qw, qx = qr % a.Qw;
+                const int r = r0 + cc;
+                if (r < R) {
+                    const int tap = r / Cs, ch = r % Cs;
+                    const int ky = tap / a.kw, kx = tap % a.kw;
+                    const int sy = qy * a.stride + ky - a.pad_t, sx = qx * a.stride + kx - a.pad_l;
+                    if (sy >= 0 && sy < SH && sx >= 0 && sx < SW)
+                        vs = S[(((size_t)b * SH + sy) * SW + sx) * Cs + ch];
+                }
+                const int c = c0 + cc;
+                if (c < Cu) vu = U[((size_t)b * qhw + qr) * Cu + c];
+            }
+            la[pp * LS + cc] = vs;
+            lb[pp * LS + cc] = vu;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int s = 0; s < KP / 2; ++s) {
+            const int p = 2 * s + lh;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(la[p * LS + wi * 32 + li], lb[p * LS + wj * 32 + li], acc, 0, 0, 0);
+        }
+    }
+    const int Rp = nr * T, Cp = nc * T;
+    float* out = a.slab + (size_t)split * Rp * Cp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        out[(size_t)(r0 + wi * 32 + row) * Cp + c0 + wj * 32 + li] = acc[r];
+    }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
+    const bool tr = a.transposed != 0;
+    const int Cs = tr ? a.C2 : a.C1, Cu = tr ? a.C1 : a.C2;
+    const int R = a.kh * a.kw * Cs;
+    const int Rp = ((R + wg::T - 1) / wg::T) * wg::T, Cp = ((Cu + wg::T - 1) / wg::T) * wg::T;
+    const size_t total = (size_t)R * Cu;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+        const size_t r = i / Cu, c = i % Cu;
+        float s = 0.f;
+        for (int k = 0; k < a.nsplit; ++k) s += a.slab[((size_t)k * Rp + r) * Cp + c];
+        a.dW[i] = s;
+    }
+}
+
+static void wgrad_dims(const WgradArgs& a, int& R, int& Cu) {
+    const int Cs = a.transposed ? a.C2 : a.C1;
+    Cu = a.transposed ? a.C1 : a.C2;
+    R = a.kh * a.kw * Cs;
+}
+
+size_t wgrad_slab_bytes(const WgradArgs& a) {
+    int R, Cu;
+    wgrad_dims(a, R, Cu);
+    const size_t Rp = ((R + wg::T - 1) / wg::T) * wg::T, Cp = ((Cu + wg::T - 1) / wg::T) * wg::T;
+    return (size_t)a.nsplit * Rp * Cp * sizeof(float);
+}
+
+int wgrad_choose_splits(const WgradArgs& a) {
+    int R, Cu;
+    wgrad_dims(a, R, Cu);
+    const long tiles = (long)((R + wg::T - 1) / wg::T) * ((Cu + wg::T - 1) / wg::T);
+    const long total = (long)a.batch * a.Qh * a.Qw;
+    long ns = 2048 / tiles;
+    if (ns < 1) ns = 1;
+    const long max_ns = (total + 511) / 512;
+    if (ns > max_ns) ns = max_ns;
+    if (ns < 1) ns = 1;
+    return (int)ns;
+}
+
+hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
+    int R, Cu;
+    wgrad_dims(a, R, Cu);
+    const long total = (long)a.batch * a.Qh * a.Qw;
+    long span = (total + a.nsplit - 1) / a.nsplit;
+    span = ((span + wg::KP - 1) / wg::KP) * wg::KP;
+    a.span = span;
+    const int nr = (R + wg::T - 1) / wg::T, nc = (Cu + wg::T - 1) / wg::T;
+    const unsigned grid = (unsigned)(nr * nc * a.nsplit);
+    hipLaunchKernelGGL(wgrad_partial_kernel, dim3(grid), dim3(256), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t n = (size_t)R * Cu;
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// bias gradient: db[c] = sum over (b, pixel) of D[..][c]; partials per block then ordered sum
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ D, long rows, int C,
+                                                             float* __restrict__ part, int nblk) {
+    __shared__ float red[256];
+    const int blk = blockIdx.x, tid = threadIdx.x;
+    const int R = 256 / C;
+    const int c = tid % C, r = tid / C;
+    const long per = (rows + nblk - 1) / nblk;
+    const long r0 = (long)blk * per, r1 = min(rows, r0 + per);
+    float s = 0.f;
+    if (r < R)
+        for (long i = r0 + r; i < r1; i += R) s += D[(size_t)i * C + c];
+    red[tid] = s;
+    __syncthreads();
+    if (tid < C) {
+        float t = 0.f;
+        for (int k = 0; k < R; ++k) t += red[k * C + tid];
+        part[(size_t)blk * C + tid] = t;
+    }
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0;
+    for (int k = 0; k < nblk; ++k) s += (double)part[(size_t)k * C + c];
+    out[c] = (float)s;
+}
+
+hipError_t bias_grad_launch(const float* D, long rows, int C, float* part, float* db, hipStream_t st) {
+    if (C > 256) return hipErrorInvalidValue;
+    int nblk = (int)(rows / 4096);
+    if (nblk < 1) nblk = 1;
+    if (nblk > 1024) nblk = 1024;
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nblk), dim3(256), 0, st, D, rows, C, part, nblk);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 63) / 64), dim3(64), 0, st, part, nblk, C, db);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// max-pool 2x2 backward: gradient to the first maximum of each window (TF MaxPoolGrad order)
+__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                                                           float* __restrict__ gx, int B, int H, int W, int C) {
+    const int Ho = H / 2, Wo = W / 2;
+    const size_t total = (size_t)B * H * W * C;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        size_t p = i / C;
+        const int xx = (int)(p % W);
+        p /= W;
+        const int yy = (int)(p % H);
+        const int b = (int)(p / H);
+        const int oy = yy / 2, ox = xx / 2;
+        float g = 0.f;
+        if (oy < Ho && ox < Wo) {
+            const float* base = x + (((size_t)b * H + 2 * oy) * W + 2 * ox) * C + c;
+            const float v0 = base[0], v1 = base[C], v2 = base[(size_t)W * C], v3 = base[(size_t)W * C + C];
+            const float m = fmaxf(fmaxf(v0, v1), fmaxf(v2, v3));
+            const int first = (v0 == m) ? 0 : (v1 == m) ? 1 : (v2 == m) ? 2 : 3;
+            const int mine = (yy - 2 * oy) * 2 + (xx - 2 * ox);
+            if (mine == first) g = gy[(((size_t)b * Ho + oy) * Wo + ox) * C + c];
+        }
+        gx[i] = g;
+    }
+}
+
+hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, hipStream_t st) {
+    const size_t n = (size_t)B * H * W * C;
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C);
+    return hipGetLastError();
+}
+
+// g (+)= scale * (a - b)   (feature-loss gradient; accumulate into an existing gradient)
+__global__ __launch_bounds__(256) void scaled_diff_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                          float scale, float* __restrict__ g, size_t n, int accumulate) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float v = scale * (a[i] - b[i]);
+        g[i] = accumulate ? g[i] + v : v;
+    }
+}
+
+hipError_t scaled_diff_launch(const float* a, const float* b, float scale, float* g, size_t n, int accumulate,
+                              hipStream_t st) {
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(scaled_diff_kernel, dim3(blocks), dim3(256), 0, st, a, b, scale, g, n, accumulate);
+    return hipGetLastError();
+}
+
+// total variation backward: d/dx of factor * (sum |x[y+1]-x[y]| + sum |x[:,x+1]-x[:,x]|), added to g
+__global__ __launch_bounds__(256) void tv_bwd_kernel(const float* __restrict__ x, float factor, float* __restrict__ g,
+                                                     int B, int H, int W, int C) {
+    const size_t total = (size_t)B * H * W * C;
+    auto sgn = [](float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); };
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+        size_t p = i / C;
+        const int xx = (int)(p % W);
+        p /= W;
+        const int yy = (int)(p % H);
+        const float v = x[i];
+        float d = 0.f;
+        const size_t row = (size_t)W * C;
+        if (yy + 1 < H) d -= sgn(x[i + row] - v);
+        if (yy > 0) d += sgn(v - x[i - row]);
+        if (xx + 1 < W) d -= sgn(x[i + C] - v);
+        if (xx > 0) d += sgn(v - x[i - C]);
+        g[i] += factor * d;
+    }
+}
+
+hipError_t tv_bwd_launch(const float* x, float factor, float* g, int B, int H, int W, int C, hipStream_t st) {
+    const size_t n = (size_t)B * H * W * C;
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(tv_bwd_kernel, dim3(blocks), dim3(256), 0, st, x, factor, g, B, H, W, C);
+    return hipGetLastError();
+}
+
+// Gram backward: dF = F (dG + dG^T) / HW = F M with M = 2 coef (Gp - Gs) / HW (symmetric).
+// Written straight into the packed 1x1-conv weight image (gather through a host-built map).
+__global__ __launch_bounds__(256) void gram_bwd_weights_kernel(const float* __restrict__ gp, const float* __restrict__ gs,
+                                                               const int* __restrict__ map, int n_packed, int CC,
+                                                               float scale, float* __restrict__ packed) {
+    const int b = blockIdx.y;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n_packed; i += gridDim.x * 256) {
+        const int m = map[i];
+        packed[(size_t)b * n_packed + i] =
+            m < 0 ? 0.f : scale * (gp[(size_t)b * CC + m] - gs[(size_t)b * CC + m]);
+    }
+}
+
+hipError_t gram_bwd_weights_launch(const float* gp, const float* gs, const int* map, int n_packed, int C, float scale,
+                                   float* packed, int B, hipStream_t st) {
+    hipLaunchKernelGGL(gram_bwd_weights_kernel, dim3((n_packed + 255) / 256, B), dim3(256), 0, st, gp, gs, map,
+                       n_packed, C * C, scale, packed);
+    return hipGetLastError();
+}
+
+// preprocess backward: x_pre[c'] = 255 x[2 - c'] - mean  ->  g_x[c] = 255 g_pre[2 - c]
+__global__ __launch_bounds__(256) void preprocess_bwd_kernel(const float* __restrict__ gpre, float* __restrict__ gx,
+                                                             size_t pixels, int accumulate) {
+    for (size_t p = blockIdx.x * 256ull + threadIdx.x; p < pixels; p += (size_t)gridDim.x * 256) {
+        for (int c = 0; c < 3; ++c) {
+            const float v = 255.f * gpre[p * 3 + (2 - c)];
+            gx[p * 3 + c] = accumulate ? gx[p * 3 + c] + v : v;
+        }
+    }
+}
+
+hipError_t preprocess_bwd_launch(const float* gpre, float* gx, size_t pixels, int accumulate, hipStream_t st) {
+    unsigned blocks = (unsigned)((pixels + 255) / 256);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3(blocks), dim3(256), 0, st, gpre, gx, pixels, accumulate);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// RMSprop (Keras OptimizerV2, centered=False, momentum=0): ms = rho ms + (1-rho) g^2;
+// w -= lr g / (sqrt(ms) + eps)
+__global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ w, float* __restrict__ ms,
+                                                      const float* __restrict__ g, size_t n, float lr, float rho,
+                                                      float eps) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float gi = g[i];
+        const float m = rho * ms[i] + (1.f - rho) * gi * gi;
+        ms[i] = m;
+        w[i] -= lr * gi / (sqrtf(m) + eps);
+    }
+}
+
+hipError_t rmsprop_launch(float* w, float* ms, const float* g, size_t n, float lr, float rho, float eps, hipStream_t st) {
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(256), 0, st, w, ms, g, n, lr, rho, eps);
+    return hipGetLastError();
+}
+
+// packed[i] = map[i] < 0 ? 0 : src[map[i]]  (re-pack canonical weights into kernel stage images)
+__global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ src, const int* __restrict__ map,
+                                                     float* __restrict__ dst, size_t n) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const int m = map[i];
+        dst[i] = m < 0 ? 0.f : src[m];
+    }
+}
+
+hipError_t gather_launch(const float* src, const int* map, float* dst, size_t n, hipStream_t st) {
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(gather_kernel, dim3(blocks), dim3(256), 0, st, src, map, dst, n);
+    return hipGetLastError();
+}
+
+}  // namespace rst
