@@ -118,6 +118,45 @@ int rst_loss_forward(rst_loss_handle* h, const float* prediction, const float* g
 /* Debug: VGG16 conv layer (0..12) output of the most recent run (the prediction). */
 int rst_loss_copy_feature(rst_loss_handle* h, int layer, float* dst, size_t count, int batch, void* stream);
 
+/* ---- Training step (train_network.py:102-138: Keras fit, RMSprop; BASELINE config 4) ----
+ * Replaces StyleTransferTrainingModel.train_step (styleTransferTrainingModel.py:26-29 +
+ * keras Model.train_step) for the transfer network: forward with BatchNorm in training mode
+ * (batch statistics, moving statistics updated with momentum 0.99), the VGG16/Gram loss
+ * (rst_loss_*), the gradient of the batch-summed loss with respect to every transfer weight
+ * (Keras get_weights() order; BN moving statistics get 0) and to the style parameters (the
+ * style predictor's output, styleTransferInferenceModel.py:23-37), and the RMSprop update
+ * (OptimizerV2, momentum 0: ms = rho ms + (1 - rho) g^2; w -= lr g / (sqrt(ms) + eps)).
+ * Gradients land in a caller-owned buffer so data-parallel callers can all-reduce them
+ * (RCCL) before rst_trainer_apply_gradients. Images must have even H, W at every stride-2
+ * level (the reference's configs all do). */
+typedef struct rst_trainer rst_trainer;
+int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t num_weights,
+                       const rst_loss_shape* loss, const float* vgg_weights_host, size_t num_vgg_weights,
+                       rst_trainer** out);
+void rst_trainer_destroy(rst_trainer* t);
+int rst_trainer_num_style_params(const rst_trainer* t);
+size_t rst_trainer_num_weights(const rst_trainer* t);
+/* content (B, in_h, in_w, in_c), style_params (B, 1, P), gt_content / gt_style (B, out_h, out_w, 3).
+ * Writes prediction (B, out_h, out_w, 3), losses (B x 4, as rst_loss_forward), grad (num_weights)
+ * and, when non-NULL, grad_style_params (B, P). All device pointers. */
+int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const float* style_params,
+                                  const float* gt_content, const float* gt_style, int batch, float* prediction,
+                                  float* losses, float* grad, float* grad_style_params, void* stream);
+/* RMSprop on the device-resident weights with gradient grad (num_weights), then re-pack them
+ * into the kernels' weight images. Keras defaults: lr 1e-3, rho 0.9, epsilon 1e-7. */
+int rst_trainer_apply_gradients(rst_trainer* t, const float* grad, float learning_rate, float rho, float epsilon,
+                                void* stream);
+/* Device copies of the current weights (Keras order) / RMSprop slots; set_weights re-packs. */
+int rst_trainer_copy_weights(rst_trainer* t, float* dst, size_t count, void* stream);
+int rst_trainer_copy_slots(rst_trainer* t, float* dst, size_t count, void* stream);
+int rst_trainer_set_weights(rst_trainer* t, const float* src, size_t count, void* stream);
+/* Debug: gradient of the batch loss w.r.t. conv layer `layer`'s activated output (before any skip
+ * add; the last layer's is d loss / d prediction) from the most recent compute_gradients. */
+int rst_trainer_copy_output_gradient(rst_trainer* t, int layer, float* dst, size_t count, int batch, void* stream);
+/* Debug: d loss / d (VGG16 conv `layer` output). The first call for a layer arms the tap (it
+ * allocates; dst may be NULL); later calls copy the value of the most recent compute_gradients. */
+int rst_trainer_debug_vgg_gradient(rst_trainer* t, int layer, float* dst, size_t count, int batch, void* stream);
+
 const char* rst_last_error(void);
 const char* rst_version(void);
 

@@ -1,0 +1,215 @@
+"""CPU oracle of one training step (torch-CPU float64 autograd) — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/`` may import this (it is the checker for ``rst_trainer_*``); the product path
+never does. It restates, in float64 with torch autograd as the differentiator:
+
+* the transfer network in Keras training mode (styleTransfer.py:95-276): BatchNormalization
+  uses the batch's biased moments over (B, H, W) for normalisation and updates the moving
+  statistics with momentum 0.99 and the Bessel-corrected variance (Keras fused batch norm);
+  conditional instance norm uses per-image moments (styleTransfer.py:57-71);
+* the VGG16 / Gram loss without the depth term (styleLoss.py:69-109, 290-369): x*255,
+  RGB->BGR, minus the caffe mean, 13 convs + 4 max-pools, feature loss on block5_conv3,
+  style loss = mean over four Gram layers, total variation (tf.image.total_variation);
+* the gradient of the batch-summed loss (Keras minimises the (B,) loss vector), w.r.t. every
+  trainable transfer weight and the style parameters;
+* RMSprop as Keras OptimizerV2 with momentum 0 (train_network.py:102):
+  ms = rho*ms + (1-rho)*g^2; w -= lr*g/(sqrt(ms)+eps); slots start at zero.
+
+Parity status: the forward pieces are the same restatement as oracle/numpy_ref.py and
+oracle/torch_ref.py (pinned by the golden fixtures and the apply_style_weights KAT);
+the gradients are torch autograd of that restatement, checked against central finite
+differences in tests/test_oracle.py. The reference's own tests pin no training numbers
+("parity unpinned" for the TF training step itself).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .numpy_ref import CONTENT_LAYERS, STYLE_LAYERS, VGG16_LAYERS, VGG_MEAN_BGR, transfer_structure
+from .torch_ref import cin, conv2d_same, conv2d_transpose_same
+
+BN_MOMENTUM = 0.99
+BN_EPS = 1e-3
+
+
+def transfer_forward_train(content, style_params, w: Sequence[torch.Tensor], blocks, bn_mode="train", taps=None):
+    """content NCHW float64; style_params (B, P); w in Keras get_weights() order.
+
+    Returns (prediction NCHW, list of (mean, unbiased var) per BatchNorm layer). With ``taps``
+    (a list), every conv layer's activated output (before a skip add) is appended with
+    ``retain_grad`` so its gradient can be read after backward."""
+    x = content
+    off = 0
+    wi = iter(w)
+    bn_stats = []
+
+    def tap(t):
+        if taps is not None and t.requires_grad:
+            t.retain_grad()
+            taps.append(t)
+        return t
+
+    for kind, k, s, f in blocks:
+        if kind == 'contract':
+            kw, b, g, be, mm, mv = (next(wi) for _ in range(6))
+            x = F.relu(conv2d_same(x, kw, b, s))
+            if bn_mode == "train":
+                mean = x.mean(dim=(0, 2, 3))
+                var = ((x - mean.view(1, -1, 1, 1)) ** 2).mean(dim=(0, 2, 3))
+                n = x.shape[0] * x.shape[2] * x.shape[3]
+                bn_stats.append((mean.detach(), var.detach() * n / max(n - 1, 1)))
+            else:
+                mean, var = mm, mv
+            inv = torch.rsqrt(var + BN_EPS)
+            x = (x - mean.view(1, -1, 1, 1)) * inv.view(1, -1, 1, 1) * g.view(1, -1, 1, 1) + be.view(1, -1, 1, 1)
+            x = tap(F.relu(x))
+        elif kind.startswith('residual'):
+            inp = x
+            for j in range(2):
+                kw, b = next(wi), next(wi)
+                x = F.relu(conv2d_same(x, kw, b, 1))
+                scale = style_params[:, off:off + f].reshape(-1, f, 1, 1)
+                bias = style_params[:, off + f:off + 2 * f].reshape(-1, f, 1, 1)
+                off += 2 * f
+                x = cin(x, scale, bias)
+                if j == 0:
+                    x = F.relu(x)
+                x = tap(x)
+            if kind != 'residual_first':
+                x = inp + x
+        else:
+            kw, b = next(wi), next(wi)
+            x = conv2d_transpose_same(x, kw, b, s)
+            scale = style_params[:, off:off + f].reshape(-1, f, 1, 1)
+            bias = style_params[:, off + f:off + 2 * f].reshape(-1, f, 1, 1)
+            off += 2 * f
+            x = cin(x, scale, bias)
+            x = tap(torch.sigmoid(x) if kind == 'expand_last' else F.relu(x))
+    return x, bn_stats
+
+
+def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None) -> Dict[str, torch.Tensor]:
+    """StyleLossModelVGG.call (styleLoss.py:106-109) on NCHW float64 images in [0, 1].
+    ``taps``: list receiving every conv output (retain_grad) when the input requires grad."""
+    x = images01 * 255.0
+    mean = torch.tensor(VGG_MEAN_BGR, dtype=x.dtype).view(1, 3, 1, 1)
+    x = x.flip(1) - mean
+    feats = {}
+    i = 0
+    for entry in VGG16_LAYERS:
+        if entry[0] == 'pool':
+            x = F.max_pool2d(x, 2)
+            continue
+        name = entry[0]
+        x = F.relu(conv2d_same(x, vgg[2 * i], vgg[2 * i + 1], 1))
+        i += 1
+        if taps is not None and x.requires_grad:
+            x.retain_grad()
+            taps.append(x)
+        if name in STYLE_LAYERS or name in CONTENT_LAYERS:
+            feats[name] = x
+        if name == CONTENT_LAYERS[0]:
+            break
+    return feats
+
+
+def _gram(f):
+    B, C, H, W = f.shape
+    f2 = f.reshape(B, C, H * W)
+    return torch.bmm(f2, f2.transpose(1, 2)) / (H * W)
+
+
+def _mean_l2(t):
+    return (0.5 * t ** 2).reshape(t.shape[0], -1).mean(dim=1)
+
+
+def style_losses(pred, content, style, vgg, content_factor=1e4, style_factor=1e-3, tv_factor=1e-1, taps=None):
+    """make_style_loss_function without depth (styleLoss.py:295-369) -> (B, 4) [loss, feature, style, tv]."""
+    fp, fc, fs = vgg_features(pred, vgg, taps), vgg_features(content, vgg), vgg_features(style, vgg)
+    feature = torch.stack([_mean_l2(fp[n] - fc[n]) for n in CONTENT_LAYERS]).mean(0) * content_factor
+    style_l = torch.stack([_mean_l2(_gram(fp[n]) - _gram(fs[n])) for n in STYLE_LAYERS]).mean(0) * style_factor
+    tv = ((pred[:, :, 1:, :] - pred[:, :, :-1, :]).abs().sum(dim=(1, 2, 3)) +
+          (pred[:, :, :, 1:] - pred[:, :, :, :-1]).abs().sum(dim=(1, 2, 3))) * tv_factor
+    return torch.stack([feature + style_l + tv, feature, style_l, tv], dim=1)
+
+
+def _nchw(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float64)).permute(0, 3, 1, 2)
+
+
+def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarray], content, style_params,
+                  gt_content, gt_style, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
+                  factors=(1e4, 1e-3, 1e-1), ms: Optional[Sequence[np.ndarray]] = None,
+                  lr=1e-3, rho=0.9, eps=1e-7) -> Dict[str, object]:
+    """One Keras train_step: forward (BN training mode), loss, gradients, RMSprop.
+
+    Inputs are NHWC numpy; returns numpy: prediction (B,H,W,3), losses (B,4), grads (Keras order;
+    zeros for the BN moving statistics), grad_style_params (B,P), weights after the update
+    (moving statistics updated by the forward), ms (RMSprop slots after the update)."""
+    blocks, P = transfer_structure(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters)
+    w = [torch.tensor(np.asarray(a, np.float64), requires_grad=True) for a in weights]
+    vgg = [torch.tensor(np.asarray(a, np.float64)) for a in vgg_weights]
+    sp = torch.tensor(np.asarray(style_params, np.float64).reshape(len(content), P), requires_grad=True)
+    gts = np.asarray(gt_style)
+    if gts.ndim == 5:
+        gts = gts[:, 0]
+    taps = []
+    pred, bn_stats = transfer_forward_train(_nchw(content), sp, w, blocks, taps=taps)
+    vtaps = []
+    losses = style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors, taps=vtaps)
+    losses[:, 0].sum().backward()
+    # Keras trainable set: conv kernels/biases, BN gamma/beta (moving statistics are not trained)
+    grads, new_w, new_ms = [], [], []
+    trainable = []
+    for kind, k, s, f in blocks:
+        n = 6 if kind == 'contract' else (4 if kind.startswith('residual') else 2)
+        trainable += [not (kind == 'contract' and j >= 4) for j in range(n)]
+    bn_i = 0
+    ms = [np.zeros_like(np.asarray(a, np.float64)) for a in weights] if ms is None else \
+        [np.asarray(m, np.float64) for m in ms]
+    for i, (t, tr) in enumerate(zip(w, trainable)):
+        g = t.grad.detach().numpy() if (tr and t.grad is not None) else np.zeros(t.shape)
+        grads.append(g)
+        m = rho * ms[i] + (1.0 - rho) * g * g
+        new_ms.append(m)
+        new_w.append(t.detach().numpy() - lr * g / (np.sqrt(m) + eps))
+    # moving statistics (contract blocks: weights 4 and 5 of each 6-group)
+    i = 0
+    for kind, k, s, f in blocks:
+        if kind == 'contract':
+            mean, var = bn_stats[bn_i]
+            bn_i += 1
+            new_w[i + 4] = BN_MOMENTUM * np.asarray(weights[i + 4], np.float64) + (1 - BN_MOMENTUM) * mean.numpy()
+            new_w[i + 5] = BN_MOMENTUM * np.asarray(weights[i + 5], np.float64) + (1 - BN_MOMENTUM) * var.numpy()
+            i += 6
+        else:
+            i += 4 if kind.startswith('residual') else 2
+    return {
+        'prediction': pred.detach().permute(0, 2, 3, 1).numpy(),
+        'losses': losses.detach().numpy(),
+        'grads': grads,
+        'grad_style_params': sp.grad.detach().numpy(),
+        'weights': new_w,
+        'ms': new_ms,
+        'output_grads': [t.grad.detach().permute(0, 2, 3, 1).numpy() for t in taps],
+        'vgg_grads': [t.grad.detach().permute(0, 2, 3, 1).numpy() for t in vtaps],
+    }
+
+
+def loss_of(weights, vgg_weights, content, style_params, gt_content, gt_style, input_shape, output_shape,
+            bottleneck_res_y, bottleneck_num_filters, factors=(1e4, 1e-3, 1e-1)) -> float:
+    """Batch-summed training-mode loss (finite-difference checks of the oracle's gradients)."""
+    blocks, P = transfer_structure(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters)
+    with torch.no_grad():
+        w = [torch.tensor(np.asarray(a, np.float64)) for a in weights]
+        vgg = [torch.tensor(np.asarray(a, np.float64)) for a in vgg_weights]
+        sp = torch.tensor(np.asarray(style_params, np.float64).reshape(len(content), P))
+        gts = np.asarray(gt_style)
+        if gts.ndim == 5:
+            gts = gts[:, 0]
+        pred, _ = transfer_forward_train(_nchw(content), sp, w, blocks)
+        return float(style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors)[:, 0].sum())

@@ -25,6 +25,10 @@ EXPORTED_SYMBOLS = [
     "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_last_error", "rst_version",
     "rst_profile_begin", "rst_profile_end", "rst_layer_kernel_id",
     "rst_loss_num_weights", "rst_loss_create", "rst_loss_destroy", "rst_loss_forward", "rst_loss_copy_feature",
+    "rst_trainer_create", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
+    "rst_trainer_compute_gradients", "rst_trainer_apply_gradients", "rst_trainer_copy_weights",
+    "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_copy_output_gradient",
+    "rst_trainer_debug_vgg_gradient",
 ]
 
 
@@ -99,6 +103,26 @@ def load() -> ctypes.CDLL:
     lib.rst_loss_forward.restype = i
     lib.rst_loss_copy_feature.argtypes = [vp, i, vp, sz, i, vp]
     lib.rst_loss_copy_feature.restype = i
+    lib.rst_trainer_create.argtypes = [ctypes.POINTER(RstShape), vp, sz, ctypes.POINTER(RstLossShape), vp, sz,
+                                       ctypes.POINTER(vp)]
+    lib.rst_trainer_create.restype = i
+    lib.rst_trainer_destroy.argtypes = [vp]
+    lib.rst_trainer_destroy.restype = None
+    lib.rst_trainer_num_style_params.argtypes = [vp]
+    lib.rst_trainer_num_style_params.restype = i
+    lib.rst_trainer_num_weights.argtypes = [vp]
+    lib.rst_trainer_num_weights.restype = sz
+    lib.rst_trainer_compute_gradients.argtypes = [vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp]
+    lib.rst_trainer_compute_gradients.restype = i
+    lib.rst_trainer_apply_gradients.argtypes = [vp, vp, fp, fp, fp, vp]
+    lib.rst_trainer_apply_gradients.restype = i
+    for name in ("rst_trainer_copy_weights", "rst_trainer_copy_slots", "rst_trainer_set_weights"):
+        getattr(lib, name).argtypes = [vp, vp, sz, vp]
+        getattr(lib, name).restype = i
+    lib.rst_trainer_copy_output_gradient.argtypes = [vp, i, vp, sz, i, vp]
+    lib.rst_trainer_copy_output_gradient.restype = i
+    lib.rst_trainer_debug_vgg_gradient.argtypes = [vp, i, vp, sz, i, vp]
+    lib.rst_trainer_debug_vgg_gradient.restype = i
     lib.rst_last_error.argtypes = []
     lib.rst_last_error.restype = ctypes.c_char_p
     lib.rst_version.argtypes = []

@@ -200,7 +200,12 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
         return iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
     };
     auto transform4 = [&](float4 v, float4 r, int c, size_t gi, int iy, int ix) __attribute__((always_inline)) {
-        if (pro != PRO_NONE) {
+        if (pro == PRO_MASK) {   // no affine table (Cin may exceed MAX_CIN here)
+            v.x = r.x > 0.f ? v.x : 0.f;
+            v.y = r.y > 0.f ? v.y : 0.f;
+            v.z = r.z > 0.f ? v.z : 0.f;
+            v.w = r.w > 0.f ? v.w : 0.f;
+        } else if (pro != PRO_NONE) {
             v.x = apply_pro(pro, v.x, pab[c + 0], r.x);
             v.y = apply_pro(pro, v.y, pab[c + 1], r.y);
             v.z = apply_pro(pro, v.z, pab[c + 2], r.z);
@@ -244,8 +249,10 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                 if (pixel_of(hp, iy, ix) && c < Cin) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
                     v = a.in[gi];
-                    if (pro != PRO_NONE) {
-                        const float r = (pro == PRO_AFF_RES || pro == PRO_MASK) ? a.res[gi] : 0.f;
+                    if (pro == PRO_MASK) {
+                        v = a.res[gi] > 0.f ? v : 0.f;
+                    } else if (pro != PRO_NONE) {
+                        const float r = pro == PRO_AFF_RES ? a.res[gi] : 0.f;
                         v = apply_pro(pro, v, pab[c], r);
                         if (do_mat && iy >= y0 * S && iy < (y0 + TH) * S && ix >= x0 * S && ix < (x0 + TW) * S) a.mat[gi] = v;
                     }

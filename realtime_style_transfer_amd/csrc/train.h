@@ -44,7 +44,8 @@ size_t wgrad_slab_bytes(const WgradArgs& a);
 hipError_t wgrad_launch(WgradArgs a, hipStream_t st);
 hipError_t bias_grad_launch(const float* D, long rows, int C, float* part, float* db, hipStream_t st);
 
-hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, hipStream_t st);
+hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, int accumulate,
+                               hipStream_t st);
 hipError_t scaled_diff_launch(const float* a, const float* b, float scale, float* g, size_t n, int accumulate,
                               hipStream_t st);
 hipError_t tv_bwd_launch(const float* x, float factor, float* g, int B, int H, int W, int C, hipStream_t st);

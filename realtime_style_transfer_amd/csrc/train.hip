@@ -326,7 +326,8 @@ hipError_t bias_grad_launch(const float* D, long rows, int C, float* part, float
 // ---------------------------------------------------------------------------------------------
 // max-pool 2x2 backward: gradient to the first maximum of each window (TF MaxPoolGrad order)
 __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gy,
-                                                           float* __restrict__ gx, int B, int H, int W, int C) {
+                                                           float* __restrict__ gx, int B, int H, int W, int C,
+                                                           int accumulate) {
     const int Ho = H / 2, Wo = W / 2;
     const size_t total = (size_t)B * H * W * C;
     for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
@@ -346,15 +347,16 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restri
             const int mine = (yy - 2 * oy) * 2 + (xx - 2 * ox);
             if (mine == first) g = gy[(((size_t)b * Ho + oy) * Wo + ox) * C + c];
         }
-        gx[i] = g;
+        gx[i] = accumulate ? gx[i] + g : g;
     }
 }
 
-hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, hipStream_t st) {
+hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, int accumulate,
+                               hipStream_t st) {
     const size_t n = (size_t)B * H * W * C;
     unsigned blocks = (unsigned)((n + 255) / 256);
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C);
+    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C, accumulate);
     return hipGetLastError();
 }
 

@@ -1,0 +1,246 @@
+"""Host mirror of ``realtime_style_transfer/models/styleTransferTrainingModel.py`` and of the
+training loop body of ``train_network.py:102-138`` on librst (MI355X).
+
+``StyleTransferTrainingModel`` owns one ``rst_trainer`` (include/rst.h): the transfer network's
+weights and RMSprop slots live on the GPU; one ``train_step`` runs the training-mode forward,
+the VGG16/Gram loss (``StyleLossModelVGG`` factors), the backward and the RMSprop update
+entirely in hand-written gfx950 kernels. There is no CPU fallback.
+
+Deviations, by construction of this build:
+
+* The style predictor (MobileNetV3Small, stylePrediction.py:25-75) is a separate, not yet
+  built component: ``style_params`` are an input of ``train_step`` and
+  their gradient is returned so a predictor can be chained in front.
+* ``compute_loss`` returns the per-image ``(B,)`` loss; Keras minimises its sum, and so does this.
+* Data parallel: with ``process_group`` set, the gradients are all-reduced (SUM, RCCL over xGMI)
+  before the update, which equals one step on the concatenated global batch except that the
+  BatchNorm statistics stay per rank (as TF without SyncBatchNorm would).
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .plan import Plan, init_weights, network_plan
+from .styleLoss import StyleLossModelVGG, make_style_loss_function
+from .styleTransfer import StyleTransferModel
+
+log = logging.getLogger(__name__)
+
+LOSS_NAMES = ('loss', 'feature_loss', 'style_loss', 'total_variation_loss')
+
+
+class RMSprop:
+    """Keras ``tf.keras.optimizers.RMSprop()`` defaults (train_network.py:102)."""
+
+    def __init__(self, learning_rate: float = 1e-3, rho: float = 0.9, momentum: float = 0.0, epsilon: float = 1e-7,
+                 centered: bool = False):
+        if momentum != 0.0 or centered:
+            raise NotImplementedError("RMSprop with momentum or centered=True is not used by the reference")
+        self.learning_rate, self.rho, self.epsilon = float(learning_rate), float(rho), float(epsilon)
+
+
+class StyleTransferTrainingModel:
+    """styleTransferTrainingModel.py:11-36 + Keras train_step, one GPU (one librst trainer)."""
+
+    def __init__(self, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
+                 loss_model: Optional[StyleLossModelVGG] = None, weights: Optional[Sequence[np.ndarray]] = None,
+                 seed: int = 2, max_batch: int = 4, optimizer: Optional[RMSprop] = None, process_group=None,
+                 device=None, name: str = "StyleTransferTrainingModel"):
+        self.name = name
+        self.plan: Plan = network_plan(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, 1)
+        self.input_shape = tuple(int(v) for v in input_shape)
+        self.output_shape = tuple(int(v) for v in output_shape)
+        self.max_batch = int(max_batch)
+        self.num_style_parameters = self.plan.num_style_params
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.optimizer = optimizer or RMSprop()
+        self.process_group = process_group
+        self.loss_model = loss_model or StyleLossModelVGG(self.output_shape, max_batch=self.max_batch,
+                                                          device=self.device)
+        if tuple(self.loss_model.input_shape) != self.output_shape:
+            raise ValueError(f"loss model input {self.loss_model.input_shape} != output shape {self.output_shape}")
+        self._shapes = [tuple(s) for s in self.plan.weight_shapes()]
+        self._sizes = [int(np.prod(s)) for s in self._shapes]
+        w = weights if weights is not None else init_weights(self.plan, seed)
+        flat = self._flatten(w)
+        lib = _lib.load()
+        H, W, C = self.input_shape
+        shape = _lib.RstShape(H, W, C, self.output_shape[0], self.output_shape[1], self.plan.bottleneck_res_y,
+                              self.plan.bottleneck_num_filters, 1, self.max_batch)
+        lm = self.loss_model
+        lshape = _lib.RstLossShape(self.output_shape[0], self.output_shape[1], self.max_batch,
+                                   lm.content_loss_factor, lm.style_loss_factor, lm.total_variation_loss_factor)
+        vgg = np.concatenate([a.reshape(-1) for a in lm.weights]).astype(np.float32)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(lib.rst_trainer_create(ctypes.byref(shape), flat.ctypes.data, flat.size, ctypes.byref(lshape),
+                                              vgg.ctypes.data, vgg.size, ctypes.byref(h)))
+        self._handle = h
+        self.num_weights = int(lib.rst_trainer_num_weights(h))
+        if self.num_weights != flat.size or lib.rst_trainer_num_style_params(h) != self.num_style_parameters:
+            raise RuntimeError("librst trainer plan disagrees with the host plan")
+        self._grad = torch.zeros(self.num_weights, dtype=torch.float32, device=self.device)
+        self.style_losses: Dict[str, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ lifecycle
+    def _flatten(self, weights: Sequence[np.ndarray]) -> np.ndarray:
+        if len(weights) != len(self._shapes) or any(tuple(np.shape(w)) != s for w, s in zip(weights, self._shapes)):
+            raise ValueError(f"weights do not match the network plan: expected {self._shapes}")
+        return np.concatenate([np.asarray(w, np.float32).reshape(-1) for w in weights])
+
+    def _unflatten(self, flat: np.ndarray) -> List[np.ndarray]:
+        out, o = [], 0
+        for s, n in zip(self._shapes, self._sizes):
+            out.append(flat[o:o + n].reshape(s).copy())
+            o += n
+        return out
+
+    def __del__(self):
+        try:
+            if getattr(self, '_handle', None) is not None:
+                _lib.load().rst_trainer_destroy(self._handle)
+                self._handle = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ Keras-like API
+    def get_weights(self) -> List[np.ndarray]:
+        t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
+        _lib.check(_lib.load().rst_trainer_copy_weights(self._handle, _lib.dev_ptr(t), t.numel(), _lib.stream_ptr()))
+        return self._unflatten(t.cpu().numpy())
+
+    def set_weights(self, weights: Sequence[np.ndarray]):
+        t = torch.from_numpy(self._flatten(weights)).to(self.device)
+        _lib.check(_lib.load().rst_trainer_set_weights(self._handle, _lib.dev_ptr(t), t.numel(), _lib.stream_ptr()))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def optimizer_slots(self) -> List[np.ndarray]:
+        """RMSprop ``rms`` slots in weight order."""
+        t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
+        _lib.check(_lib.load().rst_trainer_copy_slots(self._handle, _lib.dev_ptr(t), t.numel(), _lib.stream_ptr()))
+        return self._unflatten(t.cpu().numpy())
+
+    def output_gradient(self, idx: int, batch: int) -> torch.Tensor:
+        """Debug: d loss / d (activated output of conv layer idx) of the most recent step."""
+        layer = self.plan.layers[idx]
+        t = torch.empty((batch,) + tuple(layer.out_hw) + (layer.cout,), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.load().rst_trainer_copy_output_gradient(self._handle, idx, _lib.dev_ptr(t), t.numel(), batch,
+                                                                _lib.stream_ptr()))
+        return t
+
+    def _check(self, content, style_params, gt_content, gt_style):
+        B = content.shape[0]
+        if tuple(content.shape) != (B,) + self.input_shape:
+            raise ValueError(f"content must be (B,{self.input_shape}), got {tuple(content.shape)}")
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} exceeds max_batch={self.max_batch}")
+        sp = style_params.reshape(B, -1) if style_params.dim() == 3 and style_params.shape[1] == 1 else style_params
+        if tuple(sp.shape) != (B, self.num_style_parameters):
+            raise ValueError(f"style_params must be (B,1,{self.num_style_parameters}), got {tuple(style_params.shape)}")
+        if gt_style.dim() == 5:
+            if gt_style.shape[1] != 1:   # styleLoss.py:311-312
+                raise ValueError(f"Loss model does not support multiple styles. Found {gt_style.shape[1]}")
+            gt_style = gt_style[:, 0]
+        for t in (gt_content, gt_style):
+            if tuple(t.shape) != (B,) + self.output_shape:
+                raise ValueError(f"ground truth must be (B,{self.output_shape}), got {tuple(t.shape)}")
+        return B, content.contiguous(), sp.contiguous(), gt_content.contiguous(), gt_style.contiguous()
+
+    def compute_gradients(self, content: torch.Tensor, style_params: torch.Tensor, gt_content: torch.Tensor,
+                          gt_style: torch.Tensor, grad: Optional[torch.Tensor] = None,
+                          grad_style_params: Optional[torch.Tensor] = None):
+        """Training-mode forward + loss + backward -> (prediction, losses (B,4), grad, grad_style_params)."""
+        B, content, sp, gt_content, gt_style = self._check(content, style_params, gt_content, gt_style)
+        dev = content.device
+        pred = torch.empty((B,) + self.output_shape, dtype=torch.float32, device=dev)
+        losses = torch.empty((B, 4), dtype=torch.float32, device=dev)
+        grad = self._grad if grad is None else grad
+        if grad_style_params is None:
+            grad_style_params = torch.empty((B, self.num_style_parameters), dtype=torch.float32, device=dev)
+        _lib.check(_lib.load().rst_trainer_compute_gradients(
+            self._handle, _lib.dev_ptr(content), _lib.dev_ptr(sp), _lib.dev_ptr(gt_content), _lib.dev_ptr(gt_style),
+            B, _lib.dev_ptr(pred), _lib.dev_ptr(losses), _lib.dev_ptr(grad), _lib.dev_ptr(grad_style_params),
+            _lib.stream_ptr()))
+        return pred, losses, grad, grad_style_params
+
+    def apply_gradients(self, grad: torch.Tensor):
+        o = self.optimizer
+        _lib.check(_lib.load().rst_trainer_apply_gradients(self._handle, _lib.dev_ptr(grad), o.learning_rate, o.rho,
+                                                           o.epsilon, _lib.stream_ptr()))
+
+    def compute_loss(self, x=None, y=None, y_pred=None, sample_weight=None):
+        """styleTransferTrainingModel.py:26-29: the (B,) 'loss' of the most recent step."""
+        return self.style_losses['loss']
+
+    def compute_metrics(self, x=None, y=None, y_pred=None, sample_weight=None) -> Dict[str, torch.Tensor]:
+        """styleTransferTrainingModel.py:31-33: batch means of every loss term."""
+        return {n: l.mean() for n, l in self.style_losses.items()}
+
+    def reset_metrics(self):
+        self.style_losses = {}
+
+    def train_step(self, x: Dict[str, torch.Tensor], y: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """One Keras fit step: x = {'content', 'style_params'}, y = {'content', 'style'}."""
+        pred, losses, grad, gsp = self.compute_gradients(x['content'], x['style_params'], y['content'], y['style'])
+        if self.process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()
+                                              and torch.distributed.get_world_size() > 1):
+            # one bucket: the whole ~5.9 MB gradient in a single RCCL all-reduce over xGMI
+            torch.distributed.all_reduce(grad, op=torch.distributed.ReduceOp.SUM, group=self.process_group)
+        self.apply_gradients(grad)
+        self.style_losses = {n: losses[:, i] for i, n in enumerate(LOSS_NAMES)}
+        self.last_prediction = pred
+        self.last_grad_style_params = gsp
+        return self.compute_metrics()
+
+    def transfer_model(self, max_batch: Optional[int] = None) -> StyleTransferModel:
+        """An inference ``StyleTransferModel`` holding the current weights (BN in inference mode)."""
+        return StyleTransferModel(self.input_shape, self.output_shape, self.plan.bottleneck_res_y,
+                                  self.plan.bottleneck_num_filters, 1, weights=self.get_weights(),
+                                  max_batch=max_batch or self.max_batch, device=self.device)
+
+
+class StyleTransferModels:
+    """The object make_style_transfer_training_model returns (styleTransferTrainingModel.py:60-68)."""
+
+    def __init__(self, training: StyleTransferTrainingModel, loss_model):
+        self.training = training
+        self.loss_model = loss_model
+        self.style_predictor = None
+        self.transfer = training.transfer_model()
+
+        def inference(inputs: Dict[str, torch.Tensor]) -> torch.Tensor:
+            return self.transfer(inputs)
+
+        self.inference = inference
+
+
+def make_style_transfer_training_model(style_predictor_factory_func: Optional[Callable],
+                                       style_transfer_factory_func: Callable,
+                                       style_loss_func_factory_func: Callable,
+                                       name="StyleTransferTrainingModel", max_batch: int = 4,
+                                       optimizer: Optional[RMSprop] = None, process_group=None):
+    """styleTransferTrainingModel.py:39-70 on librst.
+
+    ``style_transfer_factory_func() -> (StyleTransferModel, P)`` supplies the architecture and
+    initial weights; ``style_loss_func_factory_func() -> (compute_loss, StyleLossModelVGG)``
+    supplies the loss model. The style predictor is not built yet: pass None and
+    feed ``style_params`` directly."""
+    if style_predictor_factory_func is not None:
+        raise NotImplementedError("the MobileNetV3 style predictor is not built yet; pass None and feed style_params")
+    transfer, _ = style_transfer_factory_func()
+    _, loss_model = style_loss_func_factory_func()
+    training = StyleTransferTrainingModel(transfer.input_shape, transfer.output_shape, transfer.plan.bottleneck_res_y,
+                                          transfer.plan.bottleneck_num_filters, loss_model=loss_model,
+                                          weights=transfer.get_weights(), max_batch=max_batch, optimizer=optimizer,
+                                          process_group=process_group, device=transfer.device, name=name)
+    return StyleTransferModels(training, loss_model)
+
+
+__all__ = ['RMSprop', 'StyleTransferTrainingModel', 'StyleTransferModels', 'make_style_transfer_training_model',
+           'make_style_loss_function']

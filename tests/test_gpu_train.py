@@ -1,0 +1,216 @@
+"""GPU parity of the training step (rst_trainer_*, librst) against the float64 autograd oracle.
+
+Config A uses the production kernel shapes of rst-960-120-128-17 at a small frame (17 input
+channels, 128 bottleneck filters); config B upsamples (output 2x the input, like the
+reference's training-model test geometry, styleTransferTrainingModelTest.py:15-20) with
+few filters. Tolerances (float32 GPU vs float64 oracle):
+  prediction max-abs 2e-5; per-image losses rel 1e-4;
+  every gradient tensor: max-abs error <= 2e-3 x that tensor's max |ref| (biases feeding an
+  instance norm are mathematically zero: there |g| <= 1e-5 x the layer's kernel-gradient scale);
+  style-parameter gradients 2e-3 x max |ref|;
+  after RMSprop: weights 1e-6 abs where |g_ref| > 1e-2 max|g_ref| of the tensor (elsewhere the
+  first RMSprop step is lr*sign(g)/sqrt(1-rho) and only its size is checked), slots rel 5e-3.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {
+    'A': dict(input_shape=(32, 64, 17), output_shape=(32, 64, 3), bottleneck_res_y=8, bottleneck_num_filters=128),
+    'B': dict(input_shape=(16, 32, 3), output_shape=(32, 64, 3), bottleneck_res_y=4, bottleneck_num_filters=4),
+}
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out')
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _case(cfg, B, seed=5):
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.styleLoss import init_vgg16_weights
+    plan = network_plan(cfg['input_shape'], cfg['output_shape'], cfg['bottleneck_res_y'], cfg['bottleneck_num_filters'])
+    w = init_weights(plan, seed=2)
+    vgg = init_vgg16_weights(seed=3)
+    rng = np.random.default_rng(seed)
+    content = rng.random((B,) + cfg['input_shape']).astype(np.float32)
+    sp = synthetic_style_params(B, 1, plan.num_style_params, plan, seed=1)
+    gtc = rng.random((B,) + cfg['output_shape']).astype(np.float32)
+    gts = rng.random((B, 1) + cfg['output_shape']).astype(np.float32)
+    return plan, w, vgg, content, sp, gtc, gts
+
+
+def _trainer(cfg, w, vgg, B):
+    from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
+    from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
+    lm = StyleLossModelVGG(cfg['output_shape'], weights=vgg, max_batch=B)
+    return StyleTransferTrainingModel(cfg['input_shape'], cfg['output_shape'], cfg['bottleneck_res_y'],
+                                      cfg['bottleneck_num_filters'], loss_model=lm, weights=w, max_batch=B)
+
+
+def _cuda(*arrs):
+    return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+@pytest.mark.parametrize("name", ["A", "B"])
+def test_training_step_matches_oracle(name):
+    _need_gpu()
+    from oracle import torch_train as T
+    cfg = CONFIGS[name]
+    B = 2
+    plan, w, vgg, content, sp, gtc, gts = _case(cfg, B)
+    ref = T.training_step(w, vgg, content, sp, gtc, gts, **cfg)
+    tr = _trainer(cfg, w, vgg, B)
+    c, s, gc, gs = _cuda(content, sp, gtc, gts)
+    pred, losses, grad, gsp = tr.compute_gradients(c, s, gc, gs)
+    torch.cuda.synchronize()
+    report = {}
+    perr = float(np.abs(pred.cpu().numpy() - ref['prediction']).max())
+    report['prediction_max_abs'] = perr
+    lrel = float((np.abs(losses.cpu().numpy() - ref['losses']) / np.abs(ref['losses'])).max())
+    report['loss_rel'] = lrel
+    grads = tr._unflatten(grad.cpu().numpy())
+    gerr = float(np.abs(gsp.cpu().numpy() - ref['grad_style_params']).max() / np.abs(ref['grad_style_params']).max())
+    report['style_grad_rel'] = gerr
+    og = []
+    for li in range(len(plan.layers) - 1, -1, -1):
+        r = ref['output_grads'][li]
+        g = tr.output_gradient(li, B).cpu().numpy()
+        og.append((plan.layers[li].name, float(np.abs(g - r).max() / np.abs(r).max())))
+    report['output_grad_rel'] = og
+    worst = []
+    failures = []
+    # kernel-gradient scale per layer (for the mathematically-zero biases before an instance norm)
+    layer_of = []
+    for layer in plan.layers:
+        layer_of += [layer] * len(layer.weight_shapes)
+    for i, (g, r) in enumerate(zip(grads, ref['grads'])):
+        layer = layer_of[i]
+        first = sum(len(l.weight_shapes) for l in plan.layers[:plan.layers.index(layer)])
+        kscale = np.abs(ref['grads'][first]).max()
+        err = float(np.abs(g - r).max())
+        scale = float(np.abs(r).max())
+        # a bias feeding an instance norm (directly, or through a ReLU that never clips) has zero gradient
+        zero_bias = (i == first + 1) and layer.norm == 'cin' and scale <= 1e-9 * kscale
+        if zero_bias:
+            worst.append((layer.name + '/bias(zero)', float(np.abs(g).max() / kscale)))
+            if not np.abs(g).max() <= 1e-5 * kscale:
+                failures.append((layer.name, 'zero-bias', float(np.abs(g).max()), float(kscale)))
+        elif scale == 0.0:
+            if g.any():
+                failures.append((layer.name, i - first, 'moving statistics got a gradient'))
+        else:
+            worst.append((f"{layer.name}/{i - first}", err / scale))
+            if not err <= 2e-3 * scale:
+                failures.append((layer.name, i - first, err, scale))
+    report['grad_rel'] = worst
+    report['failures'] = failures
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f'train_parity_{name}.json'), 'w') as f:
+        json.dump(report, f, indent=1, default=float)
+    assert not failures, failures
+    # moving statistics are updated by the forward (read back before the optimizer step)
+    w_after_fwd = tr.get_weights()
+    for i, layer in enumerate(layer_of):
+        first = sum(len(l.weight_shapes) for l in plan.layers[:plan.layers.index(layer)])
+        if layer.norm == 'bn' and i - first in (4, 5):
+            np.testing.assert_allclose(w_after_fwd[i], ref['weights'][i], rtol=1e-5, atol=1e-6)
+    # RMSprop
+    tr.apply_gradients(grad)
+    new_w = tr.get_weights()
+    slots = tr.optimizer_slots()
+    for i, (a, r, g) in enumerate(zip(new_w, ref['weights'], ref['grads'])):
+        if not np.abs(g).max():
+            continue
+        strong = np.abs(g) > 1e-2 * np.abs(g).max()
+        assert np.abs(a - r)[strong].max() <= 1e-6 + 1e-6 * np.abs(r).max(), (i, np.abs(a - r)[strong].max())
+        assert np.abs(a - np.asarray(w[i], np.float64)).max() <= 1e-3 / np.sqrt(0.1) * 1.001 + 1e-6
+        np.testing.assert_allclose(slots[i][strong], ref['ms'][i][strong], rtol=5e-3)
+    assert perr < 2e-5, perr
+    assert lrel < 1e-4, lrel
+    assert gerr < 2e-3, gerr
+
+
+def test_training_step_is_deterministic_and_learns():
+    _need_gpu()
+    cfg = CONFIGS['A']
+    B = 2
+    plan, w, vgg, content, sp, gtc, gts = _case(cfg, B)
+    tr = _trainer(cfg, w, vgg, B)
+    c, s, gc, gs = _cuda(content, sp, gtc, gts)
+    _, l1, g1, s1 = tr.compute_gradients(c, s, gc, gs)
+    g1, s1, l1 = g1.clone(), s1.clone(), l1.clone()
+    _, l2, g2, s2 = tr.compute_gradients(c, s, gc, gs)
+    assert torch.equal(g1, g2) and torch.equal(s1, s2) and torch.equal(l1, l2)   # no atomics anywhere
+    first = None
+    for _ in range(5):
+        m = tr.train_step({'content': c, 'style_params': s}, {'content': gc, 'style': gs})
+        first = first if first is not None else float(m['loss'])
+    last = float(tr.compute_metrics()['loss'])
+    assert last < first, (first, last)
+
+
+def test_trainer_rejects_bad_shapes():
+    _need_gpu()
+    from realtime_style_transfer_amd._lib import RstError
+    cfg = CONFIGS['B']
+    plan, w, vgg, content, sp, gtc, gts = _case(cfg, 1)
+    tr = _trainer(cfg, w, vgg, 1)
+    c, s, gc, gs = _cuda(content, sp, gtc, gts)
+    with pytest.raises(ValueError):
+        tr.compute_gradients(torch.cat([c, c]), s, gc, gs)            # batch > max_batch
+    with pytest.raises(ValueError):
+        tr.compute_gradients(c, s, gc, torch.cat([gs, gs], dim=1))    # two styles
+    with pytest.raises(RstError):   # contract_1 sees 5 rows: odd size at a stride-2 level
+        _trainer(dict(cfg, input_shape=(10, 20, 3), output_shape=(48, 80, 3), bottleneck_res_y=3), None, vgg, 1)
+
+
+@pytest.mark.parametrize("factors", [(1e4, 0.0, 0.0), (0.0, 1e-3, 0.0), (0.0, 0.0, 1e-1)],
+                         ids=["content", "style", "tv"])
+def test_prediction_gradient_per_loss_term(factors):
+    """d loss / d prediction (the VGG16 backward) for each loss term alone."""
+    _need_gpu()
+    from oracle import torch_train as T
+    from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
+    from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
+    cfg = CONFIGS['B']
+    B = 2
+    plan, w, vgg, content, sp, gtc, gts = _case(cfg, B)
+    ref = T.training_step(w, vgg, content, sp, gtc, gts, factors=factors, **cfg)
+    lm = StyleLossModelVGG(cfg['output_shape'], weights=vgg, max_batch=B)
+    lm.content_loss_factor, lm.style_loss_factor, lm.total_variation_loss_factor = factors
+    tr = StyleTransferTrainingModel(cfg['input_shape'], cfg['output_shape'], cfg['bottleneck_res_y'],
+                                    cfg['bottleneck_num_filters'], loss_model=lm, weights=w, max_batch=B)
+    c, s, gc, gs = _cuda(content, sp, gtc, gts)
+    from realtime_style_transfer_amd import _lib
+    from realtime_style_transfer_amd.styleLoss import VGG16_CHANNELS
+    lib = _lib.load()
+    for i in range(13):
+        _lib.check(lib.rst_trainer_debug_vgg_gradient(tr._handle, i, None, 0, B, _lib.stream_ptr()))
+    tr.compute_gradients(c, s, gc, gs)
+    g = tr.output_gradient(len(plan.layers) - 1, B).cpu().numpy()
+    r = ref['output_grads'][-1]
+    rel = float(np.abs(g - r).max() / np.abs(r).max())
+    vrel = []
+    H, W = cfg['output_shape'][:2]
+    for i in range(13):
+        div = 2 ** sum(1 for p in (1, 3, 6, 9) if p < i)
+        t = torch.empty((B, H // div, W // div, VGG16_CHANNELS[i]), device='cuda')
+        _lib.check(lib.rst_trainer_debug_vgg_gradient(tr._handle, i, _lib.dev_ptr(t), t.numel(), B, _lib.stream_ptr()))
+        rv = ref['vgg_grads'][i]
+        vrel.append(float(np.abs(t.cpu().numpy() - rv).max() / max(np.abs(rv).max(), 1e-30)))
+        if vrel[-1] > 1e-3 and not os.path.exists(os.path.join(OUT, 'vgg_grad_mismatch.npz')):
+            os.makedirs(OUT, exist_ok=True)
+            np.savez(os.path.join(OUT, 'vgg_grad_mismatch.npz'), layer=i, gpu=t.cpu().numpy(), ref=rv,
+                     pred_gpu=tr.last_pred.cpu().numpy() if hasattr(tr, 'last_pred') else 0,
+                     pred_ref=ref['prediction'])
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f'train_dpred_{factors}.json'), 'w') as f:
+        json.dump({'rel': rel, 'scale': float(np.abs(r).max()), 'vgg_rel': vrel}, f)
+    assert rel < 1e-3, rel
