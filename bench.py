@@ -65,6 +65,56 @@ def cpu_threads() -> int:
     return max(1, min(aff, int(env))) if env else aff
 
 
+def train_flops_per_sample(plan, H, W) -> dict:
+    """Algorithmic FLOPs (2 x MAC) of one training sample: transfer forward + backward (wgrad on
+    every conv, dgrad on every conv but the first), VGG16 forward x3 (style, content, prediction),
+    VGG16 dgrad on the prediction branch down to the image, Gram forward x2 and backward x1."""
+    fwd = sum(layer_flops(l) for l in plan.layers)
+    dgrad = sum(layer_flops(l) for l in plan.layers[1:])
+    vgg_fwd, gram, cin, h, w = 0.0, 0.0, 3, H, W
+    chans = [64, 64, 128, 128, 256, 256, 256, 512, 512, 512, 512, 512, 512]
+    pools = {1, 3, 6, 9}
+    for i, c in enumerate(chans):
+        vgg_fwd += 2.0 * h * w * 9 * cin * c
+        if i in pools:
+            gram += 2.0 * h * w * c * c
+            h, w = h // 2, w // 2
+        cin = c
+    return {"transfer_fwd": fwd, "transfer_bwd": fwd + dgrad, "vgg_fwd_x3": 3 * vgg_fwd, "vgg_dgrad": vgg_fwd,
+            "gram_fwd_x2_bwd_x1": 3 * gram}
+
+
+def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed):
+    from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
+    from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
+    TB = args.train_batch
+    lm = StyleLossModelVGG(outs, max_batch=TB, device=dev)
+    tr = StyleTransferTrainingModel(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, loss_model=lm,
+                                    weights=weights, max_batch=TB, device=dev)
+    rng = np.random.default_rng(3000 + rank)
+    x = {'content': torch.from_numpy(rng.random((TB,) + ins, dtype=np.float32)).to(dev),
+         'style_params': torch.from_numpy(synthetic_style_params(TB, 1, P, plan, seed=1)).to(dev)}
+    y = {'content': torch.from_numpy(rng.random((TB,) + outs, dtype=np.float32)).to(dev),
+         'style': torch.from_numpy(rng.random((TB, 1) + outs, dtype=np.float32)).to(dev)}
+    for _ in range(2):
+        m = tr.train_step(x, y)
+    torch.cuda.synchronize()
+    el = timed(lambda: tr.train_step(x, y), args.train_steps)
+    loss = float(tr.compute_metrics()['loss'])
+    fl = train_flops_per_sample(plan, outs[0], outs[1])
+    per_sample = sum(fl.values())
+    ms = el * 1e3 / args.train_steps
+    tfs = per_sample * TB / (ms * 1e-3) / 1e12
+    return {"workload": f"{SPEC} train_network.py step (BASELINE config 4): training-mode forward, VGG16/Gram loss "
+                        f"(no depth term), backward, " + ("RCCL gradient all-reduce (SUM), " if world > 1 else "") +
+                        "RMSprop", "batch_per_gpu": TB, "steps": args.train_steps, "ms_per_step": round(ms, 3),
+            "frames_per_s": round(world * TB * args.train_steps / el, 3), "dtype": "fp32 (f32 MFMA)",
+            "tflop_per_sample": round(per_sample / 1e12, 4),
+            "achieved_tflops_per_gpu": round(tfs, 2), "frac_fp32_mfma_peak": round(tfs / FP32_MFMA_PEAK_TFLOPS, 4),
+            "flop_breakdown_per_sample_gflop": {k: round(v / 1e9, 2) for k, v in fl.items()},
+            "last_loss_mean": loss}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +126,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="headline from eager launches instead of hipGraph replay")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
+    ap.add_argument("--train-steps", type=int, default=5)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -221,6 +273,11 @@ def main():
             te = float(t.item())
         stream_fps = world * SB * reps / te
 
+    # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
+    train = None
+    if args.train_batch > 0:
+        train = bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed)
+
     # ---------------- parity + CPU baseline (rank 0 only, bounded sample) -----------------------
     max_abs = None
     cpu = None
@@ -291,6 +348,7 @@ def main():
             "stream_graph_fps": None if stream_fps is None else round(stream_fps, 3),
             "stream_graph_batch": args.stream_batch,
             "layers": layer_table,
+            "training": train,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

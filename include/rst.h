@@ -136,6 +136,8 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
 void rst_trainer_destroy(rst_trainer* t);
 int rst_trainer_num_style_params(const rst_trainer* t);
 size_t rst_trainer_num_weights(const rst_trainer* t);
+/* The trainer's own loss model (e.g. rst_loss_copy_feature of the last prediction). Owned by t. */
+rst_loss_handle* rst_trainer_loss(rst_trainer* t);
 /* content (B, in_h, in_w, in_c), style_params (B, 1, P), gt_content / gt_style (B, out_h, out_w, 3).
  * Writes prediction (B, out_h, out_w, 3), losses (B x 4, as rst_loss_forward), grad (num_weights)
  * and, when non-NULL, grad_style_params (B, P). All device pointers. */

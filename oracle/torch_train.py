@@ -92,9 +92,35 @@ def transfer_forward_train(content, style_params, w: Sequence[torch.Tensor], blo
     return x, bn_stats
 
 
-def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None) -> Dict[str, torch.Tensor]:
+class _RoutedMaxPool2(torch.autograd.Function):
+    """2x2 max-pool whose backward sends each window's gradient to the first maximum of a
+    supplied routing tensor (the implementation-under-test's float32 activations) instead of
+    this float64 tensor. Forward values are the float64 maxima. Only the measure-zero choice
+    between near-equal window values is aligned; see tests/test_gpu_train.py."""
+
+    @staticmethod
+    def forward(ctx, x, route):
+        B, C, H, W = x.shape
+        win = route.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+        m = win.max(dim=-1, keepdim=True).values
+        first = (win == m).to(torch.int64).argmax(dim=-1)            # first maximum in scan order
+        ctx.save_for_backward(first)
+        ctx.shape = x.shape
+        return F.max_pool2d(x, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (first,) = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        onehot = F.one_hot(first, 4).to(gy.dtype) * gy.unsqueeze(-1)
+        gx = onehot.reshape(B, C, H // 2, W // 2, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H, W)
+        return gx, None
+
+
+def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None) -> Dict[str, torch.Tensor]:
     """StyleLossModelVGG.call (styleLoss.py:106-109) on NCHW float64 images in [0, 1].
-    ``taps``: list receiving every conv output (retain_grad) when the input requires grad."""
+    ``taps``: list receiving every conv output (retain_grad) when the input requires grad.
+    ``route``: {conv index: NCHW activations} whose window maxima route the max-pool backward."""
     x = images01 * 255.0
     mean = torch.tensor(VGG_MEAN_BGR, dtype=x.dtype).view(1, 3, 1, 1)
     x = x.flip(1) - mean
@@ -102,7 +128,10 @@ def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None) -> Dict[str, 
     i = 0
     for entry in VGG16_LAYERS:
         if entry[0] == 'pool':
-            x = F.max_pool2d(x, 2)
+            if route is not None and (i - 1) in route:
+                x = _RoutedMaxPool2.apply(x, route[i - 1])
+            else:
+                x = F.max_pool2d(x, 2)
             continue
         name = entry[0]
         x = F.relu(conv2d_same(x, vgg[2 * i], vgg[2 * i + 1], 1))
@@ -127,9 +156,10 @@ def _mean_l2(t):
     return (0.5 * t ** 2).reshape(t.shape[0], -1).mean(dim=1)
 
 
-def style_losses(pred, content, style, vgg, content_factor=1e4, style_factor=1e-3, tv_factor=1e-1, taps=None):
+def style_losses(pred, content, style, vgg, content_factor=1e4, style_factor=1e-3, tv_factor=1e-1, taps=None,
+                 route=None):
     """make_style_loss_function without depth (styleLoss.py:295-369) -> (B, 4) [loss, feature, style, tv]."""
-    fp, fc, fs = vgg_features(pred, vgg, taps), vgg_features(content, vgg), vgg_features(style, vgg)
+    fp, fc, fs = vgg_features(pred, vgg, taps, route), vgg_features(content, vgg), vgg_features(style, vgg)
     feature = torch.stack([_mean_l2(fp[n] - fc[n]) for n in CONTENT_LAYERS]).mean(0) * content_factor
     style_l = torch.stack([_mean_l2(_gram(fp[n]) - _gram(fs[n])) for n in STYLE_LAYERS]).mean(0) * style_factor
     tv = ((pred[:, :, 1:, :] - pred[:, :, :-1, :]).abs().sum(dim=(1, 2, 3)) +
@@ -144,12 +174,14 @@ def _nchw(a):
 def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarray], content, style_params,
                   gt_content, gt_style, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
                   factors=(1e4, 1e-3, 1e-1), ms: Optional[Sequence[np.ndarray]] = None,
-                  lr=1e-3, rho=0.9, eps=1e-7) -> Dict[str, object]:
+                  lr=1e-3, rho=0.9, eps=1e-7, pool_route: Optional[Dict[int, np.ndarray]] = None) -> Dict[str, object]:
     """One Keras train_step: forward (BN training mode), loss, gradients, RMSprop.
 
     Inputs are NHWC numpy; returns numpy: prediction (B,H,W,3), losses (B,4), grads (Keras order;
     zeros for the BN moving statistics), grad_style_params (B,P), weights after the update
-    (moving statistics updated by the forward), ms (RMSprop slots after the update)."""
+    (moving statistics updated by the forward), ms (RMSprop slots after the update).
+    ``pool_route``: {VGG conv index before a pool: NHWC activations of the prediction} to align
+    the max-pool backward's choice among near-equal maxima with an implementation under test."""
     blocks, P = transfer_structure(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters)
     w = [torch.tensor(np.asarray(a, np.float64), requires_grad=True) for a in weights]
     vgg = [torch.tensor(np.asarray(a, np.float64)) for a in vgg_weights]
@@ -160,7 +192,8 @@ def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarra
     taps = []
     pred, bn_stats = transfer_forward_train(_nchw(content), sp, w, blocks, taps=taps)
     vtaps = []
-    losses = style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors, taps=vtaps)
+    route = None if pool_route is None else {k: _nchw(v) for k, v in pool_route.items()}
+    losses = style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors, taps=vtaps, route=route)
     losses[:, 0].sum().backward()
     # Keras trainable set: conv kernels/biases, BN gamma/beta (moving statistics are not trained)
     grads, new_w, new_ms = [], [], []

@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = [
     "rst_trainer_create", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
     "rst_trainer_compute_gradients", "rst_trainer_apply_gradients", "rst_trainer_copy_weights",
     "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_copy_output_gradient",
-    "rst_trainer_debug_vgg_gradient",
+    "rst_trainer_debug_vgg_gradient", "rst_trainer_loss",
 ]
 
 
@@ -123,6 +123,8 @@ def load() -> ctypes.CDLL:
     lib.rst_trainer_copy_output_gradient.restype = i
     lib.rst_trainer_debug_vgg_gradient.argtypes = [vp, i, vp, sz, i, vp]
     lib.rst_trainer_debug_vgg_gradient.restype = i
+    lib.rst_trainer_loss.argtypes = [vp]
+    lib.rst_trainer_loss.restype = vp
     lib.rst_last_error.argtypes = []
     lib.rst_last_error.restype = ctypes.c_char_p
     lib.rst_version.argtypes = []

@@ -625,6 +625,7 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
 void rst_trainer_destroy(rst_trainer* t) { delete t; }
 
 int rst_trainer_num_style_params(const rst_trainer* t) { return t ? t->P : -1; }
+rst_loss_handle* rst_trainer_loss(rst_trainer* t) { return t ? t->loss : nullptr; }
 size_t rst_trainer_num_weights(const rst_trainer* t) { return t ? t->nw : 0; }
 
 int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const float* style_params,

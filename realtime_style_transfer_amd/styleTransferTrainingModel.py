@@ -45,6 +45,21 @@ class RMSprop:
         self.learning_rate, self.rho, self.epsilon = float(learning_rate), float(rho), float(epsilon)
 
 
+def allreduce_gradients(grad: torch.Tensor, group=None) -> bool:
+    """Data-parallel gradient exchange: one flat bucket (the whole ~5.9 MB fp32 gradient of
+    rst-960-120-128-17) summed in place across the process group — RCCL over xGMI with the
+    "nccl" backend on MI355X, gloo on CPU. SUM, not mean: the reference minimises the per-image
+    loss vector's sum, so the global step equals one step on the concatenated batch. Returns
+    whether a collective ran (no-op for world size 1 / no process group)."""
+    dist = torch.distributed
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    if dist.get_world_size(group) == 1:
+        return False
+    dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+    return True
+
+
 class StyleTransferTrainingModel:
     """styleTransferTrainingModel.py:11-36 + Keras train_step, one GPU (one librst trainer)."""
 
@@ -134,6 +149,18 @@ class StyleTransferTrainingModel:
                                                                 _lib.stream_ptr()))
         return t
 
+    def vgg_feature(self, layer: str, batch: int) -> torch.Tensor:
+        """Debug: a VGG16 conv output of the most recent prediction (the trainer's loss model)."""
+        from .styleLoss import VGG16_CHANNELS, VGG16_LAYER_NAMES
+        idx = VGG16_LAYER_NAMES.index(layer)
+        H, W = self.output_shape[:2]
+        div = 2 ** sum(1 for i in (1, 3, 6, 9) if i < idx)
+        t = torch.empty((batch, H // div, W // div, VGG16_CHANNELS[idx]), dtype=torch.float32, device=self.device)
+        lib = _lib.load()
+        _lib.check(lib.rst_loss_copy_feature(lib.rst_trainer_loss(self._handle), idx, _lib.dev_ptr(t), t.numel(),
+                                             batch, _lib.stream_ptr()))
+        return t
+
     def _check(self, content, style_params, gt_content, gt_style):
         B = content.shape[0]
         if tuple(content.shape) != (B,) + self.input_shape:
@@ -188,10 +215,7 @@ class StyleTransferTrainingModel:
     def train_step(self, x: Dict[str, torch.Tensor], y: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         """One Keras fit step: x = {'content', 'style_params'}, y = {'content', 'style'}."""
         pred, losses, grad, gsp = self.compute_gradients(x['content'], x['style_params'], y['content'], y['style'])
-        if self.process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()
-                                              and torch.distributed.get_world_size() > 1):
-            # one bucket: the whole ~5.9 MB gradient in a single RCCL all-reduce over xGMI
-            torch.distributed.all_reduce(grad, op=torch.distributed.ReduceOp.SUM, group=self.process_group)
+        allreduce_gradients(grad, self.process_group)
         self.apply_gradients(grad)
         self.style_losses = {n: losses[:, i] for i, n in enumerate(LOSS_NAMES)}
         self.last_prediction = pred
@@ -242,5 +266,5 @@ def make_style_transfer_training_model(style_predictor_factory_func: Optional[Ca
     return StyleTransferModels(training, loss_model)
 
 
-__all__ = ['RMSprop', 'StyleTransferTrainingModel', 'StyleTransferModels', 'make_style_transfer_training_model',
+__all__ = ['allreduce_gradients', 'RMSprop', 'StyleTransferTrainingModel', 'StyleTransferModels', 'make_style_transfer_training_model',
            'make_style_loss_function']

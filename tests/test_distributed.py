@@ -70,3 +70,42 @@ def test_two_rank_sharded_stream_matches_single_process(tmp_path):
         assert ok == "1"
         assert abs(float(t) - 0.2) < 1e-12       # MAX over ranks
         assert el == "True"
+
+
+def _dp_worker(rank, world, port, tmp):
+    """Data-parallel training exchange: each rank holds the oracle gradient of its own frame; the
+    product's allreduce_gradients must leave every rank with the sum (= the batch-sum gradient)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import torch_train as T
+        from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+        from realtime_style_transfer_amd.styleLoss import init_vgg16_weights
+        from realtime_style_transfer_amd.styleTransferTrainingModel import allreduce_gradients
+        cfg = dict(input_shape=(16, 32, 3), output_shape=(16, 32, 3), bottleneck_res_y=4, bottleneck_num_filters=4)
+        plan = network_plan(cfg['input_shape'], cfg['output_shape'], 4, 4)
+        w, vgg = init_weights(plan, seed=2), init_vgg16_weights(seed=3)
+        rng = np.random.default_rng(7)
+        c = rng.random((world, 16, 32, 3)).astype(np.float32)
+        gc = rng.random((world, 16, 32, 3)).astype(np.float32)
+        gs = rng.random((world, 1, 16, 32, 3)).astype(np.float32)
+        sp = synthetic_style_params(world, 1, plan.num_style_params, plan, seed=1)
+        flat = []
+        for r in range(world):   # every rank can compute every shard's reference gradient
+            out = T.training_step(w, vgg, c[r:r + 1], sp[r:r + 1], gc[r:r + 1], gs[r:r + 1], **cfg)
+            flat.append(np.concatenate([g.reshape(-1) for g in out['grads']]))
+        g = torch.from_numpy(flat[rank].astype(np.float32))
+        ran = allreduce_gradients(g)
+        ok = ran and np.array_equal(g.numpy(), flat[0].astype(np.float32) + flat[1].astype(np.float32))
+        with open(os.path.join(tmp, f"dp{rank}.txt"), "w") as f:
+            f.write(f"{int(ok)}\n")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_gradient_allreduce_gloo(tmp_path):
+    world = 2
+    mp.spawn(_dp_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"dp{r}.txt").read_text().split()[0] == "1"
