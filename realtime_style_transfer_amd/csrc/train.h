@@ -21,6 +21,7 @@ struct NormBwdArgs {
     int post;                // 0 relu, 1 none, 2 sigmoid
     int conv_relu;           // conv carries a built-in ReLU (mask dz by z > 0)
     int merge_images;        // BatchNorm: statistics over the whole batch
+    float* dconv_bias;       // conv bias gradient = sum of dz over images and pixels (or null)
 };
 hipError_t norm_bwd_launch(const NormBwdArgs& a, hipStream_t st);
 
@@ -42,7 +43,6 @@ struct WgradArgs {
 int wgrad_choose_splits(const WgradArgs& a);
 size_t wgrad_slab_bytes(const WgradArgs& a);
 hipError_t wgrad_launch(WgradArgs a, hipStream_t st);
-hipError_t bias_grad_launch(const float* D, long rows, int C, float* part, float* db, hipStream_t st);
 
 hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, int accumulate,
                                hipStream_t st);

@@ -9,10 +9,8 @@
 //   dz = a (dn - S1/N - x^ S2/N) [z > 0 when the conv carries a built-in ReLU]
 // reduce -> finalize (f64, fixed order) -> apply, no atomics.
 //
-// Weight gradients: split-K f32 MFMA (v_mfma_f32_32x32x2_f32) over pixels,
-//   conv : dW[tap][ci][co] = sum_{b,q} X[b][q*s + tap - pad][ci] * Dz[b][q][co]
-//   convT: dW[tap][co][ci] = sum_{b,i} X[b][i][ci] * Dz[b][i*s + tap - pad][co]
-// per-split slabs, reduced in fixed order (bitwise reproducible).
+// The conv bias gradient (sum of dz) is accumulated by the apply pass itself (per-tile partials).
+// Weight gradients: wgrad.hip.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -94,21 +92,51 @@ __global__ __launch_bounds__(64) void norm_bwd_finalize_kernel(NormBwdArgs a) {
     }
 }
 
+// dz per element, plus per-tile sums of dz -> part[b][c][tile].x (the conv bias gradient's partials;
+// part's {S1, S2} were consumed by finalize, which ran before this kernel on the same stream)
 __global__ __launch_bounds__(256) void norm_bwd_apply_kernel(NormBwdArgs a) {
-    const size_t total = (size_t)a.batch * a.hw * a.C;
-    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
-        const int c = (int)(i % a.C);
-        const int b = (int)(i / ((size_t)a.hw * a.C));
-        const float2 ab = a.ab[b * a.C + c];
-        const float2 mr = a.mr[b * a.C + c];
-        const float2 k = a.consts[b * a.C + c];
-        const float z = a.z[i];
-        const float dn = post_grad(a.post, a.g[i], z, ab);
-        const float xh = (z - mr.x) * mr.y;
-        float dz = ab.x * (dn - k.x - xh * k.y);
-        if (a.conv_relu && !(z > 0.f)) dz = 0.f;
-        a.dz[i] = dz;
+    __shared__ float red[256];
+    const int tile = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int C = a.C;
+    const int R = 256 / C;
+    const int c = tid % C, r = tid / C;
+    float sdz = 0.f;
+    if (r < R) {
+        const float2 ab = a.ab[b * C + c];
+        const float2 mr = a.mr[b * C + c];
+        const float2 k = a.consts[b * C + c];
+        const long p0 = (long)tile * a.tile, p1 = min((long)a.hw, p0 + a.tile);
+        for (long p = p0 + r; p < p1; p += R) {
+            const size_t i = ((size_t)b * a.hw + p) * C + c;
+            const float z = a.z[i];
+            const float dn = post_grad(a.post, a.g[i], z, ab);
+            const float xh = (z - mr.x) * mr.y;
+            float dz = ab.x * (dn - k.x - xh * k.y);
+            if (a.conv_relu && !(z > 0.f)) dz = 0.f;
+            a.dz[i] = dz;
+            sdz += dz;
+        }
     }
+    red[tid] = sdz;
+    __syncthreads();
+    if (tid < C) {
+        float t = 0.f;
+        for (int q = 0; q < R; ++q) t += red[q * C + tid];
+        a.part[((size_t)b * C + tid) * a.n_tiles + tile].x = t;
+    }
+}
+
+// conv bias gradient db[c] = sum over images and tiles of the dz partials (f64, fixed order)
+__global__ __launch_bounds__(64) void norm_bwd_bias_kernel(NormBwdArgs a) {
+    const int c = blockIdx.x;
+    double s = 0.0;
+    for (int b = 0; b < a.batch; ++b) {
+        const float2* p = a.part + ((size_t)b * a.C + c) * a.n_tiles;
+        for (int t = threadIdx.x; t < a.n_tiles; t += 64) s += (double)p[t].x;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (threadIdx.x == 0) a.dconv_bias[c] = (float)s;
 }
 
 hipError_t norm_bwd_launch(const NormBwdArgs& a0, hipStream_t st) {
@@ -119,11 +147,13 @@ hipError_t norm_bwd_launch(const NormBwdArgs& a0, hipStream_t st) {
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3(a.C, a.batch), dim3(64), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const size_t total = (size_t)a.batch * a.hw * a.C;
-    unsigned blocks = (unsigned)((total + 255) / 256);
-    if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(blocks), dim3(256), 0, st, a);
-    return hipGetLastError();
+    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(a.n_tiles, a.batch), dim3(256), 0, st, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (a.dconv_bias != nullptr) {
+        hipLaunchKernelGGL(norm_bwd_bias_kernel, dim3(a.C), dim3(64), 0, st, a);
+        e = hipGetLastError();
+    }
+    return e;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -137,189 +167,6 @@ hipError_t add_launch(const float* x1, const float* x2, float* y, size_t n, hipS
     unsigned blocks = (unsigned)((n + 255) / 256);
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(add_kernel, dim3(blocks), dim3(256), 0, st, x1, x2, y, n);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// weight gradients (split-K MFMA): dW[r][c] = sum_q S(q, r) U(q, c), where r = (tap, channel of the
-// shifted operand) and q runs over the unshifted operand's pixels (and images):
-//   conv : S = X at q*s + tap - pad (r = (tap, ci)), U = D at q   -> dW (kh, kw, ci, co)
-//   convT: S = D at q*s + tap - pad (r = (tap, co)), U = X at q   -> dW (kh, kw, co, ci)
-// i.e. both land in the canonical Keras kernel layout. WG: 64 rows x 64 cols x one pixel split.
-namespace wg {
-constexpr int KP = 64;       // pixels per LDS stage
-constexpr int T = 64;        // row / col tile edge
-constexpr int LS = T + 1;
-}  // namespace wg
-
-__global__ __launch_bounds__(256) void wgrad_partial_kernel(WgradArgs a) {
-    using namespace wg;
-    __shared__ float la[KP * LS];
-    __shared__ float lb[KP * LS];
-    const bool tr = a.transposed != 0;
-    const int Cs = tr ? a.C2 : a.C1;                 // channels of the shifted operand
-    const int Cu = tr ? a.C1 : a.C2;                 // channels of the unshifted operand
-    const int R = a.kh * a.kw * Cs;
-    const int nr = (R + T - 1) / T, nc = (Cu + T - 1) / T;
-    const float* S = tr ? a.D : a.X;
-    const float* U = tr ? a.X : a.D;
-    const int SH = tr ? a.DH : a.XH, SW = tr ? a.DW : a.XW;
-    int bid = blockIdx.x;
-    const int split = bid % a.nsplit;
-    bid /= a.nsplit;
-    const int tc = bid % nc;
-    const int tr_ = bid / nc;
-    const int r0 = tr_ * T, c0 = tc * T;
-    const long qhw = (long)a.Qh * a.Qw;
-    const long total = (long)a.batch * qhw;
-    const long q_begin = (long)split * a.span;
-    const long q_end = min(total, q_begin + a.span);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wi = wave >> 1, wj = wave & 1;
-    const int li = lane & 31, lh = lane >> 5;
-
-    floatx16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-
-    for (long q0 = q_begin; q0 < q_end; q0 += KP) {
-        __syncthreads();
-        for (int it = tid; it < KP * T; it += 256) {
-            const int pp = it / T, cc = it % T;
-            const long q = q0 + pp;
-            float vs = 0.f, vu = 0.f;
-            if (q < q_end) {
-                const int b = (int)(q / qhw);
-                const int qr = (int)(q % qhw);
-                const int qy = qr / a.Qw, qx = qr % a.Qw;
-                const int r = r0 + cc;
-                if (r < R) {
-                    const int tap = r / Cs, ch = r % Cs;
-                    const int ky = tap / a.kw, kx = tap % a.kw;
-                    const int sy = qy * a.stride + ky - a.pad_t, sx = qx * a.stride + kx - a.pad_l;
-                    if (sy >= 0 && sy < SH && sx >= 0 && sx < SW)
-                        vs = S[(((size_t)b * SH + sy) * SW + sx) * Cs + ch];
-                }
-                const int c = c0 + cc;
-                if (c < Cu) vu = U[((size_t)b * qhw + qr) * Cu + c];
-            }
-            la[pp * LS + cc] = vs;
-            lb[pp * LS + cc] = vu;
-        }
-        __syncthreads();
-#pragma unroll 8
-        for (int s = 0; s < KP / 2; ++s) {
-            const int p = 2 * s + lh;
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(la[p * LS + wi * 32 + li], lb[p * LS + wj * 32 + li], acc, 0, 0, 0);
-        }
-    }
-    const int Rp = nr * T, Cp = nc * T;
-    float* out = a.slab + (size_t)split * Rp * Cp;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
-        out[(size_t)(r0 + wi * 32 + row) * Cp + c0 + wj * 32 + li] = acc[r];
-    }
-}
-
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
-    const bool tr = a.transposed != 0;
-    const int Cs = tr ? a.C2 : a.C1, Cu = tr ? a.C1 : a.C2;
-    const int R = a.kh * a.kw * Cs;
-    const int Rp = ((R + wg::T - 1) / wg::T) * wg::T, Cp = ((Cu + wg::T - 1) / wg::T) * wg::T;
-    const size_t total = (size_t)R * Cu;
-    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
-        const size_t r = i / Cu, c = i % Cu;
-        float s = 0.f;
-        for (int k = 0; k < a.nsplit; ++k) s += a.slab[((size_t)k * Rp + r) * Cp + c];
-        a.dW[i] = s;
-    }
-}
-
-static void wgrad_dims(const WgradArgs& a, int& R, int& Cu) {
-    const int Cs = a.transposed ? a.C2 : a.C1;
-    Cu = a.transposed ? a.C1 : a.C2;
-    R = a.kh * a.kw * Cs;
-}
-
-size_t wgrad_slab_bytes(const WgradArgs& a) {
-    int R, Cu;
-    wgrad_dims(a, R, Cu);
-    const size_t Rp = ((R + wg::T - 1) / wg::T) * wg::T, Cp = ((Cu + wg::T - 1) / wg::T) * wg::T;
-    return (size_t)a.nsplit * Rp * Cp * sizeof(float);
-}
-
-int wgrad_choose_splits(const WgradArgs& a) {
-    int R, Cu;
-    wgrad_dims(a, R, Cu);
-    const long tiles = (long)((R + wg::T - 1) / wg::T) * ((Cu + wg::T - 1) / wg::T);
-    const long total = (long)a.batch * a.Qh * a.Qw;
-    long ns = 2048 / tiles;
-    if (ns < 1) ns = 1;
-    const long max_ns = (total + 511) / 512;
-    if (ns > max_ns) ns = max_ns;
-    if (ns < 1) ns = 1;
-    return (int)ns;
-}
-
-hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
-    int R, Cu;
-    wgrad_dims(a, R, Cu);
-    const long total = (long)a.batch * a.Qh * a.Qw;
-    long span = (total + a.nsplit - 1) / a.nsplit;
-    span = ((span + wg::KP - 1) / wg::KP) * wg::KP;
-    a.span = span;
-    const int nr = (R + wg::T - 1) / wg::T, nc = (Cu + wg::T - 1) / wg::T;
-    const unsigned grid = (unsigned)(nr * nc * a.nsplit);
-    hipLaunchKernelGGL(wgrad_partial_kernel, dim3(grid), dim3(256), 0, st, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const size_t n = (size_t)R * Cu;
-    unsigned blocks = (unsigned)((n + 255) / 256);
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// bias gradient: db[c] = sum over (b, pixel) of D[..][c]; partials per block then ordered sum
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ D, long rows, int C,
-                                                             float* __restrict__ part, int nblk) {
-    __shared__ float red[256];
-    const int blk = blockIdx.x, tid = threadIdx.x;
-    const int R = 256 / C;
-    const int c = tid % C, r = tid / C;
-    const long per = (rows + nblk - 1) / nblk;
-    const long r0 = (long)blk * per, r1 = min(rows, r0 + per);
-    float s = 0.f;
-    if (r < R)
-        for (long i = r0 + r; i < r1; i += R) s += D[(size_t)i * C + c];
-    red[tid] = s;
-    __syncthreads();
-    if (tid < C) {
-        float t = 0.f;
-        for (int k = 0; k < R; ++k) t += red[k * C + tid];
-        part[(size_t)blk * C + tid] = t;
-    }
-}
-
-__global__ void colsum_final_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += (double)part[(size_t)k * C + c];
-    out[c] = (float)s;
-}
-
-hipError_t bias_grad_launch(const float* D, long rows, int C, float* part, float* db, hipStream_t st) {
-    if (C > 256) return hipErrorInvalidValue;
-    int nblk = (int)(rows / 4096);
-    if (nblk < 1) nblk = 1;
-    if (nblk > 1024) nblk = 1024;
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nblk), dim3(256), 0, st, D, rows, C, part, nblk);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 63) / 64), dim3(64), 0, st, part, nblk, C, db);
     return hipGetLastError();
 }
 

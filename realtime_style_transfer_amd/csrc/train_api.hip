@@ -118,7 +118,6 @@ struct rst_trainer {
     float2* d_nb_part = nullptr;
     float2* d_nb_consts = nullptr;
     float* d_slab = nullptr;
-    float* d_bpart = nullptr;
     float* d_gstyle = nullptr;    // style-param gradient scratch (caller passed none)
     float* d_vg[2] = {nullptr, nullptr};
     float* d_vpool = nullptr;
@@ -336,8 +335,8 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
         nb.n_tiles = (int)((hw + nb.tile - 1) / nb.tile);
         nb.post = s.post;
         nb.conv_relu = s.conv_relu ? 1 : 0;
+        nb.dconv_bias = grad + T.boff;
         RST_HIP_TRY(norm_bwd_launch(nb, st));
-        RST_HIP_TRY(bias_grad_launch(t->d_dz, (long)B * hw, s.cout, t->d_bpart, grad + T.boff, st));
         WgradArgs w{};
         w.X = li == 0 ? content : T.d_x;
         w.D = t->d_dz;
@@ -520,6 +519,10 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
         w.C2 = s.cout;
         w.kh = w.kw = s.k;
         w.transposed = s.keras_kind;
+        w.XH = s.H;
+        w.XW = s.W;
+        w.DH = s.Ho;
+        w.DW = s.Wo;
         w.Qh = s.keras_kind == 0 ? s.Ho : s.H;
         w.Qw = s.keras_kind == 0 ? s.Wo : s.W;
         w.nsplit = wgrad_choose_splits(w);
@@ -613,7 +616,6 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
     if ((st = t->alloc(&t->d_nb_part, (size_t)max_nb * sizeof(float2))) != RST_OK) return fail_delete(t, st);
     if ((st = t->alloc(&t->d_nb_consts, (size_t)B * 256 * sizeof(float2))) != RST_OK) return fail_delete(t, st);
     if ((st = t->alloc(&t->d_slab, slab)) != RST_OK) return fail_delete(t, st);
-    if ((st = t->alloc(&t->d_bpart, (size_t)1024 * 256 * 4)) != RST_OK) return fail_delete(t, st);
     if ((st = t->alloc(&t->d_gstyle, (size_t)B * P * 4)) != RST_OK) return fail_delete(t, st);
     // the last layer's output gradient is d(loss)/d(prediction), written by the VGG backward
     if ((st = repack(t, nullptr)) != RST_OK) return fail_delete(t, st);

@@ -1,0 +1,47 @@
+"""Run a few full-size training steps (rst-960-120-128-17, B=4) — the command profiled by rocprofv3."""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params  # noqa: E402
+from realtime_style_transfer_amd.shape_config import ShapeConfig  # noqa: E402
+from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG  # noqa: E402
+from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--spec", default="rst-960-120-128-17")
+    a = ap.parse_args()
+    cfg = ShapeConfig.from_spec(a.spec)
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    dev = torch.device("cuda:0")
+    B = a.batch
+    lm = StyleLossModelVGG(outs, max_batch=B, device=dev)
+    tr = StyleTransferTrainingModel(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, loss_model=lm,
+                                    weights=init_weights(plan, seed=2), max_batch=B, device=dev)
+    rng = np.random.default_rng(0)
+    x = {'content': torch.from_numpy(rng.random((B,) + ins, dtype=np.float32)).to(dev),
+         'style_params': torch.from_numpy(synthetic_style_params(B, 1, plan.num_style_params, plan)).to(dev)}
+    y = {'content': torch.from_numpy(rng.random((B,) + outs, dtype=np.float32)).to(dev),
+         'style': torch.from_numpy(rng.random((B, 1) + outs, dtype=np.float32)).to(dev)}
+    tr.train_step(x, y)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        m = tr.train_step(x, y)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    print(f"{a.steps} steps B={B}: {el / a.steps * 1e3:.2f} ms/step, loss {float(m['loss']):.6g}")
+
+
+if __name__ == "__main__":
+    main()
