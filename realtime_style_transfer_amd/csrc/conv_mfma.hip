@@ -53,6 +53,16 @@ __device__ __forceinline__ float vget(const float4& v, int q) {
     return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
 }
 
+// two-style blending (num_styles == 2, styleTransfer.py:36-44): the per-pixel affine is
+// w0*(a0 x + b0) + w1*(a1 x + b1) with w0 = 1 - w1, i.e. y0 + w1*(y1 - y0)
+__device__ __forceinline__ float apply_pro_blend(int mode, float x, float2 ab, float2 ab1, float w, float r) {
+    const float y0 = fmaf(ab.x, x, ab.y), y1 = fmaf(ab1.x, x, ab1.y);
+    float y = fmaf(w, y1 - y0, y0);
+    if (mode == PRO_AFF_RELU) y = fmaxf(y, 0.f);
+    else if (mode == PRO_AFF_RES) y = r + y;
+    return y;
+}
+
 __device__ __forceinline__ float apply_pro(int mode, float x, float2 ab, float r) {
     if (mode == PRO_MASK) return r > 0.f ? x : 0.f;   // ReLU backward: gradient masked by the forward output
     float y = fmaf(ab.x, x, ab.y);
@@ -93,7 +103,7 @@ struct ConvCfg {
     static_assert(KSTEPS % VEC == 0, "vector k-steps");
     static_assert(WSTAGE % 4 == 0, "weight stage is a float4 copy");
     static_assert(HB == 1 || (CK % 4) == 0, "halo prefetch needs the float4 path");
-    static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+    static_assert(LDS_BYTES + MAX_CIN * 8 <= 160 * 1024, "LDS budget (incl. the two-style blend table)");
 };
 
 // Weight stages are staged through registers: global_load_dwordx4 issued at the start of a
@@ -149,6 +159,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     float* halo0 = smem;
     float* wts0 = smem + HB * C::HALO_FLOATS;
     float2* pab = reinterpret_cast<float2*>(wts0 + 2 * C::WSTAGE);
+    float2* pab1 = pab + C::MAX_CIN;   // only present when launched with the blend LDS extension
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -170,6 +181,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     const bool do_mat = (a.mat != nullptr) && nb == 0;
     const size_t img_base = (size_t)b * a.H * a.W;
     const bool vec_in = ((Cin & 3) == 0) && ((CK & 3) == 0);
+    const bool blend = a.pro_w != nullptr;
     const float* wsrc = a.wpk + (size_t)nb * a.nchunks * C::NGROUPS * C::WSTAGE;
     const int n_stages = a.nchunks * C::NGROUPS;
 
@@ -206,10 +218,18 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
             v.z = r.z > 0.f ? v.z : 0.f;
             v.w = r.w > 0.f ? v.w : 0.f;
         } else if (pro != PRO_NONE) {
-            v.x = apply_pro(pro, v.x, pab[c + 0], r.x);
-            v.y = apply_pro(pro, v.y, pab[c + 1], r.y);
-            v.z = apply_pro(pro, v.z, pab[c + 2], r.z);
-            v.w = apply_pro(pro, v.w, pab[c + 3], r.w);
+            if (blend) {
+                const float wpx = a.pro_w[img_base + (size_t)iy * a.W + ix];
+                v.x = apply_pro_blend(pro, v.x, pab[c + 0], pab1[c + 0], wpx, r.x);
+                v.y = apply_pro_blend(pro, v.y, pab[c + 1], pab1[c + 1], wpx, r.y);
+                v.z = apply_pro_blend(pro, v.z, pab[c + 2], pab1[c + 2], wpx, r.z);
+                v.w = apply_pro_blend(pro, v.w, pab[c + 3], pab1[c + 3], wpx, r.w);
+            } else {
+                v.x = apply_pro(pro, v.x, pab[c + 0], r.x);
+                v.y = apply_pro(pro, v.y, pab[c + 1], r.y);
+                v.z = apply_pro(pro, v.z, pab[c + 2], r.z);
+                v.w = apply_pro(pro, v.w, pab[c + 3], r.w);
+            }
             if (do_mat && iy >= y0 * S && iy < (y0 + TH) * S && ix >= x0 * S && ix < (x0 + TW) * S)
                 *reinterpret_cast<float4*>(a.mat + gi) = v;
         }
@@ -253,7 +273,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                         v = a.res[gi] > 0.f ? v : 0.f;
                     } else if (pro != PRO_NONE) {
                         const float r = pro == PRO_AFF_RES ? a.res[gi] : 0.f;
-                        v = apply_pro(pro, v, pab[c], r);
+                        v = blend ? apply_pro_blend(pro, v, pab[c], pab1[c],
+                                                    a.pro_w[img_base + (size_t)iy * a.W + ix], r)
+                                  : apply_pro(pro, v, pab[c], r);
                         if (do_mat && iy >= y0 * S && iy < (y0 + TH) * S && ix >= x0 * S && ix < (x0 + TW) * S) a.mat[gi] = v;
                     }
                 }
@@ -265,6 +287,8 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     // ---- prologue -----------------------------------------------------------------------------
     if (pro != PRO_NONE && a.pro_ab != nullptr) {
         for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[b * Cin + c];
+        if (blend)
+            for (int c = tid; c < Cin; c += 256) pab1[c] = a.pro_ab1[b * Cin + c];
         __syncthreads();
     }
     {
@@ -451,7 +475,9 @@ static hipError_t launch_cfg(const ConvArgs& a, hipStream_t st) {
     using C = ConvCfg<RST_TA>;
     auto kern = conv_mfma_kernel<RST_TA>;
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x * a.n_blocks);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), C::LDS_BYTES, st, a);
+    if (a.pro_w != nullptr && a.cin > C::MAX_CIN) return hipErrorInvalidValue;
+    const size_t lds = C::LDS_BYTES + (a.pro_w != nullptr ? C::MAX_CIN * sizeof(float2) : 0);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 
@@ -459,7 +485,8 @@ template <RST_TP>
 static hipError_t prepare_cfg() {
     using C = ConvCfg<RST_TA>;
     auto kern = conv_mfma_kernel<RST_TA>;
-    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES);
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(C::LDS_BYTES + C::MAX_CIN * sizeof(float2)));
 }
 
 template <RST_TP>

@@ -14,6 +14,8 @@ struct ConvArgs {
     const float* res;       // residual source (PRO_AFF_RES), same shape as in
     float* mat;             // materialise transformed input here (or null)
     const float2* pro_ab;   // [B][cin] prologue affine (a, b)
+    const float2* pro_ab1;  // [B][cin] second style's affine (two-style blending) or null
+    const float* pro_w;     // [B][H][W] per-pixel weight of the second style (with pro_ab1)
     const float* wpk;       // packed weights [n_blocks][nchunks][ngroups][wstage]
     const float* bias;      // [ntot]
     const float2* bn_ab;    // [ntot] BatchNorm affine (EPI_RELU_BN)
@@ -62,6 +64,8 @@ struct FinalizeArgs {
     const float* scale;      // alternative explicit scale [B][C] (or null)
     const float* bias;       // alternative explicit bias [B][C] (or null)
     float2* ab;              // out [B][C]
+    float2* ab1;             // optional out [B][C]: the second style's affine (num_styles == 2)
+    int style1_offset;       // offset of the second style's parameter vector (P)
     float2* mr;              // optional out [B][C] (mean, rstd) for the backward pass
     int affine_bstride;      // image stride of scale/bias (C per image; 0 = per-channel, BatchNorm)
     int merge_images;        // BatchNorm (training): statistics over the whole batch
@@ -78,6 +82,11 @@ hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st);
 // y = act(a*x + b [+ res]) element-wise, act: 0 none, 1 relu, 2 sigmoid.  x,res,y [B][HW][C]
 hipError_t affine_act_launch(const float* x, const float2* ab, const float* res, float* y, int batch, long hw, int C,
                              int act, hipStream_t st);
+// two-style blend: t = a0*x + b0 + w[pixel] * ((a1*x + b1) - (a0*x + b0)), then [+ res], act
+hipError_t affine_act_blend_launch(const float* x, const float2* ab, const float2* ab1, const float* w,
+                                   const float* res, float* y, int batch, long hw, int C, int act, hipStream_t st);
+// TF AvgPool2D(2) (valid) of a one-channel map [B][H][W] -> [B][H/2][W/2]
+hipError_t avgpool2_1ch_launch(const float* x, float* y, int batch, int H, int W, hipStream_t st);
 
 // Per-tile statistics of an NHWC tensor (standalone instance norm).
 hipError_t tile_stats_launch(const float* x, float4* part, int batch, long hw, int C, int tile, hipStream_t st);

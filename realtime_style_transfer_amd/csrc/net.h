@@ -44,6 +44,8 @@ struct LayerExec {
     float* d_out = nullptr;       // raw (CIN) or final (BN) output [max_batch][Ho][Wo][cout]
     float4* d_part = nullptr;
     float2* d_ab = nullptr;       // CIN affine of this layer's output [max_batch][cout]
+    float2* d_ab1 = nullptr;      // second style's CIN affine (num_styles == 2)
+    int out_mip = -1;             // style-weight mip level at this layer's output width (num_styles == 2)
     float* d_mat = nullptr;       // block input materialised by this layer's prologue (or null)
     // prologue (how this layer reads its input)
     int pro = PRO_NONE;
@@ -73,6 +75,12 @@ struct rst_handle {
     rst_shape shape;
     int P = 0;
     std::vector<LayerExec> layers;
+    // two-style blending: AvgPool2 mips of the second style's weight map, keyed by width
+    // (styleTransfer.py:335-345); level 0 is the caller's style_weights (out_h x out_w)
+    std::vector<float*> d_mip;
+    std::vector<int> mip_h, mip_w;
+    float* d_xlast = nullptr;     // blended input of the last (VALU) layer
+    const float* last_style_weights = nullptr;   // for the debug copies of the most recent forward
     std::vector<void*> allocs;
     // optional per-layer timing: 3 events per layer per step (before conv, after conv, after finalize)
     std::vector<hipEvent_t> prof_events;

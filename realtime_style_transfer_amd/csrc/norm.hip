@@ -69,6 +69,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
         }
         const float aa = scale * rstd;
         a.ab[b * a.C + c] = make_float2(aa, bias - (float)mean * aa);
+        if (a.ab1 != nullptr) {   // second style (styleTransfer.py:36-44 blends the affine per pixel)
+            const float* sp1 = a.style + (size_t)b * a.style_stride + a.style1_offset + a.style_offset;
+            const float a1 = sp1[c] * rstd;
+            a.ab1[b * a.C + c] = make_float2(a1, sp1[a.C + c] - (float)mean * a1);
+        }
         if (a.mr != nullptr) a.mr[b * a.C + c] = make_float2((float)mean, rstd);
         if (a.moving_mean != nullptr && b == 0) {
             const double unbiased = n > 1.0 ? m2 / (n - 1.0) : var;
@@ -104,6 +109,58 @@ hipError_t affine_act_launch(const float* x, const float2* ab, const float* res,
     long blocks = (total + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(affine_act_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, ab, res, y, total, hw * C, C, act);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void affine_act_blend_kernel(const float* __restrict__ x,
+                                                               const float2* __restrict__ ab,
+                                                               const float2* __restrict__ ab1,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ res, float* __restrict__ y,
+                                                               long total, long hwc, int C, int act) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+        const int b = (int)(i / hwc);
+        const int c = (int)(i % C);
+        const float2 p0 = ab[b * C + c], p1 = ab1[b * C + c];
+        const float xv = x[i];
+        const float y0 = fmaf(p0.x, xv, p0.y), y1 = fmaf(p1.x, xv, p1.y);
+        float v = fmaf(w[i / C], y1 - y0, y0);
+        if (res != nullptr) v += res[i];
+        if (act == 1) v = fmaxf(v, 0.f);
+        else if (act == 2) v = 1.f / (1.f + __expf(-v));
+        y[i] = v;
+    }
+}
+
+hipError_t affine_act_blend_launch(const float* x, const float2* ab, const float2* ab1, const float* w,
+                                   const float* res, float* y, int batch, long hw, int C, int act, hipStream_t st) {
+    const long total = (long)batch * hw * C;
+    long blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(affine_act_blend_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, ab, ab1, w, res, y,
+                       total, hw * C, C, act);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void avgpool2_1ch_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                           int B, int H, int W) {
+    const int Ho = H / 2, Wo = W / 2;
+    const long total = (long)B * Ho * Wo;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+        const int ox = (int)(i % Wo);
+        const int oy = (int)((i / Wo) % Ho);
+        const int b = (int)(i / ((long)Wo * Ho));
+        const float* p = x + ((size_t)b * H + 2 * oy) * W + 2 * ox;
+        y[i] = ((p[0] + p[1]) + (p[W] + p[W + 1])) * 0.25f;
+    }
+}
+
+hipError_t avgpool2_1ch_launch(const float* x, float* y, int batch, int H, int W, hipStream_t st) {
+    const long total = (long)batch * (H / 2) * (W / 2);
+    long blocks = (total + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(avgpool2_1ch_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, batch, H, W);
     return hipGetLastError();
 }
 

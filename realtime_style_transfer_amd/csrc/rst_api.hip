@@ -232,8 +232,10 @@ int rst_create(const rst_shape* shape, const float* weights_host, size_t num_wei
     if (shape == nullptr || out == nullptr || weights_host == nullptr)
         return fail(RST_ERR_INVALID, "rst_create: null argument");
     *out = nullptr;
-    if (shape->num_styles != 1)
-        return fail(RST_ERR_UNSUPPORTED, "rst_create: num_styles > 1 (style_weights blending) not implemented yet");
+    if (shape->num_styles > 2)
+        return fail(RST_ERR_UNSUPPORTED, "rst_create: num_styles > 2: the reference blends style parameters only for "
+                                         "two styles (styleTransfer.py:38-44; for more it returns them unblended, "
+                                         "which does not broadcast against the feature map)");
     if (shape->max_batch <= 0) return fail(RST_ERR_INVALID, "rst_create: max_batch must be positive");
     std::vector<LayerSpec> specs;
     int P = 0;
@@ -278,6 +280,8 @@ int rst_create(const rst_shape* shape, const float* weights_host, size_t num_wei
         } else {
             if ((st = h->alloc(&e.d_part, (size_t)B * e.ntot * e.n_part * sizeof(float4))) != RST_OK) { delete h; return st; }
             if ((st = h->alloc(&e.d_ab, (size_t)B * s.cout * sizeof(float2))) != RST_OK) { delete h; return st; }
+            if (shape->num_styles == 2 &&
+                (st = h->alloc(&e.d_ab1, (size_t)B * s.cout * sizeof(float2))) != RST_OK) { delete h; return st; }
         }
         if ((st = h->alloc(&e.d_out, (size_t)B * s.Ho * s.Wo * s.cout * 4)) != RST_OK) { delete h; return st; }
     }
@@ -306,6 +310,37 @@ int rst_create(const rst_shape* shape, const float* weights_host, size_t num_wei
         }
         if (e.s.res_block >= 1 && e.s.res_conv == 0) block_input = e.d_mat;
     }
+    // two styles: the style-weight mip chain (AvgPool2 keyed by width, num_expand_blocks + 1 levels)
+    if (shape->num_styles == 2) {
+        int mh = shape->out_h, mw = shape->out_w;
+        h->d_mip.push_back(nullptr);   // level 0: the caller's style_weights
+        h->mip_h.push_back(mh);
+        h->mip_w.push_back(mw);
+        int n_e = 0;
+        for (auto& s : specs)
+            if (s.keras_kind == 1 && s.stride == 2) ++n_e;
+        for (int k = 0; k < n_e + 1; ++k) {
+            mh /= 2;
+            mw /= 2;
+            float* m = nullptr;
+            if ((st = h->alloc(&m, (size_t)B * std::max(mh, 1) * std::max(mw, 1) * 4)) != RST_OK) { delete h; return st; }
+            h->d_mip.push_back(m);
+            h->mip_h.push_back(mh);
+            h->mip_w.push_back(mw);
+        }
+        for (auto& e : h->layers) {
+            if (e.s.norm != N_CIN) continue;
+            for (size_t k = 0; k < h->mip_w.size(); ++k)
+                if (h->mip_w[k] == e.s.Wo && h->mip_h[k] == e.s.Ho) e.out_mip = (int)k;
+            if (e.out_mip < 0) {
+                delete h;
+                return fail(RST_ERR_UNSUPPORTED, "no style-weight mip matches layer " + e.s.name + " (" +
+                                                     std::to_string(e.s.Ho) + "x" + std::to_string(e.s.Wo) + ")");
+            }
+        }
+        const LayerExec& last = h->layers.back();
+        if ((st = h->alloc(&h->d_xlast, (size_t)B * last.s.H * last.s.W * last.s.cin * 4)) != RST_OK) { delete h; return st; }
+    }
     // kernels with > 64 KB of dynamic LDS need the attribute before any (graph-captured) launch
     for (auto& e : h->layers) {
         if (e.kind == K_SMALL) continue;
@@ -321,18 +356,33 @@ int rst_create(const rst_shape* shape, const float* weights_host, size_t num_wei
 
 void rst_destroy(rst_handle* h) { delete h; }
 
-static int launch_layer(rst_handle* h, size_t li, const float* content, const float* style, int B, hipStream_t st) {
+static const float* mip_ptr(const rst_handle* h, int level, const float* style_weights) {
+    if (level < 0) return nullptr;
+    return level == 0 ? style_weights : h->d_mip[level];
+}
+
+static int launch_layer(rst_handle* h, size_t li, const float* content, const float* style, const float* sw, int B,
+                        hipStream_t st) {
     LayerExec& e = h->layers[li];
+    const bool two = h->shape.num_styles == 2;
     hipEvent_t* ev = nullptr;
     if (h->prof_on && h->prof_step < h->prof_max_steps)
         ev = &h->prof_events[((size_t)h->prof_step * h->layers.size() + li) * 3];
     if (ev) HIP_TRY(hipEventRecord(ev[0], st));
     const float* in = (e.pro_src < 0) ? content : h->layers[e.pro_src].d_out;
     const float2* pro_ab = (e.pro_src >= 0 && e.pro != PRO_NONE) ? h->layers[e.pro_src].d_ab : nullptr;
+    const bool blend = two && pro_ab != nullptr;
+    const LayerExec* src = e.pro_src >= 0 ? &h->layers[e.pro_src] : nullptr;
     if (e.kind == K_SMALL) {
         SmallConvArgs a{};
         a.in = in;
         a.pro_ab = pro_ab;
+        if (blend) {   // the VALU kernel has no blend prologue: materialise its blended input first
+            HIP_TRY(affine_act_blend_launch(in, pro_ab, src->d_ab1, mip_ptr(h, src->out_mip, sw), nullptr, h->d_xlast,
+                                            B, (long)e.s.H * e.s.W, e.s.cin, 1, st));
+            a.in = h->d_xlast;
+            a.pro_ab = nullptr;
+        }
         a.w = e.d_w;
         a.bias = e.d_bias;
         a.out = e.d_out;
@@ -352,6 +402,10 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.res = e.pro_res;
         a.mat = e.d_mat;
         a.pro_ab = pro_ab;
+        if (blend) {
+            a.pro_ab1 = src->d_ab1;
+            a.pro_w = mip_ptr(h, src->out_mip, sw);
+        }
         a.wpk = e.d_w;
         a.bias = e.d_bias;
         a.bn_ab = e.d_bn;
@@ -389,6 +443,10 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         f.phases = e.kind == K_CONVT2 ? 4 : 1;
         f.style_stride = h->shape.num_styles * h->P;
         f.style_offset = e.s.style_offset;
+        if (two) {
+            f.ab1 = e.d_ab1;
+            f.style1_offset = h->P;
+        }
         f.eps = 1e-5f;
         HIP_TRY(finalize_launch(f, st));
     }
@@ -405,13 +463,23 @@ int rst_forward(rst_handle* h, const float* content, const float* style_params, 
                                          std::to_string(h->shape.max_batch) + "]");
     if (style_weights != nullptr && h->shape.num_styles == 1)
         return fail(RST_ERR_INVALID, "rst_forward: style_weights given but num_styles == 1");
+    if (style_weights == nullptr && h->shape.num_styles == 2)
+        return fail(RST_ERR_INVALID, "rst_forward: num_styles == 2 needs style_weights (B, out_h, out_w, 1)");
     hipStream_t st = static_cast<hipStream_t>(stream);
+    for (size_t k = 1; k < h->d_mip.size(); ++k)
+        HIP_TRY(avgpool2_1ch_launch(mip_ptr(h, (int)k - 1, style_weights), h->d_mip[k], batch, h->mip_h[k - 1],
+                                    h->mip_w[k - 1], st));
     for (size_t li = 0; li < h->layers.size(); ++li) {
-        int r = launch_layer(h, li, content, style_params, batch, st);
+        int r = launch_layer(h, li, content, style_params, style_weights, batch, st);
         if (r != RST_OK) return r;
     }
     const LayerExec& last = h->layers.back();
-    HIP_TRY(affine_act_launch(last.d_out, last.d_ab, nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
+    if (h->shape.num_styles == 2)
+        HIP_TRY(affine_act_blend_launch(last.d_out, last.d_ab, last.d_ab1, mip_ptr(h, last.out_mip, style_weights),
+                                        nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
+    else
+        HIP_TRY(affine_act_launch(last.d_out, last.d_ab, nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
+    h->last_style_weights = style_weights;
     if (h->prof_on && h->prof_step < h->prof_max_steps) h->prof_step++;
     return RST_OK;
 }
@@ -475,7 +543,12 @@ int rst_copy_activation(rst_handle* h, int idx, float* dst, size_t count, int ba
         HIP_TRY(hipMemcpyAsync(dst, e.d_out, n * 4, hipMemcpyDeviceToDevice, st));
     } else {
         const int act = e.s.post == P_RELU ? 1 : (e.s.post == P_SIGMOID ? 2 : 0);
-        HIP_TRY(affine_act_launch(e.d_out, e.d_ab, e.emit_res, dst, batch, (long)e.s.Ho * e.s.Wo, e.s.cout, act, st));
+        if (h->shape.num_styles == 2)
+            HIP_TRY(affine_act_blend_launch(e.d_out, e.d_ab, e.d_ab1, mip_ptr(h, e.out_mip, h->last_style_weights),
+                                            e.emit_res, dst, batch, (long)e.s.Ho * e.s.Wo, e.s.cout, act, st));
+        else
+            HIP_TRY(affine_act_launch(e.d_out, e.d_ab, e.emit_res, dst, batch, (long)e.s.Ho * e.s.Wo, e.s.cout, act,
+                                      st));
     }
     return RST_OK;
 }

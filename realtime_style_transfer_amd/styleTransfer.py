@@ -114,15 +114,24 @@ class StyleTransferModel:
                  stream=None) -> torch.Tensor:
         content = inputs['content']
         style_params = self._check_inputs(content, inputs['style_params'])
-        if 'style_weights' in inputs and self.num_styles == 1:
+        B = content.shape[0]
+        sw = inputs.get('style_weights')
+        if sw is not None and self.num_styles == 1:
             raise ValueError("style_weights given but num_styles == 1")
+        if self.num_styles > 1:
+            # styleTransfer.py:290-296: (B, out_h, out_w, S-1), the first style's weight is 1 - sum
+            want = (B, self.output_shape[0], self.output_shape[1], self.num_styles - 1)
+            if sw is None or tuple(sw.shape) != want:
+                raise ValueError(f"style_weights must be {want} for num_styles={self.num_styles}, got "
+                                 f"{None if sw is None else tuple(sw.shape)}")
+            sw = sw.contiguous()
         content = content.contiguous()
         style_params = style_params.contiguous()
-        B = content.shape[0]
         if out is None:
             out = torch.empty((B,) + self.output_shape, dtype=torch.float32, device=content.device)
-        _lib.check(_lib.load().rst_forward(self._handle, _lib.dev_ptr(content), _lib.dev_ptr(style_params), None,
-                                           _lib.dev_ptr(out), B, _lib.stream_ptr(stream)))
+        _lib.check(_lib.load().rst_forward(self._handle, _lib.dev_ptr(content), _lib.dev_ptr(style_params),
+                                           None if sw is None else _lib.dev_ptr(sw), _lib.dev_ptr(out), B,
+                                           _lib.stream_ptr(stream)))
         return out
 
     predict = __call__

@@ -12,6 +12,9 @@ Fixtures (all float32 inputs/weights, float64 expected outputs, npz):
 * apply_style_weights_kat.npz — the reference's only numeric known-answer test,
   models/styleTransferTest.py:12-49, recomputed from its formula.
 * gram_loss.npz — gram matrices / mean_l2 / total_variation of seeded tensors.
+* transfer_two_styles.npz — config (i) with num_styles=2: per-pixel blending of the CIN
+  parameters with a (B, 32, 64, 1) style-weight map and its AvgPool2 mips
+  (styleTransfer.py:36-44, 288-303, 335-345).
 Each transfer fixture also stores ``stats`` in the metrics.get_stats format
 (realtime_style_transfer/metrics.py:4-12: mean/var/min/max).
 """
@@ -34,14 +37,22 @@ def stats(t):
     return np.array([np.mean(t), np.var(t), np.min(t), np.max(t)])
 
 
-def transfer_fixture(name, ins, outs, bres, bf, batch=2):
-    plan = network_plan(ins, outs, bres, bf)
+def transfer_fixture(name, ins, outs, bres, bf, batch=2, num_styles=1):
+    plan = network_plan(ins, outs, bres, bf, num_styles)
     w = init_weights(plan, seed=2)
-    sp = synthetic_style_params(batch, 1, plan.num_style_params, plan, seed=1)
+    sp = synthetic_style_params(batch, num_styles, plan.num_style_params, plan, seed=1)
     x = np.random.default_rng(0).random((batch,) + tuple(ins)).astype(np.float32)
-    y, inter = R.transfer_forward(x, sp, w, ins, outs, bres, bf, return_intermediates=True)
+    sw = None
+    if num_styles > 1:
+        # smooth left-to-right blend plus noise, in [0, 1]
+        ramp = np.linspace(0.0, 1.0, outs[1], dtype=np.float32)[None, None, :, None]
+        noise = np.random.default_rng(4).random((batch, outs[0], outs[1], num_styles - 1)).astype(np.float32)
+        sw = (0.8 * ramp + 0.2 * noise).astype(np.float32)
+    y, inter = R.transfer_forward(x, sp, w, ins, outs, bres, bf, style_weights=sw, return_intermediates=True)
     arrays = {'content': x, 'style_params': sp, 'output': y, 'stats': stats(y),
               'shape': np.array(list(ins) + list(outs) + [bres, bf])}
+    if sw is not None:
+        arrays['style_weights'] = sw
     for i, wi in enumerate(w):
         arrays[f'w{i:02d}'] = wi
     np.savez_compressed(os.path.join(HERE, name), **arrays)
@@ -84,8 +95,16 @@ def gram_fixture():
 
 
 if __name__ == '__main__':
-    transfer_fixture('transfer_small.npz', (32, 64, 17), (32, 64, 3), 8, 8)
-    transfer_fixture('transfer_up.npz', (24, 48, 3), (48, 96, 3), 3, 4)
-    kat_fixture()
-    gram_fixture()
+    only = sys.argv[1:]
+    jobs = {
+        'transfer_small.npz': lambda: transfer_fixture('transfer_small.npz', (32, 64, 17), (32, 64, 3), 8, 8),
+        'transfer_up.npz': lambda: transfer_fixture('transfer_up.npz', (24, 48, 3), (48, 96, 3), 3, 4),
+        'apply_style_weights_kat.npz': kat_fixture,
+        'gram_loss.npz': gram_fixture,
+        'transfer_two_styles.npz': lambda: transfer_fixture('transfer_two_styles.npz', (32, 64, 17), (32, 64, 3), 8, 8,
+                                                            num_styles=2),
+    }
+    for name, job in jobs.items():
+        if not only or name in only:
+            job()
     print('golden fixtures written to', HERE)

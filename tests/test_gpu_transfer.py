@@ -140,3 +140,28 @@ def test_instance_norm_op():
     ref = torch.relu(bias.double()[:, None, None, :] + (xd - mean) / torch.sqrt(var + 1e-5) *
                      scale.double()[:, None, None, :])
     assert (y.double() - ref).abs().max().item() < 1e-4
+
+
+def test_two_style_blending_matches_golden():
+    """num_styles=2: per-pixel blend of the CIN parameters with the style-weight mips."""
+    _need_gpu()
+    import os
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    d = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'transfer_two_styles.npz'))
+    ws = [d[k] for k in sorted(k for k in d.files if k.startswith('w') and k[1:].isdigit())]
+    shape = d['shape']
+    ins, outs, bres, bf = tuple(shape[0:3]), tuple(shape[3:6]), int(shape[6]), int(shape[7])
+    model, P = create_style_transfer_model(ins, outs, bres, bf, 2, weights=ws, max_batch=2)
+    inputs = {'content': torch.from_numpy(d['content']).cuda(), 'style_params': torch.from_numpy(d['style_params']).cuda(),
+              'style_weights': torch.from_numpy(d['style_weights']).cuda()}
+    y = model(inputs).cpu().numpy()
+    assert np.abs(y - d['output']).max() < 2e-5, np.abs(y - d['output']).max()
+    # limits: all-zero / all-one weights == single-style model with style 0 / style 1
+    single, _ = create_style_transfer_model(ins, outs, bres, bf, 1, weights=ws, max_batch=2)
+    for val, s in ((0.0, 0), (1.0, 1)):
+        inputs['style_weights'] = torch.full_like(inputs['style_weights'], val)
+        y2 = model(inputs).cpu().numpy()
+        y1 = single({'content': inputs['content'], 'style_params': inputs['style_params'][:, s:s + 1].contiguous()})
+        assert np.abs(y2 - y1.cpu().numpy()).max() < 1e-5
+    with pytest.raises(ValueError):
+        model({'content': inputs['content'], 'style_params': inputs['style_params']})   # weights missing

@@ -96,6 +96,6 @@ def test_create_rejects_bad_arguments_without_device_work():
     w = np.zeros(10, np.float32)
     rc = lib.rst_create(ctypes.byref(shape), w.ctypes.data, w.size, ctypes.byref(h))
     assert rc == L.RST_ERR_INVALID and b"expected" in lib.rst_last_error()
-    shape2 = L.RstShape(32, 64, 17, 32, 64, 8, 8, 2, 1)
-    rc = lib.rst_create(ctypes.byref(shape2), w.ctypes.data, w.size, ctypes.byref(h))
+    shape3 = L.RstShape(32, 64, 17, 32, 64, 8, 8, 3, 1)   # the reference blends only two styles
+    rc = lib.rst_create(ctypes.byref(shape3), w.ctypes.data, w.size, ctypes.byref(h))
     assert rc == L.RST_ERR_UNSUPPORTED

@@ -108,3 +108,20 @@ def test_gram_and_loss_terms_golden():
     tv = np.abs(np.diff(img, axis=1)).sum(axis=(1, 2, 3)) + np.abs(np.diff(img, axis=2)).sum(axis=(1, 2, 3))
     np.testing.assert_allclose(d['tv'], tv, atol=1e-9)
     np.testing.assert_allclose(R.mean_l2_loss_on_batch(d['img'] - 0.5), d['l2'], atol=1e-12)
+
+
+def test_two_style_golden_and_limits():
+    """num_styles=2 (styleTransfer.py:36-44, 288-303, 335-345): the oracle reproduces its fixture, and a
+    weight map of all 0 (all 1) gives the single-style network with style 0's (style 1's) parameters."""
+    d = np.load(os.path.join(GOLDEN, 'transfer_two_styles.npz'))
+    ws = [d[k] for k in sorted(k for k in d.files if k.startswith('w') and k[1:].isdigit())]
+    shape = d['shape']
+    ins, outs, bres, bf = tuple(shape[0:3]), tuple(shape[3:6]), int(shape[6]), int(shape[7])
+    y = R.transfer_forward(d['content'], d['style_params'], ws, ins, outs, bres, bf, style_weights=d['style_weights'])
+    np.testing.assert_allclose(y, d['output'], rtol=0, atol=1e-12)
+    sp = d['style_params']
+    for val, s in ((0.0, 0), (1.0, 1)):
+        sw = np.full_like(d['style_weights'], val)
+        y2 = R.transfer_forward(d['content'], sp, ws, ins, outs, bres, bf, style_weights=sw)
+        y1 = R.transfer_forward(d['content'], sp[:, s:s + 1], ws, ins, outs, bres, bf)
+        np.testing.assert_allclose(y2, y1, rtol=0, atol=1e-12)
