@@ -35,6 +35,7 @@ from realtime_style_transfer_amd.shape_config import ShapeConfig  # noqa: E402
 SPEC = "rst-960-120-128-17"
 METRIC = "stylized FPS/GPU at 960p×17ch (rst-960-120-128-17); max-abs Δ vs TF ref"
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: Peak FP32 (matrix) = vector peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: Peak BF16 MFMA ~2.5 PF dense
 HBM_PEAK_GBS = 8000.0
 
 
@@ -53,6 +54,9 @@ KERNEL_NAMES = {
     10: "conv_mfma<2x2 phase CK32 NT32>", 11: "conv_mfma<2x2 phase CK16 NT32>", 12: "conv_mfma<2x2 phase CK8 NT32>",
     13: "conv_mfma<3x3 s1 CK16 NT32>", 14: "conv_mfma<3x3 s2 CK4 NT32>", 15: "conv_mfma<3x3 s1 CK4 NT32>",
     16: "conv_mfma<2x2 phase CK4 NT32>", 17: "conv_mfma<3x3 s1 CK32 NT64>", 100: "small_conv_kernel<9x9 Cout3 VALU>",
+    101: "conv_bf3<3x3 s1 CK32 NT128 bf16x3>", 102: "conv_bf3<3x3 s1 CK32 NT64 bf16x3>",
+    111: "conv_bf3<3x3 s1 CK32 NT128 bf16x6>", 112: "conv_bf3<3x3 s1 CK32 NT64 bf16x6>",
+    113: "conv_bf3<3x3 s1 CK32 NT64 8x16 bf16x6>",
 }
 
 
@@ -84,11 +88,52 @@ def train_flops_per_sample(plan, H, W) -> dict:
             "gram_fwd_x2_bwd_x1": 3 * gram}
 
 
-def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed):
+def bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs, timed, precision):
+    """The same B=1 hipGraph frame loop with a split-bf16 precision mode on the residual convs."""
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    B = args.batch
+    model, _ = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                           weights=weights, max_batch=B, device=dev, precision=precision)
+    out = torch.empty((B,) + outs, dtype=torch.float32, device=dev)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        model(inputs, out=out)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        model(inputs, out=out)
+    for _ in range(args.warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    el = timed(g.replay, args.steps)
+    model.profile_begin(args.steps)
+    timed(lambda: model(inputs, out=out), args.steps)
+    conv_ms, _, nsteps = model.profile_end()
+    ids = [model.layer_kernel_id(i) for i in range(len(plan.layers))]
+    bf3 = [i for i, k in enumerate(ids) if k >= 101]
+    terms = 3 if precision == "bf16x3" else 6
+    ms = sum(conv_ms[i] for i in bf3) / max(nsteps, 1) / max(len(bf3), 1)
+    fl = sum(layer_flops(plan.layers[i]) for i in bf3) * B / max(len(bf3), 1)
+    eff_tf = fl / (ms * 1e-3) / 1e12
+    return model, {
+        "value": round(world * B * args.steps / el, 3), "unit": "frames/s", "ms_per_step": round(el * 1e3 / args.steps, 4),
+        "dtype": ("fp32 via 2-piece split bf16 (3 product terms, 16 significant bits per operand)" if terms == 3 else
+                  "fp32 via exact 3-piece split bf16 (24 significant bits, 6 product terms, dropped terms <= 2^-24)") +
+                 ", fp32 accumulate, on the residual convs; other layers fp32 MFMA",
+        "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES.get(ids[bf3[0]], "?") if bf3 else None,
+                     "achieved": round(terms * eff_tf, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s (bf16 MFMA)",
+                     "frac": round(terms * eff_tf / BF16_MFMA_PEAK_TFLOPS, 4), "avg_launch_ms": round(ms, 5),
+                     "fp32_equivalent_tflops": round(eff_tf, 2)},
+        "layers_ms": [round(c / max(nsteps, 1), 4) for c in conv_ms],
+    }
+
+
+def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed, precision="fp32"):
     from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
     from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
     TB = args.train_batch
-    lm = StyleLossModelVGG(outs, max_batch=TB, device=dev)
+    lm = StyleLossModelVGG(outs, max_batch=TB, device=dev, precision=precision)
     tr = StyleTransferTrainingModel(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, loss_model=lm,
                                     weights=weights, max_batch=TB, device=dev)
     rng = np.random.default_rng(3000 + rank)
@@ -108,7 +153,12 @@ def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, tim
     return {"workload": f"{SPEC} train_network.py step (BASELINE config 4): training-mode forward, VGG16/Gram loss "
                         f"(no depth term), backward, " + ("RCCL gradient all-reduce (SUM), " if world > 1 else "") +
                         "RMSprop", "batch_per_gpu": TB, "steps": args.train_steps, "ms_per_step": round(ms, 3),
-            "frames_per_s": round(world * TB * args.train_steps / el, 3), "dtype": "fp32 (f32 MFMA)",
+            "frames_per_s": round(world * TB * args.train_steps / el, 3),
+            "dtype": {"fp32": "fp32 (f32 MFMA)",
+                      "bf16x6": "VGG16 3x3 convs: exact 3-piece split bf16 MFMA (fp32-level products, fp32 accumulate); "
+                                "transfer net and the rest fp32",
+                      "bf16x3": "VGG16 3x3 convs: 2-piece split bf16 MFMA (16-bit operands, fp32 accumulate); "
+                                "transfer net and the rest fp32"}[precision],
             "tflop_per_sample": round(per_sample / 1e12, 4),
             "achieved_tflops_per_gpu": round(tfs, 2), "frac_fp32_mfma_peak": round(tfs / FP32_MFMA_PEAK_TFLOPS, 4),
             "flop_breakdown_per_sample_gflop": {k: round(v / 1e9, 2) for k, v in fl.items()},
@@ -128,6 +178,7 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
     ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--no-bf16x3", action="store_true", help="skip the split-bf16 precision-mode measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -273,10 +324,23 @@ def main():
             te = float(t.item())
         stream_fps = world * SB * reps / te
 
+    # ---------------- precision mode: split-bf16 residual convs (reported beside the fp32 headline) --
+    split_models, split = {}, {}
+    if not args.no_bf16x3:
+        for prec in ("bf16x6", "bf16x3"):
+            split_models[prec], split[prec] = bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs,
+                                                          timed, prec)
+
     # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
     train = None
     if args.train_batch > 0:
-        train = bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed)
+        # BASELINE config 4 trains in bf16: the headline training figure uses the split-bf16 VGG16
+        # (bf16x3, more accurate than plain bf16); the fp32 and bf16x6 runs are reported beside it
+        train = bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed, "bf16x3")
+        train["other_precisions"] = {p: {k: v for k, v in bench_training(args, world, rank, dev, cfg, ins, outs, plan,
+                                                                          weights, P, timed, p).items()
+                                         if k in ("ms_per_step", "frames_per_s", "achieved_tflops_per_gpu", "dtype")}
+                                     for p in ("bf16x6", "fp32")}
 
     # ---------------- parity + CPU baseline (rank 0 only, bounded sample) -----------------------
     max_abs = None
@@ -293,6 +357,10 @@ def main():
         y_gpu = model({'content': content[:1].contiguous(), 'style_params': style[:1].contiguous()})
         torch.cuda.synchronize()
         max_abs = float(np.abs(y_gpu.cpu().numpy() - y_ref).max())
+        for prec, m3 in split_models.items():
+            y3 = m3({'content': content[:1].contiguous(), 'style_params': style[:1].contiguous()})
+            torch.cuda.synchronize()
+            split[prec]["max_abs_delta_vs_oracle"] = float(np.abs(y3.cpu().numpy() - y_ref).max())
         n, tsum = 0, 0.0
         while tsum < args.cpu_budget_s and n < 20:
             ts = time.perf_counter()
@@ -348,6 +416,7 @@ def main():
             "stream_graph_fps": None if stream_fps is None else round(stream_fps, 3),
             "stream_graph_batch": args.stream_batch,
             "layers": layer_table,
+            "split_bf16_modes": split,
             "training": train,
             "cpu_baseline": cpu,
         }

@@ -60,6 +60,19 @@ typedef struct rst_handle rst_handle;
 int rst_create(const rst_shape* shape, const float* weights_host, size_t num_weights, rst_handle** out);
 void rst_destroy(rst_handle* h);
 
+/* Arithmetic of the convolutions. FP32: exact f32 products (v_mfma_f32_32x32x2_f32), the default.
+ * BF16X6: each fp32 operand split exactly into three bf16 pieces (8+8+8 = 24 significant bits, the
+ * whole fp32 mantissa) and the six product terms down to 2^-16 accumulated in fp32
+ * (6 x v_mfma_f32_32x32x16_bf16): fp32-level products (dropped terms <= 2^-24) at 6/16 of the
+ * f32-MFMA cost. BF16X3: two pieces, three terms (16 significant bits per operand; TF32,
+ * TensorFlow's default for "fp32" convs on NVIDIA Ampere, keeps 11) at 3/16 of the cost.
+ * The split modes are used for the 3x3 s1 convs with Cin % 32 == 0 (the residual blocks); the
+ * other layers stay FP32. */
+enum { RST_PRECISION_FP32 = 0, RST_PRECISION_BF16X3 = 1, RST_PRECISION_BF16X6 = 2 };
+int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_weights, int precision,
+                  rst_handle** out);
+int rst_precision(const rst_handle* h);
+
 /* Number of style parameters P per style (2662 for rst-960-120-128-17). */
 int rst_num_style_params(const rst_handle* h);
 /* Total weight count expected by rst_create for this shape (no device work). */
@@ -103,6 +116,7 @@ typedef struct rst_loss_shape {
     float content_factor;     /* StyleLossModelVGG: 1e4   (styleLoss.py:101)                      */
     float style_factor;       /*                    1e-3  (styleLoss.py:102)                      */
     float tv_factor;          /*                    1e-1  (styleLoss.py:103)                      */
+    int precision;            /* RST_PRECISION_* of the VGG16 3x3 convs (Cin % 32 == 0)            */
 } rst_loss_shape;
 typedef struct rst_loss_handle rst_loss_handle;
 

@@ -17,10 +17,11 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = _PKG / "librst.so"
 
 RST_OK, RST_ERR_INVALID, RST_ERR_UNSUPPORTED, RST_ERR_HIP, RST_ERR_ALLOC = range(5)
+PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2}   # include/rst.h RST_PRECISION_*
 
 # Symbols declared in include/rst.h — tests check that the library exports all of them.
 EXPORTED_SYMBOLS = [
-    "rst_create", "rst_destroy", "rst_num_style_params", "rst_num_weights_for_shape", "rst_forward",
+    "rst_create", "rst_create_ex", "rst_precision", "rst_destroy", "rst_num_style_params", "rst_num_weights_for_shape", "rst_forward",
     "rst_num_layers", "rst_layer_output_shape", "rst_copy_activation", "rst_gram_workspace_size", "rst_gram",
     "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_last_error", "rst_version",
     "rst_profile_begin", "rst_profile_end", "rst_layer_kernel_id",
@@ -41,7 +42,8 @@ class RstShape(ctypes.Structure):
 
 class RstLossShape(ctypes.Structure):
     _fields_ = [("h", ctypes.c_int), ("w", ctypes.c_int), ("max_batch", ctypes.c_int),
-                ("content_factor", ctypes.c_float), ("style_factor", ctypes.c_float), ("tv_factor", ctypes.c_float)]
+                ("content_factor", ctypes.c_float), ("style_factor", ctypes.c_float), ("tv_factor", ctypes.c_float),
+                ("precision", ctypes.c_int)]
 
 
 class RstError(RuntimeError):
@@ -65,6 +67,10 @@ def load() -> ctypes.CDLL:
     vp, i, sz, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_float
     lib.rst_create.argtypes = [ctypes.POINTER(RstShape), vp, sz, ctypes.POINTER(vp)]
     lib.rst_create.restype = i
+    lib.rst_create_ex.argtypes = [ctypes.POINTER(RstShape), vp, sz, i, ctypes.POINTER(vp)]
+    lib.rst_create_ex.restype = i
+    lib.rst_precision.argtypes = [vp]
+    lib.rst_precision.restype = i
     lib.rst_destroy.argtypes = [vp]
     lib.rst_destroy.restype = None
     lib.rst_num_style_params.argtypes = [vp]

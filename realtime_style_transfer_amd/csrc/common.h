@@ -13,6 +13,9 @@ int set_error(int code, const std::string& msg);
 // Pack a GEMM-form conv kernel Wg[tap][ci][n] (taps = kh*kw, row-major) into the LDS stage image
 // [n_block][cin_chunk][tap_group][tap][kgroup][lane_half][n][VEC] that conv_mfma_kernel stages.
 std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t);
+// Same for the split-bf16 kernel: [n_block][cin_chunk][tap_group][tap][kstep][hi/lo][lane_half][n][8]
+// bf16, returned as the float-sized buffer that holds those bits (2 bf16 per float).
+std::vector<float> pack_conv_tiles_bf3(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t);
 
 }  // namespace rst
 

@@ -1,0 +1,432 @@
+// conv_bf3.hip — implicit-GEMM convolution with fp32-accurate split-bf16 products on gfx950
+// (v_mfma_f32_32x32x16_bf16, 16x the f32-MFMA rate).
+//
+// Every fp32 operand x is split into hi = bf16(x) and lo = bf16(x - hi) (round-to-nearest-even),
+// and each product block is accumulated in fp32 as  A_hi*B_hi + A_hi*B_lo + A_lo*B_hi  — three
+// bf16 MFMAs ("bf16x3"). The representation keeps 16 significant bits per operand; the dropped
+// A_lo*B_lo term is 2^-16 relative. That is ~30x more accurate than TF32 (10-bit mantissa), which
+// TensorFlow uses by default for "fp32" convolutions on NVIDIA Ampere-class GPUs, at 3/16 of the
+// f32-MFMA cost. This is an opt-in precision mode (RST_PRECISION_BF16X3); the exact-f32 kernel
+// (conv_mfma.hip) stays the default.
+//
+// Structure mirrors conv_mfma_kernel (same ConvArgs, prologue and epilogue semantics): output tile
+// TH x TW pixels x NT channels per 4-wave workgroup, stage = (Cin chunk, tap group), weights of the
+// next stage prefetched in registers, LDS images:
+//   halo  [pixel][CK + 8] bf16, hi and lo planes (80-B pixel stride for CK = 32: 5 16-B slots,
+//         conflict-free ds_read_b128 across a 16-lane group)
+//   wts   [tap][kstep][hi/lo][lane half][n][8] bf16 (one ds_read_b128 per B fragment)
+// The prologue (CIN affine / ReLU / residual add / two-style blend / materialise) runs in fp32 and
+// the split happens as the value is written to LDS.
+#include <hip/hip_runtime.h>
+#include <type_traits>
+
+#include "kernels.h"
+
+namespace rst {
+
+namespace {
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef unsigned short ushort4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned short bf16_rne(float x) {
+    const unsigned u = __float_as_uint(x);
+    return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_val(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+// x = p0 + p1 [+ p2]: each remainder is exact in fp32, every piece rounds to the nearest bf16
+template <int NP>
+__device__ __forceinline__ void split_bf16(float x, unsigned short* p) {
+    p[0] = bf16_rne(x);
+    float r = x - bf16_val(p[0]);
+    p[1] = bf16_rne(r);
+    if constexpr (NP == 3) p[2] = bf16_rne(r - bf16_val(p[1]));
+}
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        sfor<I + 1, N>(f);
+    }
+}
+}  // namespace
+
+#define RST_BP int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS, int NP
+#define RST_BA KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP
+
+template <RST_BP>
+struct Bf3Cfg {
+    static constexpr int KS = CK / 16;
+    static constexpr int CSB = CK + 8;
+    static constexpr int HH = (TH - 1) * S + KH;
+    static constexpr int HWD = (TW - 1) * S + KW;
+    static constexpr int HP = HH * HWD;
+    static constexpr int MT = TH * TW / 32;
+    static constexpr int MW = MT / WM;
+    static constexpr int NTILES = NT / 32;
+    static constexpr int NW = NTILES / WN;
+    static constexpr int NTAPS = KH * KW;
+    static constexpr int NGROUPS = NTAPS / TPS;
+    static constexpr int WSTEP = 2 * NT * 8;                  // bf16 per (tap, kstep, plane)
+    static constexpr int WSTAGE = TPS * KS * NP * WSTEP;      // bf16 per stage
+    static constexpr int WCOPY = WSTAGE / 8;                  // 16-B units per stage
+    static constexpr int HALO = ((HP * CSB + 7) / 8) * 8;     // bf16 per plane
+    static constexpr int MAX_CIN = 256;
+    static constexpr size_t LDS_BYTES = (size_t)(NP * HALO + 2 * WSTAGE) * 2 + 2 * MAX_CIN * 8;
+    static_assert(NP == 2 || NP == 3, "two (bf16x3) or three (bf16x6) planes");
+    static_assert(CK % 16 == 0, "bf16 k-steps of 16 channels");
+    static_assert(WM * WN == 4 && MT % WM == 0 && NTILES % WN == 0, "4-wave tiling");
+    static_assert(NTAPS % TPS == 0, "taps per stage");
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+template <int WCOPY>
+struct Bf3WeightRegs {
+    static constexpr int N = (WCOPY + 255) / 256;
+    f32x4 r[N];
+    __device__ __forceinline__ void load(const unsigned short* __restrict__ src, int tid) {
+        sfor<0, N>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int idx = k * 256 + tid;
+            if (WCOPY % 256 == 0 || (k + 1) * 256 <= WCOPY || idx < WCOPY)
+                r[k] = reinterpret_cast<const f32x4*>(src)[idx];
+        });
+    }
+    __device__ __forceinline__ void store(unsigned short* dst, int tid) const {
+        sfor<0, N>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int idx = k * 256 + tid;
+            if (WCOPY % 256 == 0 || (k + 1) * 256 <= WCOPY || idx < WCOPY)
+                reinterpret_cast<f32x4*>(dst)[idx] = r[k];
+        });
+    }
+};
+
+__device__ __forceinline__ float bf3_pro(int mode, float x, float2 ab, float r) {
+    float y = fmaf(ab.x, x, ab.y);
+    if (mode == PRO_AFF_RELU) y = fmaxf(y, 0.f);
+    else if (mode == PRO_AFF_RES) y = r + y;
+    return y;
+}
+__device__ __forceinline__ float bf3_pro_blend(int mode, float x, float2 ab, float2 ab1, float w, float r) {
+    const float y0 = fmaf(ab.x, x, ab.y), y1 = fmaf(ab1.x, x, ab1.y);
+    float y = fmaf(w, y1 - y0, y0);
+    if (mode == PRO_AFF_RELU) y = fmaxf(y, 0.f);
+    else if (mode == PRO_AFF_RES) y = r + y;
+    return y;
+}
+
+template <RST_BP>
+__global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
+    using C = Bf3Cfg<RST_BA>;
+    constexpr int CSB = C::CSB, HWD = C::HWD, HP = C::HP, MW = C::MW, NW = C::NW, KS = C::KS;
+    constexpr int HQ = CK / 4;   // float4 per halo pixel
+
+    extern __shared__ __attribute__((aligned(16))) unsigned short smem_b[];
+    unsigned short* halo = smem_b;   // NP planes of C::HALO
+    unsigned short* wts0 = smem_b + NP * C::HALO;
+    float2* pab = reinterpret_cast<float2*>(wts0 + 2 * C::WSTAGE);
+    float2* pab1 = pab + C::MAX_CIN;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int li = lane & 31, lh = lane >> 5;
+
+    int bid = blockIdx.x;
+    const int nb = bid % a.n_blocks;
+    bid /= a.n_blocks;
+    const int tx = bid % a.tiles_x;
+    bid /= a.tiles_x;
+    const int ty = bid % a.tiles_y;
+    const int b = bid / a.tiles_y;
+    const int y0 = ty * TH, x0 = tx * TW;
+    const int iy0 = y0 * S - a.pad_t, ix0 = x0 * S - a.pad_l;
+    const int Cin = a.cin;
+    const int pro = a.pro_mode;
+    const bool do_mat = (a.mat != nullptr) && nb == 0;
+    const bool blend = a.pro_w != nullptr;
+    const size_t img_base = (size_t)b * a.H * a.W;
+    const unsigned short* wsrc = reinterpret_cast<const unsigned short*>(a.wpk) +
+                                 (size_t)nb * a.nchunks * C::NGROUPS * C::WSTAGE;
+    const int n_stages = a.nchunks * C::NGROUPS;
+
+    int pixoff[MW];
+#pragma unroll
+    for (int m = 0; m < MW; ++m) {
+        const int p = (wm * MW + m) * 32 + li;
+        const int pr = p / TW, pc = p % TW;
+        pixoff[m] = ((pr * S) * HWD + pc * S) * CSB + lh * 8;
+    }
+    int woff[NW];
+#pragma unroll
+    for (int n = 0; n < NW; ++n) woff[n] = (lh * NT + (wn * NW + n) * 32 + li) * 8;
+
+    floatx16 acc[MW][NW];
+#pragma unroll
+    for (int m = 0; m < MW; ++m)
+#pragma unroll
+        for (int n = 0; n < NW; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+
+    // synchronous staging of one Cin chunk: fp32 load -> prologue transform -> split into the planes
+    auto stage_halo = [&](int chunk) __attribute__((always_inline)) {
+        for (int it = tid; it < HP * HQ; it += 256) {
+            const int hp = it / HQ, q = it - (it / HQ) * HQ;
+            const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
+            const int iy = iy0 + hy, ix = ix0 + hx;
+            const int c = chunk * CK + q * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c < Cin) {
+                const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
+                v = *reinterpret_cast<const float4*>(a.in + gi);
+                if (pro == PRO_MASK) {   // ReLU backward: gradient masked by the forward output
+                    const float4 r = *reinterpret_cast<const float4*>(a.res + gi);
+                    v.x = r.x > 0.f ? v.x : 0.f;
+                    v.y = r.y > 0.f ? v.y : 0.f;
+                    v.z = r.z > 0.f ? v.z : 0.f;
+                    v.w = r.w > 0.f ? v.w : 0.f;
+                } else if (pro != PRO_NONE) {
+                    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (pro == PRO_AFF_RES) r = *reinterpret_cast<const float4*>(a.res + gi);
+                    if (blend) {
+                        const float wpx = a.pro_w[img_base + (size_t)iy * a.W + ix];
+                        v.x = bf3_pro_blend(pro, v.x, pab[c + 0], pab1[c + 0], wpx, r.x);
+                        v.y = bf3_pro_blend(pro, v.y, pab[c + 1], pab1[c + 1], wpx, r.y);
+                        v.z = bf3_pro_blend(pro, v.z, pab[c + 2], pab1[c + 2], wpx, r.z);
+                        v.w = bf3_pro_blend(pro, v.w, pab[c + 3], pab1[c + 3], wpx, r.w);
+                    } else {
+                        v.x = bf3_pro(pro, v.x, pab[c + 0], r.x);
+                        v.y = bf3_pro(pro, v.y, pab[c + 1], r.y);
+                        v.z = bf3_pro(pro, v.z, pab[c + 2], r.z);
+                        v.w = bf3_pro(pro, v.w, pab[c + 3], r.w);
+                    }
+                    if (do_mat && iy >= y0 * S && iy < (y0 + TH) * S && ix >= x0 * S && ix < (x0 + TW) * S)
+                        *reinterpret_cast<float4*>(a.mat + gi) = v;
+                }
+            }
+            unsigned short px[4][3];
+            split_bf16<NP>(v.x, px[0]);
+            split_bf16<NP>(v.y, px[1]);
+            split_bf16<NP>(v.z, px[2]);
+            split_bf16<NP>(v.w, px[3]);
+#pragma unroll
+            for (int pl = 0; pl < NP; ++pl) {
+                const ushort4v p4 = {px[0][pl], px[1][pl], px[2][pl], px[3][pl]};
+                *reinterpret_cast<ushort4v*>(halo + pl * C::HALO + hp * CSB + q * 4) = p4;
+            }
+        }
+    };
+
+    if (pro != PRO_NONE && a.pro_ab != nullptr) {
+        for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[b * Cin + c];
+        if (blend)
+            for (int c = tid; c < Cin; c += 256) pab1[c] = a.pro_ab1[b * Cin + c];
+        __syncthreads();
+    }
+    {
+        Bf3WeightRegs<C::WCOPY> w0;
+        w0.load(wsrc, tid);
+        stage_halo(0);
+        w0.store(wts0, tid);
+    }
+    __syncthreads();
+
+    for (int s = 0; s < n_stages; ++s) {
+        const int chunk = s / C::NGROUPS;
+        const int g = s - chunk * C::NGROUPS;
+        const int s_next = (s + 1 < n_stages) ? s + 1 : s;
+        const unsigned short* wts = wts0 + (s & 1) * C::WSTAGE;
+        Bf3WeightRegs<C::WCOPY> wnext;
+        wnext.load(wsrc + (size_t)s_next * C::WSTAGE, tid);
+        {
+            constexpr int U = TPS * KS;
+            short8 af[2][NP][MW], bf[2][NP][NW];
+            auto read_step = [&](int u, int slot) __attribute__((always_inline)) {
+                const int t = u / KS, ks = u - (u / KS) * KS;
+                const int tap = g * TPS + t;
+                const int ky = tap / KW, kx = tap - (tap / KW) * KW;
+                const int off = (ky * HWD + kx) * CSB + ks * 16;
+                const unsigned short* wb = wts + (t * KS + ks) * NP * C::WSTEP;
+#pragma unroll
+                for (int pl = 0; pl < NP; ++pl) {
+#pragma unroll
+                    for (int m = 0; m < MW; ++m)
+                        af[slot][pl][m] = *reinterpret_cast<const short8*>(halo + pl * C::HALO + pixoff[m] + off);
+#pragma unroll
+                    for (int n = 0; n < NW; ++n)
+                        bf[slot][pl][n] = *reinterpret_cast<const short8*>(wb + pl * C::WSTEP + woff[n]);
+                }
+            };
+            read_step(0, 0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (u + 1 < U) read_step(u + 1, (u + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+                const int sl = u & 1;
+#pragma unroll
+                for (int m = 0; m < MW; ++m)
+#pragma unroll
+                    for (int n = 0; n < NW; ++n) {
+                        // small terms first: 2^-16 (NP == 3), then 2^-8, then 2^0
+                        if constexpr (NP == 3) {
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][0][m], bf[sl][2][n], acc[m][n], 0, 0, 0);
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][1][m], bf[sl][1][n], acc[m][n], 0, 0, 0);
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][2][m], bf[sl][0][n], acc[m][n], 0, 0, 0);
+                        }
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][0][m], bf[sl][1][n], acc[m][n], 0, 0, 0);
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][1][m], bf[sl][0][n], acc[m][n], 0, 0, 0);
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][0][m], bf[sl][0][n], acc[m][n], 0, 0, 0);
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        wnext.store(wts0 + ((s + 1) & 1) * C::WSTAGE, tid);
+        __syncthreads();
+        if (g == C::NGROUPS - 1 && chunk + 1 < a.nchunks) {
+            stage_halo(chunk + 1);
+            __syncthreads();
+        }
+    }
+
+    // ---------------- epilogue (as conv_mfma_kernel) ------------------------------------------
+    const int epi = a.epi_mode;
+    const int n_mtiles = a.tiles_y * a.tiles_x * C::MT;
+#pragma unroll
+    for (int n = 0; n < NW; ++n) {
+        const int ng = nb * NT + (wn * NW + n) * 32 + li;
+        const bool nvalid = ng < a.ntot;
+        const float bias = nvalid ? a.bias[ng] : 0.f;
+        float2 bn = make_float2(1.f, 0.f);
+        if (epi == EPI_RELU_BN && nvalid) bn = a.bn_ab[ng];
+        int co = ng, py = 0, px = 0;
+        if (a.shuffle) {
+            const int ph = ng / a.cout;
+            co = ng - ph * a.cout;
+            py = ph >> 1;
+            px = ph & 1;
+        }
+#pragma unroll
+        for (int m = 0; m < MW; ++m) {
+            const int mt = wm * MW + m;
+            float s = 0.f, cnt = 0.f;
+            float vals[16];
+            bool ok[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int p = mt * 32 + row;
+                const int oy = y0 + p / TW, ox = x0 + p % TW;
+                const bool valid = nvalid && oy < a.Ho && ox < a.Wo;
+                float v = acc[m][n][r] + bias;
+                if (epi == EPI_RELU_BN) {
+                    v = fmaxf(v, 0.f);
+                    v = fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                } else if (epi == EPI_RELU_STATS) {
+                    v = fmaxf(v, 0.f);
+                }
+                vals[r] = v;
+                ok[r] = valid;
+                if (valid) {
+                    size_t oi;
+                    if (a.shuffle)
+                        oi = (((size_t)b * (2 * a.Ho) + 2 * oy + py) * (2 * a.Wo) + 2 * ox + px) * a.cout + co;
+                    else
+                        oi = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ng;
+                    a.out[oi] = v;
+                    s += v;
+                    cnt += 1.f;
+                }
+            }
+            if (a.part != nullptr) {
+                s += __shfl_xor(s, 32);
+                cnt += __shfl_xor(cnt, 32);
+                const float mean = cnt > 0.f ? s / cnt : 0.f;
+                float m2 = 0.f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float d = vals[r] - mean;
+                    if (ok[r]) m2 = fmaf(d, d, m2);
+                }
+                m2 += __shfl_xor(m2, 32);
+                if (lh == 0 && nvalid) {
+                    const int mtg = (ty * a.tiles_x + tx) * C::MT + mt;
+                    a.part[((size_t)b * a.ntot + ng) * n_mtiles + mtg] = make_float4(s, m2, cnt, 0.f);
+                }
+            }
+        }
+    }
+}
+
+// ---- host side ---------------------------------------------------------------------------------
+template <RST_BP>
+static ConvTile bf3_tile_of() {
+    using C = Bf3Cfg<RST_BA>;
+    ConvTile t{};
+    t.kh = KH; t.kw = KW; t.stride = S; t.ck = CK; t.nt = NT; t.th = TH; t.tw = TW; t.tps = TPS; t.hb = 1;
+    t.vec = 8; t.mt = C::MT; t.ngroups = C::NGROUPS; t.wstage = C::WSTAGE; t.lds_bytes = (int)C::LDS_BYTES;
+    t.bf3 = NP;
+    return t;
+}
+
+// (ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)
+#define RST_BF3_CONFIGS(X)                            \
+    X(101, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 2)       \
+    X(102, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 2)        \
+    X(104, 3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 2)       \
+    X(111, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 3)       \
+    X(112, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 3)        \
+    X(113, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3)
+
+bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, ConvTile* out) {
+    if (kh != 3 || stride != 1 || cin % 32 != 0 || ntot % 64 != 0 || (planes != 2 && planes != 3)) return false;
+    // measured (tools/conv_bench, residual conv of rst-960-120-128-17): bf16x3 NT64 4x16 42.8 us at B=1;
+    // bf16x6 NT64 8x16 62.8 us at B=1 / 437 us at B=8 (exact-f32 MFMA kernel: 92.5 / 611 us)
+    const int want = planes == 2 ? 102 : 113;
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)                  \
+    if (ID == want) {                                                       \
+        *out = bf3_tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>();   \
+        out->id = ID;                                                       \
+        return true;                                                        \
+    }
+    RST_BF3_CONFIGS(X)
+#undef X
+    return false;
+}
+
+hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
+    switch (t.id) {
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)                                          \
+    case ID: {                                                                                   \
+        using C = Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>;                            \
+        if ((a.cin & 3) != 0) return hipErrorInvalidValue;                                       \
+        if (a.pro_w != nullptr && a.cin > C::MAX_CIN) return hipErrorInvalidValue;               \
+        const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x * a.n_blocks);          \
+        hipLaunchKernelGGL((conv_bf3_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>), dim3(grid), \
+                           dim3(256), C::LDS_BYTES, st, a);                                      \
+        return hipGetLastError();                                                                \
+    }
+        RST_BF3_CONFIGS(X)
+#undef X
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
+hipError_t conv_bf3_prepare(const ConvTile& t) {
+    switch (t.id) {
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)                                                   \
+    case ID:                                                                                              \
+        return hipFuncSetAttribute((const void*)conv_bf3_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>, \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,                             \
+                                   (int)Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>::LDS_BYTES);
+        RST_BF3_CONFIGS(X)
+#undef X
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace rst

@@ -492,7 +492,7 @@ static hipError_t prepare_cfg() {
 template <RST_TP>
 static ConvTile tile_of() {
     using C = ConvCfg<RST_TA>;
-    ConvTile t;
+    ConvTile t{};
     t.kh = KH; t.kw = KW; t.stride = S; t.ck = CK; t.nt = NT; t.th = TH; t.tw = TW; t.tps = TPS; t.hb = HB;
     t.vec = C::VEC; t.mt = C::MT; t.ngroups = C::NGROUPS; t.wstage = C::WSTAGE;
     t.lds_bytes = (int)C::LDS_BYTES;
@@ -560,6 +560,7 @@ bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
 }
 
 hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
+    if (t.bf3) return conv_bf3_launch(t, a, st);
     switch (t.id) {
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB) \
     case ID:                                          \
@@ -572,6 +573,7 @@ hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
 }
 
 hipError_t conv_prepare(const ConvTile& t) {
+    if (t.bf3) return conv_bf3_prepare(t);
     switch (t.id) {
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB) \
     case ID:                                          \

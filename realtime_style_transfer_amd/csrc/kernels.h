@@ -34,12 +34,17 @@ struct ConvArgs {
 struct ConvTile {
     int id;
     int kh, kw, stride, ck, nt, th, tw, tps, hb, vec, mt, ngroups, wstage, lds_bytes;
+    int bf3;                // split-bf16 kernel (conv_bf3.hip): number of bf16 planes (2: bf16x3, 3: bf16x6), 0: f32
 };
 
 bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out);
 hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st);
 // one-time per-configuration setup (dynamic LDS > 64 KB); call outside graph capture
 hipError_t conv_prepare(const ConvTile& t);
+// split-bf16 variant (conv_bf3.hip): 3x3 s1, Cin % 32 == 0; conv_launch/conv_prepare dispatch on t.bf3
+bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, ConvTile* out);
+hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st);
+hipError_t conv_bf3_prepare(const ConvTile& t);
 
 // Final 9x9 transposed conv with Cout = 3 on the VALU (conv_small.hip).
 struct SmallConvArgs {

@@ -84,6 +84,8 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
     if (shape->h % 16 != 0 || shape->w % 16 != 0 || shape->h <= 0 || shape->w <= 0 || shape->max_batch <= 0)
         return set_error(RST_ERR_INVALID, "rst_loss_create: image H and W must be positive multiples of 16 "
                                           "(four 2x2 max-pools)");
+    if (shape->precision < RST_PRECISION_FP32 || shape->precision > RST_PRECISION_BF16X6)
+        return set_error(RST_ERR_INVALID, "rst_loss_create: unknown precision mode");
     if (num_weights != rst_loss_num_weights())
         return set_error(RST_ERR_INVALID, "rst_loss_create: expected " + std::to_string(rst_loss_num_weights()) +
                                               " VGG16 weights, got " + std::to_string(num_weights));
@@ -111,7 +113,9 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
         }
         const float* bias = wp + kc;
         wp += kc + c.cout;
-        if (!conv_select(3, 1, cin, c.cout, &c.tile)) {
+        const int planes = shape->precision == RST_PRECISION_BF16X3 ? 2 : (shape->precision == RST_PRECISION_BF16X6 ? 3 : 0);
+        const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cin, c.cout, planes, &c.tile);
+        if (!bf3 && !conv_select(3, 1, cin, c.cout, &c.tile)) {
             delete h;
             return set_error(RST_ERR_UNSUPPORTED, "no conv tile configuration for VGG layer " + std::to_string(i));
         }
@@ -119,7 +123,8 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
         c.tiles_x = (W + c.tile.tw - 1) / c.tile.tw;
         c.n_blocks = (c.cout + c.tile.nt - 1) / c.tile.nt;
         c.nchunks = (cin + c.tile.ck - 1) / c.tile.ck;
-        std::vector<float> pk = pack_conv_tiles(Wg, 9, cin, c.cout, c.tile);
+        std::vector<float> pk = c.tile.bf3 ? pack_conv_tiles_bf3(Wg, 9, cin, c.cout, c.tile)
+                                           : pack_conv_tiles(Wg, 9, cin, c.cout, c.tile);
         if ((st = h->alloc(&c.d_w, pk.size() * 4, pk.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&c.d_b, (size_t)c.cout * 4, bias)) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&c.d_out, (size_t)B * H * W * c.cout * 4)) != RST_OK) { delete h; return st; }

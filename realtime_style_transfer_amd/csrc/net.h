@@ -58,7 +58,7 @@ struct LayerExec {
 size_t layer_weight_count(const LayerSpec& s);
 int build_plan(const rst_shape* sh, std::vector<LayerSpec>& L, int* P);
 int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const float* bias, std::vector<float>& packed,
-                  std::vector<float>& bias_n);
+                  std::vector<float>& bias_n, int precision = RST_PRECISION_FP32);
 
 template <typename T>
 int upload(T** dst, const void* src, size_t bytes) {
@@ -74,6 +74,7 @@ struct rst_handle {
     using LayerExec = rst::LayerExec;
     rst_shape shape;
     int P = 0;
+    int precision = RST_PRECISION_FP32;
     std::vector<LayerExec> layers;
     // two-style blending: AvgPool2 mips of the second style's weight map, keyed by width
     // (styleTransfer.py:335-345); level 0 is the caller's style_weights (out_h x out_w)

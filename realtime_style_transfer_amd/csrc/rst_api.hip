@@ -127,6 +127,48 @@ std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int c
                                 }
     return out;
 }
+static unsigned short host_bf16_rne(float x) {
+    unsigned u;
+    std::memcpy(&u, &x, 4);
+    return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+std::vector<float> pack_conv_tiles_bf3(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t) {
+    const int ck = t.ck, nt = t.nt, tps = t.tps, ks_n = ck / 16, np_ = t.bf3;
+    const int nchunks = (cin + ck - 1) / ck, nblocks = (ntot + nt - 1) / nt, ngroups = taps / tps;
+    std::vector<unsigned short> out((size_t)nblocks * nchunks * ngroups * t.wstage, 0);
+    auto val = [](unsigned short h) {
+        unsigned u = (unsigned)h << 16;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f;
+    };
+    size_t idx = 0;
+    for (int nb = 0; nb < nblocks; ++nb)
+        for (int c = 0; c < nchunks; ++c)
+            for (int g = 0; g < ngroups; ++g)
+                for (int tt = 0; tt < tps; ++tt)
+                    for (int ks = 0; ks < ks_n; ++ks)
+                        for (int pl = 0; pl < np_; ++pl)
+                            for (int h = 0; h < 2; ++h)
+                                for (int n = 0; n < nt; ++n)
+                                    for (int j = 0; j < 8; ++j) {
+                                        const int tap = g * tps + tt;
+                                        const int ci = c * ck + ks * 16 + h * 8 + j;
+                                        const int ng = nb * nt + n;
+                                        float v = 0.f;
+                                        if (ci < cin && ng < ntot) v = Wg[((size_t)tap * cin + ci) * ntot + ng];
+                                        unsigned short p[3];
+                                        p[0] = host_bf16_rne(v);
+                                        const float r = v - val(p[0]);
+                                        p[1] = host_bf16_rne(r);
+                                        p[2] = host_bf16_rne(r - val(p[1]));
+                                        out[idx++] = p[pl];
+                                    }
+    std::vector<float> packed((out.size() + 1) / 2, 0.f);
+    std::memcpy(packed.data(), out.data(), out.size() * 2);
+    return packed;
+}
 }  // namespace rst
 
 namespace rst {
@@ -134,7 +176,7 @@ namespace rst {
 // point at the layer's Keras weights; passing an array of (index + 1) values instead yields the
 // gather map from canonical weights to the packed image (training re-packs after each update).
 int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const float* bias, std::vector<float>& packed,
-                  std::vector<float>& bias_n) {
+                  std::vector<float>& bias_n, int precision) {
     const size_t kcount = (size_t)s.k * s.k * s.cin * s.cout;
     (void)kcount;
     if (s.keras_kind == 1 && s.k == 9 && s.stride == 1) {
@@ -197,7 +239,10 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
             e.gWo = s.W;
             for (int n = 0; n < ntot; ++n) bias_n.push_back(bias[n % s.cout]);
         }
-        if (!conv_select(kh, s.keras_kind == 0 ? s.stride : 1, s.cin, ntot, &e.tile))
+        const int gs = s.keras_kind == 0 ? s.stride : 1;
+        const int planes = precision == RST_PRECISION_BF16X3 ? 2 : (precision == RST_PRECISION_BF16X6 ? 3 : 0);
+        const bool bf3 = planes > 0 && conv_bf3_select(kh, gs, s.cin, ntot, planes, &e.tile);
+        if (!bf3 && !conv_select(kh, gs, s.cin, ntot, &e.tile))
             return fail(RST_ERR_UNSUPPORTED, "no conv tile configuration for layer " + s.name);
         e.ntot = ntot;
         e.tiles_y = (e.gHo + e.tile.th - 1) / e.tile.th;
@@ -205,7 +250,8 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.n_blocks = (ntot + e.tile.nt - 1) / e.tile.nt;
         e.nchunks = (s.cin + e.tile.ck - 1) / e.tile.ck;
         e.n_part = e.tiles_y * e.tiles_x * e.tile.mt;
-        packed = pack_tiles(Wg, taps, s.cin, ntot, e.tile);
+        packed = e.tile.bf3 ? pack_conv_tiles_bf3(Wg, taps, s.cin, ntot, e.tile)
+                            : pack_tiles(Wg, taps, s.cin, ntot, e.tile);
     }
     return RST_OK;
 }
@@ -229,8 +275,15 @@ int rst_num_style_params(const rst_handle* h) { return h ? h->P : -1; }
 int rst_num_layers(const rst_handle* h) { return h ? (int)h->layers.size() : -1; }
 
 int rst_create(const rst_shape* shape, const float* weights_host, size_t num_weights, rst_handle** out) {
+    return rst_create_ex(shape, weights_host, num_weights, RST_PRECISION_FP32, out);
+}
+
+int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_weights, int precision,
+                  rst_handle** out) {
     if (shape == nullptr || out == nullptr || weights_host == nullptr)
         return fail(RST_ERR_INVALID, "rst_create: null argument");
+    if (precision != RST_PRECISION_FP32 && precision != RST_PRECISION_BF16X3 && precision != RST_PRECISION_BF16X6)
+        return fail(RST_ERR_INVALID, "rst_create_ex: unknown precision mode");
     *out = nullptr;
     if (shape->num_styles > 2)
         return fail(RST_ERR_UNSUPPORTED, "rst_create: num_styles > 2: the reference blends style parameters only for "
@@ -250,6 +303,7 @@ int rst_create(const rst_shape* shape, const float* weights_host, size_t num_wei
     rst_handle* h = new rst_handle();
     h->shape = *shape;
     h->P = P;
+    h->precision = precision;
     const int B = shape->max_batch;
     const float* wp = weights_host;
     h->layers.resize(specs.size());
@@ -262,7 +316,7 @@ int rst_create(const rst_shape* shape, const float* weights_host, size_t num_wei
         const float* bias = wp + kcount;
         wp += kcount + s.cout;
         std::vector<float> bias_n, packed;
-        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n)) != RST_OK) { delete h; return st; }
+        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, precision)) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
         if (s.norm == N_BN) {
@@ -514,6 +568,8 @@ int rst_profile_end(rst_handle* h, float* conv_ms, float* layer_ms, int* steps) 
     h->prof_free();
     return RST_OK;
 }
+
+int rst_precision(const rst_handle* h) { return h ? h->precision : -1; }
 
 int rst_layer_kernel_id(const rst_handle* h, int idx) {
     if (h == nullptr || idx < 0 || idx >= (int)h->layers.size()) return -1;

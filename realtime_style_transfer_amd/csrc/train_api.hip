@@ -572,13 +572,17 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
                     }
             vo += (size_t)9 * cin * cout + cout;
             ConvBwd& vb = t->vgg[i];
-            if (!conv_select(3, 1, cout, cin, &vb.tile))
+            const int lp = loss->precision;
+            const int planes = lp == RST_PRECISION_BF16X3 ? 2 : (lp == RST_PRECISION_BF16X6 ? 3 : 0);
+            const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cout, cin, planes, &vb.tile);
+            if (!bf3 && !conv_select(3, 1, cout, cin, &vb.tile))
                 return fail_delete(t, set_error(RST_ERR_UNSUPPORTED, "no tile for VGG dgrad " + std::to_string(i)));
             vb.tiles_y = (c.H + vb.tile.th - 1) / vb.tile.th;
             vb.tiles_x = (c.W + vb.tile.tw - 1) / vb.tile.tw;
             vb.n_blocks = (cin + vb.tile.nt - 1) / vb.tile.nt;
             vb.nchunks = (cout + vb.tile.ck - 1) / vb.tile.ck;
-            std::vector<float> pk = pack_conv_tiles(wd, 9, cout, cin, vb.tile);
+            std::vector<float> pk = vb.tile.bf3 ? pack_conv_tiles_bf3(wd, 9, cout, cin, vb.tile)
+                                                : pack_conv_tiles(wd, 9, cout, cin, vb.tile);
             if ((st = t->alloc(&vb.d_w, pk.size() * 4, pk.data())) != RST_OK) return fail_delete(t, st);
             hipError_t pe = conv_prepare(vb.tile);
             if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));

@@ -46,7 +46,12 @@ class StyleLossModelVGG:
     """styleLoss.py:69-109 on librst."""
 
     def __init__(self, input_shape, weights: Optional[Sequence[np.ndarray]] = None, seed: int = 3,
-                 max_batch: int = 4, device=None):
+                 max_batch: int = 4, device=None, precision: str = "fp32"):
+        """precision: arithmetic of the VGG16 3x3 convs with Cin % 32 == 0 — "fp32" (f32 MFMA),
+        "bf16x6" (exact 3-piece bf16 split, fp32-level products) or "bf16x3" (2-piece split)."""
+        if precision not in _lib.PRECISIONS:
+            raise ValueError(f"precision must be one of {list(_lib.PRECISIONS)}")
+        self.precision = precision
         self.style_layers = ['block1_conv2', 'block2_conv2', 'block3_conv3', 'block4_conv3']
         self.content_layers = ['block5_conv3']
         self.num_style_layers = len(self.style_layers)
@@ -65,7 +70,8 @@ class StyleLossModelVGG:
         if flat.size != lib.rst_loss_num_weights():
             raise ValueError(f"VGG16 trunk expects {lib.rst_loss_num_weights()} weights, got {flat.size}")
         shape = _lib.RstLossShape(self.input_shape[0], self.input_shape[1], self.max_batch,
-                                  self.content_loss_factor, self.style_loss_factor, self.total_variation_loss_factor)
+                                  self.content_loss_factor, self.style_loss_factor, self.total_variation_loss_factor,
+                                  _lib.PRECISIONS[self.precision])
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             _lib.check(lib.rst_loss_create(ctypes.byref(shape), flat.ctypes.data, flat.size, ctypes.byref(h)))

@@ -32,8 +32,11 @@ class StyleTransferModel:
 
     def __init__(self, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, num_styles=1,
                  name="StyleTransferModel", weights: Optional[Sequence[np.ndarray]] = None, seed: int = 2,
-                 max_batch: int = 8, device=None):
+                 max_batch: int = 8, device=None, precision: str = "fp32"):
         self.name = name
+        if precision not in _lib.PRECISIONS:
+            raise ValueError(f"precision must be one of {list(_lib.PRECISIONS)}, got {precision!r}")
+        self.precision = precision
         self.plan: Plan = network_plan(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
                                        num_styles)
         self.input_shape = tuple(int(v) for v in input_shape)
@@ -63,7 +66,8 @@ class StyleTransferModel:
         shape = self._shape_struct()
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            _lib.check(lib.rst_create(ctypes.byref(shape), flat.ctypes.data, flat.size, ctypes.byref(h)))
+            _lib.check(lib.rst_create_ex(ctypes.byref(shape), flat.ctypes.data, flat.size,
+                                         _lib.PRECISIONS[self.precision], ctypes.byref(h)))
         self._release()
         self._handle = h
         P = lib.rst_num_style_params(h)

@@ -90,7 +90,8 @@ class StyleTransferTrainingModel:
                               self.plan.bottleneck_num_filters, 1, self.max_batch)
         lm = self.loss_model
         lshape = _lib.RstLossShape(self.output_shape[0], self.output_shape[1], self.max_batch,
-                                   lm.content_loss_factor, lm.style_loss_factor, lm.total_variation_loss_factor)
+                                   lm.content_loss_factor, lm.style_loss_factor, lm.total_variation_loss_factor,
+                                   _lib.PRECISIONS[lm.precision])
         vgg = np.concatenate([a.reshape(-1) for a in lm.weights]).astype(np.float32)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):

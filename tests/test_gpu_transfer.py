@@ -4,6 +4,8 @@ Tolerances: the HIP path computes in exact f32 (f32-input MFMA = fmaf chains); t
 is float64 (numpy) or float32 (torch-CPU, full size). North-star bar: <= 1e-3 max-abs on
 the [0, 1] output; observed deviations are ~1e-5, so the tests assert 2e-4 on outputs.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -11,6 +13,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 OUT_TOL = 2e-4
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out')
 
 
 def _need_gpu():
@@ -145,7 +148,6 @@ def test_instance_norm_op():
 def test_two_style_blending_matches_golden():
     """num_styles=2: per-pixel blend of the CIN parameters with the style-weight mips."""
     _need_gpu()
-    import os
     from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
     d = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'transfer_two_styles.npz'))
     ws = [d[k] for k in sorted(k for k in d.files if k.startswith('w') and k[1:].isdigit())]
@@ -165,3 +167,28 @@ def test_two_style_blending_matches_golden():
         assert np.abs(y2 - y1.cpu().numpy()).max() < 1e-5
     with pytest.raises(ValueError):
         model({'content': inputs['content'], 'style_params': inputs['style_params']})   # weights missing
+
+
+@pytest.mark.parametrize("precision,tol", [("bf16x3", 2e-4), ("bf16x6", 2e-5)])
+def test_split_bf16_precision_modes(precision, tol):
+    """RST_PRECISION_BF16X3 / BF16X6: residual convs on split-bf16 MFMA, vs the float64 oracle."""
+    _need_gpu()
+    from oracle import numpy_ref as R
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    ins, outs, br, bf = (32, 64, 17), (32, 64, 3), 8, 128
+    plan = network_plan(ins, outs, br, bf)
+    w = init_weights(plan, seed=2)
+    sp = synthetic_style_params(2, 1, plan.num_style_params, plan, seed=1)
+    x = np.random.default_rng(0).random((2,) + ins).astype(np.float32)
+    ref = R.transfer_forward(x, sp, w, ins, outs, br, bf)
+    m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision=precision)
+    kid = 102 if precision == "bf16x3" else 113
+    assert [m.layer_kernel_id(i) for i in range(m.num_layers())][3:13] == [kid] * 10   # residual convs
+    inp = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}
+    err = float(np.abs(m(inp).cpu().numpy() - ref).max())
+    import json
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f'{precision}_parity.json'), 'w') as f:
+        json.dump({'max_abs': err}, f)
+    assert err < tol, err   # bf16x3: the float64 simulation of the split gives ~2e-5 here; fp32 gives ~2e-6

@@ -10,6 +10,7 @@
 #include <functional>
 #include "../realtime_style_transfer_amd/csrc/conv_mfma.hip"
 #include "../realtime_style_transfer_amd/csrc/conv_small.hip"
+#include "../realtime_style_transfer_amd/csrc/conv_bf3.hip"
 
 using namespace rst;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -60,6 +61,7 @@ struct Variant {
         grid = (unsigned)(B * a.tiles_y * a.tiles_x * a.n_blocks);
         CK(hipFuncSetAttribute((const void*)conv_mfma_kernel<RST_TA, OPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)C::LDS_BYTES));
+        printf("%-40s LDS %6zu B  grid %u\n", n, (size_t)C::LDS_BYTES, grid);
     }
     void launch() {
         using C = ConvCfg<RST_TA>;
@@ -83,7 +85,19 @@ int main(int argc, char** argv) {
     float* out_s; CK(hipMalloc(&out_s, (size_t)B * 480 * 960 * 32 * 4));
     float* w_s = dev_rand((size_t)81 * 18 * 32, -0.05f, 0.05f, 6);
 #define VARIANTS(X)                                                   \
-    X(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 1, 1, "res CK32 NT128 4x16 HB1 (prod)", res, in, w, out)
+    X(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 1, 1, "res CK32 NT128 4x16 TPS1 HB1 (prod)", res, in, w, out) \
+    X(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 2, 1, "res CK32 NT128 4x16 TPS1 HB2", res, in, w, out) \
+    X(3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 1, 1, "res CK32 NT64 8x16 TPS1 HB1", res, in, w, out) \
+    X(3, 3, 1, 32, 64, 8, 16, 2, 2, 3, 1, 1, "res CK32 NT64 8x16 TPS3 HB1", res, in, w, out) \
+    X(3, 3, 1, 16, 128, 4, 16, 2, 2, 3, 1, 1, "res CK16 NT128 4x16 TPS3 HB1", res, in, w, out) \
+    X(3, 3, 1, 16, 128, 4, 16, 2, 2, 9, 1, 1, "res CK16 NT128 4x16 TPS9 HB1", res, in, w, out) \
+    X(3, 3, 1, 32, 128, 4, 16, 2, 2, 3, 1, 1, "res CK32 NT128 4x16 TPS3 HB1", res, in, w, out) \
+    X(3, 3, 1, 32, 128, 8, 16, 4, 1, 1, 1, 1, "res CK32 NT128 8x16 WM4 TPS1", res, in, w, out) \
+    X(3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 1, 1, "res CK32 NT64 4x16 TPS1 HB1", res, in, w, out) \
+    X(3, 3, 1, 32, 64, 4, 16, 2, 2, 3, 1, 1, "res CK32 NT64 4x16 TPS3 HB1", res, in, w, out) \
+    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 3, 1, 1, "start CK18 NT32 8x16 TPS3 (prod)", start, in_s, w_s, out_s) \
+    X(9, 9, 1, 18, 32, 8, 16, 4, 1, 9, 1, 1, "start CK18 NT32 8x16 TPS9", start, in_s, w_s, out_s) \
+    X(9, 9, 1, 18, 32, 16, 16, 4, 1, 3, 1, 1, "start CK18 NT32 16x16 TPS3", start, in_s, w_s, out_s)
     int nv = 0;
     std::vector<std::function<void()>> launches;
     std::vector<const char*> names;
@@ -115,6 +129,28 @@ int main(int argc, char** argv) {
     SV(1, "small opt1 (s_load, q unrolled)")
     SV(2, "small opt2 (LDS weights)")
     SV(3, "small opt3 (LDS weights, q unrolled)")
+    // split-bf16 (bf16x3) residual conv variants: timing only (random weight bits)
+#define BV(KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP, NAME)                                               \
+    {                                                                                                    \
+        using BC = Bf3Cfg<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP>;                                  \
+        ConvArgs ba = make_args<KH, KW, S, CK_, NT, TH, TW, WM, WN, 1, 1, 1>(res, B, in, w, bias, ab, out, part); \
+        const unsigned bgrid = (unsigned)(B * ba.tiles_y * ba.tiles_x * ba.n_blocks);                    \
+        CK(hipFuncSetAttribute((const void*)conv_bf3_kernel<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP>, \
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)BC::LDS_BYTES));         \
+        printf("%-40s LDS %6zu B  grid %u\n", NAME, (size_t)BC::LDS_BYTES, bgrid);                        \
+        launches.push_back([=] {                                                                         \
+            hipLaunchKernelGGL((conv_bf3_kernel<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP>), dim3(bgrid), \
+                               dim3(256), BC::LDS_BYTES, 0, ba);                                         \
+        });                                                                                              \
+        names.push_back(NAME); flops.push_back(res.flops); ++nv;                                         \
+    }
+    BV(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 2, "bf16x3 res NT128 4x16")
+    BV(3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 2, "bf16x3 res NT64 4x16")
+    BV(3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 2, "bf16x3 res NT128 8x16")
+    BV(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 3, "bf16x6 res NT128 4x16")
+    BV(3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 3, "bf16x6 res NT64 4x16")
+    BV(3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3, "bf16x6 res NT64 8x16")
+    BV(3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 3, "bf16x6 res NT128 8x16")
     std::vector<std::vector<float>> t(nv);
     for (int r = 0; r < rounds; ++r)
         for (int i = 0; i < nv; ++i) t[i].push_back(time_ms(launches[i], iters));
