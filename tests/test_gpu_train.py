@@ -153,7 +153,8 @@ def test_training_step_matches_oracle(name, precision, gtol):
             continue   # no gradient / round-off-only gradient (bias before an instance norm): sign is arbitrary
         strong = np.abs(g) > 5e-2 * np.abs(g).max()
         assert np.abs(a - r)[strong].max() <= 1e-6 + 1e-6 * np.abs(r).max(), (i, np.abs(a - r)[strong].max())
-        assert np.linalg.norm(slots[i] - ref['ms'][i]) <= 5e-3 * np.linalg.norm(ref['ms'][i]), i
+        # ms = (1 - rho) g^2: its relative error is about twice the gradient's
+        assert np.linalg.norm(slots[i] - ref['ms'][i]) <= max(5e-3, 2.5 * gtol) * np.linalg.norm(ref['ms'][i]), i
     assert perr < 2e-5, perr
     assert lrel < (1e-4 if precision != "bf16x3" else 1e-3), lrel
     assert gerr < gtol, gerr
