@@ -21,6 +21,9 @@
  *   rst_gram                     gram_matrix / get_gram_matrix_model  models/styleLoss.py:11-37
  *   rst_instance_norm            ConditionalInstanceNormalization.call models/styleTransfer.py:57-71
  *   rst_copy_activation          (debug) per-block outputs of the Keras sub-models
+ *   rst_predictor_*              create_style_prediction_model(input_shape, feature_extractor,
+ *                                num_top_parameters, num_style_parameters=100) -> tf.keras.Model
+ *                                                                 models/stylePrediction.py:25-75
  *   rst_loss_create / _forward   StyleLossModelVGG + make_style_loss_function(..., with_depth_loss=False)
  *                                -> compute_loss(y_pred, y_true) dict      models/styleLoss.py:69-109,295-369
  */
@@ -172,6 +175,38 @@ int rst_trainer_copy_output_gradient(rst_trainer* t, int layer, float* dst, size
 /* Debug: d loss / d (VGG16 conv `layer` output). The first call for a layer arms the tap (it
  * allocates; dst may be NULL); later calls copy the value of the most recent compute_gradients. */
 int rst_trainer_debug_vgg_gradient(rst_trainer* t, int layer, float* dst, size_t count, int batch, void* stream);
+
+/* ---- Style predictor (create_style_prediction_model, models/stylePrediction.py:25-75) ----
+ * Replaces the Keras predictor that make_style_transfer_inference_model runs once per style image
+ * (styleTransferInferenceModel.py:23-26; predict_video_using_checkpoint.py:77-83):
+ *   DUMMY:      Conv2D(1, 9, strides=5, padding='same') on the raw image            (:31-32)
+ *   MOBILE_NET: Rescaling(2, -1) + keras.applications.MobileNetV3Small(include_top=False,
+ *               include_preprocessing=False), BatchNormalization in inference mode   (:33-38)
+ * then GlobalAveragePooling2D (:55), Conv2D(num_style_parameters, 1) (:60-64) and
+ * Conv2D(num_top_parameters, 1) (:67-71), squeezed to (B, num_top_parameters) (:73-74).
+ * Weights: Keras get_weights() order (per layer kernel[, bias]; BN gamma, beta, moving_mean,
+ * moving_variance), HOST pointer; rst_predictor_num_weights gives the count for a shape. */
+enum { RST_EXTRACTOR_DUMMY = 0, RST_EXTRACTOR_MOBILE_NET = 1 };
+typedef struct rst_predictor_shape {
+    int h, w, c;                  /* style image (H, W, C): ShapeConfig.input_shape['style'][1:]     */
+    int feature_extractor;        /* RST_EXTRACTOR_* (EFFICIENT_NET: RST_ERR_UNSUPPORTED)             */
+    int num_top_parameters;       /* P, the transfer network's style-parameter count (num_top_parameters) */
+    int num_style_parameters;     /* width of the StylePredictor bottleneck (default 100)            */
+    int max_batch;                /* largest batch (= images) rst_predictor_forward is called with    */
+} rst_predictor_shape;
+typedef struct rst_predictor rst_predictor;
+size_t rst_predictor_num_weights(const rst_predictor_shape* shape);
+int rst_predictor_create(const rst_predictor_shape* shape, const float* weights_host, size_t num_weights,
+                         rst_predictor** out);
+void rst_predictor_destroy(rst_predictor* p);
+/* style (B, h, w, c) -> style_params (B, num_top_parameters). Device pointers, async on stream.
+ * For num_styles S pass the (B, S, h, w, c) style stack as B*S images: the output is (B, S, P). */
+int rst_predictor_forward(rst_predictor* p, const float* style, int batch, float* style_params, void* stream);
+/* Debug: stage outputs (MOBILE_NET: stem, the 11 inverted-residual blocks, Conv_1 features;
+ * DUMMY: the conv output) of the most recent forward. */
+int rst_predictor_num_stages(const rst_predictor* p);
+int rst_predictor_stage_shape(const rst_predictor* p, int idx, int* hwc3);
+int rst_predictor_copy_stage(rst_predictor* p, int idx, float* dst, size_t count, int batch, void* stream);
 
 const char* rst_last_error(void);
 const char* rst_version(void);

@@ -30,7 +30,10 @@ EXPORTED_SYMBOLS = [
     "rst_trainer_compute_gradients", "rst_trainer_apply_gradients", "rst_trainer_copy_weights",
     "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_copy_output_gradient",
     "rst_trainer_debug_vgg_gradient", "rst_trainer_loss",
+    "rst_predictor_num_weights", "rst_predictor_create", "rst_predictor_destroy", "rst_predictor_forward",
+    "rst_predictor_num_stages", "rst_predictor_stage_shape", "rst_predictor_copy_stage",
 ]
+EXTRACTORS = {"DUMMY": 0, "MOBILE_NET": 1}   # include/rst.h RST_EXTRACTOR_*
 
 
 class RstShape(ctypes.Structure):
@@ -44,6 +47,12 @@ class RstLossShape(ctypes.Structure):
     _fields_ = [("h", ctypes.c_int), ("w", ctypes.c_int), ("max_batch", ctypes.c_int),
                 ("content_factor", ctypes.c_float), ("style_factor", ctypes.c_float), ("tv_factor", ctypes.c_float),
                 ("precision", ctypes.c_int)]
+
+
+class RstPredictorShape(ctypes.Structure):
+    _fields_ = [("h", ctypes.c_int), ("w", ctypes.c_int), ("c", ctypes.c_int), ("feature_extractor", ctypes.c_int),
+                ("num_top_parameters", ctypes.c_int), ("num_style_parameters", ctypes.c_int),
+                ("max_batch", ctypes.c_int)]
 
 
 class RstError(RuntimeError):
@@ -131,6 +140,20 @@ def load() -> ctypes.CDLL:
     lib.rst_trainer_debug_vgg_gradient.restype = i
     lib.rst_trainer_loss.argtypes = [vp]
     lib.rst_trainer_loss.restype = vp
+    lib.rst_predictor_num_weights.argtypes = [ctypes.POINTER(RstPredictorShape)]
+    lib.rst_predictor_num_weights.restype = sz
+    lib.rst_predictor_create.argtypes = [ctypes.POINTER(RstPredictorShape), vp, sz, ctypes.POINTER(vp)]
+    lib.rst_predictor_create.restype = i
+    lib.rst_predictor_destroy.argtypes = [vp]
+    lib.rst_predictor_destroy.restype = None
+    lib.rst_predictor_forward.argtypes = [vp, vp, i, vp, vp]
+    lib.rst_predictor_forward.restype = i
+    lib.rst_predictor_num_stages.argtypes = [vp]
+    lib.rst_predictor_num_stages.restype = i
+    lib.rst_predictor_stage_shape.argtypes = [vp, i, ctypes.POINTER(ctypes.c_int)]
+    lib.rst_predictor_stage_shape.restype = i
+    lib.rst_predictor_copy_stage.argtypes = [vp, i, vp, sz, i, vp]
+    lib.rst_predictor_copy_stage.restype = i
     lib.rst_last_error.argtypes = []
     lib.rst_last_error.restype = ctypes.c_char_p
     lib.rst_version.argtypes = []

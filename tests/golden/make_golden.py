@@ -15,6 +15,11 @@ Fixtures (all float32 inputs/weights, float64 expected outputs, npz):
 * transfer_two_styles.npz — config (i) with num_styles=2: per-pixel blending of the CIN
   parameters with a (B, 32, 64, 1) style-weight map and its AvgPool2 mips
   (styleTransfer.py:36-44, 288-303, 335-345).
+* predictor_mobilenet.npz / predictor_dummy.npz — the style predictor
+  (stylePrediction.py:25-75) at 64x96x3 (MOBILE_NET, B=2) and 60x90x3 (DUMMY, B=2), P=200, with
+  perturbed seeded weights (regenerated from the seed by init_predictor_weights; the fixture
+  stores a sha256 of the float32 weight bytes instead of the 1.2 M weights), the per-block
+  outputs and the (B, P) output.
 Each transfer fixture also stores ``stats`` in the metrics.get_stats format
 (realtime_style_transfer/metrics.py:4-12: mean/var/min/max).
 """
@@ -94,6 +99,30 @@ def gram_fixture():
     np.savez_compressed(os.path.join(HERE, 'gram_loss.npz'), **arrays)
 
 
+def weights_digest(ws):
+    import hashlib
+    h = hashlib.sha256()
+    for w in ws:
+        h.update(np.ascontiguousarray(w, np.float32).tobytes())
+    return h.hexdigest()
+
+
+def predictor_fixture(name, extractor, ins, batch=2, P=200, seed=3):
+    from oracle import predictor_ref as PR
+    from realtime_style_transfer_amd.stylePrediction import init_predictor_weights, predictor_weight_spec
+    spec = predictor_weight_spec(ins, extractor, P)
+    ws = init_predictor_weights(spec, seed=seed, perturb=True)
+    x = np.random.default_rng(6).random((batch,) + tuple(ins)).astype(np.float32)
+    y, feat = PR.style_predictor_forward(x, ws, extractor, return_features=True)
+    arrays = {'style': x, 'output': y, 'features': feat, 'shape': np.array(list(ins) + [P, seed]),
+              'extractor': np.array(extractor), 'weights_sha256': np.array(weights_digest(ws))}
+    if extractor == 'MOBILE_NET':
+        _, blocks = PR.mobilenet_v3_small(x * 2.0 - 1.0, iter(ws), return_blocks=True)
+        for i, b in enumerate(blocks):
+            arrays[f'block{i:02d}'] = b
+    np.savez_compressed(os.path.join(HERE, name), **arrays)
+
+
 if __name__ == '__main__':
     only = sys.argv[1:]
     jobs = {
@@ -103,6 +132,8 @@ if __name__ == '__main__':
         'gram_loss.npz': gram_fixture,
         'transfer_two_styles.npz': lambda: transfer_fixture('transfer_two_styles.npz', (32, 64, 17), (32, 64, 3), 8, 8,
                                                             num_styles=2),
+        'predictor_mobilenet.npz': lambda: predictor_fixture('predictor_mobilenet.npz', 'MOBILE_NET', (64, 96, 3)),
+        'predictor_dummy.npz': lambda: predictor_fixture('predictor_dummy.npz', 'DUMMY', (60, 90, 3)),
     }
     for name, job in jobs.items():
         if not only or name in only:
