@@ -165,6 +165,72 @@ def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, tim
             "last_loss_mean": loss}
 
 
+def predictor_bytes_per_image(ins) -> float:
+    """Algorithmic HBM bytes of one MobileNetV3Small style-predictor pass (stylePrediction.py:25-75): every
+    layer reads its input and writes its output once (fp32), plus all weights once."""
+    from realtime_style_transfer_amd.stylePrediction import _MOBILENET_V3_SMALL, _depth
+    H, W = ins[0], ins[1]
+    by = H * W * 3
+    H, W = -(-H // 2), -(-W // 2)
+    by += H * W * 16
+    cin = 16
+    for i, (e, f, k, s, se, _) in enumerate(_MOBILENET_V3_SMALL):
+        ce = _depth(cin * e)
+        if i:
+            by += 2 * H * W * ce + H * W * cin        # expand: read cin, write ce; dw reads ce
+        else:
+            by += H * W * ce
+        H, W = -(-H // s), -(-W // s)
+        by += H * W * ce * (2 if se else 1)           # dw write (+ SE-scaled re-read by project)
+        by += H * W * f + (H * W * f if (s == 1 and cin == f) else 0)
+        cin = f
+    by += H * W * cin + H * W * 576 * 2              # Conv_1 in/out, GAP read
+    return 4.0 * by
+
+
+def bench_predictor(args, dev, cfg, transfer_model, transfer_inputs, P, timed):
+    """make_style_transfer_inference_model path: the MobileNetV3Small style predictor on a 480x960x3 style image
+    (once per style in the video loop, predict_video_using_checkpoint.py:77-83) and predictor + transfer per
+    frame (the Keras inference model runs both per call, styleTransferInferenceModel.py:23-37)."""
+    from realtime_style_transfer_amd.stylePrediction import create_style_prediction_model
+    sins = tuple(cfg.input_shape['style'][1:])
+    pred = create_style_prediction_model(sins, cfg.style_feature_extractor_type, P, max_batch=1, device=dev)
+    rng = np.random.default_rng(4000)
+    style = torch.from_numpy(rng.random((1,) + sins, dtype=np.float32)).to(dev)
+    sp = torch.empty((1, P), dtype=torch.float32, device=dev)        # the predictor writes the transfer's input
+    tin = {'content': transfer_inputs['content'][:1], 'style_params': sp.view(1, 1, P)}
+    out = torch.empty((1,) + transfer_model.output_shape, dtype=torch.float32, device=dev)
+
+    def graph_of(fn):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            fn()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        return g
+
+    gp = graph_of(lambda: pred(style, out=sp))
+    el_p = timed(gp.replay, args.steps)
+    gi = graph_of(lambda: (pred(style, out=sp), transfer_model(tin, out=out)))
+    el_i = timed(gi.replay, args.steps)
+    ms_p = el_p * 1e3 / args.steps
+    by = predictor_bytes_per_image(sins)
+    return {"workload": f"MobileNetV3Small style predictor + GAP + 1x1 heads (P={P}) on one {sins[0]}x{sins[1]}x3 "
+                        f"style image, hipGraph replay", "ms_per_style_image": round(ms_p, 4),
+            "roofline": {"bound": "hbm", "achieved": round(by / (ms_p * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(by / (ms_p * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes": by,
+                         "note": "~45 small launches; latency-bound at B=1 (whole graph, not one kernel)"},
+            "inference_model_fps": round(args.steps / el_i, 3),
+            "inference_model_workload": "predictor + transfer per frame (B=1), as the Keras inference model runs"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -179,6 +245,7 @@ def main():
     ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--no-bf16x3", action="store_true", help="skip the split-bf16 precision-mode measurements")
+    ap.add_argument("--no-predictor", action="store_true", help="skip the style-predictor measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -331,6 +398,11 @@ def main():
             split_models[prec], split[prec] = bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs,
                                                           timed, prec)
 
+    # ---------------- style predictor / inference model -----------------------
+    predictor = None
+    if not args.no_predictor:
+        predictor = bench_predictor(args, dev, cfg, model, inputs, P, timed)
+
     # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
     train = None
     if args.train_batch > 0:
@@ -418,6 +490,7 @@ def main():
             "layers": layer_table,
             "split_bf16_modes": split,
             "training": train,
+            "style_predictor": predictor,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
