@@ -78,8 +78,9 @@ struct rst_predictor {
     std::vector<int> stage_buf;          // debug stages -> buffer
     std::vector<int> stage_hwc;          // 3 per stage
     int feat_buf = -1, feat_hw = 0, feat_c = 0;
+    int feat_part = -1, feat_nparts = 0; // per-tile channel sums of the features (global average pool)
     float* d_params = nullptr;           // packed parameter image (kernels' layouts)
-    float* d_gap = nullptr;              // [max_batch][feat_c]
+    float* d_hidden = nullptr;           // [max_batch][num_style_parameters]
     size_t head_w1 = 0, head_b1 = 0, head_w2 = 0, head_b2 = 0;
     std::vector<void*> allocs;
     ~rst_predictor() {
@@ -145,11 +146,14 @@ int build(Builder& B, const rst_predictor_shape* s) {
         op.w = B.put(B.take((size_t)81 * C), (size_t)81 * C);
         op.ba = B.put(B.take(1), 1);
         op.out = B.new_buf((size_t)op.Ho * op.Wo);
+        op.part = B.new_buf((size_t)dummy_conv_parts(op.Ho * op.Wo));
         B.stage(op.out, op.Ho, op.Wo, 1);
         P->ops.push_back(op);
         P->feat_buf = op.out;
         P->feat_hw = op.Ho * op.Wo;
         P->feat_c = 1;
+        P->feat_part = op.part;
+        P->feat_nparts = dummy_conv_parts(op.Ho * op.Wo);
         return RST_OK;
     }
     if (s->feature_extractor != RST_EXTRACTOR_MOBILE_NET)
@@ -237,11 +241,14 @@ int build(Builder& B, const rst_predictor_shape* s) {
     op.w = B.put(B.take((size_t)C * last), (size_t)C * last);
     B.bn(last, &op.ba, &op.bb);
     op.out = B.new_buf((size_t)H * W * last);
+    op.part = B.new_buf((size_t)pw_parts(H * W) * last);
     B.stage(op.out, H, W, last);
     P->ops.push_back(op);
     P->feat_buf = op.out;
     P->feat_hw = H * W;
     P->feat_c = last;
+    P->feat_part = op.part;
+    P->feat_nparts = pw_parts(H * W);
     return RST_OK;
 }
 
@@ -249,8 +256,8 @@ int build_all(Builder& B, const rst_predictor_shape* s) {
     if (!s || s->h <= 0 || s->w <= 0 || s->c <= 0 || s->num_top_parameters <= 0 || s->num_style_parameters <= 0 ||
         s->max_batch <= 0)
         return set_error(RST_ERR_INVALID, "rst_predictor_shape: all dimensions must be positive");
-    if (s->num_style_parameters > 512)
-        return set_error(RST_ERR_UNSUPPORTED, "rst_predictor: num_style_parameters > 512");
+    if (s->num_style_parameters > 1024)
+        return set_error(RST_ERR_UNSUPPORTED, "rst_predictor: num_style_parameters > 1024");
     int st = build(B, s);
     if (st != RST_OK) return st;
     const int C = B.p->feat_c, NS = s->num_style_parameters, P = s->num_top_parameters;
@@ -307,7 +314,10 @@ int rst_predictor_create(const rst_predictor_shape* shape, const float* weights_
         if ((st = alloc(&d, e * shape->max_batch)) != RST_OK) { delete p; return st; }
         p->bufs.push_back(d);
     }
-    if ((st = alloc(&p->d_gap, (size_t)p->feat_c * shape->max_batch)) != RST_OK) { delete p; return st; }
+    if ((st = alloc(&p->d_hidden, (size_t)shape->num_style_parameters * shape->max_batch)) != RST_OK) {
+        delete p;
+        return st;
+    }
     *out = p;
     return RST_OK;
 }
@@ -329,12 +339,12 @@ int rst_predictor_forward(rst_predictor* p, const float* style, int batch, float
                                         op.Ho, op.Wo, op.pad_t, op.pad_l, st));
                 break;
             case OP_DUMMY:
-                RST_HIP_TRY(dummy_conv_launch(style, prm + op.w, prm + op.ba, buf(op.out), batch, op.H, op.W, op.cin,
-                                              op.Ho, op.Wo, op.pad_t, op.pad_l, st));
+                RST_HIP_TRY(dummy_conv_launch(style, prm + op.w, prm + op.ba, buf(op.out), buf(op.part), batch, op.H,
+                                              op.W, op.cin, op.Ho, op.Wo, op.pad_t, op.pad_l, st));
                 break;
             case OP_PW:
                 RST_HIP_TRY(pw_launch(in, buf(op.se), prm + op.w, prm + op.ba, prm + op.bb, buf(op.res), buf(op.out),
-                                      batch, op.H * op.W, op.cin, op.cout, op.act, st));
+                                      buf(op.part), batch, op.H * op.W, op.cin, op.cout, op.act, st));
                 break;
             case OP_DW:
                 RST_HIP_TRY(dw_launch(in, prm + op.w, prm + op.ba, prm + op.bb, buf(op.out), buf(op.part), batch, op.H,
@@ -346,9 +356,9 @@ int rst_predictor_forward(rst_predictor* p, const float* style, int batch, float
                 break;
         }
     }
-    RST_HIP_TRY(gap_launch(buf(p->feat_buf), batch, p->feat_hw, p->feat_c, p->d_gap, st));
-    RST_HIP_TRY(head_launch(p->d_gap, batch, p->feat_c, p->shape.num_style_parameters, p->shape.num_top_parameters,
-                            prm + p->head_w1, prm + p->head_b1, prm + p->head_w2, prm + p->head_b2, style_params,
+    RST_HIP_TRY(head_launch(buf(p->feat_part), p->feat_nparts, p->feat_hw, batch, p->feat_c,
+                            p->shape.num_style_parameters, p->shape.num_top_parameters, prm + p->head_w1,
+                            prm + p->head_b1, prm + p->head_w2, prm + p->head_b2, p->d_hidden, style_params,
                             p->shape.num_top_parameters, st));
     return RST_OK;
 }
