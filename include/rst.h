@@ -208,6 +208,27 @@ int rst_predictor_num_stages(const rst_predictor* p);
 int rst_predictor_stage_shape(const rst_predictor* p, int idx, int* hwc3);
 int rst_predictor_copy_stage(rst_predictor* p, int idx, float* dst, size_t count, int batch, void* stream);
 
+/* ---- Style-predictor training (train_network.py:86-138 fits the predictor jointly) ----
+ * Forward in Keras training mode: BatchNormalization normalises with the batch statistics over
+ * (B, H, W) and updates its moving statistics (MobileNetV3: momentum 0.999, eps 1e-3) in the
+ * device-resident weights. Backward: gradient of sum(style_params * d_style_params) with respect to
+ * every predictor weight (Keras get_weights() order; moving statistics get 0) — chain it to
+ * rst_trainer_compute_gradients' grad_style_params. The style tensor passed to forward must stay
+ * valid until the matching backward. */
+typedef struct rst_predictor_trainer rst_predictor_trainer;
+int rst_predictor_trainer_create(const rst_predictor_shape* shape, const float* weights_host, size_t num_weights,
+                                 rst_predictor_trainer** out);
+void rst_predictor_trainer_destroy(rst_predictor_trainer* t);
+size_t rst_predictor_trainer_num_weights(const rst_predictor_trainer* t);
+int rst_predictor_trainer_forward(rst_predictor_trainer* t, const float* style, int batch, float* style_params,
+                                  void* stream);
+int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_style_params, float* grad, void* stream);
+int rst_predictor_trainer_apply_gradients(rst_predictor_trainer* t, const float* grad, float learning_rate, float rho,
+                                          float epsilon, void* stream);
+int rst_predictor_trainer_copy_weights(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
+int rst_predictor_trainer_set_weights(rst_predictor_trainer* t, const float* src, size_t count, void* stream);
+int rst_predictor_trainer_copy_slots(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
+
 const char* rst_last_error(void);
 const char* rst_version(void);
 

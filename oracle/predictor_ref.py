@@ -294,3 +294,103 @@ def torch_style_predictor_forward(style, weights: Sequence[np.ndarray], extracto
         w1, b1, w2, b2 = next(wi), next(wi), next(wi), next(wi)
         y = (g @ t(w1[0, 0]) + t(b1)) @ t(w2[0, 0]) + t(b2)
     return y.numpy()
+
+
+# ----------------------------------------------------------------------------- training mode (float64 autograd)
+
+BN_MOMENTUM = 0.999   # keras mobilenet_v3 BatchNormalization(momentum=0.999)
+
+
+def predictor_train_reference(style, weights: Sequence[np.ndarray], extractor: str, d_style_params):
+    """One training-mode forward + backward of the predictor in float64 (torch autograd).
+
+    Keras training=True: every BatchNormalization normalises with the batch's biased moments over
+    (B, H, W) and updates moving_mean / moving_variance with momentum 0.999 and the Bessel-corrected
+    batch variance. The backward is the gradient of sum(style_params * d_style_params).
+    Returns {'output', 'grads' (Keras order, zeros for moving statistics), 'weights' (moving
+    statistics updated)}."""
+    import torch
+    import torch.nn.functional as F
+
+    ws = [torch.tensor(np.asarray(w, np.float64), requires_grad=True) for w in weights]
+    new_w = [np.asarray(w, np.float64).copy() for w in weights]
+    moving = set()
+    idx = [0]
+
+    def nxt():
+        i = idx[0]
+        idx[0] += 1
+        return i
+
+    def conv(x, w, b, stride, pads, groups=1):
+        (pt, pb), (pl, pr) = pads
+        x = F.pad(x, (pl, pr, pt, pb))
+        wt = (w.permute(3, 2, 0, 1) if groups == 1 else w.permute(2, 3, 0, 1)).contiguous()
+        return F.conv2d(x, wt, b, stride=stride, groups=groups)
+
+    def same(x, k, s):
+        _, pt, pb = _same(x.shape[2], k, s)
+        _, pl, pr = _same(x.shape[3], k, s)
+        return (pt, pb), (pl, pr)
+
+    def bn(x):
+        gi, bi, mi, vi = nxt(), nxt(), nxt(), nxt()
+        moving.update((mi, vi))
+        mean = x.mean(dim=(0, 2, 3))
+        var = ((x - mean.view(1, -1, 1, 1)) ** 2).mean(dim=(0, 2, 3))
+        n = x.shape[0] * x.shape[2] * x.shape[3]
+        new_w[mi] = new_w[mi] * BN_MOMENTUM + mean.detach().numpy() * (1 - BN_MOMENTUM)
+        new_w[vi] = new_w[vi] * BN_MOMENTUM + var.detach().numpy() * n / max(n - 1, 1) * (1 - BN_MOMENTUM)
+        inv = torch.rsqrt(var + BN_EPS)
+        return (x - mean.view(1, -1, 1, 1)) * (inv * ws[gi]).view(1, -1, 1, 1) + ws[bi].view(1, -1, 1, 1)
+
+    def hsig(x):
+        return F.relu6(x + 3.0) * (1.0 / 6.0)
+
+    def hsw(x):
+        return x * hsig(x)
+
+    acts = {'relu': F.relu, 'hard_swish': hsw}
+    x = torch.tensor(np.asarray(style, np.float64)).permute(0, 3, 1, 2)
+    if extractor == 'DUMMY':
+        w, b = ws[nxt()], ws[nxt()]
+        x = conv(x, w, b, 5, same(x, 9, 5))
+    else:
+        x = x * 2.0 - 1.0
+        w = ws[nxt()]
+        x = hsw(bn(conv(x, w, None, 2, same(x, 3, 2))))
+        cin = 16
+        for bi, (e, f, k, s, se, an) in enumerate(MOBILENET_V3_SMALL_BLOCKS):
+            act = acts[an]
+            sc = x
+            ce = make_divisible(cin * e)
+            if bi:
+                w = ws[nxt()]
+                x = act(bn(conv(x, w, None, 1, ((0, 0), (0, 0)))))
+            pads = correct_pad((x.shape[2], x.shape[3]), k) if s == 2 else same(x, k, 1)
+            w = ws[nxt()]
+            x = act(bn(conv(x, w, None, s, pads, groups=ce)))
+            if se:
+                g = x.mean(dim=(2, 3), keepdim=True)
+                w1, b1, w2, b2 = ws[nxt()], ws[nxt()], ws[nxt()], ws[nxt()]
+                g = F.relu(conv(g, w1, b1, 1, ((0, 0), (0, 0))))
+                x = x * hsig(conv(g, w2, b2, 1, ((0, 0), (0, 0))))
+            w = ws[nxt()]
+            x = bn(conv(x, w, None, 1, ((0, 0), (0, 0))))
+            if s == 1 and cin == f:
+                x = sc + x
+            cin = f
+        w = ws[nxt()]
+        x = hsw(bn(conv(x, w, None, 1, ((0, 0), (0, 0)))))
+    g = x.mean(dim=(2, 3))
+    w1, b1, w2, b2 = ws[nxt()], ws[nxt()], ws[nxt()], ws[nxt()]
+    y = (g @ w1[0, 0] + b1) @ w2[0, 0] + b2
+    assert idx[0] == len(ws)
+    (y * torch.tensor(np.asarray(d_style_params, np.float64))).sum().backward()
+    grads = []
+    for i, w in enumerate(ws):
+        if i in moving or w.grad is None:
+            grads.append(np.zeros(w.shape))
+        else:
+            grads.append(w.grad.numpy().copy())
+    return {'output': y.detach().numpy(), 'grads': grads, 'weights': new_w}

@@ -32,6 +32,9 @@ EXPORTED_SYMBOLS = [
     "rst_trainer_debug_vgg_gradient", "rst_trainer_loss",
     "rst_predictor_num_weights", "rst_predictor_create", "rst_predictor_destroy", "rst_predictor_forward",
     "rst_predictor_num_stages", "rst_predictor_stage_shape", "rst_predictor_copy_stage",
+    "rst_predictor_trainer_create", "rst_predictor_trainer_destroy", "rst_predictor_trainer_num_weights",
+    "rst_predictor_trainer_forward", "rst_predictor_trainer_backward", "rst_predictor_trainer_apply_gradients",
+    "rst_predictor_trainer_copy_weights", "rst_predictor_trainer_set_weights", "rst_predictor_trainer_copy_slots",
 ]
 EXTRACTORS = {"DUMMY": 0, "MOBILE_NET": 1}   # include/rst.h RST_EXTRACTOR_*
 
@@ -154,6 +157,22 @@ def load() -> ctypes.CDLL:
     lib.rst_predictor_stage_shape.restype = i
     lib.rst_predictor_copy_stage.argtypes = [vp, i, vp, sz, i, vp]
     lib.rst_predictor_copy_stage.restype = i
+    lib.rst_predictor_trainer_create.argtypes = [ctypes.POINTER(RstPredictorShape), vp, sz, ctypes.POINTER(vp)]
+    lib.rst_predictor_trainer_create.restype = i
+    lib.rst_predictor_trainer_destroy.argtypes = [vp]
+    lib.rst_predictor_trainer_destroy.restype = None
+    lib.rst_predictor_trainer_num_weights.argtypes = [vp]
+    lib.rst_predictor_trainer_num_weights.restype = sz
+    lib.rst_predictor_trainer_forward.argtypes = [vp, vp, i, vp, vp]
+    lib.rst_predictor_trainer_forward.restype = i
+    lib.rst_predictor_trainer_backward.argtypes = [vp, vp, vp, vp]
+    lib.rst_predictor_trainer_backward.restype = i
+    lib.rst_predictor_trainer_apply_gradients.argtypes = [vp, vp, fp, fp, fp, vp]
+    lib.rst_predictor_trainer_apply_gradients.restype = i
+    for name in ("rst_predictor_trainer_copy_weights", "rst_predictor_trainer_set_weights",
+                 "rst_predictor_trainer_copy_slots"):
+        getattr(lib, name).argtypes = [vp, vp, sz, vp]
+        getattr(lib, name).restype = i
     lib.rst_last_error.argtypes = []
     lib.rst_last_error.restype = ctypes.c_char_p
     lib.rst_version.argtypes = []

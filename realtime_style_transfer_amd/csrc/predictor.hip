@@ -52,7 +52,7 @@ constexpr int STEM_TH = 8, STEM_TW = 32, STEM_PH = 2 * STEM_TH + 1, STEM_PW = 2 
 __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                    const float* __restrict__ ba, const float* __restrict__ bb,
                                                    float* __restrict__ y, int H, int W, int Ho, int Wo, int pad_t,
-                                                   int pad_l) {
+                                                   int pad_l, int act) {
     __shared__ float patch[STEM_PH * STEM_PW * 3];
     const int b = blockIdx.z, t = threadIdx.x;
     const int oy0 = blockIdx.y * STEM_TH, ox0 = blockIdx.x * STEM_TW;
@@ -97,10 +97,10 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, 
     float4* out = reinterpret_cast<float4*>(y + (((size_t)b * Ho + oy) * Wo + ox) * 16);
 #pragma unroll
     for (int j = 0; j < 16; j += 4)
-        out[j / 4] = make_float4(act_apply(fmaf(acc[j], ba[j], bb[j]), ACT_HSWISH),
-                                 act_apply(fmaf(acc[j + 1], ba[j + 1], bb[j + 1]), ACT_HSWISH),
-                                 act_apply(fmaf(acc[j + 2], ba[j + 2], bb[j + 2]), ACT_HSWISH),
-                                 act_apply(fmaf(acc[j + 3], ba[j + 3], bb[j + 3]), ACT_HSWISH));
+        out[j / 4] = make_float4(act_apply(fmaf(acc[j], ba[j], bb[j]), act),
+                                 act_apply(fmaf(acc[j + 1], ba[j + 1], bb[j + 1]), act),
+                                 act_apply(fmaf(acc[j + 2], ba[j + 2], bb[j + 2]), act),
+                                 act_apply(fmaf(acc[j + 3], ba[j + 3], bb[j + 3]), act));
 }
 
 // DUMMY extractor: Conv2D(1, 9, strides=5, padding='same') with bias, no activation
@@ -428,16 +428,27 @@ __device__ void fc_layer(const float* in, int K, const float* __restrict__ Wt, c
 __global__ __launch_bounds__(FC_THREADS) void se_kernel(const float* __restrict__ part, int n_part, float inv_hw,
                                                         int C, int R, const float* __restrict__ w1,
                                                         const float* __restrict__ b1, const float* __restrict__ w2,
-                                                        const float* __restrict__ b2, float* __restrict__ se) {
+                                                        const float* __restrict__ b2, float* __restrict__ se,
+                                                        float* __restrict__ g_out, float* __restrict__ s1_out,
+                                                        float* __restrict__ s2_out) {
     __shared__ float g[1024];
     __shared__ float h[1024];
     __shared__ float s_out[1024];
     __shared__ float red[4 * FC_THREADS];
-    const int b = blockIdx.x;
+    const int b = blockIdx.x, t = threadIdx.x;
     squeeze(part + (size_t)b * n_part * C, n_part, C, inv_hw, g, red);
-    fc_layer(g, C, w1, b1, R, ACT_RELU, h, red);
-    fc_layer(h, R, w2, b2, C, ACT_HSIGMOID, s_out, red);
-    for (int c = threadIdx.x; c < C; c += FC_THREADS) se[(size_t)b * C + c] = s_out[c];
+    fc_layer(g, C, w1, b1, R, ACT_NONE, h, red);          // pre-ReLU s1
+    for (int r = t; r < R; r += FC_THREADS) {
+        if (s1_out != nullptr) s1_out[(size_t)b * R + r] = h[r];
+        h[r] = fmaxf(h[r], 0.f);
+    }
+    __syncthreads();
+    fc_layer(h, R, w2, b2, C, ACT_NONE, s_out, red);      // pre-hard_sigmoid s2
+    for (int c = t; c < C; c += FC_THREADS) {
+        se[(size_t)b * C + c] = hsig(s_out[c]);
+        if (s2_out != nullptr) s2_out[(size_t)b * C + c] = s_out[c];
+        if (g_out != nullptr) g_out[(size_t)b * C + c] = g[c];
+    }
 }
 
 // ------------------------------------------------------------------------------ head
@@ -446,7 +457,7 @@ __global__ __launch_bounds__(FC_THREADS) void se_kernel(const float* __restrict_
 __global__ __launch_bounds__(FC_THREADS) void head1_kernel(const float* __restrict__ part, int n_part, float inv_hw,
                                                            int C, int NS, const float* __restrict__ w1,
                                                            const float* __restrict__ b1,
-                                                           float* __restrict__ hidden) {
+                                                           float* __restrict__ hidden, float* __restrict__ g_out) {
     __shared__ float g[1024];
     __shared__ float h[1024];
     __shared__ float red[4 * FC_THREADS];
@@ -454,6 +465,8 @@ __global__ __launch_bounds__(FC_THREADS) void head1_kernel(const float* __restri
     squeeze(part + (size_t)b * n_part * C, n_part, C, inv_hw, g, red);
     fc_layer(g, C, w1, b1, NS, ACT_NONE, h, red);
     for (int k = threadIdx.x; k < NS; k += FC_THREADS) hidden[(size_t)b * NS + k] = h[k];
+    if (g_out != nullptr)
+        for (int c = threadIdx.x; c < C; c += FC_THREADS) g_out[(size_t)b * C + c] = g[c];
 }
 
 // StyleNormPredictor Conv2D(P, 1) (stylePrediction.py:67-71), no activation: one output per
@@ -478,9 +491,9 @@ __global__ __launch_bounds__(256) void head2_kernel(const float* __restrict__ hi
 
 // ------------------------------------------------------------------------------ launchers
 hipError_t stem_launch(const float* x, const float* w, const float* ba, const float* bb, float* y, int B, int H,
-                       int W, int Ho, int Wo, int pad_t, int pad_l, hipStream_t st) {
+                       int W, int Ho, int Wo, int pad_t, int pad_l, int act, hipStream_t st) {
     dim3 grid((Wo + STEM_TW - 1) / STEM_TW, (Ho + STEM_TH - 1) / STEM_TH, B);
-    stem_kernel<<<grid, 256, 0, st>>>(x, w, ba, bb, y, H, W, Ho, Wo, pad_t, pad_l);
+    stem_kernel<<<grid, 256, 0, st>>>(x, w, ba, bb, y, H, W, Ho, Wo, pad_t, pad_l, act);
     return hipGetLastError();
 }
 
@@ -558,17 +571,19 @@ hipError_t dw_launch(const float* x, const float* w, const float* ba, const floa
 }
 
 hipError_t se_launch(const float* part, int n_part, int hw, int B, int C, int R, const float* w1, const float* b1,
-                     const float* w2, const float* b2, float* se, hipStream_t st) {
+                     const float* w2, const float* b2, float* se, float* g_out, float* s1_out, float* s2_out,
+                     hipStream_t st) {
     if (C > 1024 || R > 1024) return hipErrorInvalidValue;
-    se_kernel<<<B, FC_THREADS, 0, st>>>(part, n_part, 1.f / (float)hw, C, R, w1, b1, w2, b2, se);
+    se_kernel<<<B, FC_THREADS, 0, st>>>(part, n_part, 1.f / (float)hw, C, R, w1, b1, w2, b2, se, g_out, s1_out,
+                                        s2_out);
     return hipGetLastError();
 }
 
 hipError_t head_launch(const float* part, int n_part, int hw, int B, int C, int NS, int P, const float* w1,
                        const float* b1, const float* w2, const float* b2, float* hidden, float* out, int out_stride,
-                       hipStream_t st) {
+                       float* g_out, hipStream_t st) {
     if (C > 1024 || NS > 1024) return hipErrorInvalidValue;
-    head1_kernel<<<B, FC_THREADS, 0, st>>>(part, n_part, 1.f / (float)hw, C, NS, w1, b1, hidden);
+    head1_kernel<<<B, FC_THREADS, 0, st>>>(part, n_part, 1.f / (float)hw, C, NS, w1, b1, hidden, g_out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     dim3 grid((P + 255) / 256, B);

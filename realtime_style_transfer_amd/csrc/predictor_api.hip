@@ -176,7 +176,7 @@ int rst_predictor_forward(rst_predictor* p, const float* style, int batch, float
         switch (u.kind) {
             case PU_STEM:
                 RST_HIP_TRY(stem_launch(style, w + u.woff, a, b, p->out[i], batch, u.H, u.W, u.Ho, u.Wo, u.pad_t,
-                                        u.pad_l, st));
+                                        u.pad_l, ACT_HSWISH, st));
                 break;
             case PU_DUMMY:
                 RST_HIP_TRY(dummy_conv_launch(style, w + u.woff, w + u.goff, p->out[i], p->feat_part, batch, u.H,
@@ -194,7 +194,7 @@ int rst_predictor_forward(rst_predictor* p, const float* style, int batch, float
                 if (e >= 0) {
                     const PSE& s = P.ses[e];
                     RST_HIP_TRY(se_launch(p->se_part[e], p->se_nwg[e], s.Ho * s.Wo, batch, s.C, s.R, w + s.w1,
-                                          w + s.b1, w + s.w2, w + s.b2, p->se_val[e], st));
+                                          w + s.b1, w + s.w2, w + s.b2, p->se_val[e], nullptr, nullptr, nullptr, st));
                 }
                 break;
             }
@@ -202,7 +202,7 @@ int rst_predictor_forward(rst_predictor* p, const float* style, int batch, float
     }
     RST_HIP_TRY(head_launch(p->feat_part, p->feat_nparts, P.feat_hw, batch, P.feat_c, p->shape.num_style_parameters,
                             p->shape.num_top_parameters, w + P.head_w1, w + P.head_b1, w + P.head_w2,
-                            w + P.head_b2, p->d_hidden, style_params, p->shape.num_top_parameters, st));
+                            w + P.head_b2, p->d_hidden, style_params, p->shape.num_top_parameters, nullptr, st));
     return RST_OK;
 }
 

@@ -242,3 +242,106 @@ def create_style_prediction_model(input_shape, feature_extractor: str, num_top_p
     log.info(f"Bottlenecking to {num_style_parameters} parameters for {num_top_parameters} norm parameters")
     return StylePredictionModel(input_shape, feature_extractor, num_top_parameters, num_style_parameters, name=name,
                                 **kwargs)
+
+
+class StylePredictionTrainer:
+    """The style predictor in Keras training mode on one GPU (one ``rst_predictor_trainer``).
+
+    ``forward(style)`` runs with BatchNormalization on the batch statistics (and updates the moving
+    statistics, momentum 0.999); ``backward(d_style_params)`` returns the gradient of
+    ``sum(style_params * d_style_params)`` for every weight (Keras order, zeros for moving
+    statistics); ``apply_gradients`` is RMSprop on the device-resident weights. train_network.py
+    fits this model jointly with the transfer network (stylePrediction.py:25-75 is trainable,
+    styleTransferTrainingModel.py:39-70)."""
+
+    def __init__(self, input_shape, feature_extractor: str, num_top_parameters: int, num_style_parameters: int = 100,
+                 weights: Optional[Sequence[np.ndarray]] = None, seed: int = 3, max_batch: int = 4, device=None):
+        self.input_shape = tuple(int(v) for v in input_shape)
+        self.feature_extractor = feature_extractor
+        self.num_top_parameters = int(num_top_parameters)
+        self.num_style_parameters = int(num_style_parameters)
+        self.max_batch = int(max_batch)
+        self.spec = predictor_weight_spec(self.input_shape, feature_extractor, self.num_top_parameters,
+                                          self.num_style_parameters)
+        self._shapes = [s for _, s, _ in self.spec]
+        self._sizes = [int(np.prod(s)) for s in self._shapes]
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        w = weights if weights is not None else init_predictor_weights(self.spec, seed)
+        if len(w) != len(self._shapes) or any(tuple(np.shape(a)) != s for a, s in zip(w, self._shapes)):
+            raise ValueError(f"weights do not match the predictor: expected {self._shapes}")
+        flat = np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in w])
+        lib = _lib.load()
+        H, W, C = self.input_shape
+        shape = _lib.RstPredictorShape(H, W, C, _lib.EXTRACTORS[feature_extractor], self.num_top_parameters,
+                                       self.num_style_parameters, self.max_batch)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(lib.rst_predictor_trainer_create(ctypes.byref(shape), flat.ctypes.data, flat.size,
+                                                        ctypes.byref(h)))
+        self._handle = h
+        self.num_weights = int(lib.rst_predictor_trainer_num_weights(h))
+        if self.num_weights != flat.size:
+            raise RuntimeError("librst predictor trainer plan disagrees with the host weight list")
+        self._style = None
+
+    def __del__(self):
+        try:
+            if getattr(self, '_handle', None) is not None:
+                _lib.load().rst_predictor_trainer_destroy(self._handle)
+                self._handle = None
+        except Exception:
+            pass
+
+    def _unflatten(self, flat: np.ndarray) -> List[np.ndarray]:
+        out, o = [], 0
+        for s, n in zip(self._shapes, self._sizes):
+            out.append(flat[o:o + n].reshape(s).copy())
+            o += n
+        return out
+
+    def forward(self, style: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if style.dim() != 4 or tuple(style.shape[1:]) != self.input_shape:
+            raise ValueError(f"style must be (B,{','.join(map(str, self.input_shape))}), got {tuple(style.shape)}")
+        B = style.shape[0]
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} exceeds max_batch={self.max_batch}")
+        self._style = style.contiguous()          # must outlive the matching backward
+        if out is None:
+            out = torch.empty((B, self.num_top_parameters), dtype=torch.float32, device=style.device)
+        _lib.check(_lib.load().rst_predictor_trainer_forward(self._handle, _lib.dev_ptr(self._style), B,
+                                                             _lib.dev_ptr(out), _lib.stream_ptr()))
+        return out
+
+    def backward(self, d_style_params: torch.Tensor, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if grad is None:
+            grad = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
+        _lib.check(_lib.load().rst_predictor_trainer_backward(self._handle, _lib.dev_ptr(d_style_params.contiguous()),
+                                                              _lib.dev_ptr(grad), _lib.stream_ptr()))
+        return grad
+
+    def apply_gradients(self, grad: torch.Tensor, learning_rate: float = 1e-3, rho: float = 0.9,
+                        epsilon: float = 1e-7):
+        _lib.check(_lib.load().rst_predictor_trainer_apply_gradients(self._handle, _lib.dev_ptr(grad),
+                                                                     float(learning_rate), float(rho), float(epsilon),
+                                                                     _lib.stream_ptr()))
+
+    def get_weights(self) -> List[np.ndarray]:
+        t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
+        _lib.check(_lib.load().rst_predictor_trainer_copy_weights(self._handle, _lib.dev_ptr(t), t.numel(),
+                                                                  _lib.stream_ptr()))
+        return self._unflatten(t.cpu().numpy())
+
+    def optimizer_slots(self) -> List[np.ndarray]:
+        t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
+        _lib.check(_lib.load().rst_predictor_trainer_copy_slots(self._handle, _lib.dev_ptr(t), t.numel(),
+                                                                _lib.stream_ptr()))
+        return self._unflatten(t.cpu().numpy())
+
+    def unflatten(self, grad: torch.Tensor) -> List[np.ndarray]:
+        return self._unflatten(grad.detach().cpu().numpy())
+
+    def inference_model(self, max_batch: Optional[int] = None) -> StylePredictionModel:
+        """An inference StylePredictionModel with the current weights (BN on the moving statistics)."""
+        return StylePredictionModel(self.input_shape, self.feature_extractor, self.num_top_parameters,
+                                    self.num_style_parameters, weights=self.get_weights(),
+                                    max_batch=max_batch or self.max_batch, device=self.device)

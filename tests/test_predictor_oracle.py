@@ -91,3 +91,35 @@ def test_factory_errors_mirror_reference():
         create_style_prediction_model((64, 64, 3), 'RESNET', 10)
     with pytest.raises(NotImplementedError):
         create_style_prediction_model((64, 64, 3), StyleFeatureExtractor.EFFICIENT_NET, 10)
+
+
+@pytest.mark.parametrize("ext", ["MOBILE_NET", "DUMMY"])
+def test_training_oracle_matches_finite_differences(ext):
+    """predictor_train_reference (float64 autograd, BN on batch statistics) vs central differences."""
+    ins, P = (32, 48, 3), 24
+    spec = predictor_weight_spec(ins, ext, P)
+    ws = [w.astype(np.float64) for w in init_predictor_weights(spec, seed=3, perturb=True)]
+    rng = np.random.default_rng(0)
+    x = rng.random((2,) + ins)
+    dP = rng.normal(size=(2, P))
+    ref = PR.predictor_train_reference(x, ws, ext, dP)
+
+    def loss(wl):
+        return float((PR.predictor_train_reference(x, wl, ext, dP)['output'] * dP).sum())
+
+    checked = 0
+    for i, (name, shape, kind) in enumerate(spec):
+        if kind in ('mean', 'var') or (ext == 'MOBILE_NET' and i % 7 != 0):
+            continue
+        j = int(rng.integers(ws[i].size))
+        wp = [w.copy() for w in ws]
+        wm = [w.copy() for w in ws]
+        wp[i].flat[j] += 1e-6
+        wm[i].flat[j] -= 1e-6
+        fd = (loss(wp) - loss(wm)) / 2e-6
+        assert abs(fd - ref['grads'][i].flat[j]) <= 1e-5 * max(1.0, abs(fd)), (name, fd, ref['grads'][i].flat[j])
+        checked += 1
+    assert checked >= 4
+    for (name, shape, kind), g in zip(spec, ref['grads']):
+        if kind in ('mean', 'var'):
+            assert not g.any()
