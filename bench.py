@@ -134,11 +134,15 @@ def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, tim
     from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
     TB = args.train_batch
     lm = StyleLossModelVGG(outs, max_batch=TB, device=dev, precision=precision)
+    from realtime_style_transfer_amd.stylePrediction import StylePredictionTrainer
+    sins = tuple(cfg.input_shape['style'][1:])
+    # train_network.py fits the MobileNetV3Small style predictor jointly (stylePrediction.py:25-75)
+    pr = StylePredictionTrainer(sins, cfg.style_feature_extractor_type, P, max_batch=TB, device=dev)
     tr = StyleTransferTrainingModel(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, loss_model=lm,
-                                    weights=weights, max_batch=TB, device=dev)
+                                    weights=weights, max_batch=TB, device=dev, style_predictor=pr)
     rng = np.random.default_rng(3000 + rank)
     x = {'content': torch.from_numpy(rng.random((TB,) + ins, dtype=np.float32)).to(dev),
-         'style_params': torch.from_numpy(synthetic_style_params(TB, 1, P, plan, seed=1)).to(dev)}
+         'style': torch.from_numpy(rng.random((TB, 1) + sins, dtype=np.float32)).to(dev)}
     y = {'content': torch.from_numpy(rng.random((TB,) + outs, dtype=np.float32)).to(dev),
          'style': torch.from_numpy(rng.random((TB, 1) + outs, dtype=np.float32)).to(dev)}
     for _ in range(2):
@@ -150,9 +154,10 @@ def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, tim
     per_sample = sum(fl.values())
     ms = el * 1e3 / args.train_steps
     tfs = per_sample * TB / (ms * 1e-3) / 1e12
-    return {"workload": f"{SPEC} train_network.py step (BASELINE config 4): training-mode forward, VGG16/Gram loss "
-                        f"(no depth term), backward, " + ("RCCL gradient all-reduce (SUM), " if world > 1 else "") +
-                        "RMSprop", "batch_per_gpu": TB, "steps": args.train_steps, "ms_per_step": round(ms, 3),
+    return {"workload": f"{SPEC} train_network.py step (BASELINE config 4): MobileNetV3Small style predictor + "
+                        f"transfer net, training-mode forward, VGG16/Gram loss (no depth term), backward of both, " +
+                        ("RCCL gradient all-reduce (SUM, one bucket), " if world > 1 else "") +
+                        "RMSprop on both", "batch_per_gpu": TB, "steps": args.train_steps, "ms_per_step": round(ms, 3),
             "frames_per_s": round(world * TB * args.train_steps / el, 3),
             "dtype": {"fp32": "fp32 (f32 MFMA)",
                       "bf16x6": "VGG16 3x3 convs: exact 3-piece split bf16 MFMA (fp32-level products, fp32 accumulate); "

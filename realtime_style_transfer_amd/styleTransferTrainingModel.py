@@ -6,15 +6,17 @@ weights and RMSprop slots live on the GPU; one ``train_step`` runs the training-
 the VGG16/Gram loss (``StyleLossModelVGG`` factors), the backward and the RMSprop update
 entirely in hand-written gfx950 kernels. There is no CPU fallback.
 
-Deviations, by construction of this build:
+With a style predictor (``StylePredictionTrainer``, stylePrediction.py:25-75 in training mode) the
+step is the reference's joint one: ``x = {'content', 'style'}``, the predictor's output feeds the
+transfer network as its style parameters, their gradient flows back into the predictor, and both
+weight sets take an RMSprop step. Without one, ``style_params`` are an input (``x = {'content',
+'style_params'}``) and their gradient is returned.
 
-* The style predictor (MobileNetV3Small, stylePrediction.py:25-75) is a separate, not yet
-  built component: ``style_params`` are an input of ``train_step`` and
-  their gradient is returned so a predictor can be chained in front.
 * ``compute_loss`` returns the per-image ``(B,)`` loss; Keras minimises its sum, and so does this.
-* Data parallel: with ``process_group`` set, the gradients are all-reduced (SUM, RCCL over xGMI)
-  before the update, which equals one step on the concatenated global batch except that the
-  BatchNorm statistics stay per rank (as TF without SyncBatchNorm would).
+* Data parallel: with ``process_group`` set, the gradients (transfer and predictor in ONE flat
+  bucket) are all-reduced (SUM, RCCL over xGMI) before the update, which equals one step on the
+  concatenated global batch except that the BatchNorm statistics stay per rank (as TF without
+  SyncBatchNorm would).
 """
 from __future__ import annotations
 
@@ -66,7 +68,7 @@ class StyleTransferTrainingModel:
     def __init__(self, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
                  loss_model: Optional[StyleLossModelVGG] = None, weights: Optional[Sequence[np.ndarray]] = None,
                  seed: int = 2, max_batch: int = 4, optimizer: Optional[RMSprop] = None, process_group=None,
-                 device=None, name: str = "StyleTransferTrainingModel"):
+                 device=None, name: str = "StyleTransferTrainingModel", style_predictor=None):
         self.name = name
         self.plan: Plan = network_plan(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, 1)
         self.input_shape = tuple(int(v) for v in input_shape)
@@ -101,7 +103,19 @@ class StyleTransferTrainingModel:
         self.num_weights = int(lib.rst_trainer_num_weights(h))
         if self.num_weights != flat.size or lib.rst_trainer_num_style_params(h) != self.num_style_parameters:
             raise RuntimeError("librst trainer plan disagrees with the host plan")
-        self._grad = torch.zeros(self.num_weights, dtype=torch.float32, device=self.device)
+        self.style_predictor = style_predictor      # StylePredictionTrainer or None
+        n_pred = 0
+        if style_predictor is not None:
+            if style_predictor.num_top_parameters != self.num_style_parameters:
+                raise ValueError(f"style predictor emits {style_predictor.num_top_parameters} parameters, the "
+                                 f"transfer network takes {self.num_style_parameters}")
+            if style_predictor.max_batch < self.max_batch:
+                raise ValueError("style predictor max_batch is smaller than the training batch")
+            n_pred = style_predictor.num_weights
+        # one flat gradient bucket: [transfer weights | predictor weights] (a single all-reduce per step)
+        self._bucket = torch.zeros(self.num_weights + n_pred, dtype=torch.float32, device=self.device)
+        self._grad = self._bucket[:self.num_weights]
+        self._pgrad = self._bucket[self.num_weights:] if n_pred else None
         self.style_losses: Dict[str, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ lifecycle
@@ -214,12 +228,29 @@ class StyleTransferTrainingModel:
         self.style_losses = {}
 
     def train_step(self, x: Dict[str, torch.Tensor], y: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
-        """One Keras fit step: x = {'content', 'style_params'}, y = {'content', 'style'}."""
-        pred, losses, grad, gsp = self.compute_gradients(x['content'], x['style_params'], y['content'], y['style'])
-        allreduce_gradients(grad, self.process_group)
+        """One Keras fit step. With a style predictor: x = {'content', 'style' (B,1,H,W,3)}; without:
+        x = {'content', 'style_params'}. y = {'content', 'style'}."""
+        pr = self.style_predictor
+        if pr is not None:
+            style = x['style']
+            if style.dim() == 5:
+                if style.shape[1] != 1:
+                    raise ValueError("the training model takes one style (num_styles=1, styleTransferTrainingModel.py:46)")
+                style = style[:, 0]
+            sp = pr.forward(style)                                     # styleTransferInferenceModel.py:23-28
+        else:
+            sp = x['style_params']
+        pred, losses, grad, gsp = self.compute_gradients(x['content'], sp, y['content'], y['style'])
+        if pr is not None:
+            pr.backward(gsp, grad=self._pgrad)
+        allreduce_gradients(self._bucket, self.process_group)
         self.apply_gradients(grad)
+        if pr is not None:
+            o = self.optimizer
+            pr.apply_gradients(self._pgrad, o.learning_rate, o.rho, o.epsilon)
         self.style_losses = {n: losses[:, i] for i, n in enumerate(LOSS_NAMES)}
         self.last_prediction = pred
+        self.last_style_params = sp
         self.last_grad_style_params = gsp
         return self.compute_metrics()
 
@@ -231,18 +262,25 @@ class StyleTransferTrainingModel:
 
 
 class StyleTransferModels:
-    """The object make_style_transfer_training_model returns (styleTransferTrainingModel.py:60-68)."""
+    """The object make_style_transfer_training_model returns (styleTransferTrainingModel.py:60-68).
+    ``transfer`` / ``style_predictor`` / ``inference`` are inference models holding the weights of
+    the moment they are built; ``refresh()`` rebuilds them from the trainers."""
 
     def __init__(self, training: StyleTransferTrainingModel, loss_model):
         self.training = training
         self.loss_model = loss_model
-        self.style_predictor = None
-        self.transfer = training.transfer_model()
+        self.refresh()
 
-        def inference(inputs: Dict[str, torch.Tensor]) -> torch.Tensor:
-            return self.transfer(inputs)
-
-        self.inference = inference
+    def refresh(self):
+        from .styleTransferInferenceModel import StyleTransferInference
+        tr = self.training
+        self.transfer = tr.transfer_model()
+        if tr.style_predictor is not None:
+            self.style_predictor = tr.style_predictor.inference_model()
+            self.inference = StyleTransferInference(self.transfer, self.style_predictor, 1, tr.name)
+        else:
+            self.style_predictor = None
+            self.inference = lambda inputs: self.transfer(inputs)
 
 
 def make_style_transfer_training_model(style_predictor_factory_func: Optional[Callable],
@@ -253,17 +291,23 @@ def make_style_transfer_training_model(style_predictor_factory_func: Optional[Ca
     """styleTransferTrainingModel.py:39-70 on librst.
 
     ``style_transfer_factory_func() -> (StyleTransferModel, P)`` supplies the architecture and
-    initial weights; ``style_loss_func_factory_func() -> (compute_loss, StyleLossModelVGG)``
-    supplies the loss model. The style predictor is not built yet: pass None and
-    feed ``style_params`` directly."""
+    initial weights; ``style_predictor_factory_func(P) -> StylePredictionModel`` (or None: feed
+    ``style_params`` directly) the predictor trained jointly with it (stylePrediction.py:25-75);
+    ``style_loss_func_factory_func() -> (compute_loss, StyleLossModelVGG)`` the loss model."""
+    from .stylePrediction import StylePredictionTrainer
+    transfer, P = style_transfer_factory_func()
+    predictor = None
     if style_predictor_factory_func is not None:
-        raise NotImplementedError("the MobileNetV3 style predictor is not built yet; pass None and feed style_params")
-    transfer, _ = style_transfer_factory_func()
+        pm = style_predictor_factory_func(P)
+        predictor = StylePredictionTrainer(pm.input_shape, pm.feature_extractor, pm.num_top_parameters,
+                                           pm.num_style_parameters, weights=pm.get_weights(), max_batch=max_batch,
+                                           device=transfer.device)
     _, loss_model = style_loss_func_factory_func()
     training = StyleTransferTrainingModel(transfer.input_shape, transfer.output_shape, transfer.plan.bottleneck_res_y,
                                           transfer.plan.bottleneck_num_filters, loss_model=loss_model,
                                           weights=transfer.get_weights(), max_batch=max_batch, optimizer=optimizer,
-                                          process_group=process_group, device=transfer.device, name=name)
+                                          process_group=process_group, device=transfer.device, name=name,
+                                          style_predictor=predictor)
     return StyleTransferModels(training, loss_model)
 
 

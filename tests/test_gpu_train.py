@@ -232,3 +232,82 @@ def test_prediction_gradient_per_loss_term(factors):
     with open(os.path.join(OUT, f'train_dpred_{factors}.json'), 'w') as f:
         json.dump({'rel': rel, 'scale': float(np.abs(r).max()), 'vgg_rel': vrel}, f)
     assert rel < 1e-3, rel
+
+
+def test_joint_training_with_style_predictor_matches_oracle():
+    """train_network.py's joint step: MobileNetV3Small predictor (training mode) -> style params -> transfer
+    network -> VGG/Gram loss -> gradients of both weight sets (config B geometry, B=2)."""
+    _need_gpu()
+    from oracle import predictor_ref as PR
+    from oracle import torch_train as T
+    from realtime_style_transfer_amd.stylePrediction import (StylePredictionTrainer, init_predictor_weights,
+                                                             predictor_weight_spec)
+    cfg = CONFIGS['B']
+    B = 2
+    plan, w, vgg, content, _, gtc, gts = _case(cfg, B)
+    P = plan.num_style_params
+    sins = cfg['output_shape']
+    spec = predictor_weight_spec(sins, 'MOBILE_NET', P)
+    pw = init_predictor_weights(spec, seed=3, perturb=True)
+    style = np.random.default_rng(12).random((B,) + sins).astype(np.float32)
+    tr = _trainer(cfg, w, vgg, B)
+    pr = StylePredictionTrainer(sins, 'MOBILE_NET', P, weights=pw, max_batch=B)
+    c, gc, gs, st = _cuda(content, gtc, gts, style)
+    sp = pr.forward(st)
+    pred, losses, grad, gsp = tr.compute_gradients(c, sp, gc, gs)
+    pgrad = pr.backward(gsp)
+    torch.cuda.synchronize()
+    sp_ref = PR.predictor_train_reference(style, pw, 'MOBILE_NET', np.zeros((B, P)))['output']
+    assert np.abs(sp.cpu().numpy() - sp_ref).max() <= 1e-4 * np.abs(sp_ref).max()
+    ref = T.training_step(w, vgg, content, sp.cpu().numpy().astype(np.float64), gtc, gts,
+                          pool_route=_pool_route(tr, B), **cfg)
+    gerr = float(np.linalg.norm(gsp.cpu().numpy() - ref['grad_style_params']) /
+                 np.linalg.norm(ref['grad_style_params']))
+    assert gerr < 2e-3, gerr
+    pref = PR.predictor_train_reference(style, pw, 'MOBILE_NET', ref['grad_style_params'])
+    got = pr.unflatten(pgrad)
+    gscale = max(float(np.linalg.norm(r)) for r in pref['grads'])
+    worst = 0.0
+    for (name, shape, kind), a, r in zip(spec, got, pref['grads']):
+        nr = float(np.linalg.norm(r))
+        if kind in ('mean', 'var') or nr <= 1e-9 * gscale:
+            assert np.linalg.norm(a) <= 1e-5 * gscale, name
+            continue
+        e = float(np.linalg.norm(a - r) / nr)
+        worst = max(worst, e)
+        assert e < 5e-3, (name, e)
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, 'train_parity_joint_predictor.json'), 'w') as f:
+        json.dump({'style_params_rel': float(np.abs(sp.cpu().numpy() - sp_ref).max() / np.abs(sp_ref).max()),
+                   'grad_style_params_rel': gerr, 'predictor_grad_worst_rel': worst}, f, indent=1)
+
+
+def test_training_model_reference_geometry_with_dummy_predictor():
+    """styleTransferTrainingModelTest.py:15-58: 240x480x3 -> 480x960x3, bottleneck 30 rows x 4 filters,
+    DUMMY predictor, a fit over two zero samples in one batch of 2 (the VGG loss stands in for
+    StyleLossModelDummy; the MiDaS depth term is a TF-Hub download, so with_depth_loss=False)."""
+    _need_gpu()
+    from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG, make_style_loss_function
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    from realtime_style_transfer_amd.stylePrediction import StyleFeatureExtractor, create_style_prediction_model
+    from realtime_style_transfer_amd.styleTransferTrainingModel import make_style_transfer_training_model
+    ie, oe = (240, 480, 3), (480, 960, 3)
+    m = make_style_transfer_training_model(
+        style_transfer_factory_func=lambda: create_style_transfer_model(ie, oe, 30, 4, num_styles=1,
+                                                                        name="StyleTransferTestModel", max_batch=2),
+        style_predictor_factory_func=lambda P: create_style_prediction_model(oe, StyleFeatureExtractor.DUMMY, P),
+        style_loss_func_factory_func=lambda: make_style_loss_function(StyleLossModelVGG(oe, max_batch=2), oe, 1,
+                                                                  with_depth_loss=False),
+        name="StyleTransferTrainingTestModel", max_batch=2)
+    x = {'content': torch.zeros((2,) + ie, device='cuda'), 'style': torch.zeros((2, 1) + oe, device='cuda')}
+    y = {'content': torch.zeros((2,) + oe, device='cuda'), 'style': torch.zeros((2, 1) + oe, device='cuda')}
+    w0 = m.training.style_predictor.get_weights()
+    metrics = m.training.train_step(x, y)
+    torch.cuda.synchronize()
+    assert set(metrics) == {'loss', 'feature_loss', 'style_loss', 'total_variation_loss'}
+    assert all(bool(torch.isfinite(v)) for v in metrics.values())
+    w1 = m.training.style_predictor.get_weights()
+    assert any(not np.array_equal(a, b) for a, b in zip(w0, w1)), "the predictor was not trained"
+    m.refresh()
+    out = m.inference({'content': x['content'], 'style': x['style']})
+    assert tuple(out.shape) == (2,) + oe
