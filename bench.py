@@ -57,6 +57,7 @@ KERNEL_NAMES = {
     101: "conv_bf3<3x3 s1 CK32 NT128 bf16x3>", 102: "conv_bf3<3x3 s1 CK32 NT64 bf16x3>",
     111: "conv_bf3<3x3 s1 CK32 NT128 bf16x6>", 112: "conv_bf3<3x3 s1 CK32 NT64 bf16x6>",
     113: "conv_bf3<3x3 s1 CK32 NT64 8x16 bf16x6>",
+    200: "wino_conv<F(2x2,3x3) 8x16 N128 f32 MFMA>",
 }
 
 
@@ -116,6 +117,18 @@ def bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs, time
     ms = sum(conv_ms[i] for i in bf3) / max(nsteps, 1) / max(len(bf3), 1)
     fl = sum(layer_flops(plan.layers[i]) for i in bf3) * B / max(len(bf3), 1)
     eff_tf = fl / (ms * 1e-3) / 1e12
+    if precision == "fp32_winograd":
+        return model, {
+            "value": round(world * B * args.steps / el, 3), "unit": "frames/s",
+            "ms_per_step": round(el * 1e3 / args.steps, 4),
+            "dtype": "fp32 (exact-f32 MFMA products, f32 accumulate); the residual convs as fused Winograd "
+                     "F(2x2,3x3) (16 instead of 36 multiplies per 2x2 output tile), other layers direct",
+            "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES.get(200), "achieved": round(eff_tf, 2),
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s (algorithmic = direct-conv FLOPs)",
+                         "frac": round(eff_tf / FP32_MFMA_PEAK_TFLOPS, 4), "avg_launch_ms": round(ms, 5),
+                         "mfma_pipe_frac": round(eff_tf * 16.0 / 36.0 / FP32_MFMA_PEAK_TFLOPS, 4)},
+            "layers_ms": [round(c / max(nsteps, 1), 4) for c in conv_ms],
+        }
     return model, {
         "value": round(world * B * args.steps / el, 3), "unit": "frames/s", "ms_per_step": round(el * 1e3 / args.steps, 4),
         "dtype": ("fp32 via 2-piece split bf16 (3 product terms, 16 significant bits per operand)" if terms == 3 else
@@ -399,7 +412,7 @@ def main():
     # ---------------- precision mode: split-bf16 residual convs (reported beside the fp32 headline) --
     split_models, split = {}, {}
     if not args.no_bf16x3:
-        for prec in ("bf16x6", "bf16x3"):
+        for prec in ("fp32_winograd", "bf16x6", "bf16x3"):
             split_models[prec], split[prec] = bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs,
                                                           timed, prec)
 

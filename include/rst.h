@@ -70,8 +70,11 @@ void rst_destroy(rst_handle* h);
  * f32-MFMA cost. BF16X3: two pieces, three terms (16 significant bits per operand; TF32,
  * TensorFlow's default for "fp32" convs on NVIDIA Ampere, keeps 11) at 3/16 of the cost.
  * The split modes are used for the 3x3 s1 convs with Cin % 32 == 0 (the residual blocks); the
- * other layers stay FP32. */
-enum { RST_PRECISION_FP32 = 0, RST_PRECISION_BF16X3 = 1, RST_PRECISION_BF16X6 = 2 };
+ * other layers stay FP32.
+ * FP32_WINOGRAD: fp32 arithmetic (exact-f32 MFMA products, f32 accumulation) with the residual
+ * convs computed as Winograd F(2x2,3x3) (16 instead of 36 multiplies per 2x2 output tile); single
+ * style only (two-style blending keeps the direct kernel). */
+enum { RST_PRECISION_FP32 = 0, RST_PRECISION_BF16X3 = 1, RST_PRECISION_BF16X6 = 2, RST_PRECISION_FP32_WINOGRAD = 3 };
 int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_weights, int precision,
                   rst_handle** out);
 int rst_precision(const rst_handle* h);

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstddef>
+#include <vector>
 
 namespace rst {
 
@@ -45,6 +46,27 @@ hipError_t conv_prepare(const ConvTile& t);
 bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, ConvTile* out);
 hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st);
 hipError_t conv_bf3_prepare(const ConvTile& t);
+
+// Residual-block conv (3x3 s1 SAME, 128 output channels) as fused Winograd F(2x2,3x3) on f32 MFMA
+// (wino.hip). Epilogue: bias + ReLU + store + per-(workgroup, channel) {sum, M2, n}, n_part =
+// tiles_y * tiles_x per image.
+struct WinoArgs {
+    const float* in;        // NHWC [B][H][W][cin] raw producer output
+    const float* res;       // residual source (PRO_AFF_RES)
+    float* mat;             // materialise the transformed input here (or null)
+    const float2* pro_ab;   // [B][cin] prologue affine
+    const float* U;         // transformed weights [cin/8][16][128][8]
+    const float* bias;      // [128]
+    float* out;             // NHWC [B][H][W][128]
+    float4* part;           // [B][128][tiles_y*tiles_x] or null
+    int batch, H, W, cin, tiles_y, tiles_x, pro_mode;
+};
+bool wino_supported(int kh, int stride, int cin, int cout);
+int wino_tiles_y(int H);
+int wino_tiles_x(int W);
+std::vector<float> wino_pack_weights(const float* kern, int cin);
+hipError_t wino_prepare();
+hipError_t wino_launch(const WinoArgs& a, hipStream_t st);
 
 // Final 9x9 transposed conv with Cout = 3 on the VALU (conv_small.hip).
 struct SmallConvArgs {

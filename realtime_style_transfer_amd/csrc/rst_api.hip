@@ -197,6 +197,19 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.tiles_y = small_conv_tiles_y(s.Ho);
         e.tiles_x = small_conv_tiles_x(s.Wo);
         e.n_part = e.tiles_y * e.tiles_x;
+    } else if (precision == RST_PRECISION_FP32_WINOGRAD && s.keras_kind == 0 &&
+               wino_supported(s.k, s.stride, s.cin, s.cout) && s.res_block >= 0) {
+        // ---- residual conv as fused Winograd F(2x2,3x3) (wino.hip)
+        e.kind = K_WINO;
+        packed = wino_pack_weights(kern, s.cin);
+        bias_n.assign(bias, bias + s.cout);
+        e.ntot = s.cout;
+        e.pad_t = e.pad_l = 1;
+        e.gHo = s.Ho;
+        e.gWo = s.Wo;
+        e.tiles_y = wino_tiles_y(s.Ho);
+        e.tiles_x = wino_tiles_x(s.Wo);
+        e.n_part = e.tiles_y * e.tiles_x;
     } else {
         int taps, ntot, kh;
         std::vector<float> Wg;
@@ -282,7 +295,8 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
                   rst_handle** out) {
     if (shape == nullptr || out == nullptr || weights_host == nullptr)
         return fail(RST_ERR_INVALID, "rst_create: null argument");
-    if (precision != RST_PRECISION_FP32 && precision != RST_PRECISION_BF16X3 && precision != RST_PRECISION_BF16X6)
+    if (precision != RST_PRECISION_FP32 && precision != RST_PRECISION_BF16X3 && precision != RST_PRECISION_BF16X6 &&
+        precision != RST_PRECISION_FP32_WINOGRAD)
         return fail(RST_ERR_INVALID, "rst_create_ex: unknown precision mode");
     *out = nullptr;
     if (shape->num_styles > 2)
@@ -316,7 +330,10 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         const float* bias = wp + kcount;
         wp += kcount + s.cout;
         std::vector<float> bias_n, packed;
-        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, precision)) != RST_OK) { delete h; return st; }
+        // the Winograd kernel has no two-style blend prologue: those layers keep the direct kernel
+        const int lp = (precision == RST_PRECISION_FP32_WINOGRAD && shape->num_styles == 2) ? RST_PRECISION_FP32
+                                                                                            : precision;
+        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp)) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
         if (s.norm == N_BN) {
@@ -398,7 +415,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     // kernels with > 64 KB of dynamic LDS need the attribute before any (graph-captured) launch
     for (auto& e : h->layers) {
         if (e.kind == K_SMALL) continue;
-        hipError_t pe = conv_prepare(e.tile);
+        hipError_t pe = e.kind == K_WINO ? wino_prepare() : conv_prepare(e.tile);
         if (pe != hipSuccess) {
             delete h;
             return fail(RST_ERR_HIP, std::string("conv_prepare: ") + hipGetErrorString(pe));
@@ -450,6 +467,25 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         if (e.pro != PRO_AFF_RELU && e.pro != PRO_NONE)
             return fail(RST_ERR_UNSUPPORTED, "last layer prologue must be CIN+ReLU");
         HIP_TRY(small_conv_launch(a, st));
+    } else if (e.kind == K_WINO) {
+        WinoArgs a{};
+        a.in = in;
+        a.res = e.pro_res;
+        a.mat = e.d_mat;
+        a.pro_ab = pro_ab;
+        a.U = e.d_w;
+        a.bias = e.d_bias;
+        a.out = e.d_out;
+        a.part = e.d_part;
+        a.batch = B;
+        a.H = e.s.H;
+        a.W = e.s.W;
+        a.cin = e.s.cin;
+        a.tiles_y = e.tiles_y;
+        a.tiles_x = e.tiles_x;
+        a.pro_mode = e.pro;
+        if (blend) return fail(RST_ERR_UNSUPPORTED, "Winograd conv has no two-style blend prologue");
+        HIP_TRY(wino_launch(a, st));
     } else {
         ConvArgs a{};
         a.in = in;
@@ -574,7 +610,7 @@ int rst_precision(const rst_handle* h) { return h ? h->precision : -1; }
 int rst_layer_kernel_id(const rst_handle* h, int idx) {
     if (h == nullptr || idx < 0 || idx >= (int)h->layers.size()) return -1;
     const LayerExec& e = h->layers[idx];
-    return e.kind == K_SMALL ? 100 : e.tile.id;
+    return e.kind == K_SMALL ? 100 : (e.kind == K_WINO ? 200 : e.tile.id);
 }
 
 int rst_layer_output_shape(const rst_handle* h, int idx, int batch, int* hwc3) {

@@ -192,3 +192,58 @@ def test_split_bf16_precision_modes(precision, tol):
     with open(os.path.join(OUT, f'{precision}_parity.json'), 'w') as f:
         json.dump({'max_abs': err}, f)
     assert err < tol, err   # bf16x3: the float64 simulation of the split gives ~2e-5 here; fp32 gives ~2e-6
+
+
+def test_winograd_residual_convs_match_oracle():
+    """RST_PRECISION_FP32_WINOGRAD: residual convs as fused Winograd F(2x2,3x3) on f32 MFMA vs float64,
+    small geometry (production channel counts) and odd sizes (partial 8x16 tiles)."""
+    _need_gpu()
+    from oracle import numpy_ref as R
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    for ins, outs, br in (((32, 64, 17), (32, 64, 3), 8), ((44, 76, 17), (44, 76, 3), 11)):
+        bf = 128
+        plan = network_plan(ins, outs, br, bf)
+        w = init_weights(plan, seed=2)
+        sp = synthetic_style_params(2, 1, plan.num_style_params, plan, seed=1)
+        x = np.random.default_rng(0).random((2,) + ins).astype(np.float32)
+        ref = R.transfer_forward(x, sp, w, ins, outs, br, bf)
+        m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision="fp32_winograd")
+        assert [m.layer_kernel_id(i) for i in range(m.num_layers())][3:13] == [200] * 10
+        inp = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}
+        y = m(inp)
+        err = float(np.abs(y.cpu().numpy() - ref).max())
+        assert err < OUT_TOL, (ins, err)
+        assert torch.equal(y, m(inp)), "Winograd forward is not deterministic"
+        # every residual block output against the float64 oracle
+        _, inter = R.transfer_forward(x, sp, w, ins, outs, br, bf, return_intermediates=True)
+        ref_blocks = [v for k, v in inter.items() if 'residual' in k]
+        got = [m.layer_output(i, 2).cpu().numpy() for i, l in enumerate(plan.layers)
+               if l.block.startswith('residual') and l.name.endswith('conv1')]
+        assert len(got) == len(ref_blocks) == 5
+        for g, r in zip(got, ref_blocks):
+            assert np.abs(g - r).max() / max(1.0, np.abs(r).max()) < 1e-4
+
+
+def test_winograd_full_size_matches_torch_oracle():
+    _need_gpu()
+    from oracle.torch_ref import TorchTransfer
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    cfg = ShapeConfig.from_spec("rst-960-120-128-17")
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    ws = init_weights(plan, seed=2)
+    model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                           weights=ws, max_batch=1, precision="fp32_winograd")
+    x = np.random.default_rng(0).random((1,) + ins).astype(np.float32)
+    sp = synthetic_style_params(1, 1, P, plan, seed=1)
+    y = model({'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}).cpu().numpy()
+    ref = TorchTransfer(ws, ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)(x, sp)
+    err = float(np.abs(y - ref).max())
+    import json
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, 'winograd_parity.json'), 'w') as f:
+        json.dump({'max_abs_full_size': err}, f)
+    assert err < OUT_TOL, err
