@@ -12,13 +12,17 @@
 // tile) x 128 output channels; wave w owns channels [32w, 32w+32) for all 16 transform points xi,
 // so each lane's accumulators hold, for 16 Winograd tiles, all 16 xi of one channel and the output
 // transform is lane-local. 16 accumulators x 16 = 256 registers per lane (1 wave per SIMD).
-// Per 8-channel input chunk:
-//   prefetch (registers): the 10 x 18 x 8 input patch (+ residual source) and U[xi][co][8]
-//   stage: prologue (CIN affine [+ ReLU | + residual], materialised block output) -> LDS patch;
-//          U -> LDS
-//   transform: one thread per (tile, channel): V = B^T d B -> LDS [xi][tile][8]
-//   MFMA: per xi one ds_read_b128 of V and of U feeds 4 k-steps (k-step kk pairs channels kk and
-//          kk+4 of the chunk across the two lane halves); the next chunk's loads are in flight.
+// Per 8-channel input chunk c the loop body is ONE software-pipelined step with a single barrier:
+//   64 MFMAs per wave on V(c) (LDS, operands for point xi+1 read during the MFMAs of xi) x U(c)
+//   (registers: U is packed on the host in MFMA B-operand order, so each lane loads its own
+//   operands straight from global/L2 -- no LDS round trip; U(c+1)[xi] is loaded into the registers
+//   of U(c)[xi] as soon as the MFMAs of point xi have issued), interleaved with
+//   - the input transform of chunk c+1: one thread per (tile, channel), V = B^T d B from the LDS
+//     patch of c+1 into the other V buffer,
+//   - the staging of chunk c+2's patch (prologue: CIN affine [+ ReLU | + residual], materialised
+//     block output) from registers into the free patch buffer, and the global loads of chunk c+3.
+// Measured before this pipeline (tools/wino_bench.hip phase profile): 45 % of a chunk in MFMA issue,
+// the rest in staging U through LDS, load issue, the transform and three barriers.
 // Epilogue: output transform, conv bias + ReLU, store, and per-(workgroup, channel) two-pass
 // {sum, M2, n} for the conditional instance norm that follows (finalize_kernel merges them).
 #include <hip/hip_runtime.h>
@@ -39,14 +43,14 @@ constexpr int WPH = WTH + 2, WPW = WTW + 2;       // input patch
 constexpr int WNP = WPH * WPW;                    // 180 patch pixels
 constexpr int WCK = 8;                            // input channels per chunk
 constexpr int WPS = 9;                            // patch pixel stride (floats): conflict-free transform reads
-constexpr int WVS = 12;                           // V / U row stride (floats): odd count of 16-B slots
+constexpr int WVS = 12;                           // V row stride (floats): odd count of 16-B slots
 constexpr int WN = 128;                           // output channels (4 waves x 32)
 constexpr int WXI = 16;                           // transform points
 constexpr int W_PATCH_F4 = WNP * WCK / 4;         // 360 float4 per chunk
-constexpr int W_U_F4 = WXI * WN * WCK / 4;        // 4096 float4 per chunk
 constexpr int W_MAX_CIN = 256;
-constexpr size_t W_LDS_BYTES =
-    (size_t)(WNP * WPS + WXI * 32 * WVS + WXI * WN * WVS) * 4 + W_MAX_CIN * sizeof(float2);
+constexpr int W_PATCH_FL = WNP * WPS;             // one patch buffer (floats)
+constexpr int W_V_FL = WXI * 32 * WVS;            // one V buffer (floats)
+constexpr size_t W_LDS_BYTES = (size_t)(2 * W_PATCH_FL + 2 * W_V_FL) * 4 + W_MAX_CIN * sizeof(float2);
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -65,12 +69,20 @@ __device__ __forceinline__ float pro_apply(int mode, float x, float2 ab, float r
 
 }  // namespace
 
+#ifdef WINO_PROF
+// phase timestamps per (workgroup, wave, chunk) for tools/wino_bench.hip (never in the library build)
+__device__ unsigned long long wino_prof[WINO_PROF][4][16][8];
+#define WPROF(c, k) \
+    if (blockIdx.x < WINO_PROF && lane == 0) wino_prof[blockIdx.x][wave][(c)][(k)] = __builtin_amdgcn_s_memtime()
+#else
+#define WPROF(c, k)
+#endif
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino_conv_kernel(WinoArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* patch = smem;                               // [180][9]
-    float* vs = patch + WNP * WPS;                     // [16][32][12]
-    float* us = vs + WXI * 32 * WVS;                   // [16][128][12]
-    float2* pab = reinterpret_cast<float2*>(us + WXI * WN * WVS);
+    float* const patch = smem;                         // [2][180][9]
+    float* const vs = patch + 2 * W_PATCH_FL;          // [2][16][32][12]
+    float2* const pab = reinterpret_cast<float2*>(vs + 2 * W_V_FL);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
@@ -90,9 +102,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[(size_t)b * Cin + c];
     }
 
-    // ---- prefetch registers (compile-time indexed only) -------------------------------------
-    f32x4 xr[2], rr[2], ur[16];
-    auto load = [&](int chunk) __attribute__((always_inline)) {
+    // ---- patch: global -> registers (clamped, branch-free) -> prologue -> LDS -----------------
+    f32x4 xr[2], rr[2];
+    auto load_patch = [&](int chunk) __attribute__((always_inline)) {
         const int c0 = chunk * WCK;
         sfor<0, 2>([&](auto K) __attribute__((always_inline)) {
             constexpr int k = decltype(K)::value;
@@ -103,13 +115,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             xr[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
             rr[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
         });
-        const f32x4* usrc = reinterpret_cast<const f32x4*>(a.U) + (size_t)chunk * W_U_F4;
-        sfor<0, 16>([&](auto K) __attribute__((always_inline)) {
-            constexpr int k = decltype(K)::value;
-            ur[k] = usrc[k * 256 + tid];
-        });
     };
-    auto stage = [&](int chunk) __attribute__((always_inline)) {
+    auto stage = [&](int chunk, float* pbuf) __attribute__((always_inline)) {
         const int c0 = chunk * WCK;
         sfor<0, 2>([&](auto K) __attribute__((always_inline)) {
             constexpr int k = decltype(K)::value;
@@ -130,17 +137,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                         *reinterpret_cast<f32x4*>(a.mat + (img + (size_t)iy * W + ix) * Cin + c) = v;
                 }
                 if (!inside) v = f32x4{0.f, 0.f, 0.f, 0.f};
-                float* d = patch + px * WPS + 4 * q;
+                float* d = pbuf + px * WPS + 4 * q;
                 d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
             }
         });
-        // U[xi][co][8] (global, contiguous) -> LDS [xi][co][12]
-        sfor<0, 16>([&](auto K) __attribute__((always_inline)) {
-            constexpr int k = decltype(K)::value;
-            const int it = k * 256 + tid;         // float4 index: ((xi * 128 + co) * 2 + half)
-            const int row = it >> 1, half = it & 1;
-            *reinterpret_cast<f32x4*>(us + row * WVS + 4 * half) = ur[k];
-        });
+    };
+
+    // ---- U: lane (li, lh) of wave w reads U[chunk][xi][32w + li][4lh .. 4lh+3] = its B operand ----
+    // buffer loads: one VGPR lane offset, the (chunk, xi) part in the scalar offset
+    const __amdgpu_buffer_rsrc_t usrd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, nchunks * WXI * WN * WCK * 4, 0x00020000);
+    const int uvoff = ((wave * 32 + li) * 2 + lh) * 16;
+    auto load_u = [&](f32x4* u, int chunk, auto X) __attribute__((always_inline)) {
+        constexpr int x = decltype(X)::value;
+        u[x] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              usrd, uvoff, (chunk * WXI + x) * (WN * WCK * 4), 0));
+    };
+
+    // ---- input transform, one thread per (tile tt, channel tc), in pieces -----------------------
+    const int tt = tid & 31, tc = tid >> 5;
+    const int twy = tt >> 3, twx = tt & 7;
+    float d[4][4], t[4][4];
+    auto tr_read = [&](const float* pbuf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[r][c] = pbuf[((2 * twy + r) * WPW + 2 * twx + c) * WPS + tc];
+    };
+    auto tr_rows = [&]() __attribute__((always_inline)) {   // B^T d
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            t[0][c] = d[0][c] - d[2][c];
+            t[1][c] = d[1][c] + d[2][c];
+            t[2][c] = d[2][c] - d[1][c];
+            t[3][c] = d[1][c] - d[3][c];
+        }
+    };
+    auto tr_cols = [&](float* vbuf, int r) __attribute__((always_inline)) {   // (B^T d) B, row r
+        const float v0 = t[r][0] - t[r][2], v1 = t[r][1] + t[r][2];
+        const float v2 = t[r][2] - t[r][1], v3 = t[r][1] - t[r][3];
+        vbuf[((r * 4 + 0) * 32 + tt) * WVS + tc] = v0;
+        vbuf[((r * 4 + 1) * 32 + tt) * WVS + tc] = v1;
+        vbuf[((r * 4 + 2) * 32 + tt) * WVS + tc] = v2;
+        vbuf[((r * 4 + 3) * 32 + tt) * WVS + tc] = v3;
     };
 
     floatx16 acc[WXI];
@@ -149,67 +188,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
 
-    // transform thread role: (tile, channel)
-    const int tt = tid & 31, tc = tid >> 5;
-    const int twy = tt >> 3, twx = tt & 7;
+    f32x4 ur[WXI];   // U operands: point xi of chunk c+1 is loaded as soon as the MFMAs of chunk c consumed xi
 
+    // ---- pipeline fill: V(0) in vs[0], patch(1) in patch[1], patch(2) and U(0) loads in flight --
     if (pro != PRO_NONE) __syncthreads();   // pab visible before the first staging
-    load(0);
-    for (int chunk = 0; chunk < nchunks; ++chunk) {
-        stage(chunk);
+    load_patch(0);
+    sfor<0, WXI>([&](auto X) __attribute__((always_inline)) { load_u(ur, 0, X); });
+    stage(0, patch);
+    if (nchunks > 1) load_patch(1);
+    __syncthreads();
+    tr_read(patch);
+    tr_rows();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tr_cols(vs, r);
+    if (nchunks > 1) {
+        stage(1, patch + W_PATCH_FL);
+        if (nchunks > 2) load_patch(2);
+    }
+    __syncthreads();
+
+    // one chunk: P = chunk parity (V(c) in vs[P], patch(c+1) in patch[1-P], patch[P] free)
+    for (int c = 0; c < nchunks; ++c) {
+        const int P = c & 1;
+        const bool has2 = c + 2 < nchunks, has3 = c + 3 < nchunks;
+        const int c1 = min(c + 1, nchunks - 1);
+        const float* va = vs + P * W_V_FL + li * WVS + 4 * lh;
+        float* const vnext = vs + (1 - P) * W_V_FL;
+        const float* const pnext = patch + (1 - P) * W_PATCH_FL;
+        WPROF(c, 0);
+        if (has2) stage(c + 2, patch + P * W_PATCH_FL);   // patch(c+2): its loads landed during chunk c-1
+        if (has3) load_patch(c + 3);
+        WPROF(c, 1);
+        f32x4 av[2];
+        av[0] = *reinterpret_cast<const f32x4*>(va);
+        __builtin_amdgcn_sched_barrier(0);
+        sfor<0, WXI>([&](auto X) __attribute__((always_inline)) {
+            constexpr int x = decltype(X)::value;
+            if constexpr (x + 1 < WXI) av[(x + 1) & 1] = *reinterpret_cast<const f32x4*>(va + (x + 1) * 32 * WVS);
+            __builtin_amdgcn_sched_barrier(0);   // the read of point x+1 issues before the MFMAs of x
+            const f32x4 a4 = av[x & 1], b4 = ur[x];
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc[x], 0, 0, 0);
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc[x], 0, 0, 0);
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc[x], 0, 0, 0);
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc[x], 0, 0, 0);
+            // chunk c+1 (clamped: past the last chunk this re-reads and writes buffers nobody reads)
+            load_u(ur, c1, X);
+            if constexpr (x == 1) tr_read(pnext);
+            if constexpr (x == 3) tr_rows();
+            if constexpr (x >= 4 && x < 8) tr_cols(vnext, x - 4);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        WPROF(c, 2);
         __syncthreads();
-        // ---- input transform: V = B^T d B for tile tt, channel tc -----------------------------
-        {
-            float d[4][4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int s = 0; s < 4; ++s) d[r][s] = patch[((2 * twy + r) * WPW + 2 * twx + s) * WPS + tc];
-            float t[4][4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {   // rows: B^T d
-                t[0][s] = d[0][s] - d[2][s];
-                t[1][s] = d[1][s] + d[2][s];
-                t[2][s] = d[2][s] - d[1][s];
-                t[3][s] = d[1][s] - d[3][s];
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {   // columns: (B^T d) B
-                const float v0 = t[r][0] - t[r][2], v1 = t[r][1] + t[r][2];
-                const float v2 = t[r][2] - t[r][1], v3 = t[r][1] - t[r][3];
-                vs[((r * 4 + 0) * 32 + tt) * WVS + tc] = v0;
-                vs[((r * 4 + 1) * 32 + tt) * WVS + tc] = v1;
-                vs[((r * 4 + 2) * 32 + tt) * WVS + tc] = v2;
-                vs[((r * 4 + 3) * 32 + tt) * WVS + tc] = v3;
-            }
-        }
-        __syncthreads();
-        if (chunk + 1 < nchunks) load(chunk + 1);   // in flight during the MFMAs
-        // ---- 16 batched GEMMs: acc[xi] (32 tiles x 32 channels) += V[xi] (32 x 8) U[xi] (8 x 32) ----
-        // operands of point x+1 are read from LDS before the MFMAs of point x (order pinned with
-        // sched_barrier: without it the compiler reuses one register set and waits on every read)
-        {
-            const float* va = vs + li * WVS + 4 * lh;
-            const float* ub = us + (wave * 32 + li) * WVS + 4 * lh;
-            f32x4 av[2], bv[2];
-            av[0] = *reinterpret_cast<const f32x4*>(va);
-            bv[0] = *reinterpret_cast<const f32x4*>(ub);
-#pragma unroll
-            for (int x = 0; x < WXI; ++x) {
-                if (x + 1 < WXI) {
-                    av[(x + 1) & 1] = *reinterpret_cast<const f32x4*>(va + (x + 1) * 32 * WVS);
-                    bv[(x + 1) & 1] = *reinterpret_cast<const f32x4*>(ub + (x + 1) * WN * WVS);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                const f32x4 a4 = av[x & 1], b4 = bv[x & 1];
-                acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc[x], 0, 0, 0);
-                acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc[x], 0, 0, 0);
-                acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc[x], 0, 0, 0);
-                acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc[x], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        __syncthreads();   // V / U / patch free for the next chunk
+        WPROF(c, 3);
     }
 
     // ---- epilogue: output transform, bias + ReLU, store, tile statistics -----------------------
