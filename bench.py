@@ -61,6 +61,36 @@ KERNEL_NAMES = {
 }
 
 
+DTYPE_DESC = {
+    "fp32": "fp32 (exact-f32 MFMA products, f32 accumulate), every conv direct (implicit GEMM)",
+    "fp32_winograd": "fp32 (exact-f32 MFMA products, f32 accumulate); the residual convs as fused Winograd "
+                     "F(2x2,3x3) (16 instead of 36 multiplies per 2x2 output tile, f32 transforms), other layers "
+                     "direct",
+    "bf16x6": "fp32 via exact 3-piece split bf16 (24 significant bits, 6 product terms, dropped terms <= 2^-24), "
+              "fp32 accumulate, on the residual convs; other layers fp32 MFMA",
+    "bf16x3": "fp32 via 2-piece split bf16 (3 product terms, 16 significant bits per operand), fp32 accumulate, "
+              "on the residual convs; other layers fp32 MFMA",
+}
+
+
+def dominant_kernel(model, plan, conv_ms, nsteps, B) -> dict:
+    """The kernel (config id) with the largest summed time over the timed launches, with its
+    algorithmic TFLOP/s (direct-conv FLOPs per launch / average launch duration)."""
+    groups = {}
+    for i, l in enumerate(plan.layers):
+        kid = model.layer_kernel_id(i)
+        g = groups.setdefault(kid, {"ms": 0.0, "flops": 0.0, "launches": 0})
+        g["ms"] += conv_ms[i]
+        g["flops"] += layer_flops(l) * B * nsteps
+        g["launches"] += nsteps
+    kid = max(groups, key=lambda k: groups[k]["ms"])
+    g = groups[kid]
+    avg_ms = g["ms"] / max(g["launches"], 1)
+    fpl = g["flops"] / max(g["launches"], 1)
+    return {"id": kid, "kernel": KERNEL_NAMES.get(kid, str(kid)), "avg_ms": avg_ms, "flops_per_launch": fpl,
+            "launches": g["launches"], "tflops": fpl / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0}
+
+
 def cpu_threads() -> int:
     try:
         aff = len(os.sched_getaffinity(0))
@@ -116,7 +146,18 @@ def bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs, time
     terms = 3 if precision == "bf16x3" else 6
     ms = sum(conv_ms[i] for i in bf3) / max(nsteps, 1) / max(len(bf3), 1)
     fl = sum(layer_flops(plan.layers[i]) for i in bf3) * B / max(len(bf3), 1)
-    eff_tf = fl / (ms * 1e-3) / 1e12
+    eff_tf = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    if precision == "fp32":
+        dom = dominant_kernel(model, plan, conv_ms, nsteps, B)
+        return model, {
+            "value": round(world * B * args.steps / el, 3), "unit": "frames/s",
+            "ms_per_step": round(el * 1e3 / args.steps, 4), "dtype": DTYPE_DESC["fp32"],
+            "roofline": {"bound": "mfma", "kernel": dom["kernel"], "achieved": round(dom["tflops"], 2),
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(dom["tflops"] / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "avg_launch_ms": round(dom["avg_ms"], 5)},
+            "layers_ms": [round(c / max(nsteps, 1), 4) for c in conv_ms],
+        }
     if precision == "fp32_winograd":
         return model, {
             "value": round(world * B * args.steps / el, 3), "unit": "frames/s",
@@ -262,7 +303,10 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
     ap.add_argument("--train-steps", type=int, default=5)
-    ap.add_argument("--no-bf16x3", action="store_true", help="skip the split-bf16 precision-mode measurements")
+    ap.add_argument("--precision", default="fp32_winograd",
+                    help="headline precision mode: fp32_winograd (default: fp32 arithmetic, residual convs as "
+                         "fused Winograd F(2x2,3x3)), fp32 (all direct), bf16x6, bf16x3")
+    ap.add_argument("--no-bf16x3", action="store_true", help="skip the other precision-mode measurements")
     ap.add_argument("--no-predictor", action="store_true", help="skip the style-predictor measurement")
     args = ap.parse_args()
 
@@ -286,7 +330,7 @@ def main():
     B = args.batch
     max_b = max(B, args.stream_batch)
     model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
-                                           weights=weights, max_batch=max_b, device=dev)
+                                           weights=weights, max_batch=max_b, device=dev, precision=args.precision)
     # synthetic frames (distinct per rank), resident in HBM before the timed region
     rng = np.random.default_rng(1000 + rank)
     content = torch.from_numpy(rng.random((B,) + ins, dtype=np.float32)).to(dev)
@@ -348,18 +392,8 @@ def main():
 
     # ---------------- dominant kernel roofline (from the timed region's events) ----------------
     flops = [layer_flops(l) * B for l in plan.layers]
-    groups = {}
-    for i, l in enumerate(plan.layers):
-        kid = model.layer_kernel_id(i)
-        g = groups.setdefault(kid, {"ms": 0.0, "flops": 0.0, "launches": 0})
-        g["ms"] += conv_ms[i]
-        g["flops"] += flops[i] * nsteps
-        g["launches"] += nsteps
-    dom_id = max(groups, key=lambda k: groups[k]["ms"])
-    dom = groups[dom_id]
-    avg_ms = dom["ms"] / dom["launches"]
-    flops_per_launch = dom["flops"] / dom["launches"]
-    achieved_tf = flops_per_launch / (avg_ms * 1e-3) / 1e12
+    dom = dominant_kernel(model, plan, conv_ms, nsteps, B)
+    dom_id, avg_ms, flops_per_launch, achieved_tf = dom["id"], dom["avg_ms"], dom["flops_per_launch"], dom["tflops"]
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -412,7 +446,7 @@ def main():
     # ---------------- precision mode: split-bf16 residual convs (reported beside the fp32 headline) --
     split_models, split = {}, {}
     if not args.no_bf16x3:
-        for prec in ("fp32_winograd", "bf16x6", "bf16x3"):
+        for prec in [p for p in ("fp32", "fp32_winograd", "bf16x6", "bf16x3") if p != args.precision]:
             split_models[prec], split[prec] = bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs,
                                                           timed, prec)
 
@@ -476,6 +510,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
+            "precision_mode": args.precision,
+            "arithmetic": DTYPE_DESC.get(args.precision, args.precision),
             "data": "synthetic (U[0,1) 480x960x17 G-buffer frames, seeded weights; no checkpoints offline)",
             "config": {"workload": f"{SPEC} single-frame transfer inference (BASELINE config 2)", "spec": SPEC,
                        "frames_per_step_per_gpu": B, "input": list(ins), "output": list(outs),
@@ -489,12 +525,14 @@ def main():
                 "kernel": KERNEL_NAMES.get(dom_id, str(dom_id)),
                 "achieved": round(achieved_tf, 3),
                 "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
+                "unit": "TFLOP/s" if dom_id != 200 else "TFLOP/s (algorithmic = direct-conv FLOPs)",
                 "frac": round(achieved_tf / FP32_MFMA_PEAK_TFLOPS, 4),
                 "traffic": traffic,
                 "avg_launch_ms": round(avg_ms, 5),
                 "flops_per_launch": flops_per_launch,
                 "launches": dom["launches"],
+                # Winograd executes 16/36 of the direct multiplies on the MFMA pipe
+                "mfma_pipe_frac": round(achieved_tf * (16.0 / 36.0 if dom_id == 200 else 1.0) / FP32_MFMA_PEAK_TFLOPS, 4),
             },
             "network_roofline": {
                 "gflop_per_frame": round(total_flops / 1e9, 3),

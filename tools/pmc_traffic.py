@@ -32,6 +32,8 @@ def short_name(k: str) -> str:
     if m:
         args = tuple(int(v) for v in m.group(1).split(","))
         return CONFIG_NAMES.get(args[:5], "conv_mfma<" + ",".join(map(str, args)) + ">")
+    if "wino_conv_kernel" in k:
+        return "wino_conv<F(2x2,3x3) 8x16 N128 f32 MFMA>"
     if "small_conv_kernel" in k:
         return "small_conv_kernel<9x9 Cout3 VALU>"
     return k.split("(")[0]
