@@ -32,6 +32,7 @@ constexpr int WS = 28;                               // 27 weights per (ky, ci),
 }  // namespace small
 
 typedef float sf32x4 __attribute__((ext_vector_type(4)));
+typedef float sf32x2 __attribute__((ext_vector_type(2)));
 
 // SOPT bit0: unroll the 4 channels of a chunk (lets hipcc hoist the next channel's weight s_loads)
 //      bit1: weights staged in LDS once and read as broadcast ds_read_b128 (instead of s_load)
@@ -101,9 +102,11 @@ __global__ __launch_bounds__(256, 2) void small_conv_kernel(SmallConvArgs a, con
         }
     };
 
-    float acc[RX][3];
+    // accumulators as pixel pairs: acc2[p][co] = (pixel 2p, pixel 2p+1) of channel co, so every FMA
+    // is a v_pk_fma_f32 (two lanes' worth per issue: the 64 FLOP/clk/SIMD VALU peak needs packed FMA)
+    sf32x2 acc2[RX / 2][3];
 #pragma unroll
-    for (int i = 0; i < RX; ++i) acc[i][0] = acc[i][1] = acc[i][2] = 0.f;
+    for (int i = 0; i < RX / 2; ++i) acc2[i][0] = acc2[i][1] = acc2[i][2] = sf32x2{0.f, 0.f};
 
     stage_sync(0, halo);
     __syncthreads();
@@ -147,14 +150,22 @@ __global__ __launch_bounds__(256, 2) void small_conv_kernel(SmallConvArgs a, con
 #pragma unroll
                     for (int j = 0; j < WS; ++j) wv[j] = wk[j];
                 }
+                // pairs of the 12 row values: even-aligned (x0,x1),(x2,x3).. and odd-shifted (x1,x2),(x3,x4)..
+                sf32x2 xe[6], xo[5];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) xe[j] = sf32x2{x[2 * j], x[2 * j + 1]};
+#pragma unroll
+                for (int j = 0; j < 5; ++j) xo[j] = sf32x2{x[2 * j + 1], x[2 * j + 2]};
 #pragma unroll
                 for (int kx = 0; kx < K; ++kx) {
-                    const float w0 = wv[kx * 3 + 0], w1 = wv[kx * 3 + 1], w2 = wv[kx * 3 + 2];
 #pragma unroll
-                    for (int i = 0; i < RX; ++i) {
-                        acc[i][0] = fmaf(x[i + kx], w0, acc[i][0]);
-                        acc[i][1] = fmaf(x[i + kx], w1, acc[i][1]);
-                        acc[i][2] = fmaf(x[i + kx], w2, acc[i][2]);
+                    for (int co = 0; co < 3; ++co) {
+                        const sf32x2 wp = sf32x2{wv[kx * 3 + co], wv[kx * 3 + co]};
+#pragma unroll
+                        for (int p = 0; p < RX / 2; ++p) {
+                            const sf32x2 xv = (kx & 1) ? xo[p + kx / 2] : xe[p + kx / 2];
+                            acc2[p][co] = __builtin_elementwise_fma(xv, wp, acc2[p][co]);
+                        }
                     }
                 }
             }
@@ -180,6 +191,11 @@ __global__ __launch_bounds__(256, 2) void small_conv_kernel(SmallConvArgs a, con
     }
 
     // epilogue: bias, raw store, per-tile statistics per channel
+    float acc[RX][3];
+#pragma unroll
+    for (int i = 0; i < RX; ++i)
+#pragma unroll
+        for (int co = 0; co < 3; ++co) acc[i][co] = acc2[i / 2][co][i & 1];
     const int oy = y0 + r;
     float s[3] = {0.f, 0.f, 0.f}, cnt = 0.f;
     bool ok[RX];

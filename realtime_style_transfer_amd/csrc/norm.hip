@@ -4,59 +4,66 @@
 //   mean, var = tf.nn.moments(x, axes=[1,2])        (biased variance, per (b, c))
 //   x = x * rsqrt(var + eps) + (-mean * rsqrt(var + eps));  x = bias + x * scale
 // The producing conv writes per-tile {sum, M2, n} (two-pass inside the tile). finalize merges
-// them with Chan's parallel formula in f64 — deterministic (no atomics, fixed order) and
-// immune to the E[x^2]-E[x]^2 cancellation that ReLU'd, positive-weight residual convs
-// (mean/std ~ 20) would suffer — and folds scale/bias/rsqrt into one affine (a, b) per
+// them in one f64 pass (sum of M2_t + s_t^2/n_t, minus S^2/N: Chan's merge rearranged) —
+// deterministic (no atomics, fixed order) and immune to the f32 E[x^2]-E[x]^2 cancellation that
+// ReLU'd, positive-weight residual convs (mean/std ~ 20) would suffer — and folds scale/bias/rsqrt into one affine (a, b) per
 // (b, c) that the consumer applies in its prologue: y = a*x + b.
 #include <hip/hip_runtime.h>
 #include "kernels.h"
 
 namespace rst {
 
+constexpr int FIN_THREADS = 512;
+
 template <typename T>
-__device__ __forceinline__ T block_sum256(T v, T* scratch) {
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
     if (lane == 0) scratch[wave] = v;
     __syncthreads();
-    T t = scratch[0] + scratch[1] + scratch[2] + scratch[3];
+    T t = scratch[0];
+#pragma unroll
+    for (int w = 1; w < FIN_THREADS / 64; ++w) t += scratch[w];   // fixed order: deterministic
     return t;
 }
 
-__global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
-    __shared__ double scratch[4];
+// One pass over the partials of channel c: S = sum s_t, N = sum n_t, Q = sum (M2_t + s_t^2 / n_t), all
+// in f64; then M2 = Q - S^2/N. Equal to Chan's pairwise merge sum M2_t + n_t (mean_t - mean)^2; the
+// cancellation in Q - S^2/N costs log2(mean^2/var) bits of f64's 53 (mean/std ~ 20 here: ~9 bits),
+// far below f32 resolution. Four independent loads per thread per iteration keep enough reads in
+// flight for the layers with few channels and many tiles (expand_1: 16 channels x 14400 partials).
+__global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
+    __shared__ double scratch[3][FIN_THREADS / 64];
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     const int b0 = a.merge_images ? 0 : b, b1 = a.merge_images ? a.batch : b + 1;
-    double s = 0.0, n = 0.0;
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, n[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+    auto add = [&](const float4& v, int j) __attribute__((always_inline)) {
+        if (v.z > 0.f) {
+            const double sv = (double)v.x;
+            s[j] += sv;
+            n[j] += (double)v.z;
+            q[j] += (double)v.y + sv * sv / (double)v.z;
+        }
+    };
     for (int bb = b0; bb < b1; ++bb)
         for (int ph = 0; ph < a.phases; ++ph) {
             const float4* p = a.part + ((size_t)bb * a.ntot + ph * a.C + c) * a.n_part;
-            for (int t = tid; t < a.n_part; t += 256) {
-                const float4 v = p[t];
-                s += (double)v.x;
-                n += (double)v.z;
+            int t = tid;
+            for (; t + 3 * FIN_THREADS < a.n_part; t += 4 * FIN_THREADS) {
+                const float4 v0 = p[t], v1 = p[t + FIN_THREADS], v2 = p[t + 2 * FIN_THREADS],
+                             v3 = p[t + 3 * FIN_THREADS];
+                add(v0, 0); add(v1, 1); add(v2, 2); add(v3, 3);
             }
+            for (; t < a.n_part; t += FIN_THREADS) add(p[t], 0);
         }
-    s = block_sum256(s, scratch);
-    n = block_sum256(n, scratch);
-    const double mean = n > 0.0 ? s / n : 0.0;
-    double m2 = 0.0;
-    for (int bb = b0; bb < b1; ++bb)
-        for (int ph = 0; ph < a.phases; ++ph) {
-            const float4* p = a.part + ((size_t)bb * a.ntot + ph * a.C + c) * a.n_part;
-            for (int t = tid; t < a.n_part; t += 256) {
-                const float4 v = p[t];
-                if (v.z > 0.f) {
-                    const double d = (double)v.x / (double)v.z - mean;
-                    m2 += (double)v.y + (double)v.z * d * d;
-                }
-            }
-        }
-    m2 = block_sum256(m2, scratch);
+    double S = block_sum((s[0] + s[1]) + (s[2] + s[3]), scratch[0]);
+    double N = block_sum((n[0] + n[1]) + (n[2] + n[3]), scratch[1]);
+    double Q = block_sum((q[0] + q[1]) + (q[2] + q[3]), scratch[2]);
     if (tid == 0) {
-        const double var = n > 0.0 ? m2 / n : 0.0;
+        const double mean = N > 0.0 ? S / N : 0.0;
+        const double m2 = N > 0.0 ? fmax(Q - S * mean, 0.0) : 0.0;
+        const double var = N > 0.0 ? m2 / N : 0.0;
         const float rstd = (float)(1.0 / sqrt(var + (double)a.eps));
         float scale = 1.f, bias = 0.f;
         if (a.style != nullptr) {
@@ -76,7 +83,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
         }
         if (a.mr != nullptr) a.mr[b * a.C + c] = make_float2((float)mean, rstd);
         if (a.moving_mean != nullptr && b == 0) {
-            const double unbiased = n > 1.0 ? m2 / (n - 1.0) : var;
+            const double unbiased = N > 1.0 ? m2 / (N - 1.0) : var;
             a.moving_mean[c] = (float)(a.momentum * a.moving_mean[c] + (1.0 - a.momentum) * mean);
             a.moving_var[c] = (float)(a.momentum * a.moving_var[c] + (1.0 - a.momentum) * unbiased);
         }
@@ -84,7 +91,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
 }
 
 hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(a.C, a.batch), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(finalize_kernel, dim3(a.C, a.batch), dim3(FIN_THREADS), 0, st, a);
     return hipGetLastError();
 }
 

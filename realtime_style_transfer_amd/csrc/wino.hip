@@ -69,6 +69,13 @@ __device__ __forceinline__ float pro_apply(int mode, float x, float2 ab, float r
 
 }  // namespace
 
+// RST_WINO_OPT bit0: stage the patch of chunk c+2 (prologue + LDS write) and issue the loads of
+// chunk c+3 inside the MFMA loop of chunk c instead of before it (one wave per SIMD: work outside
+// the MFMA loop leaves the MFMA pipe idle)
+#ifndef RST_WINO_OPT
+#define RST_WINO_OPT 1
+#endif
+
 #ifdef WINO_PROF
 // phase timestamps per (workgroup, wave, chunk) for tools/wino_bench.hip (never in the library build)
 __device__ unsigned long long wino_prof[WINO_PROF][4][16][8];
@@ -78,6 +85,9 @@ __device__ unsigned long long wino_prof[WINO_PROF][4][16][8];
 #define WPROF(c, k)
 #endif
 
+// PRO (the prologue mode) is a template parameter: a runtime mode turned the per-element prologue
+// inside the MFMA loop into a branch tree with an lgkmcnt(0) wait per branch
+template <int PRO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino_conv_kernel(WinoArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* const patch = smem;                         // [2][180][9]
@@ -93,17 +103,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int b = bid / a.tiles_y;
     const int y0 = ty * WTH, x0 = tx * WTW;
     const int H = a.H, W = a.W, Cin = a.cin;
-    const int pro = a.pro_mode;
+    constexpr int pro = PRO;
     const size_t img = (size_t)b * H * W;
     const float* res_src = pro == PRO_AFF_RES ? a.res : a.in;
     const int nchunks = Cin / WCK;
 
-    if (pro != PRO_NONE) {
+    if constexpr (pro != PRO_NONE) {
         for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[(size_t)b * Cin + c];
     }
 
     // ---- patch: global -> registers (clamped, branch-free) -> prologue -> LDS -----------------
-    f32x4 xr[2], rr[2];
+    f32x4 xr[2], rr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     auto load_patch = [&](int chunk) __attribute__((always_inline)) {
         const int c0 = chunk * WCK;
         sfor<0, 2>([&](auto K) __attribute__((always_inline)) {
@@ -113,7 +123,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             const int iy = min(max(y0 - 1 + px / WPW, 0), H - 1), ix = min(max(x0 - 1 + px % WPW, 0), W - 1);
             const size_t gi = (img + (size_t)iy * W + ix) * Cin + c0 + 4 * q;
             xr[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
-            rr[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
+            if constexpr (pro == PRO_AFF_RES) rr[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
         });
     };
     auto stage = [&](int chunk, float* pbuf) __attribute__((always_inline)) {
@@ -127,12 +137,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 const int c = c0 + 4 * q;
                 f32x4 v = xr[k];
                 const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
-                if (pro != PRO_NONE) {
+                if constexpr (pro != PRO_NONE) {
                     const f32x4 r = rr[k];
-                    v.x = pro_apply(pro, v.x, pab[c], r.x);
-                    v.y = pro_apply(pro, v.y, pab[c + 1], r.y);
-                    v.z = pro_apply(pro, v.z, pab[c + 2], r.z);
-                    v.w = pro_apply(pro, v.w, pab[c + 3], r.w);
+                    const f32x4 p01 = *reinterpret_cast<const f32x4*>(pab + c);       // (a,b) of c, c+1
+                    const f32x4 p23 = *reinterpret_cast<const f32x4*>(pab + c + 2);   // (a,b) of c+2, c+3
+                    v.x = pro_apply(pro, v.x, float2{p01.x, p01.y}, r.x);
+                    v.y = pro_apply(pro, v.y, float2{p01.z, p01.w}, r.y);
+                    v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
+                    v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
                     if (a.mat != nullptr && inside && iy >= y0 && iy < y0 + WTH && ix >= x0 && ix < x0 + WTW)
                         *reinterpret_cast<f32x4*>(a.mat + (img + (size_t)iy * W + ix) * Cin + c) = v;
                 }
@@ -191,7 +203,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     f32x4 ur[WXI];   // U operands: point xi of chunk c+1 is loaded as soon as the MFMAs of chunk c consumed xi
 
     // ---- pipeline fill: V(0) in vs[0], patch(1) in patch[1], patch(2) and U(0) loads in flight --
-    if (pro != PRO_NONE) __syncthreads();   // pab visible before the first staging
+    if constexpr (pro != PRO_NONE) __syncthreads();   // pab visible before the first staging
     load_patch(0);
     sfor<0, WXI>([&](auto X) __attribute__((always_inline)) { load_u(ur, 0, X); });
     stage(0, patch);
@@ -216,8 +228,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         float* const vnext = vs + (1 - P) * W_V_FL;
         const float* const pnext = patch + (1 - P) * W_PATCH_FL;
         WPROF(c, 0);
-        if (has2) stage(c + 2, patch + P * W_PATCH_FL);   // patch(c+2): its loads landed during chunk c-1
-        if (has3) load_patch(c + 3);
+        if constexpr (!(RST_WINO_OPT & 1)) {
+            if (has2) stage(c + 2, patch + P * W_PATCH_FL);   // patch(c+2): its loads landed during chunk c-1
+            if (has3) load_patch(c + 3);
+        }
         WPROF(c, 1);
         f32x4 av[2];
         av[0] = *reinterpret_cast<const f32x4*>(va);
@@ -236,6 +250,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             if constexpr (x == 1) tr_read(pnext);
             if constexpr (x == 3) tr_rows();
             if constexpr (x >= 4 && x < 8) tr_cols(vnext, x - 4);
+            if constexpr ((RST_WINO_OPT & 1) && x == 9) {   // patch(c+2) -> patch[P] (free since chunk c-1's transform)
+                if (has2) stage(c + 2, patch + P * W_PATCH_FL);
+            }
+            if constexpr ((RST_WINO_OPT & 1) && x == 11) {
+                if (has3) load_patch(c + 3);
+            }
             __builtin_amdgcn_sched_barrier(0);
         });
         WPROF(c, 2);
@@ -330,17 +350,28 @@ std::vector<float> wino_pack_weights(const float* kern, int cin) {
 }
 
 hipError_t wino_prepare() {
-    return hipFuncSetAttribute((const void*)wino_conv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)W_LDS_BYTES);
+    for (const void* k : {(const void*)wino_conv_kernel<PRO_NONE>, (const void*)wino_conv_kernel<PRO_AFF_RELU>,
+                          (const void*)wino_conv_kernel<PRO_AFF>, (const void*)wino_conv_kernel<PRO_AFF_RES>}) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)W_LDS_BYTES);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t wino_launch(const WinoArgs& a, hipStream_t st) {
     if (a.cin % WCK != 0 || a.cin > W_MAX_CIN) return hipErrorInvalidValue;
-    if (!(a.pro_mode == PRO_NONE || a.pro_mode == PRO_AFF_RELU || a.pro_mode == PRO_AFF ||
-          a.pro_mode == PRO_AFF_RES))
-        return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
-    hipLaunchKernelGGL(wino_conv_kernel, dim3(grid), dim3(256), W_LDS_BYTES, st, a);
+    switch (a.pro_mode) {
+        case PRO_NONE: hipLaunchKernelGGL(wino_conv_kernel<PRO_NONE>, dim3(grid), dim3(256), W_LDS_BYTES, st, a); break;
+        case PRO_AFF_RELU:
+            hipLaunchKernelGGL(wino_conv_kernel<PRO_AFF_RELU>, dim3(grid), dim3(256), W_LDS_BYTES, st, a);
+            break;
+        case PRO_AFF: hipLaunchKernelGGL(wino_conv_kernel<PRO_AFF>, dim3(grid), dim3(256), W_LDS_BYTES, st, a); break;
+        case PRO_AFF_RES:
+            hipLaunchKernelGGL(wino_conv_kernel<PRO_AFF_RES>, dim3(grid), dim3(256), W_LDS_BYTES, st, a);
+            break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
