@@ -57,7 +57,7 @@ KERNEL_NAMES = {
     101: "conv_bf3<3x3 s1 CK32 NT128 bf16x3>", 102: "conv_bf3<3x3 s1 CK32 NT64 bf16x3>",
     111: "conv_bf3<3x3 s1 CK32 NT128 bf16x6>", 112: "conv_bf3<3x3 s1 CK32 NT64 bf16x6>",
     113: "conv_bf3<3x3 s1 CK32 NT64 8x16 bf16x6>",
-    200: "wino_conv<F(2x2,3x3) 8x16 N128 f32 MFMA>",
+    200: "wino_conv<F(2x2,3x3) 8x16 N128 f32 MFMA>", 201: "wino9_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 f32 MFMA>",
 }
 
 

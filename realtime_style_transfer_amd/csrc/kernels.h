@@ -62,6 +62,22 @@ struct WinoArgs {
     int batch, H, W, cin, tiles_y, tiles_x, pro_mode;
 };
 bool wino_supported(int kh, int stride, int cin, int cout);
+
+// First layer (Conv2D 9x9 s1 SAME, cin <= 17 -> 32, ReLU -> BN(inference) -> ReLU) as composite
+// Winograd F(2x2,3x3) over nine 3x3 sub-kernels (wino9.hip).
+struct Wino9Args {
+    const float* in;        // NHWC [B][H][W][cin] network input
+    const float* U;         // transformed weights [9][16][2][32][12]
+    const float* bias;      // [32]
+    const float2* bn_ab;    // [32] BatchNorm affine (folded moving statistics)
+    float* out;             // NHWC [B][H][W][32]
+    int batch, H, W, cin, tiles_y, tiles_x;
+};
+bool wino9_supported(int kh, int stride, int cin, int cout);
+int wino9_tiles_y(int H);
+int wino9_tiles_x(int W);
+std::vector<float> wino9_pack_weights(const float* kern, int cin);
+hipError_t wino9_launch(const Wino9Args& a, hipStream_t st);
 int wino_tiles_y(int H);
 int wino_tiles_x(int W);
 std::vector<float> wino_pack_weights(const float* kern, int cin);

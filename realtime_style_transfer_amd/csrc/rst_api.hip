@@ -198,6 +198,19 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.tiles_x = small_conv_tiles_x(s.Wo);
         e.n_part = e.tiles_y * e.tiles_x;
     } else if (precision == RST_PRECISION_FP32_WINOGRAD && s.keras_kind == 0 &&
+               wino9_supported(s.k, s.stride, s.cin, s.cout) && s.norm == N_BN && s.conv_relu) {
+        // ---- first layer (9x9 conv + ReLU + BN + ReLU) as composite Winograd (wino9.hip)
+        e.kind = K_WINO9;
+        packed = wino9_pack_weights(kern, s.cin);
+        bias_n.assign(bias, bias + s.cout);
+        e.ntot = s.cout;
+        e.pad_t = e.pad_l = 4;
+        e.gHo = s.Ho;
+        e.gWo = s.Wo;
+        e.tiles_y = wino9_tiles_y(s.Ho);
+        e.tiles_x = wino9_tiles_x(s.Wo);
+        e.n_part = 0;
+    } else if (precision == RST_PRECISION_FP32_WINOGRAD && s.keras_kind == 0 &&
                wino_supported(s.k, s.stride, s.cin, s.cout) && s.res_block >= 0) {
         // ---- residual conv as fused Winograd F(2x2,3x3) (wino.hip)
         e.kind = K_WINO;
@@ -414,7 +427,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     }
     // kernels with > 64 KB of dynamic LDS need the attribute before any (graph-captured) launch
     for (auto& e : h->layers) {
-        if (e.kind == K_SMALL) continue;
+        if (e.kind == K_SMALL || e.kind == K_WINO9) continue;
         hipError_t pe = e.kind == K_WINO ? wino_prepare() : conv_prepare(e.tile);
         if (pe != hipSuccess) {
             delete h;
@@ -467,6 +480,21 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         if (e.pro != PRO_AFF_RELU && e.pro != PRO_NONE)
             return fail(RST_ERR_UNSUPPORTED, "last layer prologue must be CIN+ReLU");
         HIP_TRY(small_conv_launch(a, st));
+    } else if (e.kind == K_WINO9) {
+        if (e.pro != PRO_NONE) return fail(RST_ERR_UNSUPPORTED, "9x9 Winograd conv reads the network input only");
+        Wino9Args a{};
+        a.in = in;
+        a.U = e.d_w;
+        a.bias = e.d_bias;
+        a.bn_ab = e.d_bn;
+        a.out = e.d_out;
+        a.batch = B;
+        a.H = e.s.H;
+        a.W = e.s.W;
+        a.cin = e.s.cin;
+        a.tiles_y = e.tiles_y;
+        a.tiles_x = e.tiles_x;
+        HIP_TRY(wino9_launch(a, st));
     } else if (e.kind == K_WINO) {
         WinoArgs a{};
         a.in = in;
@@ -610,7 +638,7 @@ int rst_precision(const rst_handle* h) { return h ? h->precision : -1; }
 int rst_layer_kernel_id(const rst_handle* h, int idx) {
     if (h == nullptr || idx < 0 || idx >= (int)h->layers.size()) return -1;
     const LayerExec& e = h->layers[idx];
-    return e.kind == K_SMALL ? 100 : (e.kind == K_WINO ? 200 : e.tile.id);
+    return e.kind == K_SMALL ? 100 : (e.kind == K_WINO ? 200 : (e.kind == K_WINO9 ? 201 : e.tile.id));
 }
 
 int rst_layer_output_shape(const rst_handle* h, int idx, int batch, int* hwc3) {

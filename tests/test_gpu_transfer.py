@@ -195,8 +195,9 @@ def test_split_bf16_precision_modes(precision, tol):
 
 
 def test_winograd_residual_convs_match_oracle():
-    """RST_PRECISION_FP32_WINOGRAD: residual convs as fused Winograd F(2x2,3x3) on f32 MFMA vs float64,
-    small geometry (production channel counts) and odd sizes (partial 8x16 tiles)."""
+    """RST_PRECISION_FP32_WINOGRAD: residual convs as fused Winograd F(2x2,3x3) and the 9x9 start conv as
+    nine F(2x2,3x3) sub-convolutions on f32 MFMA vs float64, small geometry (production channel counts)
+    and odd sizes (partial 8x16 tiles)."""
     _need_gpu()
     from oracle import numpy_ref as R
     from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
@@ -209,7 +210,8 @@ def test_winograd_residual_convs_match_oracle():
         x = np.random.default_rng(0).random((2,) + ins).astype(np.float32)
         ref = R.transfer_forward(x, sp, w, ins, outs, br, bf)
         m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision="fp32_winograd")
-        assert [m.layer_kernel_id(i) for i in range(m.num_layers())][3:13] == [200] * 10
+        ids = [m.layer_kernel_id(i) for i in range(m.num_layers())]
+        assert ids[0] == 201 and ids[3:13] == [200] * 10, ids   # 9x9 composite Winograd; residual Winograd
         inp = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}
         y = m(inp)
         err = float(np.abs(y.cpu().numpy() - ref).max())
@@ -217,6 +219,10 @@ def test_winograd_residual_convs_match_oracle():
         assert torch.equal(y, m(inp)), "Winograd forward is not deterministic"
         # every residual block output against the float64 oracle
         _, inter = R.transfer_forward(x, sp, w, ins, outs, br, bf, return_intermediates=True)
+        # the 9x9 start conv (composite Winograd, ReLU -> BN -> ReLU) against the float64 oracle
+        r0 = list(inter.values())[0]
+        g0 = m.layer_output(0, 2).cpu().numpy()
+        assert g0.shape == r0.shape and np.abs(g0 - r0).max() / max(1.0, np.abs(r0).max()) < 1e-5
         ref_blocks = [v for k, v in inter.items() if 'residual' in k]
         got = [m.layer_output(i, 2).cpu().numpy() for i, l in enumerate(plan.layers)
                if l.block.startswith('residual') and l.name.endswith('conv1')]
