@@ -247,6 +247,58 @@ def predictor_bytes_per_image(ins) -> float:
     return 4.0 * by
 
 
+def bench_ingest(args, dev, cfg, timed, rank):
+    """G-buffer ingest: a 1080x1920 Unreal screenshot's 17 channel planes (already in
+    HBM, as after the per-channel EXR uploads) -> rst_gbuffer_preprocess -> the 480x960x17 content tensor
+    (hdrScreenshots.py:14-30 + common.py:44-57 in one pass). HBM-bound: algorithmic bytes = the source
+    rows x columns the bilinear taps touch + the output."""
+    from realtime_style_transfer_amd.dataloaders.common import preprocess_planes, resized_size
+    src, C = (1080, 1920), cfg.num_channels
+    shape = cfg.input_shape['content'][:2]
+    planes = [torch.rand(src, device=dev) for _ in range(C)]
+    out = torch.empty(shape + (C,), device=dev)
+    fn = lambda: preprocess_planes(planes, shape, out=out)   # noqa: E731
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    steps = max(args.steps, 50)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    el = timed(fn, steps)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / steps
+    nh, nw = resized_size(src, shape)
+
+    def touched(n_out, n_in, off, n):
+        sc = np.float32(np.float32(n_in) / np.float32(n_out))
+        pos = (np.arange(off, off + n, dtype=np.float32) + np.float32(0.5)) * sc - np.float32(0.5)
+        lo = np.maximum(np.floor(pos).astype(np.int64), 0)
+        hi = np.minimum(np.ceil(pos).astype(np.int64), n_in - 1)
+        return len(set(lo.tolist()) | set(hi.tolist()))
+    rows = touched(nh, src[0], (nh - shape[0]) // 2, shape[0])
+    cols = touched(nw, src[1], (nw - shape[1]) // 2, shape[1])
+    alg = (rows * cols + shape[0] * shape[1]) * C * 4.0
+    res = {"workload": f"1080x1920x{C} G-buffer planes -> {shape[0]}x{shape[1]}x{C} content (TF bilinear "
+                       f"half-pixel resize to {nh}x{nw} + center crop), one frame per call",
+           "ms_per_frame": round(ms, 5), "frames_per_s": round(1e3 / ms, 1),
+           "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "algorithmic_bytes": alg}}
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle.ingest_ref import preprocess_numpy_image
+        x = np.random.default_rng(5).random(src + (C,), dtype=np.float32)
+        n, t = 0, 0.0
+        while n < 5 and t < 5.0:
+            t0 = time.perf_counter()
+            preprocess_numpy_image(x, shape)
+            t += time.perf_counter() - t0
+            n += 1
+        res["cpu_baseline"] = {"value": round(n / t, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} frames through oracle/ingest_ref.py (numpy f32, TF not installed)"}
+    return res
+
+
 def bench_predictor(args, dev, cfg, transfer_model, transfer_inputs, P, timed):
     """make_style_transfer_inference_model path: the MobileNetV3Small style predictor on a 480x960x3 style image
     (once per style in the video loop, predict_video_using_checkpoint.py:77-83) and predictor + transfer per
@@ -308,6 +360,7 @@ def main():
                          "fused Winograd F(2x2,3x3)), fp32 (all direct), bf16x6, bf16x3")
     ap.add_argument("--no-bf16x3", action="store_true", help="skip the other precision-mode measurements")
     ap.add_argument("--no-predictor", action="store_true", help="skip the style-predictor measurement")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the G-buffer ingest measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -455,6 +508,8 @@ def main():
     if not args.no_predictor:
         predictor = bench_predictor(args, dev, cfg, model, inputs, P, timed)
 
+    ingest = None if args.no_ingest else bench_ingest(args, dev, cfg, timed, rank)
+
     # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
     train = None
     if args.train_batch > 0:
@@ -547,6 +602,7 @@ def main():
             "split_bf16_modes": split,
             "training": train,
             "style_predictor": predictor,
+            "gbuffer_ingest": ingest,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

@@ -24,6 +24,9 @@
  *   rst_predictor_*              create_style_prediction_model(input_shape, feature_extractor,
  *                                num_top_parameters, num_style_parameters=100) -> tf.keras.Model
  *                                                                 models/stylePrediction.py:25-75
+ *   rst_gbuffer_preprocess       hdrScreenshots.load_unreal_hdr_screenshot channel assembly +
+ *                                common.preprocess_numpy_image     dataloaders/hdrScreenshots.py:14-30,
+ *                                                                  dataloaders/common.py:44-57
  *   rst_loss_create / _forward   StyleLossModelVGG + make_style_loss_function(..., with_depth_loss=False)
  *                                -> compute_loss(y_pred, y_true) dict      models/styleLoss.py:69-109,295-369
  */
@@ -231,6 +234,23 @@ int rst_predictor_trainer_apply_gradients(rst_predictor_trainer* t, const float*
 int rst_predictor_trainer_copy_weights(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
 int rst_predictor_trainer_set_weights(rst_predictor_trainer* t, const float* src, size_t count, void* stream);
 int rst_predictor_trainer_copy_slots(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
+
+/* ---- G-buffer ingest ----
+ * Replaces the host-side numpy/TF preprocessing of an Unreal HDR screenshot:
+ *   dataloaders/hdrScreenshots.py:14-30   per-channel EXR images stacked / concatenated (channel order
+ *                                         = `expected_channels` order) into (h, w, C)
+ *   dataloaders/common.py:44-57           preprocess_numpy_image(image, shape): tf.image.resize (bilinear,
+ *                                         half-pixel centers) to the aspect-preserving size, then
+ *                                         tf.image.resize_with_crop_or_pad to (shape[0], shape[1])
+ * in one device pass. planes: HOST array of num_planes DEVICE pointers; element (y, x) of plane k
+ * is planes[k][y * row_stride + x * pixel_stride] (planar EXR channels: pixel_stride 1, row_stride w;
+ * an interleaved (h, w, C) image: planes[k] = base + k, pixel_stride C, row_stride w * C).
+ * dst: device (dst_h, dst_w, num_planes) NHWC fp32 — directly the `content` input of rst_forward.
+ * f32 arithmetic identical to TF's ResizeBilinear kernel (no FMA contraction). */
+#define RST_GBUFFER_MAX_PLANES 32
+int rst_gbuffer_resized_size(int src_h, int src_w, int dst_h, int dst_w, int* new_hw2);
+int rst_gbuffer_preprocess(const float* const* planes, int num_planes, int src_h, int src_w, long long row_stride,
+                           long long pixel_stride, float* dst, int dst_h, int dst_w, void* stream);
 
 const char* rst_last_error(void);
 const char* rst_version(void);

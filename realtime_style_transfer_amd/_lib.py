@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = [
     "rst_predictor_trainer_create", "rst_predictor_trainer_destroy", "rst_predictor_trainer_num_weights",
     "rst_predictor_trainer_forward", "rst_predictor_trainer_backward", "rst_predictor_trainer_apply_gradients",
     "rst_predictor_trainer_copy_weights", "rst_predictor_trainer_set_weights", "rst_predictor_trainer_copy_slots",
+    "rst_gbuffer_resized_size", "rst_gbuffer_preprocess",
 ]
 EXTRACTORS = {"DUMMY": 0, "MOBILE_NET": 1}   # include/rst.h RST_EXTRACTOR_*
 
@@ -173,6 +174,11 @@ def load() -> ctypes.CDLL:
                  "rst_predictor_trainer_copy_slots"):
         getattr(lib, name).argtypes = [vp, vp, sz, vp]
         getattr(lib, name).restype = i
+    lib.rst_gbuffer_resized_size.argtypes = [i, i, i, i, ctypes.POINTER(ctypes.c_int)]
+    lib.rst_gbuffer_resized_size.restype = i
+    lib.rst_gbuffer_preprocess.argtypes = [ctypes.POINTER(vp), i, i, i, ctypes.c_longlong, ctypes.c_longlong, vp, i,
+                                           i, vp]
+    lib.rst_gbuffer_preprocess.restype = i
     lib.rst_last_error.argtypes = []
     lib.rst_last_error.restype = ctypes.c_char_p
     lib.rst_version.argtypes = []

@@ -74,6 +74,20 @@ struct Wino9Args {
     int batch, H, W, cin, tiles_y, tiles_x;
 };
 bool wino9_supported(int kh, int stride, int cin, int cout);
+
+// G-buffer ingest (ingest.hip): channel planes -> TF bilinear (half-pixel) resize -> center crop/pad
+constexpr int GBUFFER_MAX_PLANES = 32;
+struct GbufferArgs {
+    const float* planes[GBUFFER_MAX_PLANES];   // plane k: element (y, x) at planes[k][y*row_stride + x*pixel_stride]
+    int num_planes, src_h, src_w;
+    long row_stride, pixel_stride;
+    float* dst;                                 // NHWC [dst_h][dst_w][num_planes]
+    int dst_h, dst_w;
+    int new_h, new_w;                           // resized size (before the crop)
+    int off_y, off_x;                           // resized coordinate of dst (0, 0): crop offset - pad offset
+    float scale_y, scale_x;                     // float(src) / new
+};
+hipError_t gbuffer_resize_crop_launch(const GbufferArgs& a, hipStream_t st);
 int wino9_tiles_y(int H);
 int wino9_tiles_x(int W);
 std::vector<float> wino9_pack_weights(const float* kern, int cin);
