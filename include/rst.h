@@ -252,6 +252,12 @@ int rst_gbuffer_resized_size(int src_h, int src_w, int dst_h, int dst_w, int* ne
 int rst_gbuffer_preprocess(const float* const* planes, int num_planes, int src_h, int src_w, long long row_stride,
                            long long pixel_stride, float* dst, int dst_h, int dst_w, void* stream);
 
+/* ---- Checkpoint I/O helper ----
+ * CRC-32C (Castagnoli) of n bytes continuing from crc (0 to start): the checksum TF tensor bundles
+ * store for every tensor and SSTable block (tracing/checkpoint.py:21-37 writes them through
+ * tf.train.Checkpoint / Model.save_weights; predict_using_checkpoint.py:84 reads them). Host-only. */
+unsigned int rst_crc32c_extend(unsigned int crc, const void* data, size_t n);
+
 const char* rst_last_error(void);
 const char* rst_version(void);
 

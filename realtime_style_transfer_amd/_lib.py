@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = [
     "rst_predictor_trainer_create", "rst_predictor_trainer_destroy", "rst_predictor_trainer_num_weights",
     "rst_predictor_trainer_forward", "rst_predictor_trainer_backward", "rst_predictor_trainer_apply_gradients",
     "rst_predictor_trainer_copy_weights", "rst_predictor_trainer_set_weights", "rst_predictor_trainer_copy_slots",
-    "rst_gbuffer_resized_size", "rst_gbuffer_preprocess",
+    "rst_gbuffer_resized_size", "rst_gbuffer_preprocess", "rst_crc32c_extend",
 ]
 EXTRACTORS = {"DUMMY": 0, "MOBILE_NET": 1}   # include/rst.h RST_EXTRACTOR_*
 
@@ -179,6 +179,8 @@ def load() -> ctypes.CDLL:
     lib.rst_gbuffer_preprocess.argtypes = [ctypes.POINTER(vp), i, i, i, ctypes.c_longlong, ctypes.c_longlong, vp, i,
                                            i, vp]
     lib.rst_gbuffer_preprocess.restype = i
+    lib.rst_crc32c_extend.argtypes = [ctypes.c_uint, ctypes.c_char_p, sz]
+    lib.rst_crc32c_extend.restype = ctypes.c_uint
     lib.rst_last_error.argtypes = []
     lib.rst_last_error.restype = ctypes.c_char_p
     lib.rst_version.argtypes = []

@@ -93,6 +93,35 @@ class StyleTransferModel:
         self._weights = [np.ascontiguousarray(w, np.float32) for w in weights]
         self._build()
 
+    def keras_layer_attributes(self) -> List[List[str]]:
+        """Variables per weighted Keras layer, in model order: each Conv2D/Conv2DTranspose owns
+        (kernel, bias); the BatchNormalization after a contract conv (styleTransfer.py:194-203) is its
+        own layer (gamma, beta, moving_mean, moving_variance); CIN owns none (its affine is an input)."""
+        out = []
+        for layer in self.plan.layers:
+            out.append(["kernel", "bias"])
+            if layer.norm == 'bn':
+                out.append(["gamma", "beta", "moving_mean", "moving_variance"])
+        return out
+
+    def save_weights(self, filepath) -> None:
+        """Model.save_weights(filepath) in TF checkpoint format (tracing/checkpoint.py:37)."""
+        from .tf_checkpoint import save_keras_weights
+        save_keras_weights(filepath, self._weights, self.keras_layer_attributes())
+
+    def load_weights(self, filepath, model_path: str = ""):
+        """Model.load_weights(filepath) (predict_using_checkpoint.py:84) from a TF checkpoint prefix or
+        directory; ``model_path`` selects this model's subtree inside a larger model's checkpoint
+        (e.g. ``"layer_with_weights-1"``). Raises if nothing matches (assert_nontrivial_match)."""
+        from .tf_checkpoint import keras_weights, read_checkpoint
+        w = keras_weights(read_checkpoint(filepath), model_path)
+        shapes = [tuple(x.shape) for x in self._weights]
+        if [tuple(x.shape) for x in w] != shapes:
+            raise ValueError(f"checkpoint weights do not match the network plan: expected {shapes}, "
+                             f"got {[tuple(x.shape) for x in w]}")
+        self.set_weights(w)
+        return self
+
     @property
     def input(self) -> Dict[str, tuple]:
         spec = {'content': (None,) + self.input_shape, 'style_params': (None, self.num_styles,

@@ -1,0 +1,420 @@
+"""TF2 checkpoint (tensor bundle) reader / writer — weights interop.
+
+The reference persists weights with ``tf.train.Checkpoint`` / ``Model.save_weights`` (TF format,
+``tracing/checkpoint.py:21-37``) and restores them with ``Model.load_weights(path)`` /
+``Checkpoint.restore`` (``predict_using_checkpoint.py:84``, ``predict_video_using_checkpoint.py``,
+``save_using_checkpoint.py:65-68``). A checkpoint ``<prefix>`` is two files:
+
+* ``<prefix>.index`` — an SSTable (LevelDB table format: prefix-compressed key blocks with restart
+  points, an index block, a 48-byte footer ending in the magic 0xdb4775248b80fb57; every block
+  followed by a type byte and a masked CRC-32C). Key ``""`` holds a ``BundleHeaderProto``; every other
+  key is a variable's checkpoint key with a ``BundleEntryProto`` (dtype, shape, shard, offset, size,
+  masked CRC-32C of the bytes).
+* ``<prefix>.data-00000-of-0000N`` — the raw little-endian tensor bytes.
+
+Keras functional models name their variables ``layer_with_weights-<i>/<attr>/.ATTRIBUTES/VARIABLE_VALUE``
+where ``i`` counts the layers that own weights in model order and ``attr`` is the variable's attribute
+(``kernel``, ``bias``, ``gamma``, ``beta``, ``moving_mean``, ``moving_variance``, ``depthwise_kernel``);
+nested models add their own ``layer_with_weights-<j>/`` prefix. ``keras_weights`` turns such a
+subtree back into the ``get_weights()`` list that ``StyleTransferModel.set_weights`` takes.
+
+Third-party format (TensorFlow 2.9 ``core/util/tensor_bundle``, ``core/lib/io/table``; not vendored in
+the reference, TF not installed here): **parity unpinned** against files TF wrote — the reference holds
+no checkpoints. The reader is pinned by its own writer (round trip), by CRC-32C known answers, and by
+the format constants above.
+"""
+from __future__ import annotations
+
+import re
+import struct
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+
+TABLE_MAGIC = 0xdb4775248b80fb57
+_MASK_DELTA = 0xa282ead8
+# tensorflow/core/framework/types.proto DataType -> numpy
+_DTYPES = {1: np.float32, 2: np.float64, 3: np.int32, 4: np.uint8, 5: np.int16, 6: np.int8, 9: np.int64, 10: np.bool_,
+           17: np.uint16, 19: np.float16, 22: np.uint32, 23: np.uint64}
+_DT_STRING = 7
+_NP_TO_DT = {np.dtype(v): k for k, v in _DTYPES.items()}
+OBJECT_GRAPH_KEY = "_CHECKPOINTABLE_OBJECT_GRAPH"
+# Keras get_weights() order of the attributes inside one layer
+_ATTR_ORDER = {"kernel": 0, "depthwise_kernel": 0, "bias": 1, "gamma": 2, "beta": 3, "moving_mean": 4,
+               "moving_variance": 5}
+
+
+# ------------------------------------------------------------------------------------------ crc32c
+def crc32c(data: bytes, crc: int = 0) -> int:
+    return int(_lib.load().rst_crc32c_extend(crc, bytes(data), len(data)))
+
+
+def mask_crc(c: int) -> int:
+    return ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + _MASK_DELTA) & 0xFFFFFFFF
+
+
+def unmask_crc(m: int) -> int:
+    r = (m - _MASK_DELTA) & 0xFFFFFFFF
+    return ((r >> 17) | (r << 15)) & 0xFFFFFFFF
+
+
+# ------------------------------------------------------------------------------------------ varints / protobuf
+def _varint(buf: bytes, pos: int) -> Tuple[int, int]:
+    r, shift = 0, 0
+    while True:
+        b = buf[pos]
+        pos += 1
+        r |= (b & 0x7F) << shift
+        if b < 0x80:
+            return r, pos
+        shift += 7
+
+
+def _enc_varint(v: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _pb_fields(buf: bytes):
+    """Yield (field_number, wire_type, value) of a serialized protobuf message."""
+    pos = 0
+    while pos < len(buf):
+        key, pos = _varint(buf, pos)
+        fn, wt = key >> 3, key & 7
+        if wt == 0:
+            v, pos = _varint(buf, pos)
+        elif wt == 1:
+            v = struct.unpack_from('<Q', buf, pos)[0]
+            pos += 8
+        elif wt == 2:
+            n, pos = _varint(buf, pos)
+            v = buf[pos:pos + n]
+            pos += n
+        elif wt == 5:
+            v = struct.unpack_from('<I', buf, pos)[0]
+            pos += 4
+        else:
+            raise ValueError(f"unsupported protobuf wire type {wt}")
+        yield fn, wt, v
+
+
+def _pb_varint(fn: int, v: int) -> bytes:
+    return _enc_varint(fn << 3) + _enc_varint(v)
+
+
+def _pb_bytes(fn: int, b: bytes) -> bytes:
+    return _enc_varint((fn << 3) | 2) + _enc_varint(len(b)) + b
+
+
+def _pb_fixed32(fn: int, v: int) -> bytes:
+    return _enc_varint((fn << 3) | 5) + struct.pack('<I', v)
+
+
+class BundleEntry:
+    """tensorflow/core/protobuf/tensor_bundle.proto BundleEntryProto."""
+
+    def __init__(self, dtype=0, shape=(), shard_id=0, offset=0, size=0, crc32c=None):
+        self.dtype, self.shape, self.shard_id, self.offset, self.size, self.crc32c = \
+            dtype, tuple(shape), shard_id, offset, size, crc32c
+
+    @classmethod
+    def parse(cls, buf: bytes) -> "BundleEntry":
+        e = cls()
+        shape = []
+        for fn, wt, v in _pb_fields(buf):
+            if fn == 1:
+                e.dtype = v
+            elif fn == 2:                                   # TensorShapeProto
+                for f2, _, v2 in _pb_fields(v):
+                    if f2 == 2:                             # Dim
+                        size = 0
+                        for f3, _, v3 in _pb_fields(v2):
+                            if f3 == 1:
+                                size = v3 - (1 << 64) if v3 >= (1 << 63) else v3
+                        shape.append(size)
+            elif fn == 3:
+                e.shard_id = v
+            elif fn == 4:
+                e.offset = v
+            elif fn == 5:
+                e.size = v
+            elif fn == 6:
+                e.crc32c = v
+            elif fn == 7:
+                raise ValueError("partitioned (sliced) variables are not supported")
+        e.shape = tuple(shape)
+        return e
+
+    def serialize(self) -> bytes:
+        shp = b''.join(_pb_bytes(2, _pb_varint(1, d)) for d in self.shape)
+        out = _pb_varint(1, self.dtype) + _pb_bytes(2, shp)
+        if self.shard_id:
+            out += _pb_varint(3, self.shard_id)
+        if self.offset:
+            out += _pb_varint(4, self.offset)
+        out += _pb_varint(5, self.size)
+        if self.crc32c is not None:
+            out += _pb_fixed32(6, self.crc32c)
+        return out
+
+
+# ------------------------------------------------------------------------------------------ SSTable
+def _read_block(buf: bytes, offset: int, size: int, verify: bool) -> List[Tuple[bytes, bytes]]:
+    data = buf[offset:offset + size]
+    btype = buf[offset + size]
+    if btype != 0:
+        raise ValueError(f"compressed SSTable block (type {btype}) is not supported")
+    if verify:
+        stored = struct.unpack_from('<I', buf, offset + size + 1)[0]
+        if unmask_crc(stored) != crc32c(data + bytes([btype])):
+            raise ValueError(f"SSTable block at {offset}: checksum mismatch")
+    nrest = struct.unpack_from('<I', data, len(data) - 4)[0]
+    limit = len(data) - 4 - 4 * nrest
+    pos, key, out = 0, b'', []
+    while pos < limit:
+        shared, pos = _varint(data, pos)
+        non_shared, pos = _varint(data, pos)
+        vlen, pos = _varint(data, pos)
+        key = key[:shared] + data[pos:pos + non_shared]
+        pos += non_shared
+        out.append((key, data[pos:pos + vlen]))
+        pos += vlen
+    return out
+
+
+def _read_table(path: Path, verify: bool) -> List[Tuple[bytes, bytes]]:
+    buf = Path(path).read_bytes()
+    if len(buf) < 48:
+        raise ValueError(f"{path}: too short for an SSTable")
+    lo, hi = struct.unpack_from('<II', buf, len(buf) - 8)
+    if (hi << 32 | lo) != TABLE_MAGIC:
+        raise ValueError(f"{path}: not an SSTable (bad magic)")
+    pos = len(buf) - 48
+    _meta_off, pos = _varint(buf, pos)
+    _meta_size, pos = _varint(buf, pos)
+    idx_off, pos = _varint(buf, pos)
+    idx_size, pos = _varint(buf, pos)
+    entries = []
+    for _, handle in _read_block(buf, idx_off, idx_size, verify):
+        off, p = _varint(handle, 0)
+        size, _ = _varint(handle, p)
+        entries += _read_block(buf, off, size, verify)
+    return entries
+
+
+class _BlockBuilder:
+    def __init__(self, restart_interval=16):
+        self.buf, self.restarts, self.counter, self.last, self.ri = bytearray(), [0], 0, b'', restart_interval
+
+    def add(self, key: bytes, value: bytes):
+        shared = 0
+        if self.counter < self.ri:
+            n = min(len(self.last), len(key))
+            while shared < n and self.last[shared] == key[shared]:
+                shared += 1
+        else:
+            self.restarts.append(len(self.buf))
+            self.counter = 0
+        self.buf += _enc_varint(shared) + _enc_varint(len(key) - shared) + _enc_varint(len(value))
+        self.buf += key[shared:] + value
+        self.last, self.counter = key, self.counter + 1
+
+    def finish(self) -> bytes:
+        return bytes(self.buf) + b''.join(struct.pack('<I', r) for r in self.restarts) + \
+            struct.pack('<I', len(self.restarts))
+
+    def empty(self) -> bool:
+        return len(self.buf) == 0
+
+
+def _write_table(path: Path, items: List[Tuple[bytes, bytes]], block_size: int = 262144):
+    out = bytearray()
+
+    def emit(block: bytes) -> bytes:
+        off = len(out)
+        out.extend(block)
+        out.append(0)
+        out.extend(struct.pack('<I', mask_crc(crc32c(block + b'\0'))))
+        return _enc_varint(off) + _enc_varint(len(block))
+
+    index, data = _BlockBuilder(restart_interval=1), _BlockBuilder()
+    last_key = b''
+    for k, v in items:
+        data.add(k, v)
+        last_key = k
+        if len(data.buf) >= block_size:
+            index.add(last_key, emit(data.finish()))
+            data = _BlockBuilder()
+    if not data.empty():
+        index.add(last_key, emit(data.finish()))
+    meta = emit(_BlockBuilder().finish())
+    idx = emit(index.finish())
+    footer = (meta + idx).ljust(40, b'\0') + struct.pack('<II', TABLE_MAGIC & 0xFFFFFFFF, TABLE_MAGIC >> 32)
+    out.extend(footer)
+    Path(path).write_bytes(bytes(out))
+
+
+# ------------------------------------------------------------------------------------------ bundle
+def _index_path(prefix) -> Path:
+    p = str(prefix)
+    return Path(p if p.endswith('.index') else p + '.index')
+
+
+def _resolve_prefix(path) -> str:
+    """A checkpoint prefix, or a directory holding TF's ``checkpoint`` state file (latest checkpoint)."""
+    p = Path(path)
+    if p.is_dir():
+        state = p / "checkpoint"
+        if not state.exists():
+            raise FileNotFoundError(f"{p}: no 'checkpoint' state file")
+        m = re.search(r'^model_checkpoint_path:\s*"([^"]+)"', state.read_text(), re.M)
+        if not m:
+            raise ValueError(f"{state}: no model_checkpoint_path")
+        q = Path(m.group(1))
+        return str(q if q.is_absolute() else p / q)
+    s = str(p)
+    return s[:-len('.index')] if s.endswith('.index') else s
+
+
+def read_checkpoint(path, verify: bool = True, with_strings: bool = False) -> Dict[str, np.ndarray]:
+    """All tensors of a TF2 checkpoint: {checkpoint key: array} (tf.train.load_checkpoint + get_tensor)."""
+    prefix = _resolve_prefix(path)
+    entries = _read_table(_index_path(prefix), verify)
+    if not entries or entries[0][0] != b'':
+        raise ValueError(f"{prefix}: missing BundleHeaderProto")
+    num_shards = 1
+    for fn, _, v in _pb_fields(entries[0][1]):
+        if fn == 1:
+            num_shards = v
+        elif fn == 2 and v != 0:
+            raise ValueError("big-endian tensor bundles are not supported")
+    shards: Dict[int, bytes] = {}
+    out: Dict[str, np.ndarray] = {}
+    for k, v in entries[1:]:
+        e = BundleEntry.parse(v)
+        key = k.decode()
+        if e.shard_id not in shards:
+            shards[e.shard_id] = Path(f"{prefix}.data-{e.shard_id:05d}-of-{num_shards:05d}").read_bytes()
+        raw = shards[e.shard_id][e.offset:e.offset + e.size]
+        if verify and e.crc32c is not None and unmask_crc(e.crc32c) != crc32c(raw):
+            raise ValueError(f"{key}: tensor checksum mismatch")
+        if e.dtype == _DT_STRING:
+            if with_strings:
+                out[key] = _decode_strings(raw, e.shape)
+            continue
+        if e.dtype not in _DTYPES:
+            raise ValueError(f"{key}: unsupported dtype enum {e.dtype}")
+        out[key] = np.frombuffer(raw, dtype=np.dtype(_DTYPES[e.dtype]).newbyteorder('<')).reshape(e.shape).copy()
+    return out
+
+
+def _decode_strings(raw: bytes, shape) -> np.ndarray:
+    n = int(np.prod(shape)) if shape else 1
+    pos, lens = 0, []
+    for _ in range(n):
+        ln, pos = _varint(raw, pos)
+        lens.append(ln)
+    pos += 4                                                    # masked crc32c of the length varints
+    vals = []
+    for ln in lens:
+        vals.append(raw[pos:pos + ln])
+        pos += ln
+    return np.array(vals, dtype=object).reshape(shape)
+
+
+def list_variables(path) -> List[Tuple[str, Tuple[int, ...]]]:
+    """tf.train.list_variables equivalent (sorted keys, shapes)."""
+    return [(k, tuple(v.shape)) for k, v in sorted(read_checkpoint(path).items())]
+
+
+def write_checkpoint(prefix, tensors: Dict[str, np.ndarray], object_graph: Optional[bytes] = None) -> None:
+    """Write a single-shard TF2 tensor bundle (``<prefix>.index`` + ``<prefix>.data-00000-of-00001``)."""
+    prefix = str(prefix)
+    items = dict(tensors)
+    data = bytearray()
+    entries = []
+    for key in sorted(items):
+        a = np.asarray(items[key])          # (np.ascontiguousarray would turn 0-d scalars into shape (1,))
+        dt = _NP_TO_DT.get(a.dtype)
+        if dt is None:
+            raise ValueError(f"{key}: unsupported dtype {a.dtype}")
+        raw = a.astype(a.dtype.newbyteorder('<'), copy=False).tobytes(order='C')
+        entries.append((key.encode(), BundleEntry(dt, a.shape, 0, len(data), len(raw), mask_crc(crc32c(raw)))))
+        data += raw
+    if object_graph is not None:
+        lens = _enc_varint(len(object_graph))
+        raw = lens + struct.pack('<I', mask_crc(crc32c(lens))) + object_graph
+        entries.append((OBJECT_GRAPH_KEY.encode(), BundleEntry(_DT_STRING, (), 0, len(data), len(raw),
+                                                               mask_crc(crc32c(raw)))))
+        data += raw
+    entries.sort(key=lambda t: t[0])
+    header = _pb_varint(1, 1) + _pb_bytes(3, _pb_varint(1, 1))   # num_shards 1, little-endian, version{producer 1}
+    Path(f"{prefix}.data-00000-of-00001").write_bytes(bytes(data))
+    _write_table(_index_path(prefix), [(b'', header)] + [(k, e.serialize()) for k, e in entries])
+
+
+# ------------------------------------------------------------------------------------------ Keras mapping
+_KEY = re.compile(r'^(?P<path>(?:[^/]+/)*?)layer_with_weights-(?P<i>\d+)/(?P<attr>[A-Za-z_]+)/\.ATTRIBUTES/VARIABLE_VALUE$')
+
+
+def keras_weights(tensors: Dict[str, np.ndarray], model_path: str = "") -> List[np.ndarray]:
+    """The ``get_weights()`` list of the Keras model at ``model_path`` (``""`` = the checkpoint's root;
+    e.g. ``"layer_with_weights-1"`` for the second weighted sub-model of a functional model)."""
+    pre = model_path.rstrip('/') + '/' if model_path else ''
+    found = []
+    for k, v in tensors.items():
+        m = _KEY.match(k)
+        if not m or m.group('path') != pre or m.group('attr') not in _ATTR_ORDER:
+            continue
+        found.append(((int(m.group('i')), _ATTR_ORDER[m.group('attr')]), v))
+    if not found:
+        raise ValueError(f"no Keras layer variables under {model_path!r} (assert_nontrivial_match)")
+    found.sort(key=lambda t: t[0])
+    return [np.asarray(v, dtype=np.float32) for _, v in found]
+
+
+def _object_graph(layer_attrs: List[List[str]]) -> bytes:
+    """TrackableObjectGraph for a functional model: root -> layer_with_weights-i -> attr variables."""
+    nodes: List[bytes] = []
+    root_children = []
+    next_id = 1 + len(layer_attrs)
+    var_nodes = []
+    for i, attrs in enumerate(layer_attrs):
+        root_children.append(_pb_bytes(1, _pb_varint(1, 1 + i) + _pb_bytes(2, f"layer_with_weights-{i}".encode())))
+    nodes.append(b''.join(root_children))
+    for i, attrs in enumerate(layer_attrs):
+        ch = []
+        for a in attrs:
+            ch.append(_pb_bytes(1, _pb_varint(1, next_id) + _pb_bytes(2, a.encode())))
+            key = f"layer_with_weights-{i}/{a}/.ATTRIBUTES/VARIABLE_VALUE"
+            var_nodes.append(_pb_bytes(2, _pb_bytes(1, b"VARIABLE_VALUE") + _pb_bytes(2, a.encode()) +
+                                       _pb_bytes(3, key.encode())))
+            next_id += 1
+        nodes.append(b''.join(ch))
+    nodes += var_nodes
+    return b''.join(_pb_bytes(1, n) for n in nodes)
+
+
+def save_keras_weights(prefix, weights: List[np.ndarray], layer_attrs: List[List[str]]) -> None:
+    """Model.save_weights(prefix) (TF format) of a functional model whose weighted layers own the
+    attributes ``layer_attrs[i]`` in get_weights() order."""
+    tensors, it = {}, iter(weights)
+    for i, attrs in enumerate(layer_attrs):
+        for a in attrs:
+            tensors[f"layer_with_weights-{i}/{a}/.ATTRIBUTES/VARIABLE_VALUE"] = np.asarray(next(it), np.float32)
+    if next(it, None) is not None:
+        raise ValueError("more weights than layer attributes")
+    write_checkpoint(prefix, tensors, object_graph=_object_graph(layer_attrs))
+    state = Path(str(prefix)).parent / "checkpoint"
+    name = Path(str(prefix)).name
+    state.write_text(f'model_checkpoint_path: "{name}"\nall_model_checkpoint_paths: "{name}"\n')

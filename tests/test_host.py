@@ -68,7 +68,7 @@ def _lib():
 def test_library_exports_every_header_symbol():
     L, lib = _lib()
     header = open(os.path.join(ROOT, 'include', 'rst.h')).read()
-    declared = set(re.findall(r'\b(rst_[a-z_]+)\s*\(', header))
+    declared = set(re.findall(r'\b(rst_[a-z0-9_]+)\s*\(', header))
     assert declared, "no symbols parsed from rst.h"
     assert declared == set(L.EXPORTED_SYMBOLS), declared ^ set(L.EXPORTED_SYMBOLS)
     for name in declared:
