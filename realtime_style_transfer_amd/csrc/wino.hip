@@ -71,7 +71,8 @@ __device__ __forceinline__ float pro_apply(int mode, float x, float2 ab, float r
 
 // RST_WINO_OPT bit0: stage the patch of chunk c+2 (prologue + LDS write) and issue the loads of
 // chunk c+3 inside the MFMA loop of chunk c instead of before it (one wave per SIMD: work outside
-// the MFMA loop leaves the MFMA pipe idle)
+// the MFMA loop leaves the MFMA pipe idle); bit1: issue those HBM patch loads first in the chunk,
+// ahead of the chunk's L2 U loads (vmcnt drains in order)
 #ifndef RST_WINO_OPT
 #define RST_WINO_OPT 1
 #endif
@@ -253,7 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             if constexpr ((RST_WINO_OPT & 1) && x == 9) {   // patch(c+2) -> patch[P] (free since chunk c-1's transform)
                 if (has2) stage(c + 2, patch + P * W_PATCH_FL);
             }
-            if constexpr ((RST_WINO_OPT & 1) && x == 11) {
+            if constexpr ((RST_WINO_OPT & 1) && x == ((RST_WINO_OPT & 2) ? 0 : 11)) {
                 if (has3) load_patch(c + 3);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -321,6 +322,272 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
 }
 
+// ---- 8-wave variant: two waves per SIMD ------------------------------------------------------------
+// Same tile, transforms and operand layouts as wino_conv_kernel, but 8 waves: wave w owns output
+// channels 32(w&3)..+32 for the transform points 8(w>>2)..+8 only (128 accumulator registers), so
+// two waves share each SIMD and one's LDS/L2 waits and barrier skew hide behind the other's MFMAs
+// (with one wave per SIMD the MFMA issue inside the chunk loop was ~77 %). Waves 0-3 run the input
+// transform of chunk c+1, waves 4-7 the staging of chunk c+2 (each SIMD holds one of each), both
+// interleaved with their 32 MFMAs per chunk. Epilogue: A^T M A is linear in M, so the waves holding
+// points 8..15 (M rows 2, 3) push their partial 2x2 outputs through LDS to the waves holding 0..7,
+// which add them and finish bias + ReLU + store + tile statistics.
+constexpr int W8_EXCH_FL = 4 * 16 * 4 * 64;                              // [cg][j][q][lane]
+constexpr size_t W8_LDS_BYTES = (size_t)W8_EXCH_FL * 4;                  // aliases patch + V + pab
+static_assert(W8_LDS_BYTES >= W_LDS_BYTES, "exchange buffer covers the main-loop LDS");
+
+template <int PRO>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_conv8_kernel(WinoArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* const patch = smem;                         // [2][180][9]
+    float* const vs = patch + 2 * W_PATCH_FL;          // [2][16][32][12]
+    float2* const pab = reinterpret_cast<float2*>(vs + 2 * W_V_FL);
+    float* const exch = smem;                          // after the main loop
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cg = wave & 3, xh = wave >> 2;           // channel group, transform-point half
+    const int li = lane & 31, lh = lane >> 5;
+    int bid = blockIdx.x;
+    const int tx = bid % a.tiles_x;
+    bid /= a.tiles_x;
+    const int ty = bid % a.tiles_y;
+    const int b = bid / a.tiles_y;
+    const int y0 = ty * WTH, x0 = tx * WTW;
+    const int H = a.H, W = a.W, Cin = a.cin;
+    constexpr int pro = PRO;
+    const size_t img = (size_t)b * H * W;
+    const float* res_src = pro == PRO_AFF_RES ? a.res : a.in;
+    const int nchunks = Cin / WCK;
+
+    if constexpr (pro != PRO_NONE) {
+        for (int c = tid; c < Cin; c += 512) pab[c] = a.pro_ab[(size_t)b * Cin + c];
+    }
+
+    // ---- staging role (waves 4-7): items st and st + 256 of the 360 float4 of a chunk's patch ----
+    const int st = tid - 256;
+    f32x4 xr[2], rr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    auto load_patch = [&](int chunk) __attribute__((always_inline)) {
+        const int c0 = chunk * WCK;
+        sfor<0, 2>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int it = min(st + k * 256, W_PATCH_F4 - 1);
+            const int px = it >> 1, q = it & 1;
+            const int iy = min(max(y0 - 1 + px / WPW, 0), H - 1), ix = min(max(x0 - 1 + px % WPW, 0), W - 1);
+            const size_t gi = (img + (size_t)iy * W + ix) * Cin + c0 + 4 * q;
+            xr[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
+            if constexpr (pro == PRO_AFF_RES) rr[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
+        });
+    };
+    auto stage = [&](int chunk, float* pbuf) __attribute__((always_inline)) {
+        const int c0 = chunk * WCK;
+        sfor<0, 2>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int it = st + k * 256;
+            if (it < W_PATCH_F4) {
+                const int px = it >> 1, q = it & 1;
+                const int iy = y0 - 1 + px / WPW, ix = x0 - 1 + px % WPW;
+                const int c = c0 + 4 * q;
+                f32x4 v = xr[k];
+                const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
+                if constexpr (pro != PRO_NONE) {
+                    const f32x4 r = rr[k];
+                    const f32x4 p01 = *reinterpret_cast<const f32x4*>(pab + c);
+                    const f32x4 p23 = *reinterpret_cast<const f32x4*>(pab + c + 2);
+                    v.x = pro_apply(pro, v.x, float2{p01.x, p01.y}, r.x);
+                    v.y = pro_apply(pro, v.y, float2{p01.z, p01.w}, r.y);
+                    v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
+                    v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
+                    if (a.mat != nullptr && inside && iy >= y0 && iy < y0 + WTH && ix >= x0 && ix < x0 + WTW)
+                        *reinterpret_cast<f32x4*>(a.mat + (img + (size_t)iy * W + ix) * Cin + c) = v;
+                }
+                if (!inside) v = f32x4{0.f, 0.f, 0.f, 0.f};
+                float* d = pbuf + px * WPS + 4 * q;
+                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            }
+        });
+    };
+
+    // ---- U operands of this wave's points 8xh..8xh+7 -------------------------------------------
+    const __amdgpu_buffer_rsrc_t usrd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, nchunks * WXI * WN * WCK * 4, 0x00020000);
+    const int uvoff = ((cg * 32 + li) * 2 + lh) * 16;
+    auto load_u = [&](f32x4* u, int chunk, auto X) __attribute__((always_inline)) {
+        constexpr int x = decltype(X)::value;
+        u[x] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              usrd, uvoff, (chunk * WXI + 8 * xh + x) * (WN * WCK * 4), 0));
+    };
+
+    // ---- transform role (waves 0-3): one thread per (tile tt, channel tc) ------------------------
+    const int tt = tid & 31, tc = (tid >> 5) & 7;
+    const int twy = tt >> 3, twx = tt & 7;
+    float d[4][4];   // input tile, transformed in place (B^T d) to keep the register count <= 256
+    auto tr_read = [&](const float* pbuf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[r][c] = pbuf[((2 * twy + r) * WPW + 2 * twx + c) * WPS + tc];
+    };
+    auto tr_rows = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float a0 = d[0][c], a1 = d[1][c], a2 = d[2][c], a3 = d[3][c];
+            d[0][c] = a0 - a2;
+            d[1][c] = a1 + a2;
+            d[2][c] = a2 - a1;
+            d[3][c] = a1 - a3;
+        }
+    };
+    auto tr_cols = [&](float* vbuf, int r) __attribute__((always_inline)) {
+        const float v0 = d[r][0] - d[r][2], v1 = d[r][1] + d[r][2];
+        const float v2 = d[r][2] - d[r][1], v3 = d[r][1] - d[r][3];
+        vbuf[((r * 4 + 0) * 32 + tt) * WVS + tc] = v0;
+        vbuf[((r * 4 + 1) * 32 + tt) * WVS + tc] = v1;
+        vbuf[((r * 4 + 2) * 32 + tt) * WVS + tc] = v2;
+        vbuf[((r * 4 + 3) * 32 + tt) * WVS + tc] = v3;
+    };
+
+    floatx16 acc[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+    f32x4 ur[8];
+
+    // ---- pipeline fill -----------------------------------------------------------------------
+    if constexpr (pro != PRO_NONE) __syncthreads();
+    if (xh == 1) load_patch(0);
+    sfor<0, 8>([&](auto X) __attribute__((always_inline)) { load_u(ur, 0, X); });
+    if (xh == 1) {
+        stage(0, patch);
+        if (nchunks > 1) load_patch(1);
+    }
+    __syncthreads();
+    if (xh == 0) {
+        tr_read(patch);
+        tr_rows();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tr_cols(vs, r);
+    } else if (nchunks > 1) {
+        stage(1, patch + W_PATCH_FL);
+        if (nchunks > 2) load_patch(2);
+    }
+    __syncthreads();
+
+    for (int c = 0; c < nchunks; ++c) {
+        const int P = c & 1;
+        const bool has2 = c + 2 < nchunks, has3 = c + 3 < nchunks;
+        const int c1 = min(c + 1, nchunks - 1);
+        const float* va = vs + P * W_V_FL + (8 * xh * 32 + li) * WVS + 4 * lh;
+        float* const vnext = vs + (1 - P) * W_V_FL;
+        const float* const pnext = patch + (1 - P) * W_PATCH_FL;
+        f32x4 av[2];
+        av[0] = *reinterpret_cast<const f32x4*>(va);
+        __builtin_amdgcn_sched_barrier(0);
+        sfor<0, 8>([&](auto X) __attribute__((always_inline)) {
+            constexpr int x = decltype(X)::value;
+            if constexpr (x + 1 < 8) av[(x + 1) & 1] = *reinterpret_cast<const f32x4*>(va + (x + 1) * 32 * WVS);
+            __builtin_amdgcn_sched_barrier(0);
+            const f32x4 a4 = av[x & 1], b4 = ur[x];
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc[x], 0, 0, 0);
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc[x], 0, 0, 0);
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc[x], 0, 0, 0);
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc[x], 0, 0, 0);
+            load_u(ur, c1, X);
+            if (xh == 0) {
+                if constexpr (x == 0) tr_read(pnext);
+                if constexpr (x == 2) tr_rows();
+                if constexpr (x >= 3 && x < 7) tr_cols(vnext, x - 3);
+            } else {
+                if constexpr (x == 1) {
+                    if (has2) stage(c + 2, patch + P * W_PATCH_FL);
+                }
+                if constexpr (x == 4) {
+                    if (has3) load_patch(c + 3);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        __syncthreads();
+    }
+
+    // ---- epilogue ------------------------------------------------------------------------------
+    // T = A^T M (2 x 4) with A^T = [[1,1,1,0],[0,1,-1,-1]]: rows 0,1 of M come from xh == 0,
+    // rows 2,3 from xh == 1; Y = T A (2 x 2).
+    auto out_tf = [&](const float (&t0)[4], const float (&t1)[4], float (&yy)[4]) __attribute__((always_inline)) {
+        yy[0] = t0[0] + t0[1] + t0[2];
+        yy[1] = t0[1] - t0[2] - t0[3];
+        yy[2] = t1[0] + t1[1] + t1[2];
+        yy[3] = t1[1] - t1[2] - t1[3];
+    };
+    if (xh == 1) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            float t0[4], t1[4], yy[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                t0[q] = acc[q][j];                     // M[2][q]
+                t1[q] = -acc[q][j] - acc[4 + q][j];    // -M[2][q] - M[3][q]
+            }
+            out_tf(t0, t1, yy);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) exch[((cg * 16 + j) * 4 + q) * 64 + lane] = yy[q];
+        }
+    }
+    __syncthreads();
+    if (xh == 1) return;
+    const int co = cg * 32 + li;
+    const float bias = a.bias[co];
+    float yv[64];
+    float s = 0.f, cnt = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;
+        const int wy = row >> 3, wx = row & 7;
+        float t0[4], t1[4], yy[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            t0[q] = acc[q][j] + acc[4 + q][j];         // M[0][q] + M[1][q]
+            t1[q] = acc[4 + q][j];                     // M[1][q]
+        }
+        out_tf(t0, t1, yy);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float y = yy[q] + exch[((cg * 16 + j) * 4 + q) * 64 + lane];
+            const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
+            const float v = fmaxf(y + bias, 0.f);
+            const bool ok = oy < H && ox < W;
+            yv[j * 4 + q] = ok ? v : 0.f;
+            if (ok) {
+                a.out[(img + (size_t)oy * W + ox) * WN + co] = v;
+                s += v;
+                cnt += 1.f;
+            }
+        }
+    }
+    if (a.part != nullptr) {
+        s += __shfl_xor(s, 32);
+        cnt += __shfl_xor(cnt, 32);
+        const float mean = cnt > 0.f ? s / cnt : 0.f;
+        float m2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;
+            const int wy = row >> 3, wx = row & 7;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
+                const float dd = yv[j * 4 + q] - mean;
+                if (oy < H && ox < W) m2 = fmaf(dd, dd, m2);
+            }
+        }
+        m2 += __shfl_xor(m2, 32);
+        if (lh == 0) {
+            const int n_part = a.tiles_y * a.tiles_x;
+            a.part[((size_t)b * WN + co) * n_part + ty * a.tiles_x + tx] = make_float4(s, m2, cnt, 0.f);
+        }
+    }
+}
+
 bool wino_supported(int kh, int stride, int cin, int cout) {
     return kh == 3 && stride == 1 && cout == WN && cin % WCK == 0 && cin <= W_MAX_CIN;
 }
@@ -349,27 +616,45 @@ std::vector<float> wino_pack_weights(const float* kern, int cin) {
     return U;
 }
 
+// RST_WINO8: launch the 8-wave (two waves per SIMD) variant. Measured (tools/wino_bench.hip, residual
+// conv at 120x240x128): 54.6 vs 54.0 us at B=1, 394 vs 382 us at B=8 — no gain over one wave per
+// SIMD; the chunk loop is not latency-bound (interleaving the accumulators of two points, or
+// issuing the HBM patch loads ahead of the L2 U loads, did not move it either), so the 4-wave
+// kernel stays the default.
+#ifndef RST_WINO8
+#define RST_WINO8 0
+#endif
+
 hipError_t wino_prepare() {
     for (const void* k : {(const void*)wino_conv_kernel<PRO_NONE>, (const void*)wino_conv_kernel<PRO_AFF_RELU>,
                           (const void*)wino_conv_kernel<PRO_AFF>, (const void*)wino_conv_kernel<PRO_AFF_RES>}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)W_LDS_BYTES);
         if (e != hipSuccess) return e;
     }
+    for (const void* k : {(const void*)wino_conv8_kernel<PRO_NONE>, (const void*)wino_conv8_kernel<PRO_AFF_RELU>,
+                          (const void*)wino_conv8_kernel<PRO_AFF>, (const void*)wino_conv8_kernel<PRO_AFF_RES>}) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)W8_LDS_BYTES);
+        if (e != hipSuccess) return e;
+    }
     return hipSuccess;
+}
+
+template <int PRO>
+static void wino_launch_mode(const WinoArgs& a, unsigned grid, hipStream_t st) {
+    if (RST_WINO8)
+        hipLaunchKernelGGL(wino_conv8_kernel<PRO>, dim3(grid), dim3(512), W8_LDS_BYTES, st, a);
+    else
+        hipLaunchKernelGGL(wino_conv_kernel<PRO>, dim3(grid), dim3(256), W_LDS_BYTES, st, a);
 }
 
 hipError_t wino_launch(const WinoArgs& a, hipStream_t st) {
     if (a.cin % WCK != 0 || a.cin > W_MAX_CIN) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
     switch (a.pro_mode) {
-        case PRO_NONE: hipLaunchKernelGGL(wino_conv_kernel<PRO_NONE>, dim3(grid), dim3(256), W_LDS_BYTES, st, a); break;
-        case PRO_AFF_RELU:
-            hipLaunchKernelGGL(wino_conv_kernel<PRO_AFF_RELU>, dim3(grid), dim3(256), W_LDS_BYTES, st, a);
-            break;
-        case PRO_AFF: hipLaunchKernelGGL(wino_conv_kernel<PRO_AFF>, dim3(grid), dim3(256), W_LDS_BYTES, st, a); break;
-        case PRO_AFF_RES:
-            hipLaunchKernelGGL(wino_conv_kernel<PRO_AFF_RES>, dim3(grid), dim3(256), W_LDS_BYTES, st, a);
-            break;
+        case PRO_NONE: wino_launch_mode<PRO_NONE>(a, grid, st); break;
+        case PRO_AFF_RELU: wino_launch_mode<PRO_AFF_RELU>(a, grid, st); break;
+        case PRO_AFF: wino_launch_mode<PRO_AFF>(a, grid, st); break;
+        case PRO_AFF_RES: wino_launch_mode<PRO_AFF_RES>(a, grid, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
