@@ -9,6 +9,16 @@ namespace rst {
 enum ProMode { PRO_NONE = 0, PRO_AFF_RELU = 1, PRO_AFF = 2, PRO_AFF_RES = 3, PRO_MASK = 4 };
 enum EpiMode { EPI_NONE = 0, EPI_RELU_BN = 1, EPI_RELU_STATS = 2, EPI_STATS = 3 };
 
+// XCD-aware block order: the dispatcher deals workgroup ids round-robin over the 8 XCDs (each with
+// its own L2), so consecutive ids (neighbouring tiles, whose halos overlap) land on different L2s.
+// Remap so XCD x processes one contiguous run of the tile order: a bijection on [0, n).
+__device__ __forceinline__ int xcd_tile_order(int bid, int n) {
+    constexpr int NXCD = 8;
+    const int x = bid % NXCD, k = bid / NXCD;
+    const int base = n / NXCD, rem = n % NXCD;
+    return x * base + min(x, rem) + k;
+}
+
 // Arguments of the implicit-GEMM MFMA conv kernel (conv_mfma.hip).
 struct ConvArgs {
     const float* in;        // NHWC [B][H][W][cin] raw producer output

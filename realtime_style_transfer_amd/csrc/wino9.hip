@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256, 2) void wino9_conv_kernel(Wino9Args a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
-    int bid = blockIdx.x;
+    int bid = xcd_tile_order(blockIdx.x, gridDim.x);   // XCD-contiguous tile runs (halo reuse in L2)
     const int tx = bid % a.tiles_x;
     bid /= a.tiles_x;
     const int ty = bid % a.tiles_y;

@@ -32,8 +32,12 @@ def short_name(k: str) -> str:
     if m:
         args = tuple(int(v) for v in m.group(1).split(","))
         return CONFIG_NAMES.get(args[:5], "conv_mfma<" + ",".join(map(str, args)) + ">")
-    if "wino_conv_kernel" in k:
+    if "wino9_conv_kernel" in k:
+        return "wino9_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 f32 MFMA>"
+    if "wino_conv" in k:
         return "wino_conv<F(2x2,3x3) 8x16 N128 f32 MFMA>"
+    if "gbuffer_resize_crop" in k:
+        return "gbuffer_resize_crop"
     if "small_conv_kernel" in k:
         return "small_conv_kernel<9x9 Cout3 VALU>"
     return k.split("(")[0]
@@ -51,14 +55,19 @@ def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
     out = {"note": __doc__.split("\n\n")[1], "per_launch_bytes": {}, "raw": {}}
+    # instantiations that share a short name (e.g. the prologue-mode templates of one kernel) are
+    # merged launch-weighted: per_launch_bytes is the mean over every launch of that kernel
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
     for k, fv in fetch.items():
-        wv = write.get(k, [0.0])
-        f_mean = sum(fv) / len(fv)
-        w_mean = sum(wv) / len(wv)
-        b = 2.0 * f_mean * 1024 + w_mean * 1024
-        name = short_name(k)
-        out["per_launch_bytes"][name] = round(b)
-        out["raw"][name] = {"launches": len(fv), "fetch_kib_mean": f_mean, "write_kib_mean": w_mean,
+        wv = write.get(k, [0.0] * len(fv))
+        a = agg[short_name(k)]
+        a[0] += len(fv)
+        a[1] += sum(fv)
+        a[2] += sum(wv) * len(fv) / max(len(wv), 1)
+    for name, (n, fsum, wsum) in agg.items():
+        f_mean, w_mean = fsum / n, wsum / n
+        out["per_launch_bytes"][name] = round(2.0 * f_mean * 1024 + w_mean * 1024)
+        out["raw"][name] = {"launches": n, "fetch_kib_mean": f_mean, "write_kib_mean": w_mean,
                             "read_bytes_corrected": 2.0 * f_mean * 1024, "write_bytes": w_mean * 1024}
     json.dump(out, open(sys.argv[3], "w"), indent=1)
     for n, v in sorted(out["per_launch_bytes"].items(), key=lambda t: -t[1]):
