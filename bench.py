@@ -70,6 +70,7 @@ DTYPE_DESC = {
               "fp32 accumulate, on the residual convs; other layers fp32 MFMA",
     "bf16x3": "fp32 via 2-piece split bf16 (3 product terms, 16 significant bits per operand), fp32 accumulate, "
               "on the residual convs; other layers fp32 MFMA",
+    "bf16": "bf16 operands (8 significant bits), fp32 accumulate, on the residual convs; other layers fp32 MFMA",
 }
 
 
@@ -143,7 +144,7 @@ def bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs, time
     conv_ms, _, nsteps = model.profile_end()
     ids = [model.layer_kernel_id(i) for i in range(len(plan.layers))]
     bf3 = [i for i, k in enumerate(ids) if k >= 101]
-    terms = 3 if precision == "bf16x3" else 6
+    terms = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}.get(precision, 6)
     ms = sum(conv_ms[i] for i in bf3) / max(nsteps, 1) / max(len(bf3), 1)
     fl = sum(layer_flops(plan.layers[i]) for i in bf3) * B / max(len(bf3), 1)
     eff_tf = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
@@ -172,9 +173,7 @@ def bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs, time
         }
     return model, {
         "value": round(world * B * args.steps / el, 3), "unit": "frames/s", "ms_per_step": round(el * 1e3 / args.steps, 4),
-        "dtype": ("fp32 via 2-piece split bf16 (3 product terms, 16 significant bits per operand)" if terms == 3 else
-                  "fp32 via exact 3-piece split bf16 (24 significant bits, 6 product terms, dropped terms <= 2^-24)") +
-                 ", fp32 accumulate, on the residual convs; other layers fp32 MFMA",
+        "dtype": DTYPE_DESC.get(precision, precision),
         "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES.get(ids[bf3[0]], "?") if bf3 else None,
                      "achieved": round(terms * eff_tf, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s (bf16 MFMA)",
                      "frac": round(terms * eff_tf / BF16_MFMA_PEAK_TFLOPS, 4), "avg_launch_ms": round(ms, 5),
@@ -217,7 +216,9 @@ def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, tim
                       "bf16x6": "VGG16 3x3 convs: exact 3-piece split bf16 MFMA (fp32-level products, fp32 accumulate); "
                                 "transfer net and the rest fp32",
                       "bf16x3": "VGG16 3x3 convs: 2-piece split bf16 MFMA (16-bit operands, fp32 accumulate); "
-                                "transfer net and the rest fp32"}[precision],
+                                "transfer net and the rest fp32",
+                      "bf16": "VGG16 3x3 convs: bf16 operands, fp32 accumulate (mixed_bfloat16 arithmetic); "
+                              "transfer net and the rest fp32"}[precision],
             "tflop_per_sample": round(per_sample / 1e12, 4),
             "achieved_tflops_per_gpu": round(tfs, 2), "frac_fp32_mfma_peak": round(tfs / FP32_MFMA_PEAK_TFLOPS, 4),
             "flop_breakdown_per_sample_gflop": {k: round(v / 1e9, 2) for k, v in fl.items()},
@@ -499,7 +500,7 @@ def main():
     # ---------------- precision mode: split-bf16 residual convs (reported beside the fp32 headline) --
     split_models, split = {}, {}
     if not args.no_bf16x3:
-        for prec in [p for p in ("fp32", "fp32_winograd", "bf16x6", "bf16x3") if p != args.precision]:
+        for prec in [p for p in ("fp32", "fp32_winograd", "bf16x6", "bf16x3", "bf16") if p != args.precision]:
             split_models[prec], split[prec] = bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs,
                                                           timed, prec)
 
@@ -513,13 +514,13 @@ def main():
     # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
     train = None
     if args.train_batch > 0:
-        # BASELINE config 4 trains in bf16: the headline training figure uses the split-bf16 VGG16
-        # (bf16x3, more accurate than plain bf16); the fp32 and bf16x6 runs are reported beside it
-        train = bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed, "bf16x3")
+        # BASELINE config 4 trains in bf16: the headline training figure runs the VGG16 3x3 convs with bf16
+        # operands and fp32 accumulation; the split-bf16 (bf16x3, bf16x6) and fp32 runs are reported beside it
+        train = bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed, "bf16")
         train["other_precisions"] = {p: {k: v for k, v in bench_training(args, world, rank, dev, cfg, ins, outs, plan,
                                                                           weights, P, timed, p).items()
                                          if k in ("ms_per_step", "frames_per_s", "achieved_tflops_per_gpu", "dtype")}
-                                     for p in ("bf16x6", "fp32")}
+                                     for p in ("bf16x3", "bf16x6", "fp32")}
 
     # ---------------- parity + CPU baseline (rank 0 only, bounded sample) -----------------------
     max_abs = None

@@ -160,11 +160,14 @@ def transfer_structure(input_shape, output_shape, bottleneck_res_y, bottleneck_n
 
 
 def transfer_forward(content, style_params, weights: Sequence[np.ndarray], input_shape, output_shape,
-                     bottleneck_res_y, bottleneck_num_filters, style_weights=None, return_intermediates=False):
+                     bottleneck_res_y, bottleneck_num_filters, style_weights=None, return_intermediates=False,
+                     operand_round=None):
     """Forward of the transfer net in float64.
 
     content (B,H,W,C); style_params (B,S,P); weights in Keras get_weights() order;
-    style_weights (B,Ho,Wo,S-1) for S>1 (styleTransfer.py:290-303).
+    style_weights (B,Ho,Wo,S-1) for S>1 (styleTransfer.py:290-303). ``operand_round`` (e.g. bf16_round)
+    is applied to the input and kernel of the residual-block convs (the layers a bf16 precision mode
+    runs on the bf16 pipe) to simulate that mode.
     """
     blocks, P = transfer_structure(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters)
     x = np.asarray(content, np.float64)
@@ -199,6 +202,8 @@ def transfer_forward(content, style_params, weights: Sequence[np.ndarray], input
             fx = x
             for j in range(2):
                 w, b = next(wi), next(wi)
+                if operand_round is not None:
+                    fx, w = operand_round(fx), operand_round(w)
                 fx = relu(conv2d_same(fx, w, b, 1))
                 cin_params = _ParamStack(block_params.get(2 * f))
                 scale = apply_style_weights(sw, cin_params.get(f))
@@ -263,8 +268,18 @@ def max_pool2(x):
     return x[:, :H2 * 2, :W2 * 2, :].reshape(B, H2, 2, W2, 2, C).max(axis=(2, 4))
 
 
-def vgg16_features(images01, vgg_weights: Dict[str, Tuple[np.ndarray, np.ndarray]]):
-    """StyleLossModelVGG.call (styleLoss.py:106-109): x*255, RGB->BGR, -mean, VGG16 trunk."""
+def bf16_round(x):
+    """Round to bfloat16 (round-to-nearest-even) through float32, as the device does with its fp32
+    values; returned as float64 (bf16 x bf16 products are exact in fp32 and float64)."""
+    u = np.ascontiguousarray(np.asarray(x, np.float32)).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def vgg16_features(images01, vgg_weights: Dict[str, Tuple[np.ndarray, np.ndarray]], operand_round=None):
+    """StyleLossModelVGG.call (styleLoss.py:106-109): x*255, RGB->BGR, -mean, VGG16 trunk.
+    ``operand_round`` (e.g. bf16_round) is applied to the input and kernel of every conv with
+    Cin % 32 == 0 — the layers the device runs in a bf16 precision mode — to simulate that mode."""
     x = np.asarray(images01, np.float64) * 255.0
     x = x[..., ::-1] - VGG_MEAN_BGR                                   # vgg16.preprocess_input ('caffe')
     feats = {}
@@ -274,6 +289,8 @@ def vgg16_features(images01, vgg_weights: Dict[str, Tuple[np.ndarray, np.ndarray
             continue
         name = entry[0]
         w, b = vgg_weights[name]
+        if operand_round is not None and x.shape[-1] % 32 == 0:
+            x, w = operand_round(x), operand_round(w)
         x = relu(conv2d_same(x, w, b, 1))
         if name in STYLE_LAYERS or name in CONTENT_LAYERS:
             feats[name] = x
@@ -283,15 +300,15 @@ def vgg16_features(images01, vgg_weights: Dict[str, Tuple[np.ndarray, np.ndarray
 
 
 def style_loss_terms(prediction, gt_content, gt_style, vgg_weights,
-                     content_factor=1e4, style_factor=1e-3, tv_factor=1e-1):
+                     content_factor=1e4, style_factor=1e-3, tv_factor=1e-1, operand_round=None):
     """make_style_loss_function without the MiDaS depth term (styleLoss.py:295-369)."""
     style = np.asarray(gt_style, np.float64)
     if style.ndim == 5:
         assert style.shape[1] == 1
         style = style[:, 0]
-    fc = vgg16_features(gt_content, vgg_weights)
-    fs = vgg16_features(style, vgg_weights)
-    fp = vgg16_features(prediction, vgg_weights)
+    fc = vgg16_features(gt_content, vgg_weights, operand_round)
+    fs = vgg16_features(style, vgg_weights, operand_round)
+    fp = vgg16_features(prediction, vgg_weights, operand_round)
     feature_loss = np.mean([mean_l2_loss_on_batch(fp[n] - fc[n]) for n in CONTENT_LAYERS], axis=0) * content_factor
     style_loss = np.mean([mean_l2_loss_on_batch(gram_matrix(fp[n]) - gram_matrix(fs[n])) for n in STYLE_LAYERS],
                          axis=0) * style_factor

@@ -29,7 +29,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-from .numpy_ref import CONTENT_LAYERS, STYLE_LAYERS, VGG16_LAYERS, VGG_MEAN_BGR, transfer_structure
+from .numpy_ref import CONTENT_LAYERS, STYLE_LAYERS, VGG16_LAYERS, VGG_MEAN_BGR, bf16_round, transfer_structure
 from .torch_ref import cin, conv2d_same, conv2d_transpose_same
 
 BN_MOMENTUM = 0.99
@@ -117,10 +117,37 @@ class _RoutedMaxPool2(torch.autograd.Function):
         return gx, None
 
 
-def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None) -> Dict[str, torch.Tensor]:
+def _bf16(t: torch.Tensor) -> torch.Tensor:
+    return torch.from_numpy(bf16_round(t.detach().numpy())).to(t.dtype)
+
+
+class _Bf16Conv(torch.autograd.Function):
+    """A VGG16 conv in the device's RST_PRECISION_BF16 arithmetic: forward on bf16-rounded input and
+    kernel, input gradient from the bf16-rounded output gradient and kernel (products exact in
+    float64, as they are in the fp32 accumulators). The kernel is frozen (no weight gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(w)
+        ctx.xshape = x.shape
+        return conv2d_same(_bf16(x), _bf16(w), b, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (w,) = ctx.saved_tensors
+        xd = torch.zeros(ctx.xshape, dtype=gy.dtype, requires_grad=True)
+        with torch.enable_grad():
+            y = conv2d_same(xd, _bf16(w), None, 1)
+            (gx,) = torch.autograd.grad(y, xd, _bf16(gy))
+        return gx, None, None
+
+
+def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None,
+                 bf16: bool = False) -> Dict[str, torch.Tensor]:
     """StyleLossModelVGG.call (styleLoss.py:106-109) on NCHW float64 images in [0, 1].
     ``taps``: list receiving every conv output (retain_grad) when the input requires grad.
-    ``route``: {conv index: NCHW activations} whose window maxima route the max-pool backward."""
+    ``route``: {conv index: NCHW activations} whose window maxima route the max-pool backward.
+    ``bf16``: every conv but the first (Cin = 3, fp32 on the device) in bf16 arithmetic (_Bf16Conv)."""
     x = images01 * 255.0
     mean = torch.tensor(VGG_MEAN_BGR, dtype=x.dtype).view(1, 3, 1, 1)
     x = x.flip(1) - mean
@@ -134,7 +161,10 @@ def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None) -
                 x = F.max_pool2d(x, 2)
             continue
         name = entry[0]
-        x = F.relu(conv2d_same(x, vgg[2 * i], vgg[2 * i + 1], 1))
+        if bf16 and i > 0:
+            x = F.relu(_Bf16Conv.apply(x, vgg[2 * i], vgg[2 * i + 1]))
+        else:
+            x = F.relu(conv2d_same(x, vgg[2 * i], vgg[2 * i + 1], 1))
         i += 1
         if taps is not None and x.requires_grad:
             x.retain_grad()
@@ -157,9 +187,10 @@ def _mean_l2(t):
 
 
 def style_losses(pred, content, style, vgg, content_factor=1e4, style_factor=1e-3, tv_factor=1e-1, taps=None,
-                 route=None):
+                 route=None, bf16=False):
     """make_style_loss_function without depth (styleLoss.py:295-369) -> (B, 4) [loss, feature, style, tv]."""
-    fp, fc, fs = vgg_features(pred, vgg, taps, route), vgg_features(content, vgg), vgg_features(style, vgg)
+    fp = vgg_features(pred, vgg, taps, route, bf16)
+    fc, fs = vgg_features(content, vgg, bf16=bf16), vgg_features(style, vgg, bf16=bf16)
     feature = torch.stack([_mean_l2(fp[n] - fc[n]) for n in CONTENT_LAYERS]).mean(0) * content_factor
     style_l = torch.stack([_mean_l2(_gram(fp[n]) - _gram(fs[n])) for n in STYLE_LAYERS]).mean(0) * style_factor
     tv = ((pred[:, :, 1:, :] - pred[:, :, :-1, :]).abs().sum(dim=(1, 2, 3)) +
@@ -174,7 +205,8 @@ def _nchw(a):
 def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarray], content, style_params,
                   gt_content, gt_style, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
                   factors=(1e4, 1e-3, 1e-1), ms: Optional[Sequence[np.ndarray]] = None,
-                  lr=1e-3, rho=0.9, eps=1e-7, pool_route: Optional[Dict[int, np.ndarray]] = None) -> Dict[str, object]:
+                  lr=1e-3, rho=0.9, eps=1e-7, pool_route: Optional[Dict[int, np.ndarray]] = None,
+                  vgg_bf16: bool = False) -> Dict[str, object]:
     """One Keras train_step: forward (BN training mode), loss, gradients, RMSprop.
 
     Inputs are NHWC numpy; returns numpy: prediction (B,H,W,3), losses (B,4), grads (Keras order;
@@ -193,7 +225,7 @@ def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarra
     pred, bn_stats = transfer_forward_train(_nchw(content), sp, w, blocks, taps=taps)
     vtaps = []
     route = None if pool_route is None else {k: _nchw(v) for k, v in pool_route.items()}
-    losses = style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors, taps=vtaps, route=route)
+    losses = style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors, taps=vtaps, route=route, bf16=vgg_bf16)
     losses[:, 0].sum().backward()
     # Keras trainable set: conv kernels/biases, BN gamma/beta (moving statistics are not trained)
     grads, new_w, new_ms = [], [], []

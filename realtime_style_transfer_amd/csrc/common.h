@@ -7,6 +7,11 @@
 
 namespace rst {
 
+// bf16 planes of a split-bf16 precision mode (include/rst.h RST_PRECISION_*), 0 for the f32 modes
+inline int bf16_planes(int precision) {
+    return precision == 1 ? 2 : (precision == 2 ? 3 : (precision == 4 ? 1 : 0));   // BF16X3, BF16X6, BF16
+}
+
 // Record the thread-local error message returned by rst_last_error(); returns code.
 int set_error(int code, const std::string& msg);
 

@@ -7,7 +7,8 @@
 // A_lo*B_lo term is 2^-16 relative. That is ~30x more accurate than TF32 (10-bit mantissa), which
 // TensorFlow uses by default for "fp32" convolutions on NVIDIA Ampere-class GPUs, at 3/16 of the
 // f32-MFMA cost. This is an opt-in precision mode (RST_PRECISION_BF16X3); the exact-f32 kernel
-// (conv_mfma.hip) stays the default.
+// (conv_mfma.hip) stays the default. One plane (RST_PRECISION_BF16) is plain bf16 operands with fp32
+// accumulation — the arithmetic of a Keras mixed_bfloat16 policy — at 1/16 of the f32-MFMA cost.
 //
 // Structure mirrors conv_mfma_kernel (same ConvArgs, prologue and epilogue semantics): output tile
 // TH x TW pixels x NT channels per 4-wave workgroup, stage = (Cin chunk, tap group), weights of the
@@ -35,13 +36,15 @@ __device__ __forceinline__ unsigned short bf16_rne(float x) {
     return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
 }
 __device__ __forceinline__ float bf16_val(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
-// x = p0 + p1 [+ p2]: each remainder is exact in fp32, every piece rounds to the nearest bf16
+// x = p0 [+ p1 [+ p2]]: each remainder is exact in fp32, every piece rounds to the nearest bf16
 template <int NP>
 __device__ __forceinline__ void split_bf16(float x, unsigned short* p) {
     p[0] = bf16_rne(x);
-    float r = x - bf16_val(p[0]);
-    p[1] = bf16_rne(r);
-    if constexpr (NP == 3) p[2] = bf16_rne(r - bf16_val(p[1]));
+    if constexpr (NP >= 2) {
+        const float r = x - bf16_val(p[0]);
+        p[1] = bf16_rne(r);
+        if constexpr (NP == 3) p[2] = bf16_rne(r - bf16_val(p[1]));
+    }
 }
 
 template <int I, int N, typename F>
@@ -75,7 +78,7 @@ struct Bf3Cfg {
     static constexpr int HALO = ((HP * CSB + 7) / 8) * 8;     // bf16 per plane
     static constexpr int MAX_CIN = 256;
     static constexpr size_t LDS_BYTES = (size_t)(NP * HALO + 2 * WSTAGE) * 2 + 2 * MAX_CIN * 8;
-    static_assert(NP == 2 || NP == 3, "two (bf16x3) or three (bf16x6) planes");
+    static_assert(NP >= 1 && NP <= 3, "one (bf16), two (bf16x3) or three (bf16x6) planes");
     static_assert(CK % 16 == 0, "bf16 k-steps of 16 channels");
     static_assert(WM * WN == 4 && MT % WM == 0 && NTILES % WN == 0, "4-wave tiling");
     static_assert(NTAPS % TPS == 0, "taps per stage");
@@ -276,8 +279,10 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][1][m], bf[sl][1][n], acc[m][n], 0, 0, 0);
                             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][2][m], bf[sl][0][n], acc[m][n], 0, 0, 0);
                         }
-                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][0][m], bf[sl][1][n], acc[m][n], 0, 0, 0);
-                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][1][m], bf[sl][0][n], acc[m][n], 0, 0, 0);
+                        if constexpr (NP >= 2) {
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][0][m], bf[sl][1][n], acc[m][n], 0, 0, 0);
+                            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][1][m], bf[sl][0][n], acc[m][n], 0, 0, 0);
+                        }
                         acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[sl][0][m], bf[sl][0][n], acc[m][n], 0, 0, 0);
                     }
                 __builtin_amdgcn_sched_barrier(0);
@@ -378,13 +383,16 @@ static ConvTile bf3_tile_of() {
     X(104, 3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 2)       \
     X(111, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 3)       \
     X(112, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 3)        \
-    X(113, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3)
+    X(113, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3)        \
+    X(121, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 1)        \
+    X(122, 3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 1)
 
 bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, ConvTile* out) {
-    if (kh != 3 || stride != 1 || cin % 32 != 0 || ntot % 64 != 0 || (planes != 2 && planes != 3)) return false;
+    if (kh != 3 || stride != 1 || cin % 32 != 0 || ntot % 64 != 0 || planes < 1 || planes > 3) return false;
     // measured (tools/conv_bench, residual conv of rst-960-120-128-17): bf16x3 NT64 4x16 42.8 us at B=1;
     // bf16x6 NT64 8x16 62.8 us at B=1 / 437 us at B=8 (exact-f32 MFMA kernel: 92.5 / 611 us)
-    const int want = planes == 2 ? 102 : 113;
+    // plain bf16 (one plane, one MFMA per product block): the larger 8x16 x 128 tile when N allows
+    const int want = planes == 2 ? 102 : (planes == 3 ? 113 : (ntot % 128 == 0 ? 122 : 121));
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)                  \
     if (ID == want) {                                                       \
         *out = bf3_tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>();   \

@@ -84,7 +84,8 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
     if (shape->h % 16 != 0 || shape->w % 16 != 0 || shape->h <= 0 || shape->w <= 0 || shape->max_batch <= 0)
         return set_error(RST_ERR_INVALID, "rst_loss_create: image H and W must be positive multiples of 16 "
                                           "(four 2x2 max-pools)");
-    if (shape->precision < RST_PRECISION_FP32 || shape->precision > RST_PRECISION_BF16X6)
+    if (shape->precision < RST_PRECISION_FP32 || shape->precision > RST_PRECISION_BF16 ||
+        shape->precision == RST_PRECISION_FP32_WINOGRAD)
         return set_error(RST_ERR_INVALID, "rst_loss_create: unknown precision mode");
     if (num_weights != rst_loss_num_weights())
         return set_error(RST_ERR_INVALID, "rst_loss_create: expected " + std::to_string(rst_loss_num_weights()) +
@@ -113,7 +114,7 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
         }
         const float* bias = wp + kc;
         wp += kc + c.cout;
-        const int planes = shape->precision == RST_PRECISION_BF16X3 ? 2 : (shape->precision == RST_PRECISION_BF16X6 ? 3 : 0);
+        const int planes = bf16_planes(shape->precision);
         const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cin, c.cout, planes, &c.tile);
         if (!bf3 && !conv_select(3, 1, cin, c.cout, &c.tile)) {
             delete h;

@@ -266,7 +266,7 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
             for (int n = 0; n < ntot; ++n) bias_n.push_back(bias[n % s.cout]);
         }
         const int gs = s.keras_kind == 0 ? s.stride : 1;
-        const int planes = precision == RST_PRECISION_BF16X3 ? 2 : (precision == RST_PRECISION_BF16X6 ? 3 : 0);
+        const int planes = bf16_planes(precision);
         const bool bf3 = planes > 0 && conv_bf3_select(kh, gs, s.cin, ntot, planes, &e.tile);
         if (!bf3 && !conv_select(kh, gs, s.cin, ntot, &e.tile))
             return fail(RST_ERR_UNSUPPORTED, "no conv tile configuration for layer " + s.name);
@@ -309,7 +309,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     if (shape == nullptr || out == nullptr || weights_host == nullptr)
         return fail(RST_ERR_INVALID, "rst_create: null argument");
     if (precision != RST_PRECISION_FP32 && precision != RST_PRECISION_BF16X3 && precision != RST_PRECISION_BF16X6 &&
-        precision != RST_PRECISION_FP32_WINOGRAD)
+        precision != RST_PRECISION_FP32_WINOGRAD && precision != RST_PRECISION_BF16)
         return fail(RST_ERR_INVALID, "rst_create_ex: unknown precision mode");
     *out = nullptr;
     if (shape->num_styles > 2)

@@ -573,7 +573,7 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
             vo += (size_t)9 * cin * cout + cout;
             ConvBwd& vb = t->vgg[i];
             const int lp = loss->precision;
-            const int planes = lp == RST_PRECISION_BF16X3 ? 2 : (lp == RST_PRECISION_BF16X6 ? 3 : 0);
+            const int planes = bf16_planes(lp);
             const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cout, cin, planes, &vb.tile);
             if (!bf3 && !conv_select(3, 1, cout, cin, &vb.tile))
                 return fail_delete(t, set_error(RST_ERR_UNSUPPORTED, "no tile for VGG dgrad " + std::to_string(i)));

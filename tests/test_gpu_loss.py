@@ -33,8 +33,15 @@ def test_gram_golden_fixture():
         assert np.abs(g - d[f'gram_f{c}']).max() < 1e-5
 
 
-@pytest.mark.parametrize("precision,rtol", [("fp32", 1e-4), ("bf16x6", 1e-4), ("bf16x3", 1e-3)])
-def test_style_loss_matches_oracle(precision, rtol):
+# bf16: plain bf16 operands — checked against the float64 oracle with the same bf16 rounding of every
+# conv input and kernel (Cin % 32 == 0 layers), so the bound stays tight
+@pytest.mark.parametrize("precision,rtol,ftol", [("fp32", 1e-4, 1e-5), ("bf16x6", 1e-4, 1e-5), ("bf16x3", 1e-3, 1e-4),
+                                                ("bf16", 2e-2, 1e-2)])
+def test_style_loss_matches_oracle(precision, rtol, ftol):
+    """Loss terms and VGG features vs the float64 oracle. The Gram/feature differences of the loss
+    amplify feature errors ~100x; for bf16 the remaining feature mismatch against the bf16-simulating
+    oracle comes from bf16 rounding decisions the fp32 and float64 activations take differently
+    (block1_conv2 matches to 1e-6, block5_conv3 to 5.7e-3: tools/bf16_diag.py)."""
     _need_gpu()
     from oracle import numpy_ref as R
     from realtime_style_transfer_amd.styleLoss import (StyleLossModelVGG, init_vgg16_weights, make_style_loss_function,
@@ -48,17 +55,18 @@ def test_style_loss_matches_oracle(precision, rtol):
     style = rng.random((B, 1, H, W, 3)).astype(np.float32)
     out = compute_loss(torch.from_numpy(pred).cuda(), {'content': torch.from_numpy(content).cuda(),
                                                        'style': torch.from_numpy(style).cuda()})
-    ref = R.style_loss_terms(pred, content, style, vgg_weight_dict(ws))
+    rnd = R.bf16_round if precision == "bf16" else None
+    ref = R.style_loss_terms(pred, content, style, vgg_weight_dict(ws), operand_round=rnd)
     for k in ('loss', 'feature_loss', 'style_loss', 'total_variation_loss'):
         got = out[k].cpu().numpy().astype(np.float64)
         rel = np.abs(got - ref[k]) / np.maximum(np.abs(ref[k]), 1e-12)
         assert rel.max() < rtol, (k, got, ref[k])
     # the prediction's VGG features themselves (block1_conv2 and block5_conv3)
-    feats = R.vgg16_features(pred, vgg_weight_dict(ws))
+    feats = R.vgg16_features(pred, vgg_weight_dict(ws), rnd)
     for name in ('block1_conv2', 'block5_conv3'):
         got = model.feature(name, B).cpu().numpy()
         rel = np.abs(got - feats[name]).max() / np.abs(feats[name]).max()
-        assert rel < rtol / 10, (name, rel)
+        assert rel < ftol, (name, rel)
     with pytest.raises(NotImplementedError):
         make_style_loss_function(model, (H, W, 3), 1)
     with pytest.raises(ValueError):

@@ -73,8 +73,14 @@ def _pool_route(tr, B):
 # precision: arithmetic of the VGG16 3x3 convs (forward and input gradient) — BASELINE config 4 trains
 # in bf16; "bf16x6" is the exact 3-piece bf16 split (fp32-level products: same errors as fp32, L2 <= 1e-4),
 # "bf16x3" the 2-piece split (16-bit operands: median gradient L2 error 1.5e-3, worst 2.3e-2 measured)
+# "bf16": plain bf16 operands of the VGG16 convs, checked against the float64 oracle run with the same
+# bf16 rounding of every VGG conv's input/kernel (forward) and output gradient/kernel (input gradient).
+# That simulation matches block1_conv2 to 1e-6; beyond it the fp32-vs-float64 activation differences
+# flip bf16 rounding decisions and the deviation grows layer by layer (tools/bf16_diag.py: 1.5e-4 after
+# the first pool, 5.7e-3 at block5_conv3), so the transfer-net gradients carry a few % of bf16 noise
+# (worst layer 9.5 % L2 measured)
 @pytest.mark.parametrize("name,precision,gtol", [("A", "fp32", 2e-3), ("B", "fp32", 2e-3), ("A", "bf16x6", 2e-3),
-                                                  ("A", "bf16x3", 5e-2)])
+                                                  ("A", "bf16x3", 5e-2), ("A", "bf16", 0.15)])
 def test_training_step_matches_oracle(name, precision, gtol):
     _need_gpu()
     from oracle import torch_train as T
@@ -85,7 +91,8 @@ def test_training_step_matches_oracle(name, precision, gtol):
     c, s, gc, gs = _cuda(content, sp, gtc, gts)
     pred, losses, grad, gsp = tr.compute_gradients(c, s, gc, gs)
     torch.cuda.synchronize()
-    ref = T.training_step(w, vgg, content, sp, gtc, gts, pool_route=_pool_route(tr, B), **cfg)
+    ref = T.training_step(w, vgg, content, sp, gtc, gts, pool_route=_pool_route(tr, B), vgg_bf16=precision == "bf16",
+                          **cfg)
     report = {}
     perr = float(np.abs(pred.cpu().numpy() - ref['prediction']).max())
     report['prediction_max_abs'] = perr
@@ -151,12 +158,12 @@ def test_training_step_matches_oracle(name, precision, gtol):
         assert np.abs(a - w_after_fwd[i]).max() <= 1e-3 / np.sqrt(0.1) * 1.001 + 1e-6, i
         if np.abs(g).max() <= 1e-9 * gmax:
             continue   # no gradient / round-off-only gradient (bias before an instance norm): sign is arbitrary
-        strong = np.abs(g) > 5e-2 * np.abs(g).max()
+        strong = np.abs(g) > (0.5 if precision == "bf16" else 5e-2) * np.abs(g).max()   # no sign flips there
         assert np.abs(a - r)[strong].max() <= 1e-6 + 1e-6 * np.abs(r).max(), (i, np.abs(a - r)[strong].max())
         # ms = (1 - rho) g^2: its relative error is about twice the gradient's
         assert np.linalg.norm(slots[i] - ref['ms'][i]) <= max(5e-3, 2.5 * gtol) * np.linalg.norm(ref['ms'][i]), i
     assert perr < 2e-5, perr
-    assert lrel < (1e-4 if precision != "bf16x3" else 1e-3), lrel
+    assert lrel < {"bf16x3": 1e-3, "bf16": 1e-3}.get(precision, 1e-4), lrel
     assert gerr < gtol, gerr
 
 

@@ -169,9 +169,10 @@ def test_two_style_blending_matches_golden():
         model({'content': inputs['content'], 'style_params': inputs['style_params']})   # weights missing
 
 
-@pytest.mark.parametrize("precision,tol", [("bf16x3", 2e-4), ("bf16x6", 2e-5)])
+@pytest.mark.parametrize("precision,tol", [("bf16x3", 2e-4), ("bf16x6", 2e-5), ("bf16", 2e-4)])
 def test_split_bf16_precision_modes(precision, tol):
-    """RST_PRECISION_BF16X3 / BF16X6: residual convs on split-bf16 MFMA, vs the float64 oracle."""
+    """RST_PRECISION_BF16X3 / BF16X6 / BF16: residual convs on the bf16 MFMA pipe, vs the float64 oracle
+    (for plain bf16: the oracle with the same bf16 rounding of the residual convs' operands)."""
     _need_gpu()
     from oracle import numpy_ref as R
     from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
@@ -181,9 +182,10 @@ def test_split_bf16_precision_modes(precision, tol):
     w = init_weights(plan, seed=2)
     sp = synthetic_style_params(2, 1, plan.num_style_params, plan, seed=1)
     x = np.random.default_rng(0).random((2,) + ins).astype(np.float32)
-    ref = R.transfer_forward(x, sp, w, ins, outs, br, bf)
+    ref = R.transfer_forward(x, sp, w, ins, outs, br, bf,
+                             operand_round=R.bf16_round if precision == "bf16" else None)
     m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision=precision)
-    kid = 102 if precision == "bf16x3" else 113
+    kid = {"bf16x3": 102, "bf16x6": 113, "bf16": 122}[precision]
     assert [m.layer_kernel_id(i) for i in range(m.num_layers())][3:13] == [kid] * 10   # residual convs
     inp = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}
     err = float(np.abs(m(inp).cpu().numpy() - ref).max())
