@@ -37,6 +37,34 @@
 #include "net.h"
 #include "train.h"
 
+// Geometry of a layer's weight-gradient GEMM (shared by the workspace sizing at create time and the
+// launch, so the split count and slab size always agree).
+static rst::WgradArgs wgrad_geometry(const rst::LayerSpec& s, const rst::LayerExec& e, int B) {
+    rst::WgradArgs w{};
+    w.batch = B;
+    w.XH = s.H;
+    w.XW = s.W;
+    w.C1 = s.cin;
+    w.DH = s.Ho;
+    w.DW = s.Wo;
+    w.C2 = s.cout;
+    w.kh = w.kw = s.k;
+    w.stride = s.stride;
+    if (s.keras_kind == 0) {
+        w.Qh = s.Ho;
+        w.Qw = s.Wo;
+        w.pad_t = e.pad_t;
+        w.pad_l = e.pad_l;
+        w.transposed = 0;
+    } else {
+        w.Qh = s.H;
+        w.Qw = s.W;
+        w.pad_t = w.pad_l = std::max(s.k - s.stride, 0) / 2;
+        w.transposed = 1;
+    }
+    return w;
+}
+
 using namespace rst;
 
 namespace {
@@ -337,32 +365,11 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
         nb.conv_relu = s.conv_relu ? 1 : 0;
         nb.dconv_bias = grad + T.boff;
         RST_HIP_TRY(norm_bwd_launch(nb, st));
-        WgradArgs w{};
+        WgradArgs w = wgrad_geometry(s, e, B);
         w.X = li == 0 ? content : T.d_x;
         w.D = t->d_dz;
         w.slab = t->d_slab;
         w.dW = grad + T.woff;
-        w.batch = B;
-        w.XH = s.H;
-        w.XW = s.W;
-        w.C1 = s.cin;
-        w.DH = s.Ho;
-        w.DW = s.Wo;
-        w.C2 = s.cout;
-        w.kh = w.kw = s.k;
-        w.stride = s.stride;
-        if (s.keras_kind == 0) {
-            w.Qh = s.Ho;
-            w.Qw = s.Wo;
-            w.pad_t = e.pad_t;
-            w.pad_l = e.pad_l;
-            w.transposed = 0;
-        } else {
-            w.Qh = s.H;
-            w.Qw = s.W;
-            w.pad_t = w.pad_l = std::max(s.k - s.stride, 0) / 2;
-            w.transposed = 1;
-        }
         w.nsplit = wgrad_choose_splits(w);
         RST_HIP_TRY(wgrad_launch(w, st));
         if (!T.has_dgrad) continue;
@@ -513,18 +520,8 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
             max_ntot = std::max(max_ntot, T.dg.ntot);
             max_out = std::max(max_out, (size_t)B * s.H * s.W * s.cin);
         }
-        WgradArgs w{};
-        w.batch = B;
-        w.C1 = s.cin;
-        w.C2 = s.cout;
-        w.kh = w.kw = s.k;
-        w.transposed = s.keras_kind;
-        w.XH = s.H;
-        w.XW = s.W;
-        w.DH = s.Ho;
-        w.DW = s.Wo;
-        w.Qh = s.keras_kind == 0 ? s.Ho : s.H;
-        w.Qw = s.keras_kind == 0 ? s.Wo : s.W;
+        // same geometry as the launch (the split count and slab size depend on every field)
+        WgradArgs w = wgrad_geometry(s, T.e, B);
         w.nsplit = wgrad_choose_splits(w);
         slab = std::max(slab, wgrad_slab_bytes(w));
     }

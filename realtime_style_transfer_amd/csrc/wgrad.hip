@@ -103,9 +103,11 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
             const long q = q0 + pa0 + k * PSA;
             sT v = sT(0.f);
             if (rvalid && q < q_end) {
-                const int b = (int)(q / qhw);
-                const int rem = (int)(q - (long)b * qhw);
-                const int qy = rem / a.Qw, qx = rem - (rem / a.Qw) * a.Qw;
+                // 32-bit index math (B*Qh*Qw < 2^31; a 64-bit division per load dominated this loop)
+                const int qi = (int)q, qhw_i = (int)qhw;
+                const int b = qi / qhw_i;
+                const int rem = qi - b * qhw_i;
+                const int qy = rem / a.Qw, qx = rem - qy * a.Qw;
                 const int sy = qy * a.stride + dy, sx = qx * a.stride + dx;
                 if (sy >= 0 && sy < g.SH && sx >= 0 && sx < g.SW)
                     v = *reinterpret_cast<const sT*>(g.S + (((size_t)b * g.SH + sy) * g.SW + sx) * g.Cs + ch);
@@ -178,6 +180,113 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
             }
 }
 
+// ---- contract_start (9x9 s1 SAME, cin <= 17 -> 32): LDS-patch weight gradient --------------------------
+// The generic kernel above reads its S operand (the shifted input, R = 81 taps x 17 channels = 1377
+// rows) straight from global memory with 4-byte loads (17 channels: no 16-B vectors): every input
+// element is fetched 81 times, 6.4 ms per B=4 step at 480x960. Here a workgroup walks over 8 x 16
+// output-pixel tiles; per tile the 16 x 24 x 17 input patch (planar [ci][row][col] in LDS) and the
+// 128 x 32 output-gradient tile ([co][pixel]) are staged once, and
+//   dW^T[co][(tap, ci)] += dZ^T[co][pixel] X[pixel + tap][ci]
+// runs as MFMA with M = the 32 output channels (A operand = dZ, one ds_read_b128 per 4 k-steps) and
+// N = the 1377 (tap, ci) columns (44 column tiles, 11 per wave; each lane's column decode is done
+// once per kernel). K = pixels; k-step s pairs pixel s (lane half 0) with s + 64 (lane half 1), so a
+// lane's 4 consecutive k-steps are 4 consecutive pixels of one tile row. Each workgroup writes one
+// partial [1408][32] slab; wgrad_reduce_kernel sums the slabs in a fixed order.
+namespace w9 {
+constexpr int TH = 8, TW = 16, NPX = TH * TW;          // output pixels per tile
+constexpr int PR = TH + 8, PC = TW + 8, PRS = 25;      // patch rows / cols / row stride (floats)
+constexpr int PL = PR * PRS;                           // plane stride (400 floats)
+constexpr int CMAX = 17, NCOL = 81 * CMAX, NCOLP = 1408, NT = NCOLP / 32, NTW = NT / 4;   // 44 tiles, 11 per wave
+constexpr int DZS = NPX + 4;                           // dZ^T row stride (floats)
+constexpr int ZERO = CMAX * PL;                        // a zero word after the planes (padding columns)
+constexpr int LDS_FL = CMAX * PL + 8 + 32 * DZS;
+}  // namespace w9
+
+__global__ __launch_bounds__(256, 2) void wgrad9_kernel(WgradArgs a) {
+    using namespace w9;
+    __shared__ __attribute__((aligned(16))) float lds[LDS_FL];
+    float* const patch = lds;                    // [ci][PR][PRS] + zero word
+    float* const dzt = lds + CMAX * PL + 8;      // [co][DZS]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    constexpr int C = CMAX;   // wgrad9_applies: cin == 17 (the slab rows are (tap, ci) with stride 17)
+    const int tiles_x = (a.Qw + TW - 1) / TW, tiles_y = (a.Qh + TH - 1) / TH;
+    const int ntiles = a.batch * tiles_x * tiles_y;
+
+    // per-lane column decode of this wave's 11 column tiles: LDS offset of (tap, ci) at pixel (0, 0)
+    int coff[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = (wave + 4 * j) * 32 + li;   // wave w owns column tiles w, w+4, ...
+        if (n < NCOL) {
+            const int tap = n / CMAX, ci = n % CMAX;
+            coff[j] = ci * PL + (tap / 9) * PRS + tap % 9;
+        } else {
+            coff[j] = -1;                         // padding column / channel >= cin
+        }
+    }
+    floatx16 acc[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    if (tid < 8) patch[ZERO + tid] = 0.f;
+
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int b = t / (tiles_x * tiles_y), rem = t % (tiles_x * tiles_y);
+        const int y0 = (rem / tiles_x) * TH, x0 = (rem % tiles_x) * TW;
+        __syncthreads();   // previous tile's operands consumed
+        // input patch rows y0-4 .. y0+11, cols x0-4 .. x0+19 (SAME pad 4), NHWC -> planar
+        for (int i = tid; i < PR * PC * C; i += 256) {
+            const int c = i % C, px = i / C;
+            const int r = px / PC, q = px % PC;
+            const int gy = y0 - a.pad_t + r, gx = x0 - a.pad_l + q;
+            float v = 0.f;
+            if (gy >= 0 && gy < a.XH && gx >= 0 && gx < a.XW) v = a.X[(((size_t)b * a.XH + gy) * a.XW + gx) * C + c];
+            patch[c * PL + r * PRS + q] = v;
+        }
+        // output-gradient tile, transposed to [co][pixel]
+        for (int i = tid; i < NPX * 32; i += 256) {
+            const int co = i & 31, p = i >> 5;
+            const int oy = y0 + p / TW, ox = x0 + p % TW;
+            float v = 0.f;
+            if (oy < a.Qh && ox < a.Qw) v = a.D[(((size_t)b * a.DH + oy) * a.DW + ox) * 32 + co];
+            dzt[co * DZS + p] = v;
+        }
+        __syncthreads();
+        // 16 groups of 4 k-steps: pixels 4g..4g+3 (lane half 0) / 64+4g.. (lane half 1)
+#pragma unroll 2
+        for (int g = 0; g < 16; ++g) {
+            const int p0 = 4 * g + 64 * lh;
+            const f32x4 a4 = *reinterpret_cast<const f32x4*>(dzt + li * DZS + p0);
+            const int pixoff = (p0 / TW) * PRS + p0 % TW;
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                const float* src = patch + (coff[j] >= 0 ? coff[j] + pixoff : ZERO);
+                const int st = coff[j] >= 0 ? 1 : 0;
+                const float b0 = src[0], b1 = src[st], b2 = src[2 * st], b3 = src[3 * st];
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b0, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b1, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b2, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b3, acc[j], 0, 0, 0);
+            }
+        }
+    }
+    // partial slab [blockIdx][column n][co]: accumulator r of lane (li, lh) is co = (r&3) + 8(r>>2) + 4lh, n = tile*32 + li
+    float* slab = a.slab + (size_t)blockIdx.x * NCOLP * 32;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = (wave + 4 * j) * 32 + li;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) slab[(size_t)n * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh] = acc[j][r];
+    }
+}
+
+static bool wgrad9_applies(const WgradArgs& a) {
+    return !a.transposed && a.kh == 9 && a.kw == 9 && a.stride == 1 && a.C1 == w9::CMAX && a.C2 == 32 &&
+           a.pad_t == 4 && a.pad_l == 4 && a.Qh == a.XH && a.Qw == a.XW;
+}
+
 // dW[r][c] = sum over splits (fixed order)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a, int Rp, int Cp) {
     const WgradGeom g = wgrad_geom(a);
@@ -208,7 +317,10 @@ void wgrad_dims(const WgradArgs& a, int& R, int& Cu, int& Cs) {
 }
 }  // namespace
 
+constexpr int W9_BLOCKS = 512;   // two workgroups per CU, each a persistent walk over the pixel tiles
+
 int wgrad_choose_splits(const WgradArgs& a) {
+    if (wgrad9_applies(a)) return W9_BLOCKS;
     int R, Cu, Cs;
     wgrad_dims(a, R, Cu, Cs);
     const WTile t = wgrad_tile(a);
@@ -221,6 +333,7 @@ int wgrad_choose_splits(const WgradArgs& a) {
 }
 
 size_t wgrad_slab_bytes(const WgradArgs& a) {
+    if (wgrad9_applies(a)) return (size_t)a.nsplit * w9::NCOLP * 32 * sizeof(float);
     int R, Cu, Cs;
     wgrad_dims(a, R, Cu, Cs);
     const WTile t = wgrad_tile(a);
@@ -231,6 +344,15 @@ size_t wgrad_slab_bytes(const WgradArgs& a) {
 hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
     int R, Cu, Cs;
     wgrad_dims(a, R, Cu, Cs);
+    if (wgrad9_applies(a)) {
+        if (a.nsplit < 1) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(wgrad9_kernel, dim3((unsigned)a.nsplit), dim3(256), 0, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const size_t n = (size_t)R * Cu;
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, w9::NCOLP, 32);
+        return hipGetLastError();
+    }
     if (Cu % 4 != 0) return hipErrorInvalidValue;
     const WTile t = wgrad_tile(a);
     const long total = (long)a.batch * a.Qh * a.Qw;

@@ -19,13 +19,14 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--spec", default="rst-960-120-128-17")
+    ap.add_argument("--precision", default="bf16", help="VGG16 conv arithmetic (bench.py's training headline: bf16)")
     a = ap.parse_args()
     cfg = ShapeConfig.from_spec(a.spec)
     ins, outs = cfg.input_shape['content'], cfg.output_shape
     plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
     dev = torch.device("cuda:0")
     B = a.batch
-    lm = StyleLossModelVGG(outs, max_batch=B, device=dev)
+    lm = StyleLossModelVGG(outs, max_batch=B, device=dev, precision=a.precision)
     tr = StyleTransferTrainingModel(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, loss_model=lm,
                                     weights=init_weights(plan, seed=2), max_batch=B, device=dev)
     rng = np.random.default_rng(0)
