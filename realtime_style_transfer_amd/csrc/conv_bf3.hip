@@ -56,8 +56,8 @@ __device__ __forceinline__ void sfor(F&& f) {
 }
 }  // namespace
 
-#define RST_BP int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS, int NP
-#define RST_BA KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP
+#define RST_BP int KH, int KW, int S, int CK, int NT, int TH, int TW, int WM, int WN, int TPS, int NP, int PF
+#define RST_BA KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF
 
 template <RST_BP>
 struct Bf3Cfg {
@@ -174,28 +174,55 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
-    // synchronous staging of one Cin chunk: fp32 load -> prologue transform -> split into the planes
-    auto stage_halo = [&](int chunk) __attribute__((always_inline)) {
-        for (int it = tid; it < HP * HQ; it += 256) {
-            const int hp = it / HQ, q = it - (it / HQ) * HQ;
-            const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
-            const int iy = iy0 + hy, ix = ix0 + hx;
-            const int c = chunk * CK + q * 4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c < Cin) {
+    // Staging of one Cin chunk, in two halves so the global loads of chunk c+1 are issued at the start
+    // of chunk c's MFMA stages and land in registers while they run: load_halo (fp32 input [+ ReLU-mask
+    // / residual source]) and store_halo (prologue transform -> split into the planes -> LDS).
+    constexpr int HITEMS = HP * HQ;
+    constexpr int NPF = (HITEMS + 255) / 256;
+    const bool need_r = pro == PRO_MASK || pro == PRO_AFF_RES;
+    f32x4 pv[NPF], pr[NPF];
+    auto halo_item = [&](int it, int chunk, int& hp, int& q, int& iy, int& ix, int& c) __attribute__((always_inline)) {
+        hp = it / HQ;
+        q = it - hp * HQ;
+        const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
+        iy = iy0 + hy;
+        ix = ix0 + hx;
+        c = chunk * CK + q * 4;
+        return iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c < Cin;
+    };
+    auto load_halo = [&](int chunk) __attribute__((always_inline)) {
+        sfor<0, NPF>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int it = k * 256 + tid;
+            int hp, q, iy, ix, c;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f}, r = {0.f, 0.f, 0.f, 0.f};
+            if ((HITEMS % 256 == 0 || it < HITEMS) && halo_item(it, chunk, hp, q, iy, ix, c)) {
                 const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
-                v = *reinterpret_cast<const float4*>(a.in + gi);
+                v = *reinterpret_cast<const f32x4*>(a.in + gi);
+                if (need_r) r = *reinterpret_cast<const f32x4*>(a.res + gi);
+            }
+            pv[k] = v;
+            pr[k] = r;
+        });
+    };
+    auto store_halo = [&](int chunk) __attribute__((always_inline)) {
+        sfor<0, NPF>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int it = k * 256 + tid;
+            if (HITEMS % 256 != 0 && it >= HITEMS) return;
+            int hp, q, iy, ix, c;
+            float4 v = make_float4(pv[k][0], pv[k][1], pv[k][2], pv[k][3]);
+            if (halo_item(it, chunk, hp, q, iy, ix, c) && pro != PRO_NONE) {
+                const float4 r = make_float4(pr[k][0], pr[k][1], pr[k][2], pr[k][3]);
                 if (pro == PRO_MASK) {   // ReLU backward: gradient masked by the forward output
-                    const float4 r = *reinterpret_cast<const float4*>(a.res + gi);
                     v.x = r.x > 0.f ? v.x : 0.f;
                     v.y = r.y > 0.f ? v.y : 0.f;
                     v.z = r.z > 0.f ? v.z : 0.f;
                     v.w = r.w > 0.f ? v.w : 0.f;
-                } else if (pro != PRO_NONE) {
-                    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (pro == PRO_AFF_RES) r = *reinterpret_cast<const float4*>(a.res + gi);
+                } else {
+                    const size_t pix = img_base + (size_t)iy * a.W + ix;
                     if (blend) {
-                        const float wpx = a.pro_w[img_base + (size_t)iy * a.W + ix];
+                        const float wpx = a.pro_w[pix];
                         v.x = bf3_pro_blend(pro, v.x, pab[c + 0], pab1[c + 0], wpx, r.x);
                         v.y = bf3_pro_blend(pro, v.y, pab[c + 1], pab1[c + 1], wpx, r.y);
                         v.z = bf3_pro_blend(pro, v.z, pab[c + 2], pab1[c + 2], wpx, r.z);
@@ -207,7 +234,7 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                         v.w = bf3_pro(pro, v.w, pab[c + 3], r.w);
                     }
                     if (do_mat && iy >= y0 * S && iy < (y0 + TH) * S && ix >= x0 * S && ix < (x0 + TW) * S)
-                        *reinterpret_cast<float4*>(a.mat + gi) = v;
+                        *reinterpret_cast<float4*>(a.mat + pix * Cin + c) = v;
                 }
             }
             unsigned short px[4][3];
@@ -220,7 +247,7 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                 const ushort4v p4 = {px[0][pl], px[1][pl], px[2][pl], px[3][pl]};
                 *reinterpret_cast<ushort4v*>(halo + pl * C::HALO + hp * CSB + q * 4) = p4;
             }
-        }
+        });
     };
 
     if (pro != PRO_NONE && a.pro_ab != nullptr) {
@@ -232,7 +259,8 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
     {
         Bf3WeightRegs<C::WCOPY> w0;
         w0.load(wsrc, tid);
-        stage_halo(0);
+        load_halo(0);
+        store_halo(0);
         w0.store(wts0, tid);
     }
     __syncthreads();
@@ -244,6 +272,7 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
         const unsigned short* wts = wts0 + (s & 1) * C::WSTAGE;
         Bf3WeightRegs<C::WCOPY> wnext;
         wnext.load(wsrc + (size_t)s_next * C::WSTAGE, tid);
+        if (PF && g == 0 && chunk + 1 < a.nchunks) load_halo(chunk + 1);
         {
             constexpr int U = TPS * KS;
             short8 af[2][NP][MW], bf[2][NP][NW];
@@ -291,7 +320,8 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
         wnext.store(wts0 + ((s + 1) & 1) * C::WSTAGE, tid);
         __syncthreads();
         if (g == C::NGROUPS - 1 && chunk + 1 < a.nchunks) {
-            stage_halo(chunk + 1);
+            if (!PF) load_halo(chunk + 1);
+            store_halo(chunk + 1);
             __syncthreads();
         }
     }
@@ -376,28 +406,38 @@ static ConvTile bf3_tile_of() {
     return t;
 }
 
-// (ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)
-#define RST_BF3_CONFIGS(X)                            \
-    X(101, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 2)       \
-    X(102, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 2)        \
-    X(104, 3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 2)       \
-    X(111, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 3)       \
-    X(112, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 3)        \
-    X(113, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3)        \
-    X(121, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 1)        \
-    X(122, 3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 1)
+// (ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF)
+#define RST_BF3_CONFIGS(X)                               \
+    X(101, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 2, 0)       \
+    X(102, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 2, 0)        \
+    X(104, 3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 2, 0)       \
+    X(111, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 3, 0)       \
+    X(112, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 3, 0)        \
+    X(113, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3, 0)        \
+    X(132, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 1)       \
+    X(134, 3, 3, 1, 32, 64, 8, 16, 4, 1, 3, 1, 0)
 
-bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, ConvTile* out) {
+bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long long pixels, ConvTile* out) {
     if (kh != 3 || stride != 1 || cin % 32 != 0 || ntot % 64 != 0 || planes < 1 || planes > 3) return false;
     // measured (tools/conv_bench, residual conv of rst-960-120-128-17): bf16x3 NT64 4x16 42.8 us at B=1;
-    // bf16x6 NT64 8x16 62.8 us at B=1 / 437 us at B=8 (exact-f32 MFMA kernel: 92.5 / 611 us)
-    // plain bf16 (one plane, one MFMA per product block): the larger 8x16 x 128 tile when N allows
-    const int want = planes == 2 ? 102 : (planes == 3 ? 113 : (ntot % 128 == 0 ? 122 : 121));
-#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)                  \
-    if (ID == want) {                                                       \
-        *out = bf3_tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>();   \
-        out->id = ID;                                                       \
-        return true;                                                        \
+    // bf16x6 NT64 8x16 62.8 us at B=1 / 437 us at B=8 (exact-f32 MFMA kernel: 92.5 / 611 us).
+    // Plain bf16 (one plane, one MFMA per product block; tools/conv_bench vgg, VGG16 at 480x960, B=4):
+    // three taps per stage (one barrier + weight-stage swap per 24 MFMAs instead of 8) on an 8x16 x 64
+    // tile with the four waves stacked along M: block1_conv2 422 -> 312 us, block2_conv2 335 -> 231,
+    // block3_conv2 254 -> 188, block5_conv2 101 -> 57 (previous 4x16 x 64 / 8x16 x 128 one-tap tiles).
+    // Register prefetch of the next Cin chunk's halo (PF) only pays on the 512-channel layers with a
+    // 128-wide tile while that still fills the chip (block4_conv2 188 -> 174 us); elsewhere its
+    // registers cost more occupancy than it hides (bf16x3 residual: 43.8 -> 57.6 us).
+    int want;
+    if (planes == 2) want = 102;
+    else if (planes == 3) want = 113;
+    else if (ntot % 128 == 0 && cin >= 512 && (pixels / 128) * (ntot / 128) >= 1024) want = 132;
+    else want = 134;
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF)                  \
+    if (ID == want) {                                                           \
+        *out = bf3_tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>();   \
+        out->id = ID;                                                           \
+        return true;                                                            \
     }
     RST_BF3_CONFIGS(X)
 #undef X
@@ -406,13 +446,13 @@ bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, ConvTile
 
 hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
     switch (t.id) {
-#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)                                          \
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF)                                      \
     case ID: {                                                                                   \
-        using C = Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>;                            \
+        using C = Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>;                            \
         if ((a.cin & 3) != 0) return hipErrorInvalidValue;                                       \
         if (a.pro_w != nullptr && a.cin > C::MAX_CIN) return hipErrorInvalidValue;               \
         const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x * a.n_blocks);          \
-        hipLaunchKernelGGL((conv_bf3_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>), dim3(grid), \
+        hipLaunchKernelGGL((conv_bf3_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>), dim3(grid), \
                            dim3(256), C::LDS_BYTES, st, a);                                      \
         return hipGetLastError();                                                                \
     }
@@ -425,11 +465,11 @@ hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st)
 
 hipError_t conv_bf3_prepare(const ConvTile& t) {
     switch (t.id) {
-#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP)                                                   \
-    case ID:                                                                                              \
-        return hipFuncSetAttribute((const void*)conv_bf3_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>, \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,                             \
-                                   (int)Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP>::LDS_BYTES);
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF)                                                   \
+    case ID:                                                                                                  \
+        return hipFuncSetAttribute((const void*)conv_bf3_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>, \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,                                 \
+                                   (int)Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>::LDS_BYTES);
         RST_BF3_CONFIGS(X)
 #undef X
         default:

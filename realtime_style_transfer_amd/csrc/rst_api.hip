@@ -267,7 +267,7 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         }
         const int gs = s.keras_kind == 0 ? s.stride : 1;
         const int planes = bf16_planes(precision);
-        const bool bf3 = planes > 0 && conv_bf3_select(kh, gs, s.cin, ntot, planes, &e.tile);
+        const bool bf3 = planes > 0 && conv_bf3_select(kh, gs, s.cin, ntot, planes, (long long)e.gHo * e.gWo, &e.tile);
         if (!bf3 && !conv_select(kh, gs, s.cin, ntot, &e.tile))
             return fail(RST_ERR_UNSUPPORTED, "no conv tile configuration for layer " + s.name);
         e.ntot = ntot;

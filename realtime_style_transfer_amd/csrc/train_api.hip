@@ -571,7 +571,7 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
             ConvBwd& vb = t->vgg[i];
             const int lp = loss->precision;
             const int planes = bf16_planes(lp);
-            const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cout, cin, planes, &vb.tile);
+            const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cout, cin, planes, (long long)B * c.H * c.W, &vb.tile);
             if (!bf3 && !conv_select(3, 1, cout, cin, &vb.tile))
                 return fail_delete(t, set_error(RST_ERR_UNSUPPORTED, "no tile for VGG dgrad " + std::to_string(i)));
             vb.tiles_y = (c.H + vb.tile.th - 1) / vb.tile.th;

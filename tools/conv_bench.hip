@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <vector>
 #include <functional>
+#include <string>
 #include "../realtime_style_transfer_amd/csrc/conv_mfma.hip"
 #include "../realtime_style_transfer_amd/csrc/conv_small.hip"
 #include "../realtime_style_transfer_amd/csrc/conv_bf3.hip"
@@ -69,8 +70,73 @@ struct Variant {
     }
 };
 
+// VGG16 3x3 layers of the training loss (480 x 960 input, B images), plain bf16 (NP = 1) tiles
+struct VggLayer { const char* name; int H, W, Cin, Cout; };
+static int run_vgg(int B) {
+    const VggLayer L[] = {{"b1c2", 480, 960, 64, 64},   {"b2c1", 240, 480, 64, 128}, {"b2c2", 240, 480, 128, 128},
+                          {"b3c2", 120, 240, 256, 256}, {"b4c2", 60, 120, 512, 512}, {"b5c2", 30, 60, 512, 512}};
+    const int iters = 10, rounds = 5;
+    size_t maxact = 0, maxw = 0;
+    for (const auto& l : L) {
+        maxact = std::max(maxact, (size_t)B * l.H * l.W * std::max(l.Cin, l.Cout));
+        maxw = std::max(maxw, (size_t)9 * l.Cin * l.Cout);
+    }
+    float* in = dev_rand(maxact, 0.f, 1.f, 11);
+    float* out; CK(hipMalloc(&out, maxact * 4));
+    float* w = dev_rand(maxw, -0.05f, 0.05f, 12);
+    float* bias = dev_rand(512, -0.1f, 0.1f, 13);
+    for (const auto& l : L) {
+        const double fl = 2.0 * l.H * l.W * 9.0 * l.Cin * l.Cout * B;
+        std::vector<std::function<void()>> launches;
+        std::vector<const char*> names;
+#define VV(CK_, NT, TH, TW, WM, WN, TPS, PF, NAME)                                                            \
+        if (l.Cout % NT == 0) {                                                                            \
+            using BC = Bf3Cfg<3, 3, 1, CK_, NT, TH, TW, WM, WN, TPS, 1, PF>;                                   \
+            ConvArgs a{};                                                                                  \
+            a.in = in; a.res = in; a.wpk = w; a.bias = bias; a.out = out;                                  \
+            a.batch = B; a.H = l.H; a.W = l.W; a.cin = l.Cin; a.Ho = l.H; a.Wo = l.W;                      \
+            a.ntot = l.Cout; a.cout = l.Cout; a.pad_t = 1; a.pad_l = 1;                                    \
+            a.tiles_y = (l.H + TH - 1) / TH; a.tiles_x = (l.W + TW - 1) / TW;                              \
+            a.n_blocks = l.Cout / NT; a.nchunks = (l.Cin + CK_ - 1) / CK_;                                 \
+            a.pro_mode = PRO_NONE; a.epi_mode = EPI_RELU_STATS;                                            \
+            const unsigned g = (unsigned)(B * a.tiles_y * a.tiles_x * a.n_blocks);                         \
+            CK(hipFuncSetAttribute((const void*)conv_bf3_kernel<3, 3, 1, CK_, NT, TH, TW, WM, WN, TPS, 1, PF>, \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)BC::LDS_BYTES));       \
+            launches.push_back([=] {                                                                       \
+                hipLaunchKernelGGL((conv_bf3_kernel<3, 3, 1, CK_, NT, TH, TW, WM, WN, TPS, 1, PF>), dim3(g),   \
+                                   dim3(256), BC::LDS_BYTES, 0, a);                                        \
+            });                                                                                            \
+            names.push_back(NAME);                                                                         \
+        }
+        VV(32, 64, 8, 16, 4, 1, 1, 0, "131 NT64 8x16 WM4 TPS1 (prod)")
+        VV(32, 128, 8, 16, 2, 2, 3, 1, "132 NT128 8x16 TPS3 PF (prod)")
+        VV(32, 64, 8, 16, 2, 2, 3, 1, "133 NT64 8x16 TPS3 PF (prod)")
+        VV(32, 64, 8, 16, 4, 1, 1, 1, "NT64 8x16 WM4 TPS1 PF")
+        VV(32, 64, 8, 16, 4, 1, 3, 0, "NT64 8x16 WM4 TPS3")
+        VV(32, 64, 8, 16, 4, 1, 3, 1, "NT64 8x16 WM4 TPS3 PF")
+        VV(32, 64, 8, 16, 2, 2, 3, 0, "NT64 8x16 TPS3")
+        VV(32, 128, 8, 16, 2, 2, 3, 0, "NT128 8x16 TPS3")
+        VV(32, 128, 4, 16, 2, 2, 3, 1, "NT128 4x16 TPS3 PF")
+        VV(32, 64, 8, 16, 2, 2, 9, 1, "NT64 8x16 TPS9 PF")
+#undef VV
+        const int nv = (int)launches.size();
+        std::vector<std::vector<float>> t(nv);
+        for (int r = 0; r < rounds; ++r)
+            for (int i = 0; i < nv; ++i) t[i].push_back(time_ms(launches[i], iters));
+        for (int i = 0; i < nv; ++i) {
+            std::sort(t[i].begin(), t[i].end());
+            const float med = t[i][rounds / 2];
+            printf("%-5s %-34s B=%d  median %8.2f us  %7.1f TF/s\n", l.name, names[i], B, med * 1e3,
+                   fl / (med * 1e-3) / 1e12);
+        }
+    }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
+
 int main(int argc, char** argv) {
     int B = argc > 1 ? atoi(argv[1]) : 1;
+    if (argc > 2 && std::string(argv[2]) == "vgg") return run_vgg(B);
     const int iters = 20, rounds = 7;
     Layer res{120, 240, 128, 128, 3, 1, 1, 2.0 * 120 * 240 * 9 * 128 * 128};
     float* in = dev_rand((size_t)B * 120 * 240 * 128, 0.f, 1.f, 1);
@@ -130,27 +196,28 @@ int main(int argc, char** argv) {
     SV(2, "small opt2 (LDS weights)")
     SV(3, "small opt3 (LDS weights, q unrolled)")
     // split-bf16 (bf16x3) residual conv variants: timing only (random weight bits)
-#define BV(KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP, NAME)                                               \
+#define BV(KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP, PF, NAME)                                               \
     {                                                                                                    \
-        using BC = Bf3Cfg<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP>;                                  \
+        using BC = Bf3Cfg<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP, PF>;                                  \
         ConvArgs ba = make_args<KH, KW, S, CK_, NT, TH, TW, WM, WN, 1, 1, 1>(res, B, in, w, bias, ab, out, part); \
         const unsigned bgrid = (unsigned)(B * ba.tiles_y * ba.tiles_x * ba.n_blocks);                    \
-        CK(hipFuncSetAttribute((const void*)conv_bf3_kernel<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP>, \
+        CK(hipFuncSetAttribute((const void*)conv_bf3_kernel<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP, PF>, \
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)BC::LDS_BYTES));         \
         printf("%-40s LDS %6zu B  grid %u\n", NAME, (size_t)BC::LDS_BYTES, bgrid);                        \
         launches.push_back([=] {                                                                         \
-            hipLaunchKernelGGL((conv_bf3_kernel<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP>), dim3(bgrid), \
+            hipLaunchKernelGGL((conv_bf3_kernel<KH, KW, S, CK_, NT, TH, TW, WM, WN, TPS, NP, PF>), dim3(bgrid), \
                                dim3(256), BC::LDS_BYTES, 0, ba);                                         \
         });                                                                                              \
         names.push_back(NAME); flops.push_back(res.flops); ++nv;                                         \
     }
-    BV(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 2, "bf16x3 res NT128 4x16")
-    BV(3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 2, "bf16x3 res NT64 4x16")
-    BV(3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 2, "bf16x3 res NT128 8x16")
-    BV(3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 3, "bf16x6 res NT128 4x16")
-    BV(3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 3, "bf16x6 res NT64 4x16")
-    BV(3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3, "bf16x6 res NT64 8x16")
-    BV(3, 3, 1, 32, 128, 8, 16, 2, 2, 1, 3, "bf16x6 res NT128 8x16")
+    BV(3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 2, 0, "bf16x3 res NT64 4x16 (prod)")
+    BV(3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 2, 1, "bf16x3 res NT64 4x16 PF")
+    BV(3, 3, 1, 32, 64, 8, 16, 2, 2, 3, 2, 1, "bf16x3 res NT64 8x16 TPS3 PF")
+    BV(3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3, 0, "bf16x6 res NT64 8x16 (prod)")
+    BV(3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3, 1, "bf16x6 res NT64 8x16 PF")
+    BV(3, 3, 1, 32, 64, 8, 16, 2, 2, 3, 3, 1, "bf16x6 res NT64 8x16 TPS3 PF")
+    BV(3, 3, 1, 32, 64, 8, 16, 2, 2, 3, 1, 1, "bf16 res NT64 8x16 TPS3 PF (133)")
+    BV(3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 1, "bf16 res NT128 8x16 TPS3 PF (132)")
     std::vector<std::vector<float>> t(nv);
     for (int r = 0; r < rounds; ++r)
         for (int i = 0; i < nv; ++i) t[i].push_back(time_ms(launches[i], iters));
