@@ -7,7 +7,9 @@
 // each workgroup stages 64 pixels x (64 + 64) channels of F in LDS and its 4 waves each own
 // one 32x32 block of a 64x64 G tile (v_mfma_f32_32x32x2_f32: exact f32 products). Partial
 // tiles go to a slab [b][split][C][C]; a second kernel sums the splits in fixed order
-// (bitwise reproducible, no float atomics) and scales by 1/(H*W).
+// (bitwise reproducible, no float atomics) and scales by 1/(H*W). G is symmetric: only the tiles
+// ti <= tj are computed; an off-diagonal tile is written to the slab at (ti, tj) and transposed at
+// (tj, ti) (C = 512: 36 of 64 tiles).
 #include <hip/hip_runtime.h>
 #include "kernels.h"
 
@@ -22,7 +24,7 @@ constexpr int LS = TILE + 1;  // padded LDS row
 }  // namespace gram
 
 static int gram_splits(int batch, int hw, int channels) {
-    const int tiles = (channels / gram::TILE) * (channels / gram::TILE);
+    const int nt = channels / gram::TILE, tiles = nt * (nt + 1) / 2;
     int ns = 2048 / (batch * tiles);
     const int max_ns = (hw + 255) / 256;
     if (ns > max_ns) ns = max_ns;
@@ -43,10 +45,15 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restri
     int bid = blockIdx.x;
     const int split = bid % nsplit;
     bid /= nsplit;
-    const int tj = bid % ntile;
-    bid /= ntile;
-    const int ti = bid % ntile;
-    const int b = bid / ntile;
+    const int npairs = ntile * (ntile + 1) / 2;
+    int pair = bid % npairs;
+    const int b = bid / npairs;
+    int ti = 0;   // pair -> (ti, tj), ti <= tj, row-major over the upper triangle
+    while (pair >= ntile - ti) {
+        pair -= ntile - ti;
+        ++ti;
+    }
+    const int tj = ti + pair;
     const int c0 = ti * TILE, d0 = tj * TILE;
     const int p_begin = split * span;
     const int p_end = min(hw, p_begin + span);
@@ -89,18 +96,45 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restri
     for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
         out[(size_t)(c0 + wi * 32 + row) * C + d0 + wj * 32 + li] = acc[r];
+        if (ti != tj) out[(size_t)(d0 + wj * 32 + li) * C + c0 + wi * 32 + row] = acc[r];
     }
 }
 
+// Sums the splits in a fixed order: a workgroup owns 64 float4 of G; its four waves sum contiguous
+// quarters of the split range, wave 0 adds the quarters in order and scales.
 __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
                                                           int C, int nsplit, float inv_hw, int batch) {
-    const size_t cc = (size_t)C * C;
-    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < (size_t)batch * cc; i += (size_t)gridDim.x * 256) {
-        const size_t b = i / cc, e = i % cc;
-        const float* s = slab + b * nsplit * cc + e;
-        float acc = 0.f;
-        for (int k = 0; k < nsplit; ++k) acc += s[(size_t)k * cc];
-        out[i] = acc * inv_hw;
+    const size_t cc4 = (size_t)C * C / 4;
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const size_t i = (size_t)blockIdx.x * 64 + lane;
+    __shared__ float4 part[3][64];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool ok = i < (size_t)batch * cc4;
+    if (ok) {
+        const size_t b = i / cc4, e = i - b * cc4;
+        const float4* s = reinterpret_cast<const float4*>(slab) + b * nsplit * cc4 + e;
+        const int k0 = (nsplit * q) / 4, k1 = (nsplit * (q + 1)) / 4;
+#pragma unroll 8
+        for (int k = k0; k < k1; ++k) {
+            const float4 v = s[(size_t)k * cc4];
+            acc.x += v.x;
+            acc.y += v.y;
+            acc.z += v.z;
+            acc.w += v.w;
+        }
+    }
+    if (q > 0) part[q - 1][lane] = acc;
+    __syncthreads();
+    if (q == 0 && ok) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float4 v = part[j][lane];
+            acc.x += v.x;
+            acc.y += v.y;
+            acc.z += v.z;
+            acc.w += v.w;
+        }
+        reinterpret_cast<float4*>(out)[i] = make_float4(acc.x * inv_hw, acc.y * inv_hw, acc.z * inv_hw, acc.w * inv_hw);
     }
 }
 
@@ -110,16 +144,15 @@ hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float
     int span = (hw + ns - 1) / ns;
     span = ((span + gram::KP - 1) / gram::KP) * gram::KP;
     const int ntile = channels / gram::TILE;
-    const unsigned grid = (unsigned)(batch * ntile * ntile * ns);
+    const unsigned grid = (unsigned)(batch * (ntile * (ntile + 1) / 2) * ns);
     float* slab = static_cast<float*>(ws);
     hipLaunchKernelGGL(gram_partial_kernel, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns, span);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const size_t total = (size_t)batch * channels * channels;
-    unsigned rb = (unsigned)((total + 255) / 256);
-    if (rb > 4096) rb = 4096;
-    hipLaunchKernelGGL(gram_reduce_kernel, dim3(rb), dim3(256), 0, st, slab, out, channels, ns, 1.0f / (float)hw,
-                       batch);
+    if ((reinterpret_cast<uintptr_t>(out) & 15) != 0) return hipErrorInvalidValue;
+    const size_t total4 = (size_t)batch * channels * channels / 4;
+    hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((total4 + 63) / 64)), dim3(256), 0, st, slab, out, channels,
+                       ns, 1.0f / (float)hw, batch);
     return hipGetLastError();
 }
 

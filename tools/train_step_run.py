@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--spec", default="rst-960-120-128-17")
     ap.add_argument("--precision", default="bf16", help="VGG16 conv arithmetic (bench.py's training headline: bf16)")
+    ap.add_argument("--losses", action="store_true", help="print the loss of every step (syncs per step)")
     a = ap.parse_args()
     cfg = ShapeConfig.from_spec(a.spec)
     ins, outs = cfg.input_shape['content'], cfg.output_shape
@@ -34,11 +35,15 @@ def main():
          'style_params': torch.from_numpy(synthetic_style_params(B, 1, plan.num_style_params, plan)).to(dev)}
     y = {'content': torch.from_numpy(rng.random((B,) + outs, dtype=np.float32)).to(dev),
          'style': torch.from_numpy(rng.random((B, 1) + outs, dtype=np.float32)).to(dev)}
-    tr.train_step(x, y)
+    m = tr.train_step(x, y)
     torch.cuda.synchronize()
+    if a.losses:
+        print(f"step 0: loss {float(m['loss']):.9g}")
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         m = tr.train_step(x, y)
+        if a.losses:
+            print(f"step {i + 1}: loss {float(m['loss']):.9g}")
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     print(f"{a.steps} steps B={B}: {el / a.steps * 1e3:.2f} ms/step, loss {float(m['loss']):.6g}")
