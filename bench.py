@@ -214,11 +214,15 @@ def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, tim
             "frames_per_s": round(world * TB * args.train_steps / el, 3),
             "dtype": {"fp32": "fp32 (f32 MFMA)",
                       "bf16x6": "VGG16 3x3 convs: exact 3-piece split bf16 MFMA (fp32-level products, fp32 accumulate); "
-                                "transfer net and the rest fp32",
+                                "transfer net and the rest fp32 (transfer_precision)",
                       "bf16x3": "VGG16 3x3 convs: 2-piece split bf16 MFMA (16-bit operands, fp32 accumulate); "
-                                "transfer net and the rest fp32",
+                                "transfer net and the rest fp32 (transfer_precision)",
                       "bf16": "VGG16 3x3 convs: bf16 operands, fp32 accumulate (mixed_bfloat16 arithmetic); "
-                              "transfer net and the rest fp32"}[precision],
+                              "transfer net and the rest fp32 (transfer_precision)"}[precision],
+            "transfer_precision": {"fp32": "exact f32 MFMA",
+                                   "fp32_winograd": "residual 3x3 convs (forward + input gradient) as Winograd "
+                                                    "F(2x2,3x3) on f32 MFMA, the other transfer convs exact f32"}[
+                tr.precision],
             "tflop_per_sample": round(per_sample / 1e12, 4),
             "achieved_tflops_per_gpu": round(tfs, 2), "frac_fp32_mfma_peak": round(tfs / FP32_MFMA_PEAK_TFLOPS, 4),
             "flop_breakdown_per_sample_gflop": {k: round(v / 1e9, 2) for k, v in fl.items()},

@@ -159,6 +159,13 @@ typedef struct rst_trainer rst_trainer;
 int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t num_weights,
                        const rst_loss_shape* loss, const float* vgg_weights_host, size_t num_vgg_weights,
                        rst_trainer** out);
+/* As rst_trainer_create with the transfer network's conv arithmetic: RST_PRECISION_FP32 (exact-f32
+ * MFMA, what rst_trainer_create uses) or RST_PRECISION_FP32_WINOGRAD (the residual-block 3x3 convs,
+ * forward and input gradient, as Winograd F(2x2,3x3) on f32 MFMA; weight images re-transformed on
+ * the device after every update). Same training loop as train_network.py:128-138 (Keras fit). */
+int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, size_t num_weights,
+                          const rst_loss_shape* loss, const float* vgg_weights_host, size_t num_vgg_weights,
+                          int precision, rst_trainer** out);
 void rst_trainer_destroy(rst_trainer* t);
 int rst_trainer_num_style_params(const rst_trainer* t);
 size_t rst_trainer_num_weights(const rst_trainer* t);

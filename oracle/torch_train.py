@@ -117,6 +117,24 @@ class _RoutedMaxPool2(torch.autograd.Function):
         return gx, None
 
 
+class _RoutedRelu(torch.autograd.Function):
+    """ReLU whose backward mask (which units pass the gradient) comes from a supplied routing tensor
+    (the implementation-under-test's float32 post-ReLU activations: unit active iff > 0) instead of
+    this float64 tensor's sign. Forward values are the float64 ReLU. Only the measure-zero decision at
+    pre-activations within rounding distance of 0 is aligned (same idea as _RoutedMaxPool2)."""
+
+    @staticmethod
+    def forward(ctx, x, route):
+        mask = (route > 0).to(x.dtype)
+        ctx.save_for_backward(mask)
+        return F.relu(x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (mask,) = ctx.saved_tensors
+        return gy * mask, None
+
+
 def _bf16(t: torch.Tensor) -> torch.Tensor:
     return torch.from_numpy(bf16_round(t.detach().numpy())).to(t.dtype)
 
@@ -143,11 +161,12 @@ class _Bf16Conv(torch.autograd.Function):
 
 
 def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None,
-                 bf16: bool = False) -> Dict[str, torch.Tensor]:
+                 bf16: bool = False, relu_route=None) -> Dict[str, torch.Tensor]:
     """StyleLossModelVGG.call (styleLoss.py:106-109) on NCHW float64 images in [0, 1].
     ``taps``: list receiving every conv output (retain_grad) when the input requires grad.
     ``route``: {conv index: NCHW activations} whose window maxima route the max-pool backward.
-    ``bf16``: every conv but the first (Cin = 3, fp32 on the device) in bf16 arithmetic (_Bf16Conv)."""
+    ``bf16``: every conv but the first (Cin = 3, fp32 on the device) in bf16 arithmetic (_Bf16Conv).
+    ``relu_route``: {conv index: NCHW post-ReLU activations} whose positive units set the ReLU backward mask."""
     x = images01 * 255.0
     mean = torch.tensor(VGG_MEAN_BGR, dtype=x.dtype).view(1, 3, 1, 1)
     x = x.flip(1) - mean
@@ -162,9 +181,10 @@ def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None,
             continue
         name = entry[0]
         if bf16 and i > 0:
-            x = F.relu(_Bf16Conv.apply(x, vgg[2 * i], vgg[2 * i + 1]))
+            x = _Bf16Conv.apply(x, vgg[2 * i], vgg[2 * i + 1])
         else:
-            x = F.relu(conv2d_same(x, vgg[2 * i], vgg[2 * i + 1], 1))
+            x = conv2d_same(x, vgg[2 * i], vgg[2 * i + 1], 1)
+        x = _RoutedRelu.apply(x, relu_route[i]) if relu_route is not None and i in relu_route else F.relu(x)
         i += 1
         if taps is not None and x.requires_grad:
             x.retain_grad()
@@ -187,9 +207,9 @@ def _mean_l2(t):
 
 
 def style_losses(pred, content, style, vgg, content_factor=1e4, style_factor=1e-3, tv_factor=1e-1, taps=None,
-                 route=None, bf16=False):
+                 route=None, bf16=False, relu_route=None):
     """make_style_loss_function without depth (styleLoss.py:295-369) -> (B, 4) [loss, feature, style, tv]."""
-    fp = vgg_features(pred, vgg, taps, route, bf16)
+    fp = vgg_features(pred, vgg, taps, route, bf16, relu_route)
     fc, fs = vgg_features(content, vgg, bf16=bf16), vgg_features(style, vgg, bf16=bf16)
     feature = torch.stack([_mean_l2(fp[n] - fc[n]) for n in CONTENT_LAYERS]).mean(0) * content_factor
     style_l = torch.stack([_mean_l2(_gram(fp[n]) - _gram(fs[n])) for n in STYLE_LAYERS]).mean(0) * style_factor
@@ -206,14 +226,16 @@ def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarra
                   gt_content, gt_style, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
                   factors=(1e4, 1e-3, 1e-1), ms: Optional[Sequence[np.ndarray]] = None,
                   lr=1e-3, rho=0.9, eps=1e-7, pool_route: Optional[Dict[int, np.ndarray]] = None,
-                  vgg_bf16: bool = False) -> Dict[str, object]:
+                  vgg_bf16: bool = False, relu_route: Optional[Dict[int, np.ndarray]] = None) -> Dict[str, object]:
     """One Keras train_step: forward (BN training mode), loss, gradients, RMSprop.
 
     Inputs are NHWC numpy; returns numpy: prediction (B,H,W,3), losses (B,4), grads (Keras order;
     zeros for the BN moving statistics), grad_style_params (B,P), weights after the update
     (moving statistics updated by the forward), ms (RMSprop slots after the update).
     ``pool_route``: {VGG conv index before a pool: NHWC activations of the prediction} to align
-    the max-pool backward's choice among near-equal maxima with an implementation under test."""
+    the max-pool backward's choice among near-equal maxima with an implementation under test;
+    ``relu_route``: {VGG conv index: NHWC post-ReLU activations of the prediction} aligning the ReLU
+    backward masks the same way (pre-activations within rounding distance of 0)."""
     blocks, P = transfer_structure(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters)
     w = [torch.tensor(np.asarray(a, np.float64), requires_grad=True) for a in weights]
     vgg = [torch.tensor(np.asarray(a, np.float64)) for a in vgg_weights]
@@ -225,7 +247,9 @@ def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarra
     pred, bn_stats = transfer_forward_train(_nchw(content), sp, w, blocks, taps=taps)
     vtaps = []
     route = None if pool_route is None else {k: _nchw(v) for k, v in pool_route.items()}
-    losses = style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors, taps=vtaps, route=route, bf16=vgg_bf16)
+    rroute = None if relu_route is None else {k: _nchw(v) for k, v in relu_route.items()}
+    losses = style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors, taps=vtaps, route=route, bf16=vgg_bf16,
+                          relu_route=rroute)
     losses[:, 0].sum().backward()
     # Keras trainable set: conv kernels/biases, BN gamma/beta (moving statistics are not trained)
     grads, new_w, new_ms = [], [], []

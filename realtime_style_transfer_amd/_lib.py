@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = [
     "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_last_error", "rst_version",
     "rst_profile_begin", "rst_profile_end", "rst_layer_kernel_id",
     "rst_loss_num_weights", "rst_loss_create", "rst_loss_destroy", "rst_loss_forward", "rst_loss_copy_feature",
-    "rst_trainer_create", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
+    "rst_trainer_create", "rst_trainer_create_ex", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
     "rst_trainer_compute_gradients", "rst_trainer_apply_gradients", "rst_trainer_copy_weights",
     "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_copy_output_gradient",
     "rst_trainer_debug_vgg_gradient", "rst_trainer_loss",
@@ -125,6 +125,9 @@ def load() -> ctypes.CDLL:
     lib.rst_trainer_create.argtypes = [ctypes.POINTER(RstShape), vp, sz, ctypes.POINTER(RstLossShape), vp, sz,
                                        ctypes.POINTER(vp)]
     lib.rst_trainer_create.restype = i
+    lib.rst_trainer_create_ex.argtypes = [ctypes.POINTER(RstShape), vp, sz, ctypes.POINTER(RstLossShape), vp, sz, i,
+                                          ctypes.POINTER(vp)]
+    lib.rst_trainer_create_ex.restype = i
     lib.rst_trainer_destroy.argtypes = [vp]
     lib.rst_trainer_destroy.restype = None
     lib.rst_trainer_num_style_params.argtypes = [vp]

@@ -70,6 +70,7 @@ struct WinoArgs {
     float* out;             // NHWC [B][H][W][128]
     float4* part;           // [B][128][tiles_y*tiles_x] or null
     int batch, H, W, cin, tiles_y, tiles_x, pro_mode;
+    int linear;             // 0: out = ReLU(conv + bias) (the residual convs); 1: conv + bias (input gradient)
 };
 bool wino_supported(int kh, int stride, int cin, int cout);
 
@@ -106,6 +107,8 @@ int wino_tiles_y(int H);
 int wino_tiles_x(int W);
 std::vector<float> wino_pack_weights(const float* kern, int cin);
 hipError_t wino_prepare();
+// wino_pack_weights on the device (kern: HWIO [3][3][cin][128] float32 on the device)
+hipError_t wino_transform_launch(const float* kern, int cin, float* U, hipStream_t st);
 hipError_t wino_launch(const WinoArgs& a, hipStream_t st);
 
 // Final 9x9 transposed conv with Cout = 3 on the VALU (conv_small.hip).

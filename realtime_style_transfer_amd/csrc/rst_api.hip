@@ -512,6 +512,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.tiles_y = e.tiles_y;
         a.tiles_x = e.tiles_x;
         a.pro_mode = e.pro;
+        a.linear = e.s.conv_relu ? 0 : 1;
         if (blend) return fail(RST_ERR_UNSUPPORTED, "Winograd conv has no two-style blend prologue");
         HIP_TRY(wino_launch(a, st));
     } else {

@@ -86,6 +86,11 @@ struct TLayer {
     int* d_map_dg = nullptr;
     size_t n_dg = 0;
     int norm_tile = 0;
+    // Winograd residual convs (precision FP32_WINOGRAD): the weight images are transforms, not gathers —
+    // the forward image is computed from the canonical HWIO kernel, the input-gradient image from the
+    // flipped kernel gathered into d_kflip (d_map_dg then maps canonical -> flipped HWIO)
+    bool wino_fwd = false, wino_dg = false;
+    float* d_kflip = nullptr;
 };
 
 struct ConvBwd {   // a backward conv with static weights (VGG dgrad, Gram 1x1)
@@ -169,9 +174,15 @@ namespace {
 
 int repack(rst_trainer* t, hipStream_t st) {
     for (TLayer& T : t->L) {
-        RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_w, T.e.d_w, T.n_w, st));
+        if (T.wino_fwd) RST_HIP_TRY(wino_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
+        else RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_w, T.e.d_w, T.n_w, st));
         RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_b, T.e.d_bias, T.n_b, st));
-        if (T.has_dgrad) RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_dg, T.d_wdg, T.n_dg, st));
+        if (T.has_dgrad && T.wino_dg) {
+            RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_dg, T.d_kflip, T.n_dg, st));
+            RST_HIP_TRY(wino_transform_launch(T.d_kflip, T.dg.s.cin, T.d_wdg, st));
+        } else if (T.has_dgrad) {
+            RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_dg, T.d_wdg, T.n_dg, st));
+        }
     }
     return RST_OK;
 }
@@ -200,6 +211,25 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.tiles_y = e.tiles_y;
             a.tiles_x = e.tiles_x;
             RST_HIP_TRY(small_conv_launch(a, st));
+        } else if (e.kind == K_WINO) {
+            WinoArgs a{};
+            a.in = Pv->e.d_out;
+            a.res = e.pro_res;
+            a.mat = T.d_x;
+            a.pro_ab = Pv->e.d_ab;
+            a.U = e.d_w;
+            a.bias = e.d_bias;
+            a.out = e.d_out;
+            a.part = e.d_part;
+            a.batch = B;
+            a.H = e.s.H;
+            a.W = e.s.W;
+            a.cin = e.s.cin;
+            a.tiles_y = e.tiles_y;
+            a.tiles_x = e.tiles_x;
+            a.pro_mode = e.pro;
+            a.linear = e.s.conv_relu ? 0 : 1;
+            RST_HIP_TRY(wino_launch(a, st));
         } else {
             ConvArgs a = conv_geometry(e, B);
             a.in = Pv ? Pv->e.d_out : content;
@@ -378,14 +408,31 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
         TLayer& Pv = t->L[li - 1];
         const bool open_block = s.res_block > 0 && s.res_conv == 0;   // conv0 of residual block r > 0
         float* target = open_block ? t->d_tmp : Pv.d_g;
-        ConvArgs a = conv_geometry(T.dg, B);
-        a.in = t->d_dz;
-        a.wpk = T.d_wdg;
-        a.bias = t->d_zero;
-        a.out = target;
-        a.pro_mode = PRO_NONE;
-        a.epi_mode = EPI_NONE;
-        RST_HIP_TRY(conv_launch(T.dg.tile, a, st));
+        if (T.wino_dg) {
+            WinoArgs a{};
+            a.in = t->d_dz;
+            a.U = T.d_wdg;
+            a.bias = t->d_zero;
+            a.out = target;
+            a.batch = B;
+            a.H = T.dg.s.H;
+            a.W = T.dg.s.W;
+            a.cin = T.dg.s.cin;
+            a.tiles_y = T.dg.tiles_y;
+            a.tiles_x = T.dg.tiles_x;
+            a.pro_mode = PRO_NONE;
+            a.linear = 1;
+            RST_HIP_TRY(wino_launch(a, st));
+        } else {
+            ConvArgs a = conv_geometry(T.dg, B);
+            a.in = t->d_dz;
+            a.wpk = T.d_wdg;
+            a.bias = t->d_zero;
+            a.out = target;
+            a.pro_mode = PRO_NONE;
+            a.epi_mode = EPI_NONE;
+            RST_HIP_TRY(conv_launch(T.dg.tile, a, st));
+        }
         if (open_block) {
             // g_r = (conv path) + g_{r+1}; g_{r+1} is the gradient of conv1 of block r (= T(li+1).d_g)
             const TLayer& c1 = t->L[li + 1];
@@ -407,9 +454,19 @@ extern "C" {
 int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t num_weights,
                        const rst_loss_shape* loss, const float* vgg_weights_host, size_t num_vgg_weights,
                        rst_trainer** out) {
+    return rst_trainer_create_ex(shape, weights_host, num_weights, loss, vgg_weights_host, num_vgg_weights,
+                                 RST_PRECISION_FP32, out);
+}
+
+int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, size_t num_weights,
+                          const rst_loss_shape* loss, const float* vgg_weights_host, size_t num_vgg_weights,
+                          int precision, rst_trainer** out) {
     if (!shape || !weights_host || !loss || !vgg_weights_host || !out)
         return set_error(RST_ERR_INVALID, "rst_trainer_create: null argument");
     *out = nullptr;
+    if (precision != RST_PRECISION_FP32 && precision != RST_PRECISION_FP32_WINOGRAD)
+        return set_error(RST_ERR_INVALID, "rst_trainer_create_ex: transfer-network precision must be FP32 or "
+                                          "FP32_WINOGRAD");
     if (shape->num_styles != 1)
         return set_error(RST_ERR_UNSUPPORTED, "rst_trainer_create: num_styles must be 1 (train_network.py:55)");
     if (shape->max_batch <= 0) return set_error(RST_ERR_INVALID, "rst_trainer_create: max_batch must be positive");
@@ -458,13 +515,17 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
         for (size_t i = 0; i < T.kcount; ++i) kidx[i] = (float)(T.woff + i + 1);
         for (int c = 0; c < s.cout; ++c) bidx[c] = (float)(T.boff + c + 1);
         std::vector<float> packed, bias_n;
-        if ((st = prepare_layer(T.e, s, kidx.data(), bidx.data(), packed, bias_n)) != RST_OK) return fail_delete(t, st);
-        std::vector<int> mw = to_map(packed), mb = to_map(bias_n);
-        T.n_w = mw.size();
+        // residual convs on Winograd when asked (their prologue always materialises the input for wgrad)
+        const int lp = (precision == RST_PRECISION_FP32_WINOGRAD && s.res_block >= 0) ? precision : RST_PRECISION_FP32;
+        if ((st = prepare_layer(T.e, s, kidx.data(), bidx.data(), packed, bias_n, lp)) != RST_OK)
+            return fail_delete(t, st);
+        T.wino_fwd = T.e.kind == K_WINO;
+        std::vector<int> mw = T.wino_fwd ? std::vector<int>() : to_map(packed), mb = to_map(bias_n);
+        T.n_w = packed.size();
         T.n_b = mb.size();
-        if ((st = t->alloc(&T.d_map_w, mw.size() * 4, mw.data())) != RST_OK) return fail_delete(t, st);
+        if (!T.wino_fwd && (st = t->alloc(&T.d_map_w, mw.size() * 4, mw.data())) != RST_OK) return fail_delete(t, st);
         if ((st = t->alloc(&T.d_map_b, mb.size() * 4, mb.data())) != RST_OK) return fail_delete(t, st);
-        if ((st = t->alloc(&T.e.d_w, mw.size() * 4)) != RST_OK) return fail_delete(t, st);
+        if ((st = t->alloc(&T.e.d_w, T.n_w * 4)) != RST_OK) return fail_delete(t, st);
         if ((st = t->alloc(&T.e.d_bias, mb.size() * 4)) != RST_OK) return fail_delete(t, st);
         const size_t nout = (size_t)B * s.Ho * s.Wo * s.cout;
         if ((st = t->alloc(&T.e.d_out, nout * 4)) != RST_OK) return fail_delete(t, st);
@@ -509,13 +570,15 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
                 ds.keras_kind = 0;
             }
             std::vector<float> zb(ds.cout, 0.f), pdg, bdg;
-            if ((st = prepare_layer(T.dg, ds, kd.data(), zb.data(), pdg, bdg)) != RST_OK) return fail_delete(t, st);
+            if ((st = prepare_layer(T.dg, ds, kd.data(), zb.data(), pdg, bdg, lp)) != RST_OK) return fail_delete(t, st);
             if (T.dg.kind == K_SMALL) return fail_delete(t, set_error(RST_ERR_UNSUPPORTED, "dgrad kind"));
             T.dg.s = ds;
-            std::vector<int> md = to_map(pdg);
+            T.wino_dg = T.dg.kind == K_WINO;
+            std::vector<int> md = to_map(T.wino_dg ? kd : pdg);   // Winograd: canonical -> flipped HWIO
             T.n_dg = md.size();
             if ((st = t->alloc(&T.d_map_dg, md.size() * 4, md.data())) != RST_OK) return fail_delete(t, st);
-            if ((st = t->alloc(&T.d_wdg, md.size() * 4)) != RST_OK) return fail_delete(t, st);
+            if ((st = t->alloc(&T.d_wdg, pdg.size() * 4)) != RST_OK) return fail_delete(t, st);
+            if (T.wino_dg && (st = t->alloc(&T.d_kflip, kd.size() * 4)) != RST_OK) return fail_delete(t, st);
             T.has_dgrad = true;
             max_ntot = std::max(max_ntot, T.dg.ntot);
             max_out = std::max(max_out, (size_t)B * s.H * s.W * s.cin);
@@ -542,11 +605,11 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
     }
     for (auto& T : t->L) {
         if (T.e.kind != K_SMALL) {
-            hipError_t pe = conv_prepare(T.e.tile);
+            hipError_t pe = T.wino_fwd ? wino_prepare() : conv_prepare(T.e.tile);
             if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));
         }
         if (T.has_dgrad) {
-            hipError_t pe = conv_prepare(T.dg.tile);
+            hipError_t pe = T.wino_dg ? wino_prepare() : conv_prepare(T.dg.tile);
             if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));
         }
     }

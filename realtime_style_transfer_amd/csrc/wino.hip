@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
-            const float v = fmaxf(yy[q] + bias, 0.f);
+            const float v = a.linear ? yy[q] + bias : fmaxf(yy[q] + bias, 0.f);
             const bool ok = oy < H && ox < W;
             yv[j * 4 + q] = ok ? v : 0.f;
             if (ok) {
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int q = 0; q < 4; ++q) {
             const float y = yy[q] + exch[((cg * 16 + j) * 4 + q) * 64 + lane];
             const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
-            const float v = fmaxf(y + bias, 0.f);
+            const float v = a.linear ? y + bias : fmaxf(y + bias, 0.f);
             const bool ok = oy < H && ox < W;
             yv[j * 4 + q] = ok ? v : 0.f;
             if (ok) {
@@ -597,6 +597,7 @@ int wino_tiles_x(int W) { return (W + WTW - 1) / WTW; }
 
 // U[chunk][xi][co][8] = (G g G^T)[xi] for input channel chunk*8 + c; g = Keras HWIO kernel (3,3,cin,128)
 std::vector<float> wino_pack_weights(const float* kern, int cin) {
+#pragma clang fp contract(off)   // same operation order as wino_transform_kernel
     static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
     std::vector<float> U((size_t)cin / WCK * WXI * WN * WCK);
     for (int ci = 0; ci < cin; ++ci)
@@ -614,6 +615,41 @@ std::vector<float> wino_pack_weights(const float* kern, int cin) {
                 }
         }
     return U;
+}
+
+// Device form of wino_pack_weights (training re-packs after every optimizer step): one thread per
+// (ci, co), U = G g G^T in float64 with the host's operation order and no contraction, so the image
+// is bitwise the host's.
+__global__ __launch_bounds__(256) void wino_transform_kernel(const float* __restrict__ kern, int cin,
+                                                             float* __restrict__ U) {
+#pragma clang fp contract(off)
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= cin * WN) return;
+    const int ci = idx / WN, co = idx - (idx / WN) * WN;
+    const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    double g[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) g[i][j] = kern[(((size_t)i * 3 + j) * cin + ci) * WN + co];
+    const int chunk = ci / WCK, c = ci % WCK;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double u = 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) u = u + G[p][i] * g[i][j] * G[q][j];
+            U[(((size_t)chunk * WXI + p * 4 + q) * WN + co) * WCK + c] = (float)u;
+        }
+}
+
+hipError_t wino_transform_launch(const float* kern, int cin, float* U, hipStream_t st) {
+    if (cin % WCK != 0 || cin > W_MAX_CIN) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wino_transform_kernel, dim3((unsigned)((cin * WN + 255) / 256)), dim3(256), 0, st, kern, cin, U);
+    return hipGetLastError();
 }
 
 // RST_WINO8: launch the 8-wave (two waves per SIMD) variant. Measured (tools/wino_bench.hip, residual

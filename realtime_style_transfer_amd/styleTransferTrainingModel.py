@@ -68,8 +68,12 @@ class StyleTransferTrainingModel:
     def __init__(self, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
                  loss_model: Optional[StyleLossModelVGG] = None, weights: Optional[Sequence[np.ndarray]] = None,
                  seed: int = 2, max_batch: int = 4, optimizer: Optional[RMSprop] = None, process_group=None,
-                 device=None, name: str = "StyleTransferTrainingModel", style_predictor=None):
+                 device=None, name: str = "StyleTransferTrainingModel", style_predictor=None,
+                 precision: str = "fp32_winograd"):
+        if precision not in ("fp32", "fp32_winograd"):
+            raise ValueError(f"transfer-network training precision must be 'fp32' or 'fp32_winograd', got {precision!r}")
         self.name = name
+        self.precision = precision
         self.plan: Plan = network_plan(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, 1)
         self.input_shape = tuple(int(v) for v in input_shape)
         self.output_shape = tuple(int(v) for v in output_shape)
@@ -97,8 +101,9 @@ class StyleTransferTrainingModel:
         vgg = np.concatenate([a.reshape(-1) for a in lm.weights]).astype(np.float32)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            _lib.check(lib.rst_trainer_create(ctypes.byref(shape), flat.ctypes.data, flat.size, ctypes.byref(lshape),
-                                              vgg.ctypes.data, vgg.size, ctypes.byref(h)))
+            _lib.check(lib.rst_trainer_create_ex(ctypes.byref(shape), flat.ctypes.data, flat.size,
+                                                 ctypes.byref(lshape), vgg.ctypes.data, vgg.size,
+                                                 _lib.PRECISIONS[precision], ctypes.byref(h)))
         self._handle = h
         self.num_weights = int(lib.rst_trainer_num_weights(h))
         if self.num_weights != flat.size or lib.rst_trainer_num_style_params(h) != self.num_style_parameters:

@@ -14,7 +14,11 @@ few filters. Tolerances (float32 GPU vs float64 oracle):
   the float64 oracle; one such flip moved a gradient entry to its neighbour and shifted every
   upstream gradient by ~1%. The oracle therefore takes the pool routing (only the choice of
   WHICH maximum) from the GPU's float32 activations of the four pooled layers; all arithmetic
-  stays float64. Max-norm errors are reported in gpurun_out/train_parity_*.json.
+  stays float64. The same holds for VGG16's ReLU masks: a pre-activation within rounding distance
+  of 0 is active in one float32 forward and not in another (the exact-f32 and Winograd transfer
+  convs give predictions 1.7e-6 apart, and one such unit moved dL/dprediction by 1.9 %), so the
+  oracle's ReLU backward masks come from the GPU's post-ReLU activations too (relu_route).
+  Max-norm errors are reported in gpurun_out/train_parity_*.json.
   after RMSprop: weights 1e-6 abs where |g_ref| > 5e-2 max|g_ref| of the tensor (elsewhere the
   first RMSprop step is lr*sign(g)/sqrt(1-rho) and only its size is checked), slots L2 5e-3.
 """
@@ -53,16 +57,26 @@ def _case(cfg, B, seed=5):
     return plan, w, vgg, content, sp, gtc, gts
 
 
-def _trainer(cfg, w, vgg, B, precision="fp32"):
+def _trainer(cfg, w, vgg, B, precision="fp32", transfer="fp32"):
     from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
     from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
     lm = StyleLossModelVGG(cfg['output_shape'], weights=vgg, max_batch=B, precision=precision)
     return StyleTransferTrainingModel(cfg['input_shape'], cfg['output_shape'], cfg['bottleneck_res_y'],
-                                      cfg['bottleneck_num_filters'], loss_model=lm, weights=w, max_batch=B)
+                                      cfg['bottleneck_num_filters'], loss_model=lm, weights=w, max_batch=B,
+                                      precision=transfer)
 
 
 def _cuda(*arrs):
     return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+VGG_CONV_NAMES = ['block1_conv1', 'block1_conv2', 'block2_conv1', 'block2_conv2', 'block3_conv1', 'block3_conv2',
+                  'block3_conv3', 'block4_conv1', 'block4_conv2', 'block4_conv3', 'block5_conv1', 'block5_conv2',
+                  'block5_conv3']
+
+
+def _relu_route(tr, B):
+    return {i: tr.vgg_feature(n, B).cpu().numpy() for i, n in enumerate(VGG_CONV_NAMES)}
 
 
 def _pool_route(tr, B):
@@ -77,22 +91,27 @@ def _pool_route(tr, B):
 # bf16 rounding of every VGG conv's input/kernel (forward) and output gradient/kernel (input gradient).
 # That simulation matches block1_conv2 to 1e-6; beyond it the fp32-vs-float64 activation differences
 # flip bf16 rounding decisions and the deviation grows layer by layer (tools/bf16_diag.py: 1.5e-4 after
-# the first pool, 5.7e-3 at block5_conv3), so the transfer-net gradients carry a few % of bf16 noise
-# (worst layer 9.5 % L2 measured)
-@pytest.mark.parametrize("name,precision,gtol", [("A", "fp32", 2e-3), ("B", "fp32", 2e-3), ("A", "bf16x6", 2e-3),
-                                                  ("A", "bf16x3", 5e-2), ("A", "bf16", 0.15)])
-def test_training_step_matches_oracle(name, precision, gtol):
+# the first pool, 5.7e-3 at block5_conv3), so the transfer-net gradients carry bf16 noise (with the
+# ReLU masks aligned: worst layer 1.8 % L2, loss terms 9e-4 / 1.8e-3 relative with the exact-f32 /
+# Winograd transfer convs, measured)
+# transfer: arithmetic of the transfer network's convs — "fp32" (exact-f32 MFMA) or "fp32_winograd"
+# (residual-block convs, forward + input gradient, as Winograd F(2x2,3x3): ~1e-6 relative per conv)
+@pytest.mark.parametrize("name,precision,gtol,transfer", [
+    ("A", "fp32", 2e-3, "fp32"), ("B", "fp32", 2e-3, "fp32"), ("A", "bf16x6", 2e-3, "fp32"),
+    ("A", "bf16x3", 5e-2, "fp32"), ("A", "bf16", 0.05, "fp32"),
+    ("A", "fp32", 2e-3, "fp32_winograd"), ("B", "fp32", 2e-3, "fp32_winograd"), ("A", "bf16", 0.05, "fp32_winograd")])
+def test_training_step_matches_oracle(name, precision, gtol, transfer):
     _need_gpu()
     from oracle import torch_train as T
     cfg = CONFIGS[name]
     B = 2
     plan, w, vgg, content, sp, gtc, gts = _case(cfg, B)
-    tr = _trainer(cfg, w, vgg, B, precision)
+    tr = _trainer(cfg, w, vgg, B, precision, transfer)
     c, s, gc, gs = _cuda(content, sp, gtc, gts)
     pred, losses, grad, gsp = tr.compute_gradients(c, s, gc, gs)
     torch.cuda.synchronize()
     ref = T.training_step(w, vgg, content, sp, gtc, gts, pool_route=_pool_route(tr, B), vgg_bf16=precision == "bf16",
-                          **cfg)
+                          relu_route=_relu_route(tr, B), **cfg)
     report = {}
     perr = float(np.abs(pred.cpu().numpy() - ref['prediction']).max())
     report['prediction_max_abs'] = perr
@@ -138,7 +157,8 @@ def test_training_step_matches_oracle(name, precision, gtol):
     report['grad_rel'] = worst
     report['failures'] = failures
     os.makedirs(OUT, exist_ok=True)
-    with open(os.path.join(OUT, f'train_parity_{name}_{precision}.json'), 'w') as f:
+    tag = '' if transfer == 'fp32' else '_' + transfer
+    with open(os.path.join(OUT, f'train_parity_{name}_{precision}{tag}.json'), 'w') as f:
         json.dump(report, f, indent=1, default=float)
     assert not failures, failures
     # moving statistics are updated by the forward (read back before the optimizer step)
@@ -163,7 +183,7 @@ def test_training_step_matches_oracle(name, precision, gtol):
         # ms = (1 - rho) g^2: its relative error is about twice the gradient's
         assert np.linalg.norm(slots[i] - ref['ms'][i]) <= max(5e-3, 2.5 * gtol) * np.linalg.norm(ref['ms'][i]), i
     assert perr < 2e-5, perr
-    assert lrel < {"bf16x3": 1e-3, "bf16": 1e-3}.get(precision, 1e-4), lrel
+    assert lrel < {"bf16x3": 1e-3, "bf16": 5e-3}.get(precision, 1e-4), lrel
     assert gerr < gtol, gerr
 
 
@@ -223,7 +243,8 @@ def test_prediction_gradient_per_loss_term(factors):
     for i in range(13):
         _lib.check(lib.rst_trainer_debug_vgg_gradient(tr._handle, i, None, 0, B, _lib.stream_ptr()))
     tr.compute_gradients(c, s, gc, gs)
-    ref = T.training_step(w, vgg, content, sp, gtc, gts, factors=factors, pool_route=_pool_route(tr, B), **cfg)
+    ref = T.training_step(w, vgg, content, sp, gtc, gts, factors=factors, pool_route=_pool_route(tr, B),
+                          relu_route=_relu_route(tr, B), **cfg)
     g = tr.output_gradient(len(plan.layers) - 1, B).cpu().numpy()
     r = ref['output_grads'][-1]
     rel = float(np.linalg.norm(g - r) / np.linalg.norm(r))
@@ -267,7 +288,7 @@ def test_joint_training_with_style_predictor_matches_oracle():
     sp_ref = PR.predictor_train_reference(style, pw, 'MOBILE_NET', np.zeros((B, P)))['output']
     assert np.abs(sp.cpu().numpy() - sp_ref).max() <= 1e-4 * np.abs(sp_ref).max()
     ref = T.training_step(w, vgg, content, sp.cpu().numpy().astype(np.float64), gtc, gts,
-                          pool_route=_pool_route(tr, B), **cfg)
+                          pool_route=_pool_route(tr, B), relu_route=_relu_route(tr, B), **cfg)
     gerr = float(np.linalg.norm(gsp.cpu().numpy() - ref['grad_style_params']) /
                  np.linalg.norm(ref['grad_style_params']))
     assert gerr < 2e-3, gerr

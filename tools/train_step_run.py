@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--spec", default="rst-960-120-128-17")
     ap.add_argument("--precision", default="bf16", help="VGG16 conv arithmetic (bench.py's training headline: bf16)")
+    ap.add_argument("--transfer", default="fp32_winograd", help="transfer-network conv arithmetic (fp32 | fp32_winograd)")
     ap.add_argument("--losses", action="store_true", help="print the loss of every step (syncs per step)")
     a = ap.parse_args()
     cfg = ShapeConfig.from_spec(a.spec)
@@ -29,7 +30,8 @@ def main():
     B = a.batch
     lm = StyleLossModelVGG(outs, max_batch=B, device=dev, precision=a.precision)
     tr = StyleTransferTrainingModel(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, loss_model=lm,
-                                    weights=init_weights(plan, seed=2), max_batch=B, device=dev)
+                                    weights=init_weights(plan, seed=2), max_batch=B, device=dev,
+                                    precision=a.transfer)
     rng = np.random.default_rng(0)
     x = {'content': torch.from_numpy(rng.random((B,) + ins, dtype=np.float32)).to(dev),
          'style_params': torch.from_numpy(synthetic_style_params(B, 1, plan.num_style_params, plan)).to(dev)}
