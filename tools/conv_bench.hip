@@ -134,9 +134,83 @@ static int run_vgg(int B) {
     return 0;
 }
 
+
+// The small transfer-net layers of rst-960-120-128-17 at B=1: stride-2 contract convs and the
+// 4-phase (2x2) expand convs (output channel shuffle to 2H x 2W)
+struct SmallLayer { const char* name; int kh, s, H, W, Cin, Ntot, shuffle; };
+static int run_small(int B) {
+    const SmallLayer L[] = {{"c0", 3, 2, 480, 960, 32, 16, 0}, {"c1", 3, 2, 240, 480, 16, 32, 0},
+                            {"e0", 2, 1, 120, 240, 128, 128, 1}, {"e1", 2, 1, 240, 480, 32, 64, 1}};
+    const int iters = 20, rounds = 7;
+    const size_t maxact = (size_t)B * 480 * 960 * 64;
+    float* in = dev_rand(maxact, 0.f, 1.f, 21);
+    float* out; CK(hipMalloc(&out, maxact * 4));
+    float* w = dev_rand((size_t)9 * 128 * 256 * 2, -0.05f, 0.05f, 22);
+    float* bias = dev_rand(512, -0.1f, 0.1f, 23);
+    float2* ab = (float2*)dev_rand(2 * 512 * B, 0.5f, 1.5f, 24);
+    float4* part; CK(hipMalloc(&part, (size_t)B * 256 * 8192 * 16));
+    for (const auto& l : L) {
+        const int Ho = l.shuffle ? l.H : (l.H + l.s - 1) / l.s, Wo = l.shuffle ? l.W : (l.W + l.s - 1) / l.s;
+        const double fl = l.shuffle ? 2.0 * Ho * Wo * 4 * l.Cin * l.Ntot * B
+                                    : 2.0 * Ho * Wo * 9.0 * l.Cin * l.Ntot * B;
+        const double by = 4.0 * B * ((double)l.H * l.W * l.Cin + (double)Ho * Wo * l.Ntot);
+        std::vector<std::function<void()>> launches;
+        std::vector<const char*> names;
+#define VM(KH, S, CK_, NT, TH, TW, WM, WN, TPS, NAME)                                                          \
+        if (l.kh == KH && l.s == S && (l.Ntot % NT == 0 || l.Ntot < NT) && l.Cin % CK_ == 0) {                                   \
+            using C = ConvCfg<KH, KH, S, CK_, NT, TH, TW, WM, WN, TPS, 1>;                                      \
+            ConvArgs a{};                                                                                       \
+            a.in = in; a.res = in; a.pro_ab = ab; a.wpk = w; a.bias = bias; a.bn_ab = ab; a.out = out;          \
+            a.part = part;                                                                                      \
+            a.batch = B; a.H = l.H; a.W = l.W; a.cin = l.Cin; a.Ho = Ho; a.Wo = Wo;                             \
+            a.ntot = l.Ntot; a.cout = l.shuffle ? l.Ntot / 4 : l.Ntot; a.shuffle = l.shuffle;                  \
+            a.pad_t = l.shuffle ? 0 : 0; a.pad_l = a.pad_t;                                                     \
+            a.tiles_y = (Ho + TH - 1) / TH; a.tiles_x = (Wo + TW - 1) / TW;                                     \
+            a.n_blocks = (l.Ntot + NT - 1) / NT; a.nchunks = (l.Cin + CK_ - 1) / CK_;                              \
+            a.pro_mode = PRO_AFF_RELU; a.epi_mode = EPI_RELU_STATS;                                            \
+            const unsigned g = (unsigned)(B * a.tiles_y * a.tiles_x * a.n_blocks);                              \
+            CK(hipFuncSetAttribute((const void*)conv_mfma_kernel<KH, KH, S, CK_, NT, TH, TW, WM, WN, TPS, 1, 1>, \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES));             \
+            launches.push_back([=] {                                                                             \
+                hipLaunchKernelGGL((conv_mfma_kernel<KH, KH, S, CK_, NT, TH, TW, WM, WN, TPS, 1, 1>), dim3(g),   \
+                                   dim3(256), C::LDS_BYTES, 0, a);                                              \
+            });                                                                                                  \
+            names.push_back(NAME);                                                                               \
+        }
+        VM(3, 2, 16, 32, 8, 16, 4, 1, 3, "3 s2 CK16 NT32 8x16 TPS3 (prod)")
+        VM(3, 2, 16, 32, 16, 16, 4, 1, 3, "s2 CK16 NT32 16x16 TPS3")
+        VM(3, 2, 16, 32, 8, 16, 4, 1, 9, "s2 CK16 NT32 8x16 TPS9")
+        VM(3, 2, 16, 32, 8, 16, 4, 1, 1, "s2 CK16 NT32 8x16 TPS1")
+        VM(3, 2, 32, 32, 8, 16, 4, 1, 3, "s2 CK32 NT32 8x16 TPS3")
+        VM(3, 2, 32, 32, 8, 16, 4, 1, 1, "s2 CK32 NT32 8x16 TPS1")
+        VM(3, 2, 8, 32, 8, 16, 4, 1, 3, "4 s2 CK8 NT32 8x16 TPS3")
+        VM(2, 1, 32, 128, 4, 16, 2, 2, 1, "8 2x2 CK32 NT128 4x16 (prod)")
+        VM(2, 1, 32, 64, 8, 16, 2, 2, 1, "9 2x2 CK32 NT64 8x16 (prod)")
+        VM(2, 1, 32, 128, 8, 16, 2, 2, 1, "2x2 CK32 NT128 8x16")
+        VM(2, 1, 32, 32, 8, 16, 4, 1, 4, "10 2x2 CK32 NT32 8x16 TPS4")
+        VM(2, 1, 32, 64, 4, 16, 2, 2, 1, "2x2 CK32 NT64 4x16")
+        VM(2, 1, 32, 64, 16, 16, 4, 1, 1, "2x2 CK32 NT64 16x16 WM4")
+        VM(2, 1, 16, 64, 8, 16, 2, 2, 1, "2x2 CK16 NT64 8x16")
+#undef VM
+        const int nv = (int)launches.size();
+        std::vector<std::vector<float>> t(nv);
+        for (int r = 0; r < rounds; ++r)
+            for (int i = 0; i < nv; ++i) t[i].push_back(time_ms(launches[i], iters));
+        for (int i = 0; i < nv; ++i) {
+            std::sort(t[i].begin(), t[i].end());
+            const float med = t[i][rounds / 2];
+            printf("%-3s %-34s B=%d  median %7.2f us  %6.1f TF/s  %6.0f GB/s\n", l.name, names[i], B, med * 1e3,
+                   fl / (med * 1e-3) / 1e12, by / (med * 1e-3) / 1e9);
+        }
+    }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
+
 int main(int argc, char** argv) {
     int B = argc > 1 ? atoi(argv[1]) : 1;
     if (argc > 2 && std::string(argv[2]) == "vgg") return run_vgg(B);
+    if (argc > 2 && std::string(argv[2]) == "small") return run_small(B);
     const int iters = 20, rounds = 7;
     Layer res{120, 240, 128, 128, 3, 1, 1, 2.0 * 120 * 240 * 9 * 128 * 128};
     float* in = dev_rand((size_t)B * 120 * 240 * 128, 0.f, 1.f, 1);
