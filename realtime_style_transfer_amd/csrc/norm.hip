@@ -15,17 +15,21 @@ namespace rst {
 
 constexpr int FIN_THREADS = 512;
 
-template <typename T>
+template <int NT, typename T>
 __device__ __forceinline__ T block_sum(T v, T* scratch) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) scratch[wave] = v;
-    __syncthreads();
-    T t = scratch[0];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);   // a + b == b + a: every lane ends equal
+    if constexpr (NT == 64) {
+        return v;
+    } else {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (lane == 0) scratch[wave] = v;
+        __syncthreads();
+        T t = scratch[0];
 #pragma unroll
-    for (int w = 1; w < FIN_THREADS / 64; ++w) t += scratch[w];   // fixed order: deterministic
-    return t;
+        for (int w = 1; w < NT / 64; ++w) t += scratch[w];   // fixed order: deterministic
+        return t;
+    }
 }
 
 // One pass over the partials of channel c: S = sum s_t, N = sum n_t, Q = sum (M2_t + s_t^2 / n_t), all
@@ -33,8 +37,11 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
 // cancellation in Q - S^2/N costs log2(mean^2/var) bits of f64's 53 (mean/std ~ 20 here: ~9 bits),
 // far below f32 resolution. Four independent loads per thread per iteration keep enough reads in
 // flight for the layers with few channels and many tiles (expand_1: 16 channels x 14400 partials).
-__global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
-    __shared__ double scratch[3][FIN_THREADS / 64];
+// NT = 512 for the layers with many partials per channel; NT = 64 (one wave: no LDS, no barrier —
+// the kernel is pure latency) when a channel has at most 2048 (the residual convs: 225 at B=1).
+template <int NT>
+__global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
+    __shared__ double scratch[3][NT / 64];
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     const int b0 = a.merge_images ? 0 : b, b1 = a.merge_images ? a.batch : b + 1;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, n[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
@@ -50,16 +57,15 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
         for (int ph = 0; ph < a.phases; ++ph) {
             const float4* p = a.part + ((size_t)bb * a.ntot + ph * a.C + c) * a.n_part;
             int t = tid;
-            for (; t + 3 * FIN_THREADS < a.n_part; t += 4 * FIN_THREADS) {
-                const float4 v0 = p[t], v1 = p[t + FIN_THREADS], v2 = p[t + 2 * FIN_THREADS],
-                             v3 = p[t + 3 * FIN_THREADS];
+            for (; t + 3 * NT < a.n_part; t += 4 * NT) {
+                const float4 v0 = p[t], v1 = p[t + NT], v2 = p[t + 2 * NT], v3 = p[t + 3 * NT];
                 add(v0, 0); add(v1, 1); add(v2, 2); add(v3, 3);
             }
-            for (; t < a.n_part; t += FIN_THREADS) add(p[t], 0);
+            for (; t < a.n_part; t += NT) add(p[t], 0);
         }
-    double S = block_sum((s[0] + s[1]) + (s[2] + s[3]), scratch[0]);
-    double N = block_sum((n[0] + n[1]) + (n[2] + n[3]), scratch[1]);
-    double Q = block_sum((q[0] + q[1]) + (q[2] + q[3]), scratch[2]);
+    double S = block_sum<NT>((s[0] + s[1]) + (s[2] + s[3]), scratch[0]);
+    double N = block_sum<NT>((n[0] + n[1]) + (n[2] + n[3]), scratch[1]);
+    double Q = block_sum<NT>((q[0] + q[1]) + (q[2] + q[3]), scratch[2]);
     if (tid == 0) {
         const double mean = N > 0.0 ? S / N : 0.0;
         const double m2 = N > 0.0 ? fmax(Q - S * mean, 0.0) : 0.0;
@@ -91,7 +97,11 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
 }
 
 hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(a.C, a.batch), dim3(FIN_THREADS), 0, st, a);
+    const long per_channel = (long)a.n_part * a.phases * (a.merge_images ? a.batch : 1);
+    if (per_channel <= 2048)
+        hipLaunchKernelGGL(finalize_kernel<64>, dim3(a.C, a.batch), dim3(64), 0, st, a);
+    else
+        hipLaunchKernelGGL(finalize_kernel<FIN_THREADS>, dim3(a.C, a.batch), dim3(FIN_THREADS), 0, st, a);
     return hipGetLastError();
 }
 
