@@ -37,8 +37,9 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
 // cancellation in Q - S^2/N costs log2(mean^2/var) bits of f64's 53 (mean/std ~ 20 here: ~9 bits),
 // far below f32 resolution. Four independent loads per thread per iteration keep enough reads in
 // flight for the layers with few channels and many tiles (expand_1: 16 channels x 14400 partials).
-// NT = 512 for the layers with many partials per channel; NT = 64 (one wave: no LDS, no barrier —
-// the kernel is pure latency) when a channel has at most 2048 (the residual convs: 225 at B=1).
+// NT = 512 for the layers with many partials per channel (1024 threads measured no faster for
+// expand_1's 16 x 14400); NT = 64 (one wave: no LDS, no barrier — the kernel is pure latency) when a
+// channel has at most 2048 (the residual convs: 225 at B=1).
 template <int NT>
 __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
     __shared__ double scratch[3][NT / 64];
