@@ -187,12 +187,13 @@ def test_training_step_matches_oracle(name, precision, gtol, transfer):
     assert gerr < gtol, gerr
 
 
-def test_training_step_is_deterministic_and_learns():
+@pytest.mark.parametrize("transfer", ["fp32", "fp32_winograd"])
+def test_training_step_is_deterministic_and_learns(transfer):
     _need_gpu()
     cfg = CONFIGS['A']
     B = 2
     plan, w, vgg, content, sp, gtc, gts = _case(cfg, B)
-    tr = _trainer(cfg, w, vgg, B)
+    tr = _trainer(cfg, w, vgg, B, transfer=transfer)
     c, s, gc, gs = _cuda(content, sp, gtc, gts)
     _, l1, g1, s1 = tr.compute_gradients(c, s, gc, gs)
     g1, s1, l1 = g1.clone(), s1.clone(), l1.clone()
