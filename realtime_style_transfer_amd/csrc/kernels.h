@@ -80,8 +80,10 @@ struct Wino9Args {
     const float* in;        // NHWC [B][H][W][cin] network input
     const float* U;         // transformed weights [9][16][2][32][12]
     const float* bias;      // [32]
-    const float2* bn_ab;    // [32] BatchNorm affine (folded moving statistics)
+    const float2* bn_ab;    // [32] BatchNorm affine (folded moving statistics); inference only
     float* out;             // NHWC [B][H][W][32]
+    float4* part;           // training: out = ReLU(conv + bias) and per-tile {sum, M2, n} at
+                            // [B][32][tiles_y*tiles_x] for the batch-statistics BatchNorm; null: inference
     int batch, H, W, cin, tiles_y, tiles_x;
 };
 bool wino9_supported(int kh, int stride, int cin, int cout);
@@ -102,6 +104,8 @@ hipError_t gbuffer_resize_crop_launch(const GbufferArgs& a, hipStream_t st);
 int wino9_tiles_y(int H);
 int wino9_tiles_x(int W);
 std::vector<float> wino9_pack_weights(const float* kern, int cin);
+// wino9_pack_weights on the device (kern: HWIO [9][9][cin][32] on the device; U zero-initialised)
+hipError_t wino9_transform_launch(const float* kern, int cin, float* U, hipStream_t st);
 hipError_t wino9_launch(const Wino9Args& a, hipStream_t st);
 int wino_tiles_y(int H);
 int wino_tiles_x(int W);

@@ -174,7 +174,8 @@ namespace {
 
 int repack(rst_trainer* t, hipStream_t st) {
     for (TLayer& T : t->L) {
-        if (T.wino_fwd) RST_HIP_TRY(wino_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
+        if (T.e.kind == K_WINO9) RST_HIP_TRY(wino9_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
+        else if (T.wino_fwd) RST_HIP_TRY(wino_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
         else RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_w, T.e.d_w, T.n_w, st));
         RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_b, T.e.d_bias, T.n_b, st));
         if (T.has_dgrad && T.wino_dg) {
@@ -211,6 +212,20 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.tiles_y = e.tiles_y;
             a.tiles_x = e.tiles_x;
             RST_HIP_TRY(small_conv_launch(a, st));
+        } else if (e.kind == K_WINO9) {
+            Wino9Args a{};
+            a.in = content;
+            a.U = e.d_w;
+            a.bias = e.d_bias;
+            a.out = e.d_out;
+            a.part = e.d_part;
+            a.batch = B;
+            a.H = e.s.H;
+            a.W = e.s.W;
+            a.cin = e.s.cin;
+            a.tiles_y = e.tiles_y;
+            a.tiles_x = e.tiles_x;
+            RST_HIP_TRY(wino9_launch(a, st));
         } else if (e.kind == K_WINO) {
             WinoArgs a{};
             a.in = Pv->e.d_out;
@@ -516,10 +531,13 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
         for (int c = 0; c < s.cout; ++c) bidx[c] = (float)(T.boff + c + 1);
         std::vector<float> packed, bias_n;
         // residual convs on Winograd when asked (their prologue always materialises the input for wgrad)
-        const int lp = (precision == RST_PRECISION_FP32_WINOGRAD && s.res_block >= 0) ? precision : RST_PRECISION_FP32;
+        // and the 9x9 start conv on the composite Winograd kernel (training mode: raw ReLU output + tile stats)
+        const int lp = (precision == RST_PRECISION_FP32_WINOGRAD && (s.res_block >= 0 || li == 0))
+                           ? precision : RST_PRECISION_FP32;
         if ((st = prepare_layer(T.e, s, kidx.data(), bidx.data(), packed, bias_n, lp)) != RST_OK)
             return fail_delete(t, st);
-        T.wino_fwd = T.e.kind == K_WINO;
+        T.wino_fwd = T.e.kind == K_WINO || T.e.kind == K_WINO9;
+        if (T.e.kind == K_WINO9) T.e.n_part = T.e.tiles_y * T.e.tiles_x;   // batch statistics per tile
         std::vector<int> mw = T.wino_fwd ? std::vector<int>() : to_map(packed), mb = to_map(bias_n);
         T.n_w = packed.size();
         T.n_b = mb.size();
@@ -605,7 +623,7 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
     }
     for (auto& T : t->L) {
         if (T.e.kind != K_SMALL) {
-            hipError_t pe = T.wino_fwd ? wino_prepare() : conv_prepare(T.e.tile);
+            hipError_t pe = T.e.kind == K_WINO9 ? hipSuccess : (T.wino_fwd ? wino_prepare() : conv_prepare(T.e.tile));
             if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));
         }
         if (T.has_dgrad) {

@@ -64,6 +64,7 @@ __device__ __forceinline__ void sfor(F&& f) {
 template <int CINT>
 __global__ __launch_bounds__(256, 2) void wino9_conv_kernel(Wino9Args a) {
     __shared__ __attribute__((aligned(16))) float smem[LDS_FL];
+    __shared__ float red[2][4][NT];   // training statistics: per-wave partial sums
     float* const patch = smem;              // [384][19]
     float* const vs = smem + PATCH_FL;      // [16][32][20]
     float* const ms = smem;                 // [16][32][33] after the main loop
@@ -218,7 +219,10 @@ __global__ __launch_bounds__(256, 2) void wino9_conv_kernel(Wino9Args a) {
     // ---- output transform + epilogue: thread = (channel co, tiles 4g..4g+3) ----------------------
     const int co = tid & 31, g = tid >> 5;
     const float bias = a.bias[co];
-    const float2 bn = a.bn_ab[co];
+    const bool train = a.part != nullptr;
+    const float2 bn = train ? make_float2(1.f, 0.f) : a.bn_ab[co];
+    float yv[16];
+    float s = 0.f, cnt = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int tile = g * 4 + k;
@@ -238,10 +242,47 @@ __global__ __launch_bounds__(256, 2) void wino9_conv_kernel(Wino9Args a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
-            if (oy < H && ox < W) {
-                const float v = fmaxf(yy[q] + bias, 0.f);                 // Conv2D(..., activation='relu')
-                a.out[(img + (size_t)oy * W + ox) * NT + co] = fmaxf(fmaf(bn.x, v, bn.y), 0.f);   // BN -> ReLU
+            const bool ok = oy < H && ox < W;
+            const float v = fmaxf(yy[q] + bias, 0.f);                 // Conv2D(..., activation='relu')
+            yv[k * 4 + q] = ok ? v : 0.f;
+            if (ok) {
+                // inference: BN (folded moving statistics) -> ReLU; training: the raw ReLU output, the
+                // consumer's prologue applies the batch-statistics BN + ReLU
+                a.out[(img + (size_t)oy * W + ox) * NT + co] = train ? v : fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                s += v;
+                cnt += 1.f;
             }
+        }
+    }
+    if (train) {   // per-tile {sum, M2, n} of channel co over the 128 pixels (two-pass, fixed order)
+        s += __shfl_xor(s, 32);
+        cnt += __shfl_xor(cnt, 32);
+        if (lane < 32) {
+            red[0][wave][co] = s;
+            red[1][wave][co] = cnt;
+        }
+        __syncthreads();
+        const float S = (red[0][0][co] + red[0][1][co]) + (red[0][2][co] + red[0][3][co]);
+        const float N = (red[1][0][co] + red[1][1][co]) + (red[1][2][co] + red[1][3][co]);
+        const float mean = N > 0.f ? S / N : 0.f;
+        float m2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int tile = g * 4 + k;
+                const int oy = y0 + 2 * (tile >> 3) + (q >> 1), ox = x0 + 2 * (tile & 7) + (q & 1);
+                const float d = yv[k * 4 + q] - mean;
+                if (oy < H && ox < W) m2 = fmaf(d, d, m2);
+            }
+        m2 += __shfl_xor(m2, 32);
+        __syncthreads();
+        if (lane < 32) red[0][wave][co] = m2;
+        __syncthreads();
+        if (tid < 32) {
+            const float M2 = (red[0][0][co] + red[0][1][co]) + (red[0][2][co] + red[0][3][co]);
+            const int n_part = a.tiles_y * a.tiles_x;
+            a.part[((size_t)b * NT + co) * n_part + ty * a.tiles_x + tx] = make_float4(S, M2, N, 0.f);
         }
     }
 }
@@ -254,6 +295,7 @@ int wino9_tiles_x(int W) { return (W + TW - 1) / TW; }
 // ch(kk, lh) (kk 0..3: kk + 4lh; 4..7: 8 + (kk-4) + 4lh; 8: 16 + lh) and output channel li;
 // g_ab[i][j] = Keras HWIO kernel (9, 9, cin, 32) at tap (3a + i, 3b + j); channels >= cin are zero.
 std::vector<float> wino9_pack_weights(const float* kern, int cin) {
+#pragma clang fp contract(off)   // same operation order as wino9_transform_kernel
     static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
     std::vector<float> U((size_t)9 * NXI * 64 * USTR, 0.f);
     for (int ab = 0; ab < 9; ++ab) {
@@ -279,6 +321,43 @@ std::vector<float> wino9_pack_weights(const float* kern, int cin) {
             }
     }
     return U;
+}
+
+// Device form of wino9_pack_weights (training re-packs after every optimizer step): one thread per
+// (ab, lh, kk, co); f64 with the host's operation order and no contraction (bitwise the host image).
+// Entries for channels >= cin and the 3 pad slots are never written (U is zero-initialised).
+__global__ __launch_bounds__(256) void wino9_transform_kernel(const float* __restrict__ kern, int cin,
+                                                              float* __restrict__ U) {
+#pragma clang fp contract(off)
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= 9 * 2 * 9 * NT) return;
+    const int co = idx % NT, kk = (idx / NT) % 9, lh = (idx / (NT * 9)) % 2, ab = idx / (NT * 9 * 2);
+    const int ci = kk < 4 ? kk + 4 * lh : (kk < 8 ? 8 + (kk - 4) + 4 * lh : 16 + lh);
+    if (ci >= cin) return;
+    const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    const int sa = ab / 3, sb = ab % 3;
+    double gg[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) gg[i][j] = kern[(((size_t)(3 * sa + i) * 9 + (3 * sb + j)) * cin + ci) * NT + co];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double u = 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) u = u + G[p][i] * gg[i][j] * G[q][j];
+            U[((((size_t)ab * NXI + p * 4 + q) * 2 + lh) * 32 + co) * USTR + kk] = (float)u;
+        }
+}
+
+hipError_t wino9_transform_launch(const float* kern, int cin, float* U, hipStream_t st) {
+    if (cin > 17 || cin <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wino9_transform_kernel, dim3((9 * 2 * 9 * NT + 255) / 256), dim3(256), 0, st, kern, cin, U);
+    return hipGetLastError();
 }
 
 hipError_t wino9_launch(const Wino9Args& a, hipStream_t st) {
