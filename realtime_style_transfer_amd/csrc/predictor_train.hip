@@ -315,14 +315,23 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const float* __restrict__
         *reinterpret_cast<float4*>(slab + ((size_t)blockIdx.z * cin + ci) * cout + co) = acc;
 }
 
-// out[i] (=|+=) sum_s slab[s][i], fixed order
+// out[i] = sum_s slab[s][i], fixed order: a workgroup owns 64 consecutive outputs; its four waves sum
+// contiguous quarters of the split range (8 loads in flight per lane) and wave 0 adds the quarters in
+// order (one lane per output walking all S splits serially was latency-bound: 34 us for S = 512)
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int S, size_t n,
                                                        float* __restrict__ out) {
-    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        float s = 0.f;
-        for (int k = 0; k < S; ++k) s += slab[(size_t)k * n + i];
-        out[i] = s;
+    __shared__ float part[3][64];
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const size_t i = (size_t)blockIdx.x * 64 + lane;
+    float s = 0.f;
+    if (i < n) {
+        const int k0 = (S * q) / 4, k1 = (S * (q + 1)) / 4;
+#pragma unroll 8
+        for (int k = k0; k < k1; ++k) s += slab[(size_t)k * n + i];
     }
+    if (q > 0) part[q - 1][lane] = s;
+    __syncthreads();
+    if (q == 0 && i < n) out[i] = ((s + part[0][lane]) + part[1][lane]) + part[2][lane];
 }
 
 // w [rows][cols] -> wt [cols][rows]
@@ -712,7 +721,7 @@ hipError_t pw_wgrad_launch(const float* x, const float* se, const float* dz, int
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t n = (size_t)cin * cout;
-    slab_sum_kernel<<<grid1d(n, 1024), 256, 0, st>>>(slab, S, n, dW);
+    slab_sum_kernel<<<(unsigned)((n + 63) / 64), 256, 0, st>>>(slab, S, n, dW);
     return hipGetLastError();
 }
 
@@ -761,7 +770,7 @@ hipError_t dw_wgrad_launch(const float* x, const float* dz, int B, int H, int W,
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t n = (size_t)k * k * C;
-    slab_sum_kernel<<<grid1d(n, 1024), 256, 0, st>>>(slab, S, n, dW);
+    slab_sum_kernel<<<(unsigned)((n + 63) / 64), 256, 0, st>>>(slab, S, n, dW);
     return hipGetLastError();
 }
 
@@ -782,7 +791,7 @@ hipError_t stem_wgrad_launch(const float* x, const float* dz, int B, int H, int 
     stem_wgrad_kernel<<<S, 128, 0, st>>>(x, dz, B, H, W, Ho, Wo, pad_t, pad_l, pps, slab);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    slab_sum_kernel<<<grid1d(432, 1024), 256, 0, st>>>(slab, S, 432, dW);
+    slab_sum_kernel<<<(432 + 63) / 64, 256, 0, st>>>(slab, S, 432, dW);
     return hipGetLastError();
 }
 
