@@ -368,6 +368,7 @@ def main():
     ap.add_argument("--no-bf16x3", action="store_true", help="skip the other precision-mode measurements")
     ap.add_argument("--no-predictor", action="store_true", help="skip the style-predictor measurement")
     ap.add_argument("--no-ingest", action="store_true", help="skip the G-buffer ingest measurement")
+    ap.add_argument("--pcie-steps", type=int, default=50, help="host-resident frame loop (PCIe-inclusive); 0 to skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -437,6 +438,69 @@ def main():
             graph.replay()
         torch.cuda.synchronize()
         elapsed = timed(graph.replay, args.steps)
+    # ---------------- PCIe-inclusive rate (reported beside the headline, never as `value`) ------
+    # The C-ABI hands over device pointers; a host-resident frame loop adds H2D of the 31 MB
+    # G-buffer and D2H of the 5.5 MB output per frame. "serial": upload -> graph -> download on one
+    # stream. "pipelined": two input/output buffer pairs and two graphs; frame i+1 is uploaded and
+    # frame i-1 downloaded on a copy stream while frame i computes (pinned host buffers).
+    pcie = None
+    if graph is not None and args.pcie_steps > 0:
+        n = args.pcie_steps
+        h_in = [torch.from_numpy(rng.random((B,) + ins, dtype=np.float32)).pin_memory() for _ in range(2)]
+        h_out = [torch.empty((B,) + outs, dtype=torch.float32).pin_memory() for _ in range(2)]
+
+        def serial():
+            content.copy_(h_in[0], non_blocking=True)
+            graph.replay()
+            h_out[0].copy_(out, non_blocking=True)
+
+        serial()
+        torch.cuda.synchronize()
+        el_serial = timed(serial, n)
+        d_in = [content, torch.empty_like(content)]
+        d_out = [out, torch.empty_like(out)]
+        graphs = [graph, torch.cuda.CUDAGraph()]
+        inputs2 = {'content': d_in[1], 'style_params': style}
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            model(inputs2, out=d_out[1])
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.cuda.graph(graphs[1]):
+            model(inputs2, out=d_out[1])
+        comp, copy = torch.cuda.current_stream(), torch.cuda.Stream()
+        up_done = [torch.cuda.Event(), torch.cuda.Event()]
+        comp_done = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def pipelined():
+            # frame i in slot 0/1 alternately: upload(i) on copy, compute(i) on comp, download(i) on copy
+            torch.cuda.synchronize()
+            with torch.cuda.stream(copy):
+                d_in[0].copy_(h_in[0], non_blocking=True)
+                up_done[0].record(copy)
+            for i in range(n):
+                s = i & 1
+                comp.wait_event(up_done[s])
+                graphs[s].replay()
+                comp_done[s].record(comp)
+                with torch.cuda.stream(copy):
+                    if i + 1 < n:
+                        if i >= 1:
+                            copy.wait_event(comp_done[s ^ 1])   # slot reuse: frame i-1 has computed
+                        d_in[s ^ 1].copy_(h_in[s ^ 1], non_blocking=True)
+                        up_done[s ^ 1].record(copy)
+                    copy.wait_event(comp_done[s])
+                    h_out[s].copy_(d_out[s], non_blocking=True)
+            comp.wait_stream(copy)
+
+        el_pipe = timed(pipelined, 1)
+        frame_bytes = B * (int(np.prod(ins)) + int(np.prod(outs))) * 4
+        pcie = {"serial_fps": round(world * B * n / el_serial, 3),
+                "pipelined_fps": round(world * B * n / el_pipe, 3),
+                "frames": n, "bytes_per_frame_h2d_d2h": frame_bytes // B,
+                "note": "pinned host frames; serial = H2D + graph + D2H per frame on one stream; pipelined = "
+                        "double-buffered, copies on a second stream overlapping the compute"}
+        torch.cuda.synchronize()
     # ---------------- timed region 2: eager launches with per-layer HIP events -----------------
     # (every kernel recorded between events on the forward's stream -> per-kernel durations for
     # the roofline; also the eager FPS)
@@ -581,6 +645,7 @@ def main():
             "fps_per_gpu": round(fps / world, 3),
             "timing": "hipGraph replay per step" if graph is not None else "eager launches",
             "eager_fps": round(fps_eager, 3),
+            "pcie_inclusive": pcie,
             "max_abs_delta_vs_oracle": max_abs,
             "roofline": {
                 "bound": "mfma",

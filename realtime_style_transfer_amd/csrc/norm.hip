@@ -35,16 +35,35 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
 // One pass over the partials of channel c: S = sum s_t, N = sum n_t, Q = sum (M2_t + s_t^2 / n_t), all
 // in f64; then M2 = Q - S^2/N. Equal to Chan's pairwise merge sum M2_t + n_t (mean_t - mean)^2; the
 // cancellation in Q - S^2/N costs log2(mean^2/var) bits of f64's 53 (mean/std ~ 20 here: ~9 bits),
-// far below f32 resolution. Four independent loads per thread per iteration keep enough reads in
-// flight for the layers with few channels and many tiles (expand_1: 16 channels x 14400 partials).
-// NT = 512 for the layers with many partials per channel (1024 threads measured no faster for
-// expand_1's 16 x 14400); NT = 64 (one wave: no LDS, no barrier — the kernel is pure latency) when a
-// channel has at most 2048 (the residual convs: 225 at B=1).
+// far below f32 resolution. The kernel is pure latency (a few thousand float4 per channel, few
+// channels), so the (image, phase, tile) index space is walked as ONE flat range with FIN_UNROLL
+// independent loads issued per thread before any is consumed: every residual CIN (225 partials, one
+// wave) and expand_1 / expand_last (3600 partials, 512 threads) finish in a single memory round trip
+// (the former per-phase loop with a 4-deep main body left most lanes in a serial remainder loop:
+// 3-8 dependent round trips). The style affine is fetched before the loop so its latency overlaps.
+// Summation order is fixed (accumulator j = k mod 4, then a fixed-order block sum): deterministic.
+constexpr int FIN_UNROLL = 8;
+
 template <int NT>
 __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
     __shared__ double scratch[3][NT / 64];
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-    const int b0 = a.merge_images ? 0 : b, b1 = a.merge_images ? a.batch : b + 1;
+    const int b0 = a.merge_images ? 0 : b, nb = a.merge_images ? a.batch : 1;
+    float scale = 1.f, bias = 0.f, scale1 = 0.f, bias1 = 0.f;
+    if (tid == 0) {   // issued before the partial loads: independent of them
+        if (a.style != nullptr) {
+            const float* sp = a.style + (size_t)b * a.style_stride + a.style_offset;
+            scale = sp[c];
+            bias = sp[a.C + c];
+            if (a.ab1 != nullptr) {
+                scale1 = sp[a.style1_offset + c];
+                bias1 = sp[a.style1_offset + a.C + c];
+            }
+        } else if (a.scale != nullptr) {
+            scale = a.scale[b * a.affine_bstride + c];
+            bias = a.bias[b * a.affine_bstride + c];
+        }
+    }
     double s[4] = {0.0, 0.0, 0.0, 0.0}, n[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
     auto add = [&](const float4& v, int j) __attribute__((always_inline)) {
         if (v.z > 0.f) {
@@ -54,16 +73,22 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
             q[j] += (double)v.y + sv * sv / (double)v.z;
         }
     };
-    for (int bb = b0; bb < b1; ++bb)
-        for (int ph = 0; ph < a.phases; ++ph) {
-            const float4* p = a.part + ((size_t)bb * a.ntot + ph * a.C + c) * a.n_part;
-            int t = tid;
-            for (; t + 3 * NT < a.n_part; t += 4 * NT) {
-                const float4 v0 = p[t], v1 = p[t + NT], v2 = p[t + 2 * NT], v3 = p[t + 3 * NT];
-                add(v0, 0); add(v1, 1); add(v2, 2); add(v3, 3);
-            }
-            for (; t < a.n_part; t += NT) add(p[t], 0);
+    const int per_img = a.phases * a.n_part, total = nb * per_img;
+    auto item = [&](int i) __attribute__((always_inline)) -> const float4* {
+        const int bi = i / per_img, r = i - bi * per_img;
+        const int ph = r / a.n_part, t = r - ph * a.n_part;
+        return a.part + ((size_t)(b0 + bi) * a.ntot + ph * a.C + c) * a.n_part + t;
+    };
+    for (int base = tid; base < total; base += FIN_UNROLL * NT) {
+        float4 v[FIN_UNROLL];
+#pragma unroll
+        for (int k = 0; k < FIN_UNROLL; ++k) {
+            const int i = base + k * NT;
+            v[k] = i < total ? *item(i) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+#pragma unroll
+        for (int k = 0; k < FIN_UNROLL; ++k) add(v[k], k & 3);
+    }
     double S = block_sum<NT>((s[0] + s[1]) + (s[2] + s[3]), scratch[0]);
     double N = block_sum<NT>((n[0] + n[1]) + (n[2] + n[3]), scratch[1]);
     double Q = block_sum<NT>((q[0] + q[1]) + (q[2] + q[3]), scratch[2]);
@@ -72,21 +97,11 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
         const double m2 = N > 0.0 ? fmax(Q - S * mean, 0.0) : 0.0;
         const double var = N > 0.0 ? m2 / N : 0.0;
         const float rstd = (float)(1.0 / sqrt(var + (double)a.eps));
-        float scale = 1.f, bias = 0.f;
-        if (a.style != nullptr) {
-            const float* sp = a.style + (size_t)b * a.style_stride + a.style_offset;
-            scale = sp[c];
-            bias = sp[a.C + c];
-        } else if (a.scale != nullptr) {
-            scale = a.scale[b * a.affine_bstride + c];
-            bias = a.bias[b * a.affine_bstride + c];
-        }
         const float aa = scale * rstd;
         a.ab[b * a.C + c] = make_float2(aa, bias - (float)mean * aa);
         if (a.ab1 != nullptr) {   // second style (styleTransfer.py:36-44 blends the affine per pixel)
-            const float* sp1 = a.style + (size_t)b * a.style_stride + a.style1_offset + a.style_offset;
-            const float a1 = sp1[c] * rstd;
-            a.ab1[b * a.C + c] = make_float2(a1, sp1[a.C + c] - (float)mean * a1);
+            const float a1 = scale1 * rstd;
+            a.ab1[b * a.C + c] = make_float2(a1, bias1 - (float)mean * a1);
         }
         if (a.mr != nullptr) a.mr[b * a.C + c] = make_float2((float)mean, rstd);
         if (a.moving_mean != nullptr && b == 0) {
@@ -99,7 +114,7 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
 
 hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st) {
     const long per_channel = (long)a.n_part * a.phases * (a.merge_images ? a.batch : 1);
-    if (per_channel <= 2048)
+    if (per_channel <= FIN_UNROLL * 64)
         hipLaunchKernelGGL(finalize_kernel<64>, dim3(a.C, a.batch), dim3(64), 0, st, a);
     else
         hipLaunchKernelGGL(finalize_kernel<FIN_THREADS>, dim3(a.C, a.batch), dim3(FIN_THREADS), 0, st, a);
