@@ -35,16 +35,17 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
 // One pass over the partials of channel c: S = sum s_t, N = sum n_t, Q = sum (M2_t + s_t^2 / n_t), all
 // in f64; then M2 = Q - S^2/N. Equal to Chan's pairwise merge sum M2_t + n_t (mean_t - mean)^2; the
 // cancellation in Q - S^2/N costs log2(mean^2/var) bits of f64's 53 (mean/std ~ 20 here: ~9 bits),
-// far below f32 resolution. The kernel is pure latency (a few thousand float4 per channel, few
-// channels), so the (image, phase, tile) index space is walked as ONE flat range with FIN_UNROLL
-// independent loads issued per thread before any is consumed: every residual CIN (225 partials, one
-// wave) and expand_1 / expand_last (3600 partials, 512 threads) finish in a single memory round trip
-// (the former per-phase loop with a 4-deep main body left most lanes in a serial remainder loop:
-// 3-8 dependent round trips). The style affine is fetched before the loop so its latency overlaps.
+// far below f32 resolution. The (image, phase, tile) index space is walked as ONE flat range with
+// FIN_UNROLL unconditional loads per thread (index clamped, value masked) issued before any is
+// consumed — a guarded load per item made hipcc wait on each load before the next. Shapes at B=1:
+// residual CINs 128 x 225 partials (one wave per channel), expand_0 32 x 3600 and expand_1 16 x 14400
+// (512 threads), expand_last 3 x 450. tools/fin_probe: a launch costs ~1.5-1.9 us empty and ~3.8 us
+// for the residual shape; expand_1 (11 us) is bound by the f64 statistics arithmetic on its 16 CUs.
+// The style affine is fetched before the loop so its latency overlaps the partial reads.
 // Summation order is fixed (accumulator j = k mod 4, then a fixed-order block sum): deterministic.
 constexpr int FIN_UNROLL = 8;
 
-template <int NT>
+template <int NT, int U = FIN_UNROLL>
 __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
     __shared__ double scratch[3][NT / 64];
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -64,13 +65,20 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
             bias = a.bias[b * a.affine_bstride + c];
         }
     }
-    double s[4] = {0.0, 0.0, 0.0, 0.0}, n[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+    // s_t^2 / n_t uses v_rcp_f64 plus one Newton step (error ~1 ulp of f64, 2^-52 relative: far below
+    // the f32 result) instead of the IEEE f64 division sequence (~11 f64 instructions, the bulk of
+    // this kernel's time: the statistics arithmetic, not the reads, set expand_1's 12 us);
+    // n accumulates in f32 (tile counts are small integers: exact below 2^24 per accumulator).
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+    float n[4] = {0.f, 0.f, 0.f, 0.f};
     auto add = [&](const float4& v, int j) __attribute__((always_inline)) {
         if (v.z > 0.f) {
-            const double sv = (double)v.x;
+            const double sv = (double)v.x, nv = (double)v.z;
+            double r = __builtin_amdgcn_rcp(nv);
+            r = fma(fma(-nv, r, 1.0), r, r);
             s[j] += sv;
-            n[j] += (double)v.z;
-            q[j] += (double)v.y + sv * sv / (double)v.z;
+            n[j] += v.z;
+            q[j] += (double)v.y + sv * sv * r;
         }
     };
     const int per_img = a.phases * a.n_part, total = nb * per_img;
@@ -79,18 +87,19 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
         const int ph = r / a.n_part, t = r - ph * a.n_part;
         return a.part + ((size_t)(b0 + bi) * a.ntot + ph * a.C + c) * a.n_part + t;
     };
-    for (int base = tid; base < total; base += FIN_UNROLL * NT) {
-        float4 v[FIN_UNROLL];
+    const int hi = total;
+    for (int base = tid; base < hi; base += U * NT) {
+        // unconditional loads (index clamped into range, the value masked afterwards): a guarded load
+        // per k made hipcc wait for each load before issuing the next (one load in flight per lane)
+        float4 v[U];
 #pragma unroll
-        for (int k = 0; k < FIN_UNROLL; ++k) {
-            const int i = base + k * NT;
-            v[k] = i < total ? *item(i) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int k = 0; k < U; ++k) v[k] = *item(min(base + k * NT, hi - 1));
 #pragma unroll
-        for (int k = 0; k < FIN_UNROLL; ++k) add(v[k], k & 3);
+        for (int k = 0; k < U; ++k)
+            if (base + k * NT < hi) add(v[k], k & 3);
     }
     double S = block_sum<NT>((s[0] + s[1]) + (s[2] + s[3]), scratch[0]);
-    double N = block_sum<NT>((n[0] + n[1]) + (n[2] + n[3]), scratch[1]);
+    double N = block_sum<NT>(((double)n[0] + (double)n[1]) + ((double)n[2] + (double)n[3]), scratch[1]);
     double Q = block_sum<NT>((q[0] + q[1]) + (q[2] + q[3]), scratch[2]);
     if (tid == 0) {
         const double mean = N > 0.0 ? S / N : 0.0;
@@ -116,7 +125,10 @@ hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st) {
     const long per_channel = (long)a.n_part * a.phases * (a.merge_images ? a.batch : 1);
     if (per_channel <= FIN_UNROLL * 64)
         hipLaunchKernelGGL(finalize_kernel<64>, dim3(a.C, a.batch), dim3(64), 0, st, a);
-    else
+    else   // expand_1 (16 x 14400 at B=1) is f64-arithmetic-bound on its 16 CUs (tools/fin_probe: the
+           // same reads alone take 4 us of its 11); a 1024-thread variant measured no faster, and a
+           // split over 15 workgroups per channel with a last-arriver merge no faster either (the
+           // agent-scope release each writer needs costs an L2 write-back)
         hipLaunchKernelGGL(finalize_kernel<FIN_THREADS>, dim3(a.C, a.batch), dim3(FIN_THREADS), 0, st, a);
     return hipGetLastError();
 }

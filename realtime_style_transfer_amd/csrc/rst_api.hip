@@ -567,6 +567,10 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             f.style1_offset = h->P;
         }
         f.eps = 1e-5f;
+        static const bool dbg = std::getenv("RST_DEBUG_FINALIZE") != nullptr;
+        if (dbg)
+            std::fprintf(stderr, "finalize %s: C=%d ntot=%d n_part=%d phases=%d batch=%d\n", e.s.name.c_str(), f.C,
+                         f.ntot, f.n_part, f.phases, f.batch);
         HIP_TRY(finalize_launch(f, st));
     }
     if (ev) HIP_TRY(hipEventRecord(ev[2], st));

@@ -97,6 +97,40 @@ def test_full_size_matches_torch_oracle():
     assert mism < 1e-3
 
 
+def test_full_size_repeated_calls_mixed_batch():
+    """Full size, one handle: B=2, then B=1 on other content, then B=2 again all match the oracle and
+    the repeated call is bitwise equal (no state — CIN partials, affines, workspaces — carries over
+    from a previous call; expand_1's finalize walks 14400 partials per channel here)."""
+    _need_gpu()
+    from oracle.torch_ref import TorchTransfer
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    cfg = ShapeConfig.from_spec("rst-960-120-128-17")
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    ws = init_weights(plan, seed=2)
+    model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                           weights=ws, max_batch=2)
+    ref_net = TorchTransfer(ws, ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    rng = np.random.default_rng(7)
+    x2 = rng.random((2,) + ins).astype(np.float32)
+    x1 = rng.random((1,) + ins).astype(np.float32)
+    sp2 = synthetic_style_params(2, 1, P, plan, seed=3)
+
+    def run(x, sp):
+        return model({'content': torch.from_numpy(x).cuda(),
+                      'style_params': torch.from_numpy(np.ascontiguousarray(sp)).cuda()}).cpu().numpy()
+
+    ya = run(x2, sp2)
+    yb = run(x1, sp2[1:])
+    yc = run(x2, sp2)
+    assert np.array_equal(ya, yc)
+    for y, x, sp in ((ya[:1], x2[:1], sp2[:1]), (ya[1:], x2[1:], sp2[1:]), (yb, x1, sp2[1:])):
+        err = np.abs(y - ref_net(x, sp)).max()
+        assert err < OUT_TOL, f"max abs err {err}"
+
+
 def test_batch_and_determinism():
     _need_gpu()
     from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
