@@ -20,7 +20,14 @@
 namespace rst {
 
 namespace small {
-constexpr int K = 9, PAD = 4, RX = 4, TH = 32, TW = 32, CC = 4;
+#ifndef RST_SMALL_RX
+#define RST_SMALL_RX 4
+#endif
+// RX = 8 (64-wide tiles: 4 input + 7 weight ds_read_b128 per 108 packed FMAs instead of 3 + 7 per 54)
+// measured slower at B=1 (77.7 vs 69.6 us): its 113 KB of LDS leaves one workgroup (4 waves) per CU
+// and 225 workgroups for 256 CUs
+constexpr int K = 9, PAD = 4, RX = RST_SMALL_RX, TW = RX == 8 ? 64 : 32, TH = 256 / (TW / RX), CC = 4;
+constexpr int NX = RX + K - 1;                       // input row values per thread and (ci, ky)
 constexpr int HH = TH + K - 1, HWD = TW + K - 1;   // 40 x 40
 constexpr int RS = HWD + 4;                          // padded row stride (floats), 16-B multiple
 constexpr int SEGS = TW / RX;                        // 8 segments per row
@@ -40,7 +47,7 @@ typedef float sf32x2 __attribute__((ext_vector_type(2)));
 #define RST_SMALL_OPT 2
 #endif
 template <int SOPT>
-__global__ __launch_bounds__(256, 2) void small_conv_kernel(SmallConvArgs a, const float* __restrict__ w,
+__global__ __launch_bounds__(256, RST_SMALL_RX == 8 ? 1 : 2) void small_conv_kernel(SmallConvArgs a, const float* __restrict__ w,
                                                             const float* __restrict__ in) {
     using namespace small;
     constexpr bool WLDS = (SOPT & 2) != 0;
@@ -133,10 +140,12 @@ __global__ __launch_bounds__(256, 2) void small_conv_kernel(SmallConvArgs a, con
 #pragma unroll
             for (int ky = 0; ky < K; ++ky) {
                 const float* row = cur + q * PLANE + (r + ky) * RS + seg * RX;
-                const sf32x4 i0 = *reinterpret_cast<const sf32x4*>(row);
-                const sf32x4 i1 = *reinterpret_cast<const sf32x4*>(row + 4);
-                const sf32x4 i2 = *reinterpret_cast<const sf32x4*>(row + 8);
-                const float x[12] = {i0[0], i0[1], i0[2], i0[3], i1[0], i1[1], i1[2], i1[3], i2[0], i2[1], i2[2], i2[3]};
+                float x[NX];
+#pragma unroll
+                for (int j = 0; j < NX / 4; ++j) {
+                    const sf32x4 t = *reinterpret_cast<const sf32x4*>(row + 4 * j);
+                    x[4 * j] = t[0]; x[4 * j + 1] = t[1]; x[4 * j + 2] = t[2]; x[4 * j + 3] = t[3];
+                }
                 float wv[WS];
                 if constexpr (WLDS) {
                     const float* wk = wl + (ky * Cin + ci) * WS;
@@ -150,12 +159,12 @@ __global__ __launch_bounds__(256, 2) void small_conv_kernel(SmallConvArgs a, con
 #pragma unroll
                     for (int j = 0; j < WS; ++j) wv[j] = wk[j];
                 }
-                // pairs of the 12 row values: even-aligned (x0,x1),(x2,x3).. and odd-shifted (x1,x2),(x3,x4)..
-                sf32x2 xe[6], xo[5];
+                // pairs of the NX row values: even-aligned (x0,x1),(x2,x3).. and odd-shifted (x1,x2),(x3,x4)..
+                sf32x2 xe[NX / 2], xo[NX / 2 - 1];
 #pragma unroll
-                for (int j = 0; j < 6; ++j) xe[j] = sf32x2{x[2 * j], x[2 * j + 1]};
+                for (int j = 0; j < NX / 2; ++j) xe[j] = sf32x2{x[2 * j], x[2 * j + 1]};
 #pragma unroll
-                for (int j = 0; j < 5; ++j) xo[j] = sf32x2{x[2 * j + 1], x[2 * j + 2]};
+                for (int j = 0; j < NX / 2 - 1; ++j) xo[j] = sf32x2{x[2 * j + 1], x[2 * j + 2]};
 #pragma unroll
                 for (int kx = 0; kx < K; ++kx) {
 #pragma unroll
