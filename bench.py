@@ -74,22 +74,66 @@ DTYPE_DESC = {
 }
 
 
+def executed_mfma(model, plan, i: int, B: int):
+    """(FLOPs the kernel of layer i actually issues on its pipe for B images, peak TFLOP/s of that pipe).
+
+    Direct implicit-GEMM convs issue the algorithmic 2*MAC. Winograd F(2x2,3x3) issues 16 products per
+    2x2 output tile and (cin, cout) pair instead of 36 (tiles counted over the padded 8x16-pixel workgroup
+    blocks); the composite 9x9 start conv issues 16 x 9 sub-kernels x 18 channels (17 + one zero) per tile
+    and output channel. The split-bf16 kernels issue `terms` bf16 products per fp32 product on the bf16
+    pipe. The VALU 9x9 Cout=3 kernel issues the algorithmic FMAs on the f32 vector pipe (same peak)."""
+    kid = model.layer_kernel_id(i)
+    l = plan.layers[i]
+    Ho, Wo = l.out_hw
+    tiles = B * (-(-Ho // 8) * 4) * (-(-Wo // 16) * 8)
+    if kid == 200:
+        return 2.0 * tiles * 16 * l.cin * l.cout, FP32_MFMA_PEAK_TFLOPS
+    if kid == 201:
+        return 2.0 * tiles * 16 * 9 * 18 * l.cout, FP32_MFMA_PEAK_TFLOPS
+    if 101 <= kid < 200:
+        terms = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}.get(model.precision, 6)
+        return terms * layer_flops(l) * B, BF16_MFMA_PEAK_TFLOPS
+    return layer_flops(l) * B, FP32_MFMA_PEAK_TFLOPS
+
+
 def dominant_kernel(model, plan, conv_ms, nsteps, B) -> dict:
-    """The kernel (config id) with the largest summed time over the timed launches, with its
-    algorithmic TFLOP/s (direct-conv FLOPs per launch / average launch duration)."""
+    """The kernel (config id) with the largest summed time over the timed launches: its executed-work
+    rate (executed_mfma FLOPs per launch / average launch duration, against the peak of the pipe it
+    issues on) and, separately, the algorithmic (direct-conv) rate."""
     groups = {}
     for i, l in enumerate(plan.layers):
         kid = model.layer_kernel_id(i)
-        g = groups.setdefault(kid, {"ms": 0.0, "flops": 0.0, "launches": 0})
+        ex, peak = executed_mfma(model, plan, i, B)
+        g = groups.setdefault(kid, {"ms": 0.0, "flops": 0.0, "exec": 0.0, "launches": 0, "peak": peak})
         g["ms"] += conv_ms[i]
         g["flops"] += layer_flops(l) * B * nsteps
+        g["exec"] += ex * nsteps
         g["launches"] += nsteps
     kid = max(groups, key=lambda k: groups[k]["ms"])
     g = groups[kid]
     avg_ms = g["ms"] / max(g["launches"], 1)
     fpl = g["flops"] / max(g["launches"], 1)
+    epl = g["exec"] / max(g["launches"], 1)
+    sec = avg_ms * 1e-3
     return {"id": kid, "kernel": KERNEL_NAMES.get(kid, str(kid)), "avg_ms": avg_ms, "flops_per_launch": fpl,
-            "launches": g["launches"], "tflops": fpl / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0}
+            "exec_flops_per_launch": epl, "launches": g["launches"], "peak": g["peak"],
+            "tflops": fpl / sec / 1e12 if avg_ms > 0 else 0.0, "exec_tflops": epl / sec / 1e12 if avg_ms > 0 else 0.0}
+
+
+def roofline_of(dom: dict, traffic=None) -> dict:
+    """BASELINE roofline object of the dominant kernel: `achieved` = executed FLOPs per launch / average
+    launch duration (HIP events on the forward's stream in the timed region), `frac` = achieved / peak of the
+    pipe those FLOPs issue on; the direct-conv-equivalent rate is reported beside it, never as `frac`."""
+    peak = dom["peak"]
+    return {"bound": "mfma", "kernel": dom["kernel"], "achieved": round(dom["exec_tflops"], 3), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(dom["exec_tflops"] / peak, 4), "traffic": traffic,
+            "avg_launch_ms": round(dom["avg_ms"], 5), "exec_flops_per_launch": dom["exec_flops_per_launch"],
+            "launches": dom["launches"],
+            "pipe": "bf16 MFMA" if peak == BF16_MFMA_PEAK_TFLOPS else "f32 MFMA",
+            "direct_equivalent": {"flops_per_launch": dom["flops_per_launch"],
+                                  "tflops": round(dom["tflops"], 3),
+                                  "note": "algorithmic direct-conv FLOPs / launch time; > peak is possible for "
+                                          "Winograd (it issues fewer products), so this is not a roofline fraction"}}
 
 
 def cpu_threads() -> int:
@@ -120,71 +164,87 @@ def train_flops_per_sample(plan, H, W) -> dict:
             "gram_fwd_x2_bwd_x1": 3 * gram}
 
 
-def bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs, timed, precision):
-    """The same B=1 hipGraph frame loop with a split-bf16 precision mode on the residual convs."""
-    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
-    B = args.batch
-    model, _ = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
-                                           weights=weights, max_batch=B, device=dev, precision=precision)
-    out = torch.empty((B,) + outs, dtype=torch.float32, device=dev)
+def capture_graph(fn):
+    """Capture fn (one forward on torch's current stream) into a hipGraph after a warm-up launch on a side
+    stream (torch.cuda.graphs' recipe)."""
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        model(inputs, out=out)
+        fn()
     torch.cuda.current_stream().wait_stream(side)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        model(inputs, out=out)
+        fn()
+    return g
+
+
+def bench_split(args, ctx, cfg, ins, outs, plan, weights, P, inputs, precision):
+    """The same B=1 hipGraph frame loop with another precision mode (reported beside the headline)."""
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    B = args.batch
+    model, _ = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                           weights=weights, max_batch=B, device=ctx.device, precision=precision,
+                                           allow_reduced_precision=precision == "bf16")
+    out = torch.empty((B,) + outs, dtype=torch.float32, device=ctx.device)
+    g = capture_graph(lambda: model(inputs, out=out))
     for _ in range(args.warmup):
         g.replay()
     torch.cuda.synchronize()
-    el = timed(g.replay, args.steps)
+    el = ctx.timed(g.replay, args.steps)
     model.profile_begin(args.steps)
-    timed(lambda: model(inputs, out=out), args.steps)
+    ctx.timed(lambda: model(inputs, out=out), args.steps)
     conv_ms, _, nsteps = model.profile_end()
-    ids = [model.layer_kernel_id(i) for i in range(len(plan.layers))]
-    bf3 = [i for i, k in enumerate(ids) if k >= 101]
-    terms = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}.get(precision, 6)
-    ms = sum(conv_ms[i] for i in bf3) / max(nsteps, 1) / max(len(bf3), 1)
-    fl = sum(layer_flops(plan.layers[i]) for i in bf3) * B / max(len(bf3), 1)
-    eff_tf = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-    if precision == "fp32":
-        dom = dominant_kernel(model, plan, conv_ms, nsteps, B)
-        return model, {
-            "value": round(world * B * args.steps / el, 3), "unit": "frames/s",
-            "ms_per_step": round(el * 1e3 / args.steps, 4), "dtype": DTYPE_DESC["fp32"],
-            "roofline": {"bound": "mfma", "kernel": dom["kernel"], "achieved": round(dom["tflops"], 2),
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(dom["tflops"] / FP32_MFMA_PEAK_TFLOPS, 4),
-                         "avg_launch_ms": round(dom["avg_ms"], 5)},
-            "layers_ms": [round(c / max(nsteps, 1), 4) for c in conv_ms],
-        }
-    if precision == "fp32_winograd":
-        return model, {
-            "value": round(world * B * args.steps / el, 3), "unit": "frames/s",
-            "ms_per_step": round(el * 1e3 / args.steps, 4),
-            "dtype": "fp32 (exact-f32 MFMA products, f32 accumulate); the residual convs as fused Winograd "
-                     "F(2x2,3x3) (16 instead of 36 multiplies per 2x2 output tile), other layers direct",
-            "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES.get(200), "achieved": round(eff_tf, 2),
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s (algorithmic = direct-conv FLOPs)",
-                         "frac": round(eff_tf / FP32_MFMA_PEAK_TFLOPS, 4), "avg_launch_ms": round(ms, 5),
-                         "mfma_pipe_frac": round(eff_tf * 16.0 / 36.0 / FP32_MFMA_PEAK_TFLOPS, 4)},
-            "layers_ms": [round(c / max(nsteps, 1), 4) for c in conv_ms],
-        }
+    dom = dominant_kernel(model, plan, conv_ms, nsteps, B)
     return model, {
-        "value": round(world * B * args.steps / el, 3), "unit": "frames/s", "ms_per_step": round(el * 1e3 / args.steps, 4),
-        "dtype": DTYPE_DESC.get(precision, precision),
-        "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES.get(ids[bf3[0]], "?") if bf3 else None,
-                     "achieved": round(terms * eff_tf, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s (bf16 MFMA)",
-                     "frac": round(terms * eff_tf / BF16_MFMA_PEAK_TFLOPS, 4), "avg_launch_ms": round(ms, 5),
-                     "fp32_equivalent_tflops": round(eff_tf, 2)},
+        "value": round(ctx.world * B * args.steps / el, 3), "unit": "frames/s",
+        "ms_per_step": round(el * 1e3 / args.steps, 4), "dtype": DTYPE_DESC.get(precision, precision),
+        "roofline": roofline_of(dom),
         "layers_ms": [round(c / max(nsteps, 1), 4) for c in conv_ms],
     }
 
 
-def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed, precision="fp32"):
+def train_executed_work(plan, H, W, vgg_precision: str, transfer_precision: str) -> dict:
+    """Per-sample FLOPs the training step issues, split by the pipe they issue on (bf16 / f32 MFMA), for the
+    mixed roofline: ideal time = bf16 FLOPs / bf16 peak + f32 FLOPs / f32 peak. Transfer net: forward (the
+    residual and start convs on Winograd in fp32_winograd mode), weight gradient of every conv (direct GEMM),
+    input gradient of every conv but the first (residual ones on Winograd). VGG16: forward of three images
+    and the prediction's input gradient; the 3x3 convs after the first on bf16 with `terms` products per fp32
+    product (bf16: 1, bf16x3: 3, bf16x6: 6), the 3-channel first conv and fp32 mode on f32. Gram: forward of
+    two images and one backward on f32 MFMA."""
+    wino = transfer_precision == "fp32_winograd"
+
+    def conv_exec(i, l):
+        Ho, Wo = l.out_hw
+        tiles = (-(-Ho // 8) * 4) * (-(-Wo // 16) * 8)
+        if wino and i == 0 and l.k == 9:
+            return 2.0 * tiles * 16 * 9 * 18 * l.cout
+        if wino and l.block.startswith('residual'):
+            return 2.0 * tiles * 16 * l.cin * l.cout
+        return layer_flops(l)
+    t_fwd = sum(conv_exec(i, l) for i, l in enumerate(plan.layers))
+    t_wgrad = sum(layer_flops(l) for l in plan.layers)
+    t_dgrad = sum(conv_exec(i, l) for i, l in enumerate(plan.layers) if i > 0)
+    terms = {"bf16": 1, "bf16x3": 3, "bf16x6": 6}.get(vgg_precision, 0)
+    chans = [64, 64, 128, 128, 256, 256, 256, 512, 512, 512, 512, 512, 512]
+    pools = {1, 3, 6, 9}
+    vgg_f32, vgg_bf16, gram, cin, h, w = 0.0, 0.0, 0.0, 3, H, W
+    for i, c in enumerate(chans):
+        f = 2.0 * h * w * 9 * cin * c * 4                    # three forwards + one input gradient
+        if i == 0 or terms == 0:
+            vgg_f32 += f
+        else:
+            vgg_bf16 += terms * f
+        if i in pools:
+            gram += 3 * 2.0 * h * w * c * c
+            h, w = h // 2, w // 2
+        cin = c
+    return {"transfer_f32": t_fwd + t_wgrad + t_dgrad, "vgg_f32": vgg_f32, "vgg_bf16": vgg_bf16, "gram_f32": gram}
+
+
+def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"):
     from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
     from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
+    dev = ctx.device
     TB = args.train_batch
     lm = StyleLossModelVGG(outs, max_batch=TB, device=dev, precision=precision)
     from realtime_style_transfer_amd.stylePrediction import StylePredictionTrainer
@@ -193,25 +253,29 @@ def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, tim
     pr = StylePredictionTrainer(sins, cfg.style_feature_extractor_type, P, max_batch=TB, device=dev)
     tr = StyleTransferTrainingModel(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, loss_model=lm,
                                     weights=weights, max_batch=TB, device=dev, style_predictor=pr)
-    rng = np.random.default_rng(3000 + rank)
+    rng = np.random.default_rng(3000 + ctx.rank)
     x = {'content': torch.from_numpy(rng.random((TB,) + ins, dtype=np.float32)).to(dev),
          'style': torch.from_numpy(rng.random((TB, 1) + sins, dtype=np.float32)).to(dev)}
     y = {'content': torch.from_numpy(rng.random((TB,) + outs, dtype=np.float32)).to(dev),
          'style': torch.from_numpy(rng.random((TB, 1) + outs, dtype=np.float32)).to(dev)}
     for _ in range(2):
-        m = tr.train_step(x, y)
+        tr.train_step(x, y)
     torch.cuda.synchronize()
-    el = timed(lambda: tr.train_step(x, y), args.train_steps)
+    el = ctx.timed(lambda: tr.train_step(x, y), args.train_steps)
     loss = float(tr.compute_metrics()['loss'])
     fl = train_flops_per_sample(plan, outs[0], outs[1])
     per_sample = sum(fl.values())
     ms = el * 1e3 / args.train_steps
     tfs = per_sample * TB / (ms * 1e-3) / 1e12
+    ex = train_executed_work(plan, outs[0], outs[1], precision, tr.precision)
+    ideal_ms = TB * ((ex["vgg_bf16"]) / (BF16_MFMA_PEAK_TFLOPS * 1e12) +
+                     (ex["transfer_f32"] + ex["vgg_f32"] + ex["gram_f32"]) / (FP32_MFMA_PEAK_TFLOPS * 1e12)) * 1e3
     return {"workload": f"{SPEC} train_network.py step (BASELINE config 4): MobileNetV3Small style predictor + "
                         f"transfer net, training-mode forward, VGG16/Gram loss (no depth term), backward of both, " +
-                        ("RCCL gradient all-reduce (SUM, one bucket), " if world > 1 else "") +
-                        "RMSprop on both", "batch_per_gpu": TB, "steps": args.train_steps, "ms_per_step": round(ms, 3),
-            "frames_per_s": round(world * TB * args.train_steps / el, 3),
+                        ("RCCL gradient all-reduce (SUM, one bucket) + BN moving-statistics average, "
+                         if ctx.world > 1 else "") + "RMSprop on both", "batch_per_gpu": TB, "steps": args.train_steps,
+            "ms_per_step": round(ms, 3),
+            "frames_per_s": round(ctx.world * TB * args.train_steps / el, 3),
             "dtype": {"fp32": "fp32 (f32 MFMA)",
                       "bf16x6": "VGG16 3x3 convs: exact 3-piece split bf16 MFMA (fp32-level products, fp32 accumulate); "
                                 "transfer net and the rest fp32 (transfer_precision)",
@@ -220,13 +284,18 @@ def bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, tim
                       "bf16": "VGG16 3x3 convs: bf16 operands, fp32 accumulate (mixed_bfloat16 arithmetic); "
                               "transfer net and the rest fp32 (transfer_precision)"}[precision],
             "transfer_precision": {"fp32": "exact f32 MFMA",
-                                   "fp32_winograd": "residual 3x3 convs (forward + input gradient) as Winograd "
-                                                    "F(2x2,3x3) on f32 MFMA, the other transfer convs exact f32"}[
-                tr.precision],
+                                   "fp32_winograd": "residual 3x3 convs (forward + input gradient) and the 9x9 start "
+                                                    "conv (forward) as Winograd F(2x2,3x3) on f32 MFMA, the other "
+                                                    "transfer convs exact f32"}[tr.precision],
             "tflop_per_sample": round(per_sample / 1e12, 4),
-            "achieved_tflops_per_gpu": round(tfs, 2), "frac_fp32_mfma_peak": round(tfs / FP32_MFMA_PEAK_TFLOPS, 4),
-            "frac_note": "algorithmic (direct-conv, f32-equivalent) FLOPs over the f32 MFMA peak; the bf16 VGG16 "
-                         "convs and the Winograd transfer convs execute fewer f32 MFMA operations, so > 1 is possible",
+            "algorithmic_tflops_per_gpu": round(tfs, 2),
+            "roofline": {"bound": "mfma (mixed)", "ideal_ms": round(ideal_ms, 3), "achieved_ms": round(ms, 3),
+                         "frac": round(ideal_ms / ms, 4),
+                         "executed_gflop_per_sample": {k: round(v / 1e9, 2) for k, v in ex.items()},
+                         "peaks_tflops": {"bf16": BF16_MFMA_PEAK_TFLOPS, "f32": FP32_MFMA_PEAK_TFLOPS},
+                         "note": "ideal = bf16 FLOPs / bf16 peak + f32 FLOPs / f32 peak (executed work: Winograd "
+                                 "and split-bf16 counted as issued); the style predictor (~1 GFLOP/sample, VALU) "
+                                 "is left out of the ideal"},
             "flop_breakdown_per_sample_gflop": {k: round(v / 1e9, 2) for k, v in fl.items()},
             "last_loss_mean": loss}
 
@@ -254,7 +323,7 @@ def predictor_bytes_per_image(ins) -> float:
     return 4.0 * by
 
 
-def bench_ingest(args, dev, cfg, timed, rank):
+def bench_ingest(args, ctx, cfg):
     """G-buffer ingest: a 1080x1920 Unreal screenshot's 17 channel planes (already in
     HBM, as after the per-channel EXR uploads) -> rst_gbuffer_preprocess -> the 480x960x17 content tensor
     (hdrScreenshots.py:14-30 + common.py:44-57 in one pass). HBM-bound: algorithmic bytes = the source
@@ -262,6 +331,7 @@ def bench_ingest(args, dev, cfg, timed, rank):
     from realtime_style_transfer_amd.dataloaders.common import preprocess_planes, resized_size
     src, C = (1080, 1920), cfg.num_channels
     shape = cfg.input_shape['content'][:2]
+    dev = ctx.device
     planes = [torch.rand(src, device=dev) for _ in range(C)]
     out = torch.empty(shape + (C,), device=dev)
     fn = lambda: preprocess_planes(planes, shape, out=out)   # noqa: E731
@@ -271,7 +341,7 @@ def bench_ingest(args, dev, cfg, timed, rank):
     steps = max(args.steps, 50)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    el = timed(fn, steps)
+    ctx.timed(fn, steps)
     ev1.record()
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / steps
@@ -292,7 +362,7 @@ def bench_ingest(args, dev, cfg, timed, rank):
            "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "algorithmic_bytes": alg}}
-    if rank == 0 and not args.no_cpu_baseline:
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         from oracle.ingest_ref import preprocess_numpy_image
         x = np.random.default_rng(5).random(src + (C,), dtype=np.float32)
         n, t = 0, 0.0
@@ -306,11 +376,12 @@ def bench_ingest(args, dev, cfg, timed, rank):
     return res
 
 
-def bench_predictor(args, dev, cfg, transfer_model, transfer_inputs, P, timed):
+def bench_predictor(args, ctx, cfg, transfer_model, transfer_inputs, P):
     """make_style_transfer_inference_model path: the MobileNetV3Small style predictor on a 480x960x3 style image
     (once per style in the video loop, predict_video_using_checkpoint.py:77-83) and predictor + transfer per
     frame (the Keras inference model runs both per call, styleTransferInferenceModel.py:23-37)."""
     from realtime_style_transfer_amd.stylePrediction import create_style_prediction_model
+    dev = ctx.device
     sins = tuple(cfg.input_shape['style'][1:])
     pred = create_style_prediction_model(sins, cfg.style_feature_extractor_type, P, max_batch=1, device=dev)
     rng = np.random.default_rng(4000)
@@ -334,9 +405,9 @@ def bench_predictor(args, dev, cfg, transfer_model, transfer_inputs, P, timed):
         return g
 
     gp = graph_of(lambda: pred(style, out=sp))
-    el_p = timed(gp.replay, args.steps)
+    el_p = ctx.timed(gp.replay, args.steps)
     gi = graph_of(lambda: (pred(style, out=sp), transfer_model(tin, out=out)))
-    el_i = timed(gi.replay, args.steps)
+    el_i = ctx.timed(gi.replay, args.steps)
     ms_p = el_p * 1e3 / args.steps
     by = predictor_bytes_per_image(sins)
     return {"workload": f"MobileNetV3Small style predictor + GAP + 1x1 heads (P={P}) on one {sins[0]}x{sins[1]}x3 "
@@ -349,41 +420,84 @@ def bench_predictor(args, dev, cfg, transfer_model, transfer_inputs, P, timed):
             "inference_model_workload": "predictor + transfer per frame (B=1), as the Keras inference model runs"}
 
 
-def main():
+DEFAULT_PRECISION = "fp32_winograd"
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); >1 without WORLD_SIZE launches them")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1, help="frames per step per GPU (config 2: 1)")
     ap.add_argument("--stream-batch", type=int, default=8, help="config 3 (hipGraph stream) batch; 0 to skip")
+    ap.add_argument("--stream-frames", type=int, default=500, help="config 3 timed frames (after 50 warm-up)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0, help="bounded CPU-baseline sample (seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="headline from eager launches instead of hipGraph replay")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
     ap.add_argument("--train-steps", type=int, default=5)
-    ap.add_argument("--precision", default="fp32_winograd",
+    ap.add_argument("--precision", default=DEFAULT_PRECISION,
                     help="headline precision mode: fp32_winograd (default: fp32 arithmetic, residual convs as "
                          "fused Winograd F(2x2,3x3)), fp32 (all direct), bf16x6, bf16x3")
     ap.add_argument("--no-bf16x3", action="store_true", help="skip the other precision-mode measurements")
     ap.add_argument("--no-predictor", action="store_true", help="skip the style-predictor measurement")
     ap.add_argument("--no-ingest", action="store_true", help="skip the G-buffer ingest measurement")
     ap.add_argument("--pcie-steps", type=int, default=50, help="host-resident frame loop (PCIe-inclusive); 0 to skip")
-    args = ap.parse_args()
+    ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
+                    help="process-group backend for N>1 (default RCCL; gloo lets ranks share one GPU)")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="CPU only: launch the ranks, shard, time and report with no device work (tests the "
+                         "multi-rank path; prints value null)")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device(f"cuda:{torch.cuda.current_device()}")
 
+def plumbing_check(args, ctx):
+    """The multi-rank path of main() with the per-step device work removed: rank setup, the frame stream
+    sharded over ranks (frames.shard_batches), the barrier-bracketed timed region with the MAX over ranks,
+    the SUM of frames processed, and rank 0's JSON line. Used by the CPU gloo test."""
+    from realtime_style_transfer_amd.frames import shard_batches, sum_over_ranks
+    B = args.batch
+    n_frames = ctx.world * B * args.steps
+    mine = shard_batches(n_frames, B, ctx.rank, ctx.world)
+    it, done = iter(mine), [0]
+
+    def step():                     # "process" the next owned batch: count its frames
+        done[0] += len(next(it))
+
+    el = ctx.timed(step, args.steps)
+    total = sum_over_ranks(float(done[0]))
+    if ctx.rank == 0:
+        print(json.dumps({"metric": "plumbing-check (no device work)", "value": None, "unit": "frames/s",
+                          "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
+                          "frames_processed": int(total), "frames_expected": n_frames, "elapsed_max_s": el,
+                          "backend": ctx.backend, "scaling": "weak"}), flush=True)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    from realtime_style_transfer_amd.frames import init_ranks, launch_ranks
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # driver contract: `python bench.py --gpus N` runs N ranks. Start them as children before anything
+        # touches the GPU (this process never initialises HIP and is not replaced).
+        return launch_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:] if argv is None else list(argv))
+    ctx = init_ranks(args.dist_backend, "cpu" if args.plumbing_check else "cuda")
+    if ctx.world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ctx.world}")
+    try:
+        if args.plumbing_check:
+            plumbing_check(args, ctx)
+        else:
+            run(args, ctx)
+    finally:
+        ctx.close()
+    return 0
+
+
+def run(args, ctx):
+    from realtime_style_transfer_amd.frames import shard_batches
     from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
-
+    rank, world, dev = ctx.rank, ctx.world, ctx.device
     cfg = ShapeConfig.from_spec(SPEC)
     ins, outs = cfg.input_shape['content'], cfg.output_shape
     plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
@@ -392,52 +506,32 @@ def main():
     max_b = max(B, args.stream_batch)
     model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
                                            weights=weights, max_batch=max_b, device=dev, precision=args.precision)
-    # synthetic frames (distinct per rank), resident in HBM before the timed region
-    rng = np.random.default_rng(1000 + rank)
-    content = torch.from_numpy(rng.random((B,) + ins, dtype=np.float32)).to(dev)
+    # The synthetic stream has world * B * steps frames; rank r owns the batches r, r + world, ...
+    # (frames.shard_batches). Frame i's content is drawn from a generator seeded with i, so every rank's
+    # frames differ; the first owned batch is resident in HBM before the timed region starts.
+    first = shard_batches(world * B * args.steps, B, rank, world)[0]
+    content = torch.from_numpy(np.concatenate([np.random.default_rng(1000 + i).random((1,) + ins, dtype=np.float32)
+                                               for i in first])).to(dev)
     sp_np = synthetic_style_params(B, 1, P, plan, seed=1)
     style = torch.from_numpy(sp_np).to(dev)
     out = torch.empty((B,) + outs, dtype=torch.float32, device=dev)
     inputs = {'content': content, 'style_params': style}
+    rng = np.random.default_rng(1000 + rank)
 
     for _ in range(args.warmup):
         model(inputs, out=out)
     torch.cuda.synchronize()
-
-    def timed(fn, steps):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            fn()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
 
     # ---------------- timed region 1 (headline): one hipGraph replay per step -------------------
     # The forward (~30 kernel launches) is captured once into a hipGraph on torch's stream —
     # how a real-time frame loop drives it; the per-frame host cost is one graph launch.
     graph = None
     if not args.eager:
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            model(inputs, out=out)
-        torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            model(inputs, out=out)
+        graph = capture_graph(lambda: model(inputs, out=out))
         for _ in range(args.warmup):
             graph.replay()
         torch.cuda.synchronize()
-        elapsed = timed(graph.replay, args.steps)
+        elapsed = ctx.timed(graph.replay, args.steps)
     # ---------------- PCIe-inclusive rate (reported beside the headline, never as `value`) ------
     # The C-ABI hands over device pointers; a host-resident frame loop adds H2D of the 31 MB
     # G-buffer and D2H of the 5.5 MB output per frame. "serial": upload -> graph -> download on one
@@ -456,18 +550,11 @@ def main():
 
         serial()
         torch.cuda.synchronize()
-        el_serial = timed(serial, n)
+        el_serial = ctx.timed(serial, n)
         d_in = [content, torch.empty_like(content)]
         d_out = [out, torch.empty_like(out)]
-        graphs = [graph, torch.cuda.CUDAGraph()]
         inputs2 = {'content': d_in[1], 'style_params': style}
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            model(inputs2, out=d_out[1])
-        torch.cuda.current_stream().wait_stream(side)
-        with torch.cuda.graph(graphs[1]):
-            model(inputs2, out=d_out[1])
+        graphs = [graph, capture_graph(lambda: model(inputs2, out=d_out[1]))]
         # uploads and downloads on one copy stream (two separate copy streams measured slower: 661 vs
         # 747 FPS); every buffer reuse waits on the event of its previous user
         comp = torch.cuda.current_stream()
@@ -501,7 +588,7 @@ def main():
                     down_done[s].record(down)
             comp.wait_stream(up)
 
-        el_pipe = timed(pipelined, 1)
+        el_pipe = ctx.timed(pipelined, 1)
         frame_bytes = B * (int(np.prod(ins)) + int(np.prod(outs))) * 4
         pcie = {"serial_fps": round(world * B * n / el_serial, 3),
                 "pipelined_fps": round(world * B * n / el_pipe, 3),
@@ -509,11 +596,12 @@ def main():
                 "note": "pinned host frames; serial = H2D + graph + D2H per frame on one stream; pipelined = "
                         "double-buffered, copies on a second stream overlapping the compute"}
         torch.cuda.synchronize()
+        content.copy_(d_in[0])
     # ---------------- timed region 2: eager launches with per-layer HIP events -----------------
     # (every kernel recorded between events on the forward's stream -> per-kernel durations for
     # the roofline; also the eager FPS)
     model.profile_begin(args.steps)
-    elapsed_eager = timed(lambda: model(inputs, out=out), args.steps)
+    elapsed_eager = ctx.timed(lambda: model(inputs, out=out), args.steps)
     conv_ms, layer_ms, nsteps = model.profile_end()
     if graph is None:
         elapsed = elapsed_eager
@@ -525,85 +613,68 @@ def main():
     # ---------------- dominant kernel roofline (from the timed region's events) ----------------
     flops = [layer_flops(l) * B for l in plan.layers]
     dom = dominant_kernel(model, plan, conv_ms, nsteps, B)
-    dom_id, avg_ms, flops_per_launch, achieved_tf = dom["id"], dom["avg_ms"], dom["flops_per_launch"], dom["tflops"]
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            traffic = tj.get("per_launch_bytes", {}).get(KERNEL_NAMES.get(dom_id, ""), None)
+            traffic = tj.get("per_launch_bytes", {}).get(dom["kernel"], None)
         except Exception:
             traffic = None
     total_flops = sum(flops) / B
     conv_ms_per_frame = sum(conv_ms) / max(nsteps, 1) / B
-    layer_table = [{"layer": l.name, "kernel": KERNEL_NAMES.get(model.layer_kernel_id(i), "?"),
-                    "ms": round(conv_ms[i] / max(nsteps, 1), 4),
-                    "tflops": round(flops[i] / (conv_ms[i] / max(nsteps, 1) * 1e-3) / 1e12, 2) if conv_ms[i] > 0 else None}
-                   for i, l in enumerate(plan.layers)]
+    layer_table = []
+    for i, l in enumerate(plan.layers):
+        ms_i = conv_ms[i] / max(nsteps, 1)
+        ex, peak = executed_mfma(model, plan, i, B)
+        layer_table.append({"layer": l.name, "kernel": KERNEL_NAMES.get(model.layer_kernel_id(i), "?"),
+                            "ms": round(ms_i, 4),
+                            "tflops_direct_equiv": round(flops[i] / (ms_i * 1e-3) / 1e12, 2) if ms_i > 0 else None,
+                            "exec_frac": round(ex / (ms_i * 1e-3) / 1e12 / peak, 4) if ms_i > 0 else None})
 
-    # ---------------- config 3: batch-8 stream, hipGraph steady state -------------------------
-    stream_fps = None
+    # ---------------- config 3: batch-8 stream, hipGraph steady state (50 warm-up + 500 frames) ----------
+    stream = None
     if args.stream_batch > 0:
         SB = args.stream_batch
-        rng2 = np.random.default_rng(2000 + rank)
-        c8 = torch.from_numpy(rng2.random((SB,) + ins, dtype=np.float32)).to(dev)
+        c8 = torch.from_numpy(np.random.default_rng(2000 + rank).random((SB,) + ins, dtype=np.float32)).to(dev)
         s8 = torch.from_numpy(synthetic_style_params(SB, 1, P, plan, seed=1)).to(dev)
         o8 = torch.empty((SB,) + outs, dtype=torch.float32, device=dev)
         in8 = {'content': c8, 'style_params': s8}
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(3):
-                model(in8, out=o8)
-        torch.cuda.current_stream().wait_stream(side)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            model(in8, out=o8)
-        for _ in range(5):
+        g = capture_graph(lambda: model(in8, out=o8))
+        for _ in range(-(-50 // SB)):
             g.replay()
         torch.cuda.synchronize()
-        reps = 20
-        if world > 1:
-            dist.barrier()
-        ts = time.perf_counter()
-        for _ in range(reps):
-            g.replay()
-        torch.cuda.synchronize()
-        te = time.perf_counter() - ts
-        if world > 1:
-            t = torch.tensor([te], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            te = float(t.item())
-        stream_fps = world * SB * reps / te
+        reps = -(-args.stream_frames // SB)
+        te = ctx.timed(g.replay, reps)
+        stream = {"fps": round(world * SB * reps / te, 3), "batch": SB, "frames_per_gpu": SB * reps,
+                  "warmup_frames": SB * -(-50 // SB), "ms_per_batch": round(te * 1e3 / reps, 4),
+                  "workload": "predict_video_using_checkpoint.py stream (BASELINE config 3): batch-8 480x960x17 "
+                              "frames, one hipGraph replay per batch"}
 
-    # ---------------- precision mode: split-bf16 residual convs (reported beside the fp32 headline) --
+    # ---------------- other precision modes (reported beside the headline) ---------------------
     split_models, split = {}, {}
     if not args.no_bf16x3:
         for prec in [p for p in ("fp32", "fp32_winograd", "bf16x6", "bf16x3", "bf16") if p != args.precision]:
-            split_models[prec], split[prec] = bench_split(args, world, dev, cfg, ins, outs, plan, weights, P, inputs,
-                                                          timed, prec)
+            split_models[prec], split[prec] = bench_split(args, ctx, cfg, ins, outs, plan, weights, P, inputs, prec)
 
     # ---------------- style predictor / inference model -----------------------
-    predictor = None
-    if not args.no_predictor:
-        predictor = bench_predictor(args, dev, cfg, model, inputs, P, timed)
-
-    ingest = None if args.no_ingest else bench_ingest(args, dev, cfg, timed, rank)
+    predictor = None if args.no_predictor else bench_predictor(args, ctx, cfg, model, inputs, P)
+    ingest = None if args.no_ingest else bench_ingest(args, ctx, cfg)
 
     # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
     train = None
     if args.train_batch > 0:
         # BASELINE config 4 trains in bf16: the headline training figure runs the VGG16 3x3 convs with bf16
         # operands and fp32 accumulation; the split-bf16 (bf16x3, bf16x6) and fp32 runs are reported beside it
-        train = bench_training(args, world, rank, dev, cfg, ins, outs, plan, weights, P, timed, "bf16")
-        train["other_precisions"] = {p: {k: v for k, v in bench_training(args, world, rank, dev, cfg, ins, outs, plan,
-                                                                          weights, P, timed, p).items()
-                                         if k in ("ms_per_step", "frames_per_s", "achieved_tflops_per_gpu", "dtype")}
+        train = bench_training(args, ctx, cfg, ins, outs, plan, weights, P, "bf16")
+        keep = ("ms_per_step", "frames_per_s", "algorithmic_tflops_per_gpu", "dtype", "roofline")
+        train["other_precisions"] = {p: {k: v for k, v in bench_training(args, ctx, cfg, ins, outs, plan, weights, P,
+                                                                          p).items() if k in keep}
                                      for p in ("bf16x3", "bf16x6", "fp32")}
 
-    # ---------------- parity + CPU baseline (rank 0 only, bounded sample) -----------------------
+    # ---------------- parity + CPU baseline (rank 0 at N=1 only, bounded sample) ----------------
     max_abs = None
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0:
         from oracle.torch_ref import TorchTransfer
         threads = cpu_threads()
         torch.set_num_threads(threads)
@@ -619,17 +690,18 @@ def main():
             y3 = m3({'content': content[:1].contiguous(), 'style_params': style[:1].contiguous()})
             torch.cuda.synchronize()
             split[prec]["max_abs_delta_vs_oracle"] = float(np.abs(y3.cpu().numpy() - y_ref).max())
-        n, tsum = 0, 0.0
-        while tsum < args.cpu_budget_s and n < 20:
-            ts = time.perf_counter()
-            ref(x0, sp_np[:1])
-            tsum += time.perf_counter() - ts
-            n += 1
-            if first > args.cpu_budget_s:
-                break
-        cpu = {"value": round(n / tsum, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-               "sample": f"{n} frames of 480x960x17 (B=1) after 1 warm-up frame; torch-CPU f32 restatement of the "
-                         f"same graph (oracle/torch_ref.py; TF-CPU not installed), {n} x {tsum / n:.3f} s"}
+        if world == 1 and not args.no_cpu_baseline:
+            n, tsum = 0, 0.0
+            while tsum < args.cpu_budget_s and n < 20:
+                ts = time.perf_counter()
+                ref(x0, sp_np[:1])
+                tsum += time.perf_counter() - ts
+                n += 1
+                if first > args.cpu_budget_s:
+                    break
+            cpu = {"value": round(n / tsum, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+                   "sample": f"{n} frames of 480x960x17 (B=1) after 1 warm-up frame; torch-CPU f32 restatement of "
+                             f"the same graph (oracle/torch_ref.py; TF-CPU not installed), {n} x {tsum / n:.3f} s"}
 
     if rank == 0:
         line = {
@@ -649,35 +721,21 @@ def main():
             "data": "synthetic (U[0,1) 480x960x17 G-buffer frames, seeded weights; no checkpoints offline)",
             "config": {"workload": f"{SPEC} single-frame transfer inference (BASELINE config 2)", "spec": SPEC,
                        "frames_per_step_per_gpu": B, "input": list(ins), "output": list(outs),
-                       "parallelism": f"frame-sharded x{world}, no data-path collective"},
+                       "parallelism": f"frame-sharded x{world}, no data-path collective"
+                                      + (f" ({ctx.backend} bookkeeping)" if world > 1 else "")},
             "fps_per_gpu": round(fps / world, 3),
             "timing": "hipGraph replay per step" if graph is not None else "eager launches",
             "eager_fps": round(fps_eager, 3),
             "pcie_inclusive": pcie,
             "max_abs_delta_vs_oracle": max_abs,
-            "roofline": {
-                "bound": "mfma",
-                "kernel": KERNEL_NAMES.get(dom_id, str(dom_id)),
-                "achieved": round(achieved_tf, 3),
-                "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s" if dom_id != 200 else "TFLOP/s (algorithmic = direct-conv FLOPs)",
-                "frac": round(achieved_tf / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": traffic,
-                "avg_launch_ms": round(avg_ms, 5),
-                "flops_per_launch": flops_per_launch,
-                "launches": dom["launches"],
-                # Winograd executes 16/36 of the direct multiplies on the MFMA pipe
-                "mfma_pipe_frac": round(achieved_tf * (16.0 / 36.0 if dom_id == 200 else 1.0) / FP32_MFMA_PEAK_TFLOPS, 4),
-            },
+            "roofline": roofline_of(dom, traffic),
             "network_roofline": {
                 "gflop_per_frame": round(total_flops / 1e9, 3),
                 "conv_kernel_ms_per_frame": round(conv_ms_per_frame, 4),
-                "achieved_tflops_conv_kernels": round(total_flops / (conv_ms_per_frame * 1e-3) / 1e12, 3),
-                "achieved_tflops_end_to_end": round(total_flops * fps / world / 1e12, 3),
-                "frac_end_to_end": round(total_flops * fps / world / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                "direct_equiv_tflops_conv_kernels": round(total_flops / (conv_ms_per_frame * 1e-3) / 1e12, 3),
+                "direct_equiv_tflops_end_to_end": round(total_flops * fps / world / 1e12, 3),
             },
-            "stream_graph_fps": None if stream_fps is None else round(stream_fps, 3),
-            "stream_graph_batch": args.stream_batch,
+            "stream_graph": stream,
             "layers": layer_table,
             "split_bf16_modes": split,
             "training": train,
@@ -685,11 +743,8 @@ def main():
             "gbuffer_ingest": ingest,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line))
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -115,6 +115,14 @@ int rst_layer_kernel_id(const rst_handle* h, int idx);
 size_t rst_gram_workspace_size(int batch, int hw, int channels);
 int rst_gram(const float* feat, int batch, int hw, int channels, float* out, void* workspace, void* stream);
 
+/* Per-pixel style parameters of a two-style model (num_styles == 2): out (B, hw, n) =
+ * (1 - w1) * style_params[b][0] + w1 * style_params[b][1], w1 = style_weights (B, hw) — the
+ * model's style_weights input (B, out_h, out_w, S-1) at one mip level. Replaces
+ * _apply_style_weights(concat[1 - w1, w1], style_params)          models/styleTransfer.py:36-44,297-302
+ * with the same device formula the conv prologues blend the CIN affine with (debug / KAT entry). */
+int rst_style_param_map(const float* style_weights, const float* style_params, int batch, int hw, int num_styles,
+                        int n, float* out, void* stream);
+
 /* Conditional instance norm: y = bias + scale * (x - mean) * rsqrt(var + eps) per (b, c)
  * over H*W, optional ReLU. scale/bias (B, C). workspace: rst_instance_norm_workspace_size(). */
 size_t rst_instance_norm_workspace_size(int batch, int hw, int channels);

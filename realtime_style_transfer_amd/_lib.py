@@ -23,7 +23,7 @@ PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "fp32_winograd": 3, "bf16": 4
 EXPORTED_SYMBOLS = [
     "rst_create", "rst_create_ex", "rst_precision", "rst_destroy", "rst_num_style_params", "rst_num_weights_for_shape", "rst_forward",
     "rst_num_layers", "rst_layer_output_shape", "rst_copy_activation", "rst_gram_workspace_size", "rst_gram",
-    "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_last_error", "rst_version",
+    "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_style_param_map", "rst_last_error", "rst_version",
     "rst_profile_begin", "rst_profile_end", "rst_layer_kernel_id",
     "rst_loss_num_weights", "rst_loss_create", "rst_loss_destroy", "rst_loss_forward", "rst_loss_copy_feature",
     "rst_trainer_create", "rst_trainer_create_ex", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
@@ -106,6 +106,8 @@ def load() -> ctypes.CDLL:
     lib.rst_instance_norm_workspace_size.restype = sz
     lib.rst_instance_norm.argtypes = [vp, i, i, i, vp, vp, fp, i, vp, vp, vp]
     lib.rst_instance_norm.restype = i
+    lib.rst_style_param_map.argtypes = [vp, vp, i, i, i, i, vp, vp]
+    lib.rst_style_param_map.restype = i
     lib.rst_profile_begin.argtypes = [vp, i]
     lib.rst_profile_begin.restype = i
     lib.rst_profile_end.argtypes = [vp, ctypes.POINTER(fp), ctypes.POINTER(fp), ctypes.POINTER(i)]

@@ -115,7 +115,7 @@ __device__ __forceinline__ float bf3_pro(int mode, float x, float2 ab, float r) 
 }
 __device__ __forceinline__ float bf3_pro_blend(int mode, float x, float2 ab, float2 ab1, float w, float r) {
     const float y0 = fmaf(ab.x, x, ab.y), y1 = fmaf(ab1.x, x, ab1.y);
-    float y = fmaf(w, y1 - y0, y0);
+    float y = style_blend(w, y0, y1);
     if (mode == PRO_AFF_RELU) y = fmaxf(y, 0.f);
     else if (mode == PRO_AFF_RES) y = r + y;
     return y;

@@ -9,6 +9,11 @@ namespace rst {
 enum ProMode { PRO_NONE = 0, PRO_AFF_RELU = 1, PRO_AFF = 2, PRO_AFF_RES = 3, PRO_MASK = 4 };
 enum EpiMode { EPI_NONE = 0, EPI_RELU_BN = 1, EPI_RELU_STATS = 2, EPI_STATS = 3 };
 
+// Two-style blending (num_styles == 2, styleTransfer.py:36-44 with the weights completed as
+// [1 - w1, w1] at :297-302): w0*v0 + w1*v1 = v0 + w1*(v1 - v0). The one formula every blend site
+// uses (conv prologues, the standalone affine kernel, rst_style_param_map).
+__device__ __forceinline__ float style_blend(float w1, float v0, float v1) { return fmaf(w1, v1 - v0, v0); }
+
 // XCD-aware block order: the dispatcher deals workgroup ids round-robin over the 8 XCDs (each with
 // its own L2), so consecutive ids (neighbouring tiles, whose halos overlap) land on different L2s.
 // Remap so XCD x processes one contiguous run of the tile order: a bijection on [0, n).
@@ -157,6 +162,8 @@ hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st);
 hipError_t affine_act_launch(const float* x, const float2* ab, const float* res, float* y, int batch, long hw, int C,
                              int act, hipStream_t st);
 // two-style blend: t = a0*x + b0 + w[pixel] * ((a1*x + b1) - (a0*x + b0)), then [+ res], act
+hipError_t style_param_map_launch(const float* w1, const float* params, float* out, int batch, long hw, int n,
+                                  hipStream_t st);
 hipError_t affine_act_blend_launch(const float* x, const float2* ab, const float2* ab1, const float* w,
                                    const float* res, float* y, int batch, long hw, int C, int act, hipStream_t st);
 // TF AvgPool2D(2) (valid) of a one-channel map [B][H][W] -> [B][H/2][W/2]

@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void affine_act_blend_kernel(const float* __re
         const float2 p0 = ab[b * C + c], p1 = ab1[b * C + c];
         const float xv = x[i];
         const float y0 = fmaf(p0.x, xv, p0.y), y1 = fmaf(p1.x, xv, p1.y);
-        float v = fmaf(w[i / C], y1 - y0, y0);
+        float v = style_blend(w[i / C], y0, y1);
         if (res != nullptr) v += res[i];
         if (act == 1) v = fmaxf(v, 0.f);
         else if (act == 2) v = 1.f / (1.f + __expf(-v));
@@ -184,6 +184,30 @@ hipError_t affine_act_blend_launch(const float* x, const float2* ab, const float
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(affine_act_blend_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, ab, ab1, w, res, y,
                        total, hw * C, C, act);
+    return hipGetLastError();
+}
+
+// Per-pixel style parameters of a two-style model: out[b][p][c] = blend(w1[b][p], params[b][0][c],
+// params[b][1][c]) — the affine the conv prologues apply, exposed for the _apply_style_weights KAT.
+__global__ __launch_bounds__(256) void style_param_map_kernel(const float* __restrict__ w1,
+                                                              const float* __restrict__ params,
+                                                              float* __restrict__ out, long total, long hw, int n) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
+        const int c = (int)(i % n);
+        const long p = i / n;
+        const int b = (int)(p / hw);
+        const float* pb = params + (size_t)b * 2 * n;
+        out[i] = style_blend(w1[p], pb[c], pb[n + c]);
+    }
+}
+
+hipError_t style_param_map_launch(const float* w1, const float* params, float* out, int batch, long hw, int n,
+                                  hipStream_t st) {
+    const long total = (long)batch * hw * n;
+    long blocks = (total + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(style_param_map_kernel, dim3((unsigned)blocks), dim3(256), 0, st, w1, params, out, total, hw, n);
     return hipGetLastError();
 }
 

@@ -690,6 +690,17 @@ int rst_gram(const float* feat, int batch, int hw, int channels, float* out, voi
 
 static const int IN_TILE = 256;
 
+int rst_style_param_map(const float* style_weights, const float* style_params, int batch, int hw, int num_styles,
+                        int n, float* out, void* stream) {
+    if (style_weights == nullptr || style_params == nullptr || out == nullptr || batch <= 0 || hw <= 0 || n <= 0)
+        return fail(RST_ERR_INVALID, "rst_style_param_map: null pointer or empty shape");
+    if (num_styles != 2)
+        return fail(RST_ERR_UNSUPPORTED, "rst_style_param_map: the per-pixel blend exists only for num_styles == 2 "
+                                         "(styleTransfer.py:38-44 returns the params unblended otherwise)");
+    HIP_TRY(style_param_map_launch(style_weights, style_params, out, batch, hw, n, (hipStream_t)stream));
+    return RST_OK;
+}
+
 size_t rst_instance_norm_workspace_size(int batch, int hw, int channels) {
     const size_t n_tiles = (size_t)(hw + IN_TILE - 1) / IN_TILE;
     return (size_t)batch * channels * n_tiles * sizeof(float4) + (size_t)batch * channels * sizeof(float2);

@@ -80,10 +80,15 @@ __device__ __forceinline__ float pro_apply(int mode, float x, float2 ab, float r
 #ifdef WINO_PROF
 // phase timestamps per (workgroup, wave, chunk) for tools/wino_bench.hip (never in the library build)
 __device__ unsigned long long wino_prof[WINO_PROF][4][16][8];
+// timeline per (workgroup, wave) on the constant 100 MHz clock: start, pipeline filled, chunk loop done, end
+__device__ unsigned long long wino_tl[WINO_PROF][4][4];
 #define WPROF(c, k) \
     if (blockIdx.x < WINO_PROF && lane == 0) wino_prof[blockIdx.x][wave][(c)][(k)] = __builtin_amdgcn_s_memtime()
+#define WTL(k) \
+    if (blockIdx.x < WINO_PROF && lane == 0) wino_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define WPROF(c, k)
+#define WTL(k)
 #endif
 
 // PRO (the prologue mode) is a template parameter: a runtime mode turned the per-element prologue
@@ -97,6 +102,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
+    WTL(0);
     int bid = xcd_tile_order(blockIdx.x, gridDim.x);   // XCD-contiguous tile runs (halo reuse in L2)
     const int tx = bid % a.tiles_x;
     bid /= a.tiles_x;
@@ -219,6 +225,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (nchunks > 2) load_patch(2);
     }
     __syncthreads();
+    WTL(1);
 
     // one chunk: P = chunk parity (V(c) in vs[P], patch(c+1) in patch[1-P], patch[P] free)
     for (int c = 0; c < nchunks; ++c) {
@@ -263,6 +270,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __syncthreads();
         WPROF(c, 3);
     }
+    WTL(2);
 
     // ---- epilogue: output transform, bias + ReLU, store, tile statistics -----------------------
     const int co = wave * 32 + li;
@@ -320,6 +328,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             a.part[((size_t)b * WN + co) * n_part + ty * a.tiles_x + tx] = make_float4(s, m2, cnt, 0.f);
         }
     }
+    WTL(3);
 }
 
 // ---- 8-wave variant: two waves per SIMD ------------------------------------------------------------

@@ -325,11 +325,27 @@ class StylePredictionTrainer:
                                                                      float(learning_rate), float(rho), float(epsilon),
                                                                      _lib.stream_ptr()))
 
-    def get_weights(self) -> List[np.ndarray]:
+    def weights_tensor(self) -> torch.Tensor:
+        """Device copy of the flat weights (Keras get_weights() order)."""
         t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
         _lib.check(_lib.load().rst_predictor_trainer_copy_weights(self._handle, _lib.dev_ptr(t), t.numel(),
                                                                   _lib.stream_ptr()))
-        return self._unflatten(t.cpu().numpy())
+        return t
+
+    def set_weights_tensor(self, t: torch.Tensor):
+        _lib.check(_lib.load().rst_predictor_trainer_set_weights(self._handle, _lib.dev_ptr(t.contiguous()), t.numel(),
+                                                                 _lib.stream_ptr()))
+
+    @property
+    def moving_statistics_index(self) -> torch.Tensor:
+        """Flat indices of the BN moving_mean / moving_variance entries (averaged across data-parallel ranks)."""
+        if getattr(self, '_ms_index', None) is None:
+            from .styleTransferTrainingModel import moving_statistics_index
+            self._ms_index = torch.from_numpy(moving_statistics_index([(n, s) for n, s, _ in self.spec])).to(self.device)
+        return self._ms_index
+
+    def get_weights(self) -> List[np.ndarray]:
+        return self._unflatten(self.weights_tensor().cpu().numpy())
 
     def optimizer_slots(self) -> List[np.ndarray]:
         t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)

@@ -26,16 +26,23 @@ from .plan import CIN_EPS, Plan, init_weights, network_plan
 
 log = logging.getLogger(__name__)
 
+# precision modes whose inference output misses the fp32 parity bar (opt-in only)
+REDUCED_PRECISIONS = ("bf16",)
+
 
 class StyleTransferModel:
     """A built transfer network resident on one GPU (one librst handle)."""
 
     def __init__(self, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, num_styles=1,
                  name="StyleTransferModel", weights: Optional[Sequence[np.ndarray]] = None, seed: int = 2,
-                 max_batch: int = 8, device=None, precision: str = "fp32"):
+                 max_batch: int = 8, device=None, precision: str = "fp32", allow_reduced_precision: bool = False):
         self.name = name
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"precision must be one of {list(_lib.PRECISIONS)}, got {precision!r}")
+        if precision in REDUCED_PRECISIONS and not allow_reduced_precision:
+            raise ValueError(f"precision {precision!r} computes the residual convs with bf16 operands (8 significant "
+                             f"bits; ~0.1 max-abs output deviation, above the 1e-3 parity bar of an fp32 model); pass "
+                             f"allow_reduced_precision=True to use it for inference")
         self.precision = precision
         self.plan: Plan = network_plan(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
                                        num_styles)
@@ -207,6 +214,25 @@ def create_style_transfer_model(input_shape, output_shape, bottleneck_res_y, bot
     model = StyleTransferModel(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, num_styles,
                                name=name, **kwargs)
     return model, model.num_style_parameters
+
+
+def apply_style_weights(style_weights: torch.Tensor, style_params: torch.Tensor) -> torch.Tensor:
+    """``_apply_style_weights`` (styleTransfer.py:36-44) on librst: style_weights (B,H,W,S) already completed
+    as ``[1 - sum(w), w]`` (:297-302), style_params (B,1,S,n) -> per-pixel params (B,H,W,n) for S == 2; for any
+    other S the params come back unblended, as in the reference (:38-44). The blend is the device formula the
+    conv prologues apply to the CIN affine (``rst_style_param_map``), which takes w0 as 1 - w1."""
+    B, H, W, S = style_weights.shape
+    if tuple(style_params.shape[:3]) != (B, 1, S):
+        raise ValueError(f"style_params must be (B,1,S,n) = ({B},1,{S},n), got {tuple(style_params.shape)}")
+    if S != 2:
+        return style_params
+    n = style_params.shape[-1]
+    w1 = style_weights[..., 1].contiguous()
+    p = style_params.reshape(B, 2, n).contiguous()
+    out = torch.empty((B, H, W, n), dtype=torch.float32, device=style_weights.device)
+    _lib.check(_lib.load().rst_style_param_map(_lib.dev_ptr(w1), _lib.dev_ptr(p), B, H * W, S, n, _lib.dev_ptr(out),
+                                               _lib.stream_ptr()))
+    return out
 
 
 def instance_norm(x: torch.Tensor, scale: torch.Tensor, bias: torch.Tensor, eps: float = CIN_EPS,

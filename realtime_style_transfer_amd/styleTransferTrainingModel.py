@@ -13,10 +13,14 @@ weight sets take an RMSprop step. Without one, ``style_params`` are an input (``
 'style_params'}``) and their gradient is returned.
 
 * ``compute_loss`` returns the per-image ``(B,)`` loss; Keras minimises its sum, and so does this.
-* Data parallel: with ``process_group`` set, the gradients (transfer and predictor in ONE flat
-  bucket) are all-reduced (SUM, RCCL over xGMI) before the update, which equals one step on the
-  concatenated global batch except that the BatchNorm statistics stay per rank (as TF without
-  SyncBatchNorm would).
+* Data parallel: under an initialised process group, the gradients (transfer and predictor in ONE
+  flat bucket) are all-reduced (SUM, RCCL over xGMI) before the update, which equals one step on the
+  concatenated global batch except that each rank normalises with its own BatchNorm batch statistics
+  (TF without SyncBatchNorm does the same). The BN *moving* statistics are then averaged over the ranks
+  after every step (one more small all-reduce), which is what TF's MirroredStrategy does with them
+  (sync-on-read variables, MEAN aggregation): the moving-average update is linear, so the average of the
+  per-rank updates equals the update with the mean of the per-rank batch statistics, and every rank
+  keeps bitwise identical weights.
 """
 from __future__ import annotations
 
@@ -47,6 +51,17 @@ class RMSprop:
         self.learning_rate, self.rho, self.epsilon = float(learning_rate), float(rho), float(epsilon)
 
 
+def _all_reduce_sum(t: torch.Tensor, group=None):
+    """SUM over the group in place; gloo gets a host copy of a device tensor (RCCL reduces in HBM)."""
+    dist = torch.distributed
+    if t.is_cuda and dist.get_backend(group) != "nccl":
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+
+
 def allreduce_gradients(grad: torch.Tensor, group=None) -> bool:
     """Data-parallel gradient exchange: one flat bucket (the whole ~5.9 MB fp32 gradient of
     rst-960-120-128-17) summed in place across the process group — RCCL over xGMI with the
@@ -58,8 +73,30 @@ def allreduce_gradients(grad: torch.Tensor, group=None) -> bool:
         return False
     if dist.get_world_size(group) == 1:
         return False
-    dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+    _all_reduce_sum(grad, group)
     return True
+
+
+def average_over_ranks(values: torch.Tensor, group=None) -> bool:
+    """values <- mean over the ranks (in place); False when there is nothing to average with."""
+    dist = torch.distributed
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return False
+    _all_reduce_sum(values, group)
+    values /= dist.get_world_size(group)
+    return True
+
+
+def moving_statistics_index(weight_names_or_layers) -> np.ndarray:
+    """Flat indices (Keras get_weights() order, concatenated) of every BatchNormalization moving_mean /
+    moving_variance entry, from [(name, shape)] pairs."""
+    idx, o = [], 0
+    for name, shape in weight_names_or_layers:
+        n = int(np.prod(shape))
+        if name.endswith('moving_mean') or name.endswith('moving_variance'):
+            idx.append(np.arange(o, o + n))
+        o += n
+    return np.concatenate(idx) if idx else np.zeros(0, np.int64)
 
 
 class StyleTransferTrainingModel:
@@ -119,6 +156,13 @@ class StyleTransferTrainingModel:
             n_pred = style_predictor.num_weights
         # one flat gradient bucket: [transfer weights | predictor weights] (a single all-reduce per step)
         self._bucket = torch.zeros(self.num_weights + n_pred, dtype=torch.float32, device=self.device)
+        # BN moving statistics (contract blocks: layer weights kernel, bias, gamma, beta, moving_mean,
+        # moving_variance — styleTransfer.py:190-203) for the cross-rank average after each step
+        named = []
+        for layer in self.plan.layers:
+            attrs = ['kernel', 'bias'] + (['gamma', 'beta', 'moving_mean', 'moving_variance'] if layer.norm == 'bn' else [])
+            named += list(zip(attrs, layer.weight_shapes))
+        self._bn_index = torch.from_numpy(moving_statistics_index(named)).to(self.device)
         self._grad = self._bucket[:self.num_weights]
         self._pgrad = self._bucket[self.num_weights:] if n_pred else None
         self.style_losses: Dict[str, torch.Tensor] = {}
@@ -221,6 +265,31 @@ class StyleTransferTrainingModel:
         _lib.check(_lib.load().rst_trainer_apply_gradients(self._handle, _lib.dev_ptr(grad), o.learning_rate, o.rho,
                                                            o.epsilon, _lib.stream_ptr()))
 
+    def sync_moving_statistics(self) -> bool:
+        """Average the BatchNorm moving statistics (transfer net and, if trained jointly, the predictor) over the
+        ranks; no-op without a multi-rank process group. The statistics are not read by any training-mode kernel,
+        so writing them back changes nothing else (set_weights re-packs identical conv images)."""
+        dist = torch.distributed
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.process_group) == 1:
+            return False
+        lib = _lib.load()
+        pr = self.style_predictor
+        w = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
+        _lib.check(lib.rst_trainer_copy_weights(self._handle, _lib.dev_ptr(w), w.numel(), _lib.stream_ptr()))
+        parts = [w[self._bn_index]]
+        if pr is not None:
+            pw = pr.weights_tensor()
+            parts.append(pw[pr.moving_statistics_index])
+        stats = torch.cat(parts)
+        average_over_ranks(stats, self.process_group)
+        n0 = self._bn_index.numel()
+        w[self._bn_index] = stats[:n0]
+        _lib.check(lib.rst_trainer_set_weights(self._handle, _lib.dev_ptr(w), w.numel(), _lib.stream_ptr()))
+        if pr is not None:
+            pw[pr.moving_statistics_index] = stats[n0:]
+            pr.set_weights_tensor(pw)
+        return True
+
     def compute_loss(self, x=None, y=None, y_pred=None, sample_weight=None):
         """styleTransferTrainingModel.py:26-29: the (B,) 'loss' of the most recent step."""
         return self.style_losses['loss']
@@ -253,6 +322,7 @@ class StyleTransferTrainingModel:
         if pr is not None:
             o = self.optimizer
             pr.apply_gradients(self._pgrad, o.learning_rate, o.rho, o.epsilon)
+        self.sync_moving_statistics()
         self.style_losses = {n: losses[:, i] for i, n in enumerate(LOSS_NAMES)}
         self.last_prediction = pred
         self.last_style_params = sp

@@ -306,30 +306,63 @@ def read_checkpoint(path, verify: bool = True, with_strings: bool = False) -> Di
         if e.shard_id not in shards:
             shards[e.shard_id] = Path(f"{prefix}.data-{e.shard_id:05d}-of-{num_shards:05d}").read_bytes()
         raw = shards[e.shard_id][e.offset:e.offset + e.size]
+        if e.dtype == _DT_STRING:
+            # string tensors carry their own checksum layout (tensor_bundle.cc ReadStringTensor)
+            vals, crc = _decode_strings(raw, e.shape, verify)
+            if verify and e.crc32c is not None and unmask_crc(e.crc32c) != crc:
+                raise ValueError(f"{key}: tensor checksum mismatch")
+            if with_strings:
+                out[key] = vals
+            continue
         if verify and e.crc32c is not None and unmask_crc(e.crc32c) != crc32c(raw):
             raise ValueError(f"{key}: tensor checksum mismatch")
-        if e.dtype == _DT_STRING:
-            if with_strings:
-                out[key] = _decode_strings(raw, e.shape)
-            continue
         if e.dtype not in _DTYPES:
             raise ValueError(f"{key}: unsupported dtype enum {e.dtype}")
         out[key] = np.frombuffer(raw, dtype=np.dtype(_DTYPES[e.dtype]).newbyteorder('<')).reshape(e.shape).copy()
     return out
 
 
-def _decode_strings(raw: bytes, shape) -> np.ndarray:
+def _length_bytes(n: int) -> bytes:
+    """A string length as TF checksums it: the in-memory little-endian uint32 (uint64 above 4 GiB),
+    not the varint written to the file (tensor_bundle.cc WriteStringTensor, 'backwards compatibility')."""
+    return struct.pack('<I', n) if n <= 0xFFFFFFFF else struct.pack('<Q', n)
+
+
+def _encode_strings(vals) -> Tuple[bytes, int]:
+    """On-disk string tensor ``[varint len_0..len_L][masked crc of the lengths][bytes]`` and its entry
+    checksum (unmasked): CRC-32C over the fixed-width lengths, then the 4 stored checksum bytes, then the
+    string bytes (tensor_bundle.cc WriteStringTensor)."""
+    vals = [bytes(v) for v in vals]
+    lens = b''.join(_enc_varint(len(v)) for v in vals)
+    crc = 0
+    for v in vals:
+        crc = crc32c(_length_bytes(len(v)), crc)
+    stored = struct.pack('<I', mask_crc(crc))
+    crc = crc32c(stored, crc)
+    for v in vals:
+        crc = crc32c(v, crc)
+    return lens + stored + b''.join(vals), crc
+
+
+def _decode_strings(raw: bytes, shape, verify: bool = True) -> Tuple[np.ndarray, int]:
+    """Inverse of ``_encode_strings``: (values, entry checksum computed TF's way)."""
     n = int(np.prod(shape)) if shape else 1
-    pos, lens = 0, []
+    pos, lens, crc = 0, [], 0
     for _ in range(n):
         ln, pos = _varint(raw, pos)
         lens.append(ln)
-    pos += 4                                                    # masked crc32c of the length varints
+        crc = crc32c(_length_bytes(ln), crc)
+    stored = raw[pos:pos + 4]
+    if verify and unmask_crc(struct.unpack('<I', stored)[0]) != crc:
+        raise ValueError("string tensor: length checksum mismatch")
+    crc = crc32c(stored, crc)
+    pos += 4
     vals = []
     for ln in lens:
         vals.append(raw[pos:pos + ln])
+        crc = crc32c(raw[pos:pos + ln], crc)
         pos += ln
-    return np.array(vals, dtype=object).reshape(shape)
+    return np.array(vals, dtype=object).reshape(shape), crc
 
 
 def list_variables(path) -> List[Tuple[str, Tuple[int, ...]]]:
@@ -352,10 +385,9 @@ def write_checkpoint(prefix, tensors: Dict[str, np.ndarray], object_graph: Optio
         entries.append((key.encode(), BundleEntry(dt, a.shape, 0, len(data), len(raw), mask_crc(crc32c(raw)))))
         data += raw
     if object_graph is not None:
-        lens = _enc_varint(len(object_graph))
-        raw = lens + struct.pack('<I', mask_crc(crc32c(lens))) + object_graph
+        raw, crc = _encode_strings([object_graph])
         entries.append((OBJECT_GRAPH_KEY.encode(), BundleEntry(_DT_STRING, (), 0, len(data), len(raw),
-                                                               mask_crc(crc32c(raw)))))
+                                                               mask_crc(crc))))
         data += raw
     entries.sort(key=lambda t: t[0])
     header = _pb_varint(1, 1) + _pb_bytes(3, _pb_varint(1, 1))   # num_shards 1, little-endian, version{producer 1}

@@ -97,3 +97,48 @@ def test_model_restored_from_checkpoint_reproduces_output(tmp_path):
     sp = torch.from_numpy(synthetic_style_params(1, 1, P, plan, seed=1)).cuda()
     ya, yb = a({'content': x, 'style_params': sp}), b({'content': x, 'style_params': sp})
     assert torch.equal(ya, yb)
+
+
+def _crc32c_py(data: bytes, crc: int = 0) -> int:
+    """Bitwise CRC-32C (reflected polynomial 0x82F63B78), independent of librst's slicing-by-8 table code."""
+    crc ^= 0xFFFFFFFF
+    for b in data:
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
+    return crc ^ 0xFFFFFFFF
+
+
+def _mask_py(c: int) -> int:
+    return ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xa282ead8) & 0xFFFFFFFF
+
+
+def test_string_tensor_checksums_follow_tensorflow(tmp_path):
+    """TF's WriteStringTensor (tensor_bundle.cc) stores [varint len]*[masked crc of the lengths][bytes] and
+    checksums each length as the fixed-width little-endian uint32 (uint64 above 4 GiB), not the varint;
+    the entry checksum covers those fixed-width lengths, then the 4 stored checksum bytes, then the string
+    bytes. Known answer worked out here from that algorithm with an independent CRC; a 300-byte object
+    graph makes the varint two bytes long, so varint and uint32 checksums would differ."""
+    assert _crc32c_py(b"123456789") == 0xE3069283
+    graph = bytes(range(256)) + b"x" * 44                      # 300 bytes: varint 0xAC 0x02
+    lens = b"\xac\x02"
+    len_crc = _crc32c_py(struct.pack('<I', 300))
+    stored = struct.pack('<I', _mask_py(len_crc))
+    want_raw = lens + stored + graph
+    want_entry_crc = _mask_py(_crc32c_py(graph, _crc32c_py(stored, len_crc)))
+    assert _crc32c_py(lens) != len_crc                          # the varint form would be wrong
+    prefix = tmp_path / "g"
+    ck.write_checkpoint(prefix, {"v": np.ones(3, np.float32)}, object_graph=graph)
+    entries = dict(ck._read_table(ck._index_path(str(prefix)), True))
+    e = ck.BundleEntry.parse(entries[ck.OBJECT_GRAPH_KEY.encode()])
+    data = (tmp_path / "g.data-00000-of-00001").read_bytes()
+    assert data[e.offset:e.offset + e.size] == want_raw
+    assert e.crc32c == want_entry_crc
+    r = ck.read_checkpoint(prefix, with_strings=True)             # verify=True accepts TF's layout
+    assert r[ck.OBJECT_GRAPH_KEY].item() == graph
+    # a corrupted length checksum is detected
+    bad = bytearray(data)
+    bad[e.offset + 2] ^= 1
+    (tmp_path / "g.data-00000-of-00001").write_bytes(bytes(bad))
+    with pytest.raises(ValueError):
+        ck.read_checkpoint(prefix, with_strings=True)

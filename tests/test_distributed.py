@@ -109,3 +109,46 @@ def test_data_parallel_gradient_allreduce_gloo(tmp_path):
     mp.spawn(_dp_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"dp{r}.txt").read_text().split()[0] == "1"
+
+
+def _bench_json(stdout: str) -> dict:
+    import json
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout          # rank 0 prints ONE JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_gpus_2_launches_two_gloo_ranks():
+    """`python bench.py --gpus 2` (driver contract) with WORLD_SIZE unset starts two ranks as children
+    (torch.distributed.run, 127.0.0.1), and the rank-0 line reports n_gpus 2 with every frame of the
+    sharded stream processed exactly once (frames.shard_batches + timed_region + SUM over ranks). The
+    device work is removed (--plumbing-check); this is bench.py's own multi-rank code path on gloo."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--plumbing-check", "--steps", "3", "--warmup", "1", "--batch", "2"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _bench_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["backend"] == "gloo"
+    assert line["frames_processed"] == line["frames_expected"] == 2 * 2 * 3
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing-check"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_moving_statistics_index():
+    from realtime_style_transfer_amd.styleTransferTrainingModel import moving_statistics_index
+    named = [("k", (3, 3, 2, 4)), ("gamma", (4,)), ("beta", (4,)), ("bn/moving_mean", (4,)),
+             ("bn/moving_variance", (4,)), ("bias", (2,))]
+    idx = moving_statistics_index(named)
+    assert idx.tolist() == list(range(72 + 8, 72 + 16))

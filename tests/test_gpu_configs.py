@@ -1,0 +1,108 @@
+"""GPU parity of the BASELINE.json configurations the other tests do not cover directly.
+
+* config 1 — one 256x256x3 SDR frame, one style, through the inference model (style predictor ->
+  transfer) as ``predict_using_saved_models.py:26-42`` runs it (``transfer_model({'content', 'style'})``);
+* config 3 — the ``predict_video_using_checkpoint.py:91-98`` stream: batch-8 480x960x17 frames, the
+  forward captured once into a hipGraph and replayed, as bench.py's config-3 line times it.
+
+Oracles: the torch-CPU f32 restatements (oracle/torch_ref.py, oracle/predictor_ref.py) of the same
+graphs on the same seeded inputs; tolerance 2e-4 max-abs on the [0, 1] output (north-star bar 1e-3).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+OUT_TOL = 2e-4
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32_winograd"])
+def test_config1_sdr_256x256_inference_model(precision):
+    _need_gpu()
+    from oracle import predictor_ref as PR
+    from oracle.torch_ref import TorchTransfer
+    from realtime_style_transfer_amd.plan import init_weights, network_plan
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    from realtime_style_transfer_amd.stylePrediction import (create_style_prediction_model, init_predictor_weights,
+                                                             predictor_weight_spec)
+    from realtime_style_transfer_amd.styleTransferInferenceModel import make_style_transfer_inference_model
+    cfg = ShapeConfig.explicit((256, 256), (256, 256), num_channels=3, hdr=False)
+    ins, outs, sins = cfg.input_shape['content'], cfg.output_shape, tuple(cfg.input_shape['style'][1:])
+    assert ins == (256, 256, 3) and outs == (256, 256, 3) and sins == (256, 256, 3)
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    tw = init_weights(plan, seed=2)
+    pw = init_predictor_weights(predictor_weight_spec(sins, cfg.style_feature_extractor_type, plan.num_style_params),
+                                seed=3, perturb=True)
+    m = make_style_transfer_inference_model(
+        num_styles=1,
+        style_predictor_factory_func=lambda P: create_style_prediction_model(
+            sins, cfg.style_feature_extractor_type, P, weights=pw, max_batch=1),
+        style_transfer_factory_func=lambda: create_style_transfer_model(
+            ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1, weights=tw, max_batch=1,
+            precision=precision))
+    rng = np.random.default_rng(11)
+    content = rng.random((1,) + ins).astype(np.float32)
+    style = rng.random((1, 1) + sins).astype(np.float32)
+    y = m.inference({'content': torch.from_numpy(content).cuda(), 'style': torch.from_numpy(style).cuda()})
+    y = y.cpu().numpy()
+    sp = PR.torch_style_predictor_forward(style[:, 0], pw, 'MOBILE_NET')[:, None, :].astype(np.float32)
+    ref = TorchTransfer(tw, ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)(content, sp)
+    assert y.shape == (1, 256, 256, 3)
+    err = float(np.abs(y - ref).max())
+    assert err < OUT_TOL, err
+    # pixel export (predict_using_saved_models.py:42: np.uint8(result * 255))
+    assert np.mean(np.uint8(y * 255) != np.uint8(ref * 255)) < 1e-3
+
+
+def test_config3_batch8_stream_graph_replay():
+    """BASELINE config 3 on the bench's headline precision: B=8 frames captured once into a hipGraph and
+    replayed; every frame is bitwise equal to its own B=1 forward (frames are independent: CIN per instance,
+    BN in inference mode), replays are bitwise repeatable, and frame 0 matches the torch-CPU oracle."""
+    _need_gpu()
+    import bench
+    from oracle.torch_ref import TorchTransfer
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    cfg = ShapeConfig.from_spec("rst-960-120-128-17")
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    ws = init_weights(plan, seed=2)
+    SB = 8
+    model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                           weights=ws, max_batch=SB, precision=bench.DEFAULT_PRECISION)
+    rng = np.random.default_rng(2000)
+    x = rng.random((SB,) + ins, dtype=np.float32)
+    sp = synthetic_style_params(SB, 1, P, plan, seed=1)
+    c8, s8 = torch.from_numpy(x).cuda(), torch.from_numpy(sp).cuda()
+    o8 = torch.empty((SB,) + outs, device='cuda')
+    inputs = {'content': c8, 'style_params': s8}
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        model(inputs, out=o8)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        model(inputs, out=o8)
+    o8.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    first = o8.clone()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(first, o8), "graph replays are not bitwise repeatable"
+    for i in range(SB):
+        yi = model({'content': c8[i:i + 1].contiguous(), 'style_params': s8[i:i + 1].contiguous()})
+        assert torch.equal(yi[0], o8[i]), f"frame {i}: batched graph result differs from its B=1 forward"
+    ref = TorchTransfer(ws, ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)(x[:1], sp[:1])
+    err = float(np.abs(o8[:1].cpu().numpy() - ref).max())
+    assert err < OUT_TOL, err

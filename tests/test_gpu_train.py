@@ -340,3 +340,37 @@ def test_training_model_reference_geometry_with_dummy_predictor():
     m.refresh()
     out = m.inference({'content': x['content'], 'style': x['style']})
     assert tuple(out.shape) == (2,) + oe
+
+
+def test_full_size_bf16_training_step_properties():
+    """BASELINE config 4 at its real size (train_network.py:61: B=4, 480x960 frames, rst-960-120-128-17;
+    the VGG16 convs in bf16 as bench.py's training headline): the float64 oracle cannot run this size, so
+    the test checks size-independent properties — every loss / gradient / weight finite, two trainers from
+    the same weights and inputs bitwise identical after three steps (no atomics, fixed reduction order),
+    and the batch loss decreasing over three RMSprop steps on one batch."""
+    _need_gpu()
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    sc = ShapeConfig.from_spec("rst-960-120-128-17")
+    cfg = dict(input_shape=sc.input_shape['content'], output_shape=sc.output_shape,
+               bottleneck_res_y=sc.bottleneck_res_y, bottleneck_num_filters=sc.bottleneck_num_filters)
+    B = 4
+    plan, w, vgg, content, sp, gtc, gts = _case(cfg, B)
+    c, s, gc, gs = _cuda(content, sp, gtc, gts)
+    runs = []
+    for _ in range(2):
+        tr = _trainer(cfg, w, vgg, B, precision="bf16", transfer="fp32_winograd")
+        losses = []
+        for _step in range(3):
+            m = tr.train_step({'content': c, 'style_params': s}, {'content': gc, 'style': gs})
+            losses.append(float(m['loss']))
+            assert all(np.isfinite(float(v)) for v in m.values())
+            assert bool(torch.isfinite(tr._grad).all())
+        torch.cuda.synchronize()
+        flat = np.concatenate([a.reshape(-1) for a in tr.get_weights()])
+        assert np.all(np.isfinite(flat))
+        runs.append((losses, flat, tr.last_prediction.cpu().numpy()))
+        del tr
+        torch.cuda.empty_cache()
+    (l0, w0, p0), (l1, w1, p1) = runs
+    assert l0 == l1 and np.array_equal(w0, w1) and np.array_equal(p0, p1), "training is not bitwise deterministic"
+    assert l0[2] < l0[1] < l0[0], l0

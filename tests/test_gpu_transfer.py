@@ -218,7 +218,8 @@ def test_split_bf16_precision_modes(precision, tol):
     x = np.random.default_rng(0).random((2,) + ins).astype(np.float32)
     ref = R.transfer_forward(x, sp, w, ins, outs, br, bf,
                              operand_round=R.bf16_round if precision == "bf16" else None)
-    m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision=precision)
+    m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision=precision,
+                                       allow_reduced_precision=precision == "bf16")
     kid = {"bf16x3": 102, "bf16x6": 113, "bf16": 134}[precision]
     assert [m.layer_kernel_id(i) for i in range(m.num_layers())][3:13] == [kid] * 10   # residual convs
     inp = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}
@@ -289,3 +290,30 @@ def test_winograd_full_size_matches_torch_oracle():
     with open(os.path.join(OUT, 'winograd_parity.json'), 'w') as f:
         json.dump({'max_abs_full_size': err}, f)
     assert err < OUT_TOL, err
+
+
+def test_apply_style_weights_kat_on_gpu():
+    """The reference's only numeric known answer, styleTransferTest.py:28-49 (``_apply_style_weights``,
+    two styles, vertical-gradient weights), through the device blend formula the conv prologues use.
+    The KAT's weights satisfy w0 == 1 - w1 exactly (as the model completes them, styleTransfer.py:297-302),
+    and every value is a small dyadic rational, so the f32 result is exact: assert_almost_equal(decimal=7)."""
+    _need_gpu()
+    from realtime_style_transfer_amd.styleTransfer import apply_style_weights
+    d = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'apply_style_weights_kat.npz'))
+    w, p = d['style_weights'], d['style_params']
+    assert np.array_equal(w[..., 0], (1.0 - w[..., 1]).astype(np.float32))
+    got = apply_style_weights(torch.from_numpy(w).cuda(), torch.from_numpy(p).cuda()).cpu().numpy()
+    assert got.shape == (2, 10, 20, 6)                                      # expected_shape
+    np.testing.assert_almost_equal(got, d['expected'])
+    # S != 2: the reference returns the params unblended
+    p3 = torch.ones((2, 1, 3, 6), device='cuda')
+    assert apply_style_weights(torch.zeros((2, 10, 20, 3), device='cuda'), p3) is p3
+
+
+def test_bf16_inference_needs_explicit_opt_in():
+    """Plain bf16 operands miss the 1e-3 fp32 parity bar: the factory refuses it by default."""
+    _need_gpu()
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    d, ws, ins, outs, bres, bf = _load_fixture("transfer_small.npz")
+    with pytest.raises(ValueError, match="allow_reduced_precision"):
+        create_style_transfer_model(ins, outs, bres, bf, 1, weights=ws, max_batch=2, precision="bf16")

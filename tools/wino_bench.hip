@@ -65,6 +65,30 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 4; ++k) printf("  %-11s %8.1f  (%.1f%%)\n", nm[k], ph[k] / n, 100 * ph[k] / tot);
     const unsigned long long* p0 = &pr[0];
     printf("WG0 wave0 first chunk start->end of chunk 15: %llu ticks\n", p0[15 * 8 + 3] - p0[0]);
+    // timeline of the LAST launch (100 MHz clock, 10 ns ticks), over all profiled workgroups
+    std::vector<unsigned long long> tl((size_t)nwg * 4 * 4);
+    CK(hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(wino_tl), tl.size() * 8));
+    unsigned long long t0 = ~0ull, tend = 0, s_last = 0;
+    double fill = 0, loop = 0, epi = 0;
+    for (int g = 0; g < nwg; ++g)
+        for (int w = 0; w < 4; ++w) {
+            const unsigned long long* q = &tl[((size_t)g * 4 + w) * 4];
+            t0 = q[0] < t0 ? q[0] : t0;
+            tend = q[3] > tend ? q[3] : tend;
+            s_last = q[0] > s_last ? q[0] : s_last;
+            fill += (double)(q[1] - q[0]); loop += (double)(q[2] - q[1]); epi += (double)(q[3] - q[2]);
+        }
+    const double nw = nwg * 4.0;
+    printf("timeline (us): first start -> last end %.2f, last wave start at +%.2f; per wave: fill %.2f, "
+           "chunk loop %.2f, epilogue %.2f\n", (tend - t0) * 0.01, (s_last - t0) * 0.01, fill / nw * 0.01,
+           loop / nw * 0.01, epi / nw * 0.01);
+    // histogram of wave end times
+    int hist[10] = {0};
+    for (int g = 0; g < nwg; ++g) {
+        const unsigned long long e = tl[((size_t)g * 4 + 0) * 4 + 3];
+        int k = (int)(10.0 * (e - t0) / (double)(tend - t0 + 1)); hist[k > 9 ? 9 : k]++;
+    }
+    printf("WG end-time deciles:"); for (int k = 0; k < 10; ++k) printf(" %d", hist[k]); printf("\n");
 #endif
     return 0;
 }
