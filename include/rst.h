@@ -77,10 +77,14 @@ void rst_destroy(rst_handle* h);
  * FP32_WINOGRAD: fp32 arithmetic (exact-f32 MFMA products, f32 accumulation) with the residual
  * convs computed as Winograd F(2x2,3x3) (16 instead of 36 multiplies per 2x2 output tile); single
  * style only (two-style blending keeps the direct kernel).
+ * WINOGRAD_BF16X6: as FP32_WINOGRAD, with the residual convs' transform-domain products (V = B^T d B times
+ * U = G g G^T) computed as BF16X6 terms: each fp32 operand split exactly into three bf16 pieces, six
+ * terms, fp32 accumulation (dropped terms <= 2^-25 of each product) — fp32-level products on the bf16
+ * MFMA pipe; the start conv stays f32-MFMA Winograd.
  * BF16: plain bf16 operands (round-to-nearest-even), fp32 accumulation — a Keras mixed_bfloat16
  * policy's arithmetic (BASELINE config 4 trains in bf16) — on the same layers as the split modes. */
 enum { RST_PRECISION_FP32 = 0, RST_PRECISION_BF16X3 = 1, RST_PRECISION_BF16X6 = 2, RST_PRECISION_FP32_WINOGRAD = 3,
-       RST_PRECISION_BF16 = 4 };
+       RST_PRECISION_BF16 = 4, RST_PRECISION_WINOGRAD_BF16X6 = 5 };
 int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_weights, int precision,
                   rst_handle** out);
 int rst_precision(const rst_handle* h);

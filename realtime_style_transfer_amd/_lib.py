@@ -17,7 +17,7 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = _PKG / "librst.so"
 
 RST_OK, RST_ERR_INVALID, RST_ERR_UNSUPPORTED, RST_ERR_HIP, RST_ERR_ALLOC = range(5)
-PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "fp32_winograd": 3, "bf16": 4}   # include/rst.h RST_PRECISION_*
+PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "fp32_winograd": 3, "bf16": 4, "winograd_bf16x6": 5}   # include/rst.h RST_PRECISION_*
 
 # Symbols declared in include/rst.h — tests check that the library exports all of them.
 EXPORTED_SYMBOLS = [

@@ -21,11 +21,16 @@ OBJ = PKG / "_build"
 SOURCES = ["conv_mfma.hip", "conv_small.hip", "norm.hip", "gram.hip", "loss.hip", "rst_api.hip", "loss_api.hip",
            "train.hip", "train_api.hip", "wgrad.hip",
            "conv_bf3.hip", "predictor.hip", "predictor_api.hip",
-           "predictor_train.hip", "predictor_train_api.hip", "wino.hip", "wino9.hip", "ingest.hip", "ingest_api.hip", "crc32c.hip"]
+           "predictor_train.hip", "predictor_train_api.hip", "wino.hip", "wino_x6.hip", "wino9.hip", "ingest.hip", "ingest_api.hip", "crc32c.hip"]
 ARCH = os.environ.get("RST_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", str(ROOT / "include"), "-I", str(CSRC),
           "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-munsafe-fp-atomics"]
+
+
+# per-source extra flags: the split-bf16 Winograd kernel keeps its transform in scalar f32 ops (packed f32
+# VALU beside MFMAs costs more issue cycles than two scalar ops on gfx950)
+EXTRA = {"wino_x6.hip": ["-fno-slp-vectorize"]}
 
 
 def _digest() -> str:
@@ -34,6 +39,7 @@ def _digest() -> str:
         h.update(f.name.encode())
         h.update(f.read_bytes())
     h.update(" ".join(CFLAGS).encode())
+    h.update(repr(sorted(EXTRA.items())).encode())
     return h.hexdigest()[:16]
 
 
@@ -46,7 +52,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 
     def compile_one(src: str) -> Path:
         obj = OBJ / (Path(src).stem + ".o")
-        cmd = [HIPCC, *CFLAGS, "-c", str(CSRC / src), "-o", str(obj)]
+        cmd = [HIPCC, *CFLAGS, *EXTRA.get(src, []), "-c", str(CSRC / src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

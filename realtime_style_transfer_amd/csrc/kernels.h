@@ -119,6 +119,12 @@ hipError_t wino_prepare();
 // wino_pack_weights on the device (kern: HWIO [3][3][cin][128] float32 on the device)
 hipError_t wino_transform_launch(const float* kern, int cin, float* U, hipStream_t st);
 hipError_t wino_launch(const WinoArgs& a, hipStream_t st);
+// Residual convs as Winograd F(2x2,3x3) with the transform-domain products as exact 3-piece split-bf16
+// MFMA terms (wino_x6.hip); same WinoArgs, U = wino_x6_pack_weights (bf16 pieces [cin/16][16][3][128][16]).
+bool wino_x6_supported(int kh, int stride, int cin, int cout);
+std::vector<float> wino_x6_pack_weights(const float* kern, int cin);
+hipError_t wino_x6_prepare();
+hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st);
 
 // Final 9x9 transposed conv with Cout = 3 on the VALU (conv_small.hip).
 struct SmallConvArgs {

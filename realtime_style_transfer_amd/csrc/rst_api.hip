@@ -197,8 +197,8 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.tiles_y = small_conv_tiles_y(s.Ho);
         e.tiles_x = small_conv_tiles_x(s.Wo);
         e.n_part = e.tiles_y * e.tiles_x;
-    } else if (precision == RST_PRECISION_FP32_WINOGRAD && s.keras_kind == 0 &&
-               wino9_supported(s.k, s.stride, s.cin, s.cout) && s.norm == N_BN && s.conv_relu) {
+    } else if ((precision == RST_PRECISION_FP32_WINOGRAD || precision == RST_PRECISION_WINOGRAD_BF16X6) &&
+               s.keras_kind == 0 && wino9_supported(s.k, s.stride, s.cin, s.cout) && s.norm == N_BN && s.conv_relu) {
         // ---- first layer (9x9 conv + ReLU + BN + ReLU) as composite Winograd (wino9.hip)
         e.kind = K_WINO9;
         packed = wino9_pack_weights(kern, s.cin);
@@ -210,11 +210,14 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.tiles_y = wino9_tiles_y(s.Ho);
         e.tiles_x = wino9_tiles_x(s.Wo);
         e.n_part = 0;
-    } else if (precision == RST_PRECISION_FP32_WINOGRAD && s.keras_kind == 0 &&
-               wino_supported(s.k, s.stride, s.cin, s.cout) && s.res_block >= 0) {
-        // ---- residual conv as fused Winograd F(2x2,3x3) (wino.hip)
-        e.kind = K_WINO;
-        packed = wino_pack_weights(kern, s.cin);
+    } else if ((precision == RST_PRECISION_FP32_WINOGRAD && wino_supported(s.k, s.stride, s.cin, s.cout) ||
+                precision == RST_PRECISION_WINOGRAD_BF16X6 && wino_x6_supported(s.k, s.stride, s.cin, s.cout)) &&
+               s.keras_kind == 0 && s.res_block >= 0) {
+        // ---- residual conv as fused Winograd F(2x2,3x3): f32 MFMA (wino.hip) or exact split-bf16 MFMA
+        // products (wino_x6.hip)
+        const bool x6 = precision == RST_PRECISION_WINOGRAD_BF16X6;
+        e.kind = x6 ? K_WINOX6 : K_WINO;
+        packed = x6 ? wino_x6_pack_weights(kern, s.cin) : wino_pack_weights(kern, s.cin);
         bias_n.assign(bias, bias + s.cout);
         e.ntot = s.cout;
         e.pad_t = e.pad_l = 1;
@@ -309,7 +312,8 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     if (shape == nullptr || out == nullptr || weights_host == nullptr)
         return fail(RST_ERR_INVALID, "rst_create: null argument");
     if (precision != RST_PRECISION_FP32 && precision != RST_PRECISION_BF16X3 && precision != RST_PRECISION_BF16X6 &&
-        precision != RST_PRECISION_FP32_WINOGRAD && precision != RST_PRECISION_BF16)
+        precision != RST_PRECISION_FP32_WINOGRAD && precision != RST_PRECISION_BF16 &&
+        precision != RST_PRECISION_WINOGRAD_BF16X6)
         return fail(RST_ERR_INVALID, "rst_create_ex: unknown precision mode");
     *out = nullptr;
     if (shape->num_styles > 2)
@@ -344,8 +348,8 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         wp += kcount + s.cout;
         std::vector<float> bias_n, packed;
         // the Winograd kernel has no two-style blend prologue: those layers keep the direct kernel
-        const int lp = (precision == RST_PRECISION_FP32_WINOGRAD && shape->num_styles == 2) ? RST_PRECISION_FP32
-                                                                                            : precision;
+        const bool wino_mode = precision == RST_PRECISION_FP32_WINOGRAD || precision == RST_PRECISION_WINOGRAD_BF16X6;
+        const int lp = (wino_mode && shape->num_styles == 2) ? RST_PRECISION_FP32 : precision;
         if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp)) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
@@ -428,7 +432,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     // kernels with > 64 KB of dynamic LDS need the attribute before any (graph-captured) launch
     for (auto& e : h->layers) {
         if (e.kind == K_SMALL || e.kind == K_WINO9) continue;
-        hipError_t pe = e.kind == K_WINO ? wino_prepare() : conv_prepare(e.tile);
+        hipError_t pe = e.kind == K_WINO ? wino_prepare() : (e.kind == K_WINOX6 ? wino_x6_prepare() : conv_prepare(e.tile));
         if (pe != hipSuccess) {
             delete h;
             return fail(RST_ERR_HIP, std::string("conv_prepare: ") + hipGetErrorString(pe));
@@ -495,7 +499,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.tiles_y = e.tiles_y;
         a.tiles_x = e.tiles_x;
         HIP_TRY(wino9_launch(a, st));
-    } else if (e.kind == K_WINO) {
+    } else if (e.kind == K_WINO || e.kind == K_WINOX6) {
         WinoArgs a{};
         a.in = in;
         a.res = e.pro_res;
@@ -514,7 +518,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.pro_mode = e.pro;
         a.linear = e.s.conv_relu ? 0 : 1;
         if (blend) return fail(RST_ERR_UNSUPPORTED, "Winograd conv has no two-style blend prologue");
-        HIP_TRY(wino_launch(a, st));
+        HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
     } else {
         ConvArgs a{};
         a.in = in;
@@ -643,7 +647,8 @@ int rst_precision(const rst_handle* h) { return h ? h->precision : -1; }
 int rst_layer_kernel_id(const rst_handle* h, int idx) {
     if (h == nullptr || idx < 0 || idx >= (int)h->layers.size()) return -1;
     const LayerExec& e = h->layers[idx];
-    return e.kind == K_SMALL ? 100 : (e.kind == K_WINO ? 200 : (e.kind == K_WINO9 ? 201 : e.tile.id));
+    return e.kind == K_SMALL ? 100
+                             : (e.kind == K_WINO ? 200 : (e.kind == K_WINO9 ? 201 : (e.kind == K_WINOX6 ? 202 : e.tile.id)));
 }
 
 int rst_layer_output_shape(const rst_handle* h, int idx, int batch, int* hwc3) {

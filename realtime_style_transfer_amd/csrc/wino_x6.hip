@@ -1,0 +1,521 @@
+// wino_x6.hip — the residual-block convolutions (3x3, stride 1, SAME, 128 output channels;
+// realtime_style_transfer/models/styleTransfer.py:144-185) as fused Winograd F(2x2, 3x3) whose
+// transform-domain products run on the bf16 MFMA pipe with fp32-level accuracy
+// (v_mfma_f32_32x32x16_bf16, 16x the f32-MFMA rate).
+//
+// Same algorithm as wino.hip: Y = A^T [ (G g G^T) (.) (B^T d B) ] A per 2x2 output tile. Every fp32
+// operand of the 16 batched GEMMs (V = B^T d B and U = G g G^T) is split exactly into three bf16 pieces
+// x = x0 + x1 + x2 (round-to-nearest-even at each step; the remainders are exact in fp32, so the three
+// pieces hold all 24 significant bits), and a product becomes the six terms with i + j <= 2:
+//     a b = a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0  (+ dropped terms <= 2^-25 |a b|),
+// each term exact in the fp32 accumulator's input (bf16 x bf16), accumulated in fp32 — the products
+// carry fp32 precision at 6/16 of the f32-MFMA cost. U is formed on the host in f64, rounded once to
+// f32 (as wino.hip) and split on the host; V is split by the input-transform threads as they write it.
+//
+// Workgroup = 4 waves, output tile 8 x 16 pixels = 32 Winograd tiles (one 32-row MFMA M tile) x 128
+// output channels; wave w owns channels [32w, 32w+32) for all 16 transform points (16 accumulators,
+// 256 AGPRs; one wave per SIMD). Input channels go in chunks of 16 = the MFMA K: per chunk and point
+// the six terms are six MFMAs whose A operands are the V pieces (LDS, [piece][xi][tile][16 ch] bf16,
+// one ds_read_b128 per lane per piece) and B operands the U pieces (L2, packed on the host in MFMA
+// B-operand order, one 16-B load per lane per piece, kept in an 8-point register ring).
+// Per chunk c one software-pipelined step with one barrier: the 96 MFMAs on V(c) interleave with the
+// input transform + split of chunk c+1 (thread = (tile, channel pair): 16 ds_read_b64, 64 adds,
+// 3 v_cvt_pk_bf16_f32 per channel pair and point, 48 ds_write_b32), the staging of chunk c+2
+// (CIN affine [+ ReLU | + residual] prologue, materialised block output) and the loads of chunk c+3.
+// Epilogue (as wino.hip): output transform, conv bias + ReLU, store, per-(workgroup, channel) two-pass
+// {sum, M2, n} for the conditional instance norm that follows.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstring>
+#include <type_traits>
+#include <vector>
+
+#include "kernels.h"
+
+namespace rst {
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int XTH = 8, XTW = 16;                  // output pixels per workgroup
+constexpr int XPH = XTH + 2, XPW = XTW + 2;       // input patch 10 x 18
+constexpr int XNP = XPH * XPW;                    // 180 patch pixels
+constexpr int XCK = 16;                           // input channels per chunk (= MFMA K)
+constexpr int XPS = 24;                           // patch pixel stride (floats): 4 tiles' 64-B reads hit disjoint banks
+constexpr int XN = 128;                           // output channels (4 waves x 32)
+constexpr int XXI = 16;                           // transform points
+constexpr int XPF4 = XNP * XCK / 4;               // 720 float4 per chunk patch
+constexpr int XST = (XPF4 + 255) / 256;           // 3 staging float4 per thread
+constexpr int XMAX_CIN = 256;
+constexpr int XPATCH_FL = XNP * XPS;              // one patch buffer (floats)
+constexpr int XVROW = 32;                         // bytes per (piece, xi, tile) row: 16 bf16
+constexpr int XV_BYTES = 3 * XXI * 32 * XVROW;    // one V buffer: 48 KB
+constexpr int XRING = 4;                          // U register ring (points in flight)
+constexpr size_t XLDS_BYTES = (size_t)2 * XPATCH_FL * 4 + 2 * XV_BYTES + XMAX_CIN * sizeof(float2);
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        sfor<I + 1, N>(f);
+    }
+}
+
+__device__ __forceinline__ float pro_apply(int mode, float x, float2 ab, float r) {
+    float y = fmaf(ab.x, x, ab.y);
+    if (mode == PRO_AFF_RELU) y = fmaxf(y, 0.f);
+    else if (mode == PRO_AFF_RES) y = r + y;
+    return y;
+}
+
+// (x, y) -> three packed bf16 pairs (lo half: x's piece, hi half: y's piece), x = x0 + x1 + x2 exactly
+__device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned& p1, unsigned& p2) {
+    p0 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
+    const float rx = x - __uint_as_float(p0 << 16), ry = y - __uint_as_float(p0 & 0xFFFF0000u);
+    p1 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){rx, ry}, bf16x2));
+    const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xFFFF0000u);
+    p2 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){sx, sy}, bf16x2));
+}
+
+}  // namespace
+
+// Experiment knobs (tools/wino_x6_bench only; never set in the library build): X6_SKIP bit0 = no U reloads
+// in the loop, bit1 = no transform of the next chunk, bit2 = no staging / patch loads in the loop.
+#ifndef X6_SKIP
+#define X6_SKIP 0
+#endif
+#ifdef X6_PROF
+// timeline per (workgroup, wave) on the constant 100 MHz clock: start, pipeline filled, chunk loop done, end
+__device__ unsigned long long x6_tl[X6_PROF][4][4];
+#define XTL(k) \
+    if (blockIdx.x < X6_PROF && lane == 0) x6_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define XTL(k)
+#endif
+#ifdef X6_PROF2
+// s_memtime at the start of every point of every chunk, per (workgroup < X6_PROF2, wave)
+__device__ unsigned long long x6_pt[X6_PROF2][4][16][17];
+#define XPT(cc, pp) \
+    if (blockIdx.x < X6_PROF2 && lane == 0 && (cc) < 16) x6_pt[blockIdx.x][wave][(cc)][(pp)] = __builtin_amdgcn_s_memtime()
+#else
+#define XPT(cc, pp)
+#endif
+
+template <int PRO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino_x6_kernel(WinoArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* const patch = smem;                                            // [2][180][24] f32
+    unsigned char* const vbytes = reinterpret_cast<unsigned char*>(smem + 2 * XPATCH_FL);   // [2][3][16][32][32 B]
+    float2* const pab = reinterpret_cast<float2*>(vbytes + 2 * XV_BYTES);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    XTL(0);
+    int bid = xcd_tile_order(blockIdx.x, gridDim.x);   // XCD-contiguous tile runs (halo reuse in L2)
+    const int tx = bid % a.tiles_x;
+    bid /= a.tiles_x;
+    const int ty = bid % a.tiles_y;
+    const int b = bid / a.tiles_y;
+    const int y0 = ty * XTH, x0 = tx * XTW;
+    const int H = a.H, W = a.W, Cin = a.cin;
+    constexpr int pro = PRO;
+    const size_t img = (size_t)b * H * W;
+    const float* res_src = pro == PRO_AFF_RES ? a.res : a.in;
+    const int nchunks = Cin / XCK;
+
+    if constexpr (pro != PRO_NONE) {
+        for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[(size_t)b * Cin + c];
+    }
+
+    // ---- patch staging: global -> registers (clamped, branch-free) -> prologue -> LDS ----------
+    f32x4 xr[XST], rr[XST];
+#pragma unroll
+    for (int k = 0; k < XST; ++k) rr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto load_patch = [&](int chunk) __attribute__((always_inline)) {
+        const int c0 = chunk * XCK;
+        sfor<0, XST>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int it = min(tid + k * 256, XPF4 - 1);
+            const int px = it >> 2, q = it & 3;
+            const int iy = min(max(y0 - 1 + px / XPW, 0), H - 1), ix = min(max(x0 - 1 + px % XPW, 0), W - 1);
+            const size_t gi = (img + (size_t)iy * W + ix) * Cin + c0 + 4 * q;
+            xr[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
+            if constexpr (pro == PRO_AFF_RES) rr[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
+        });
+    };
+    auto stage_one = [&](int chunk, float* pbuf, auto K) __attribute__((always_inline)) {
+        constexpr int k = decltype(K)::value;
+        const int it = tid + k * 256;
+        if (k < XST - 1 || it < XPF4) {
+            const int px = it >> 2, q = it & 3;
+            const int iy = y0 - 1 + px / XPW, ix = x0 - 1 + px % XPW;
+            const int c = chunk * XCK + 4 * q;
+            f32x4 v = xr[k];
+            const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
+            if constexpr (pro != PRO_NONE) {
+                const f32x4 r = rr[k];
+                const f32x4 p01 = *reinterpret_cast<const f32x4*>(pab + c);       // (a,b) of c, c+1
+                const f32x4 p23 = *reinterpret_cast<const f32x4*>(pab + c + 2);   // (a,b) of c+2, c+3
+                v.x = pro_apply(pro, v.x, float2{p01.x, p01.y}, r.x);
+                v.y = pro_apply(pro, v.y, float2{p01.z, p01.w}, r.y);
+                v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
+                v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
+                if (a.mat != nullptr && inside && iy >= y0 && iy < y0 + XTH && ix >= x0 && ix < x0 + XTW)
+                    *reinterpret_cast<f32x4*>(a.mat + (img + (size_t)iy * W + ix) * Cin + c) = v;
+            }
+            if (!inside) v = f32x4{0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<f32x4*>(pbuf + px * XPS + 4 * q) = v;
+        }
+    };
+    auto stage = [&](int chunk, float* pbuf) __attribute__((always_inline)) {
+        sfor<0, XST>([&](auto K) __attribute__((always_inline)) { stage_one(chunk, pbuf, K); });
+    };
+
+    // ---- U pieces: lane (li, lh) of wave w reads U[chunk][xi][piece][32w + li][8lh .. 8lh+7] -------
+    const __amdgpu_buffer_rsrc_t usrd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.U), 0, nchunks * XXI * 3 * XN * XVROW, 0x00020000);
+    const int uvoff = (wave * 32 + li) * XVROW + 16 * lh;
+    short8 ur[XRING][3];
+    auto load_u = [&](int chunk, auto X, auto S) __attribute__((always_inline)) {
+        constexpr int x = decltype(X)::value, s = decltype(S)::value;
+        sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+            constexpr int p = decltype(Pc)::value;
+            ur[s][p] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     usrd, uvoff, ((chunk * XXI + x) * 3 + p) * (XN * XVROW), 0));
+        });
+    };
+
+    // ---- input transform + split, one thread per (tile tt, channel pair cp) ---------------------
+    const int tt = tid >> 3, cp = tid & 7;
+    const int twy = tt >> 3, twx = tt & 7;
+    // byte offset of this thread's bf16 pair inside a V row: 16-B halves swapped for odd tile groups
+    const int vwoff = tt * XVROW + 16 * ((cp >> 2) ^ ((tt >> 3) & 1)) + 4 * (cp & 3);
+    float dx[4][4], dy[4][4];   // the tile of channels 2cp (x) and 2cp + 1 (y); scalar f32 ops only
+    auto tr_read = [&](const float* pbuf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const f32x2 v = *reinterpret_cast<const f32x2*>(pbuf + ((2 * twy + r) * XPW + 2 * twx + c) * XPS + 2 * cp);
+                dx[r][c] = v.x;
+                dy[r][c] = v.y;
+            }
+    };
+    auto rows1 = [&](float (&d)[4][4], int c) __attribute__((always_inline)) {   // B^T d, column c, in place
+        const float a0 = d[0][c], a1 = d[1][c], a2 = d[2][c], a3 = d[3][c];
+        d[0][c] = a0 - a2;
+        d[1][c] = a1 + a2;
+        d[2][c] = a2 - a1;
+        d[3][c] = a1 - a3;
+    };
+    auto tr_rows = [&](int half) __attribute__((always_inline)) {   // columns 2 half, 2 half + 1
+        rows1(dx, 2 * half);
+        rows1(dx, 2 * half + 1);
+        rows1(dy, 2 * half);
+        rows1(dy, 2 * half + 1);
+    };
+    // (B^T d) B for row r, points q0 and q0 + 1 (q0 = 0 or 2), split and written to vbuf
+    auto tr_cols = [&](unsigned char* vbuf, int r, int q0) __attribute__((always_inline)) {
+        float v0x, v0y, v1x, v1y;
+        if (q0 == 0) {
+            v0x = dx[r][0] - dx[r][2];
+            v0y = dy[r][0] - dy[r][2];
+            v1x = dx[r][1] + dx[r][2];
+            v1y = dy[r][1] + dy[r][2];
+        } else {
+            v0x = dx[r][2] - dx[r][1];
+            v0y = dy[r][2] - dy[r][1];
+            v1x = dx[r][1] - dx[r][3];
+            v1y = dy[r][1] - dy[r][3];
+        }
+        unsigned p0, p1, p2;
+        const int xi0 = r * 4 + q0;
+        split3(v0x, v0y, p0, p1, p2);
+        *reinterpret_cast<unsigned*>(vbuf + ((0 * XXI + xi0) * 32) * XVROW + vwoff) = p0;
+        *reinterpret_cast<unsigned*>(vbuf + ((1 * XXI + xi0) * 32) * XVROW + vwoff) = p1;
+        *reinterpret_cast<unsigned*>(vbuf + ((2 * XXI + xi0) * 32) * XVROW + vwoff) = p2;
+        split3(v1x, v1y, p0, p1, p2);
+        *reinterpret_cast<unsigned*>(vbuf + ((0 * XXI + xi0 + 1) * 32) * XVROW + vwoff) = p0;
+        *reinterpret_cast<unsigned*>(vbuf + ((1 * XXI + xi0 + 1) * 32) * XVROW + vwoff) = p1;
+        *reinterpret_cast<unsigned*>(vbuf + ((2 * XXI + xi0 + 1) * 32) * XVROW + vwoff) = p2;
+    };
+
+    floatx16 acc[XXI];
+#pragma unroll
+    for (int x = 0; x < XXI; ++x)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+
+    // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..7) in flight --
+    if constexpr (pro != PRO_NONE) __syncthreads();   // pab visible before the first staging
+    load_patch(0);
+    sfor<0, XRING>([&](auto X) __attribute__((always_inline)) { load_u(0, X, X); });
+    stage(0, patch);
+    if (nchunks > 1) load_patch(1);
+    __syncthreads();
+    tr_read(patch);
+    tr_rows(0);
+    tr_rows(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        tr_cols(vbytes, r, 0);
+        tr_cols(vbytes, r, 2);
+    }
+    if (nchunks > 1) {
+        stage(1, patch + XPATCH_FL);
+        if (nchunks > 2) load_patch(2);
+    }
+    __syncthreads();
+    XTL(1);
+
+    // A operands of point x: the three pieces of this lane's tile row, 16-B half lh (swizzled)
+    const int varow = li * XVROW + 16 * (lh ^ ((li >> 3) & 1));
+    // one chunk: P = chunk parity (V(c) in V[P], patch(c+1) in patch[1-P], patch[P] free)
+    for (int c = 0; c < nchunks; ++c) {
+        const int P = c & 1;
+        // past the last chunk the pipeline repeats the last chunk's work into buffers nobody reads (branch-
+        // free, so the transform / staging instructions can interleave with the MFMAs); restaging a chunk
+        // writes the same materialised values again
+        const int c1 = min(c + 1, nchunks - 1), c2 = min(c + 2, nchunks - 1), c3 = min(c + 3, nchunks - 1);
+        const unsigned char* va = vbytes + P * XV_BYTES + varow;
+        unsigned char* const vnext = vbytes + (1 - P) * XV_BYTES;
+        const float* const pnext = patch + (1 - P) * XPATCH_FL;
+        short8 av[2][3];
+        sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+            constexpr int p = decltype(Pc)::value;
+            av[0][p] = *reinterpret_cast<const short8*>(va + (p * XXI) * 32 * XVROW);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        sfor<0, XXI>([&](auto X) __attribute__((always_inline)) {
+            constexpr int x = decltype(X)::value;
+            constexpr int s = x & (XRING - 1);
+            XPT(c, x);
+            if constexpr (x + 1 < XXI) {
+                sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+                    constexpr int p = decltype(Pc)::value;
+                    av[(x + 1) & 1][p] = *reinterpret_cast<const short8*>(va + (p * XXI + x + 1) * 32 * XVROW);
+                });
+            }
+            __builtin_amdgcn_sched_barrier(0);   // the reads of point x+1 issue before the MFMAs of x
+            const short8* A = av[x & 1];
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], ur[s][0], acc[x], 0, 0, 0);   // a0 b0
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], ur[s][1], acc[x], 0, 0, 0);   // a0 b1
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], ur[s][0], acc[x], 0, 0, 0);   // a1 b0
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], ur[s][2], acc[x], 0, 0, 0);   // a0 b2
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], ur[s][1], acc[x], 0, 0, 0);   // a1 b1
+            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], ur[s][0], acc[x], 0, 0, 0);   // a2 b0
+            // refill the ring slot: point x + 8 of this chunk, or point x - 8 of the next (clamped:
+            // past the last chunk this re-reads U nobody uses)
+            if constexpr (!(X6_SKIP & 1)) {
+                if constexpr (x < XXI - XRING) load_u(c, std::integral_constant<int, x + XRING>{}, std::integral_constant<int, s>{});
+                else load_u(c1, std::integral_constant<int, x + XRING - XXI>{}, std::integral_constant<int, s>{});
+            }
+            // transform + split of chunk c+1 into V[1-P]
+            if constexpr (!(X6_SKIP & 2)) {
+                if constexpr (x == 0) tr_read(pnext);
+                if constexpr (x == 1 || x == 2) tr_rows(x - 1);
+                if constexpr (x >= 3 && x < 11) tr_cols(vnext, (x - 3) >> 1, ((x - 3) & 1) * 2);
+            }
+            // staging of chunk c+2 into patch[P] (free since chunk c's transform), loads of chunk c+3
+            if constexpr (!(X6_SKIP & 4) && x >= 11 && x < 11 + XST)
+                stage_one(c2, patch + P * XPATCH_FL, std::integral_constant<int, x - 11>{});
+            if constexpr (!(X6_SKIP & 4) && x == 11 + XST) load_patch(c3);
+            // interleave: each MFMA followed by up to 6 VALU / LDS / VMEM instructions of this point
+            sfor<0, 6>([&](auto) __attribute__((always_inline)) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x322, 6, 0);
+            });
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        XPT(c, 16);
+        __syncthreads();
+    }
+    XTL(2);
+
+    // ---- epilogue: output transform, bias + ReLU, store, tile statistics -----------------------
+    const int co = wave * 32 + li;
+    const float bias = a.bias[co];
+    float yv[64];
+    float s = 0.f, cnt = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;   // Winograd tile of this accumulator row
+        const int wy = row >> 3, wx = row & 7;
+        float m[16];
+#pragma unroll
+        for (int x = 0; x < XXI; ++x) m[x] = acc[x][j];
+        // T = A^T M (2 x 4), Y = T A (2 x 2); A^T = [[1,1,1,0],[0,1,-1,-1]]
+        float t0[4], t1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            t0[c] = m[0 * 4 + c] + m[1 * 4 + c] + m[2 * 4 + c];
+            t1[c] = m[1 * 4 + c] - m[2 * 4 + c] - m[3 * 4 + c];
+        }
+        const float yy[4] = {t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3], t1[0] + t1[1] + t1[2],
+                             t1[1] - t1[2] - t1[3]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
+            const float v = a.linear ? yy[q] + bias : fmaxf(yy[q] + bias, 0.f);
+            const bool ok = oy < H && ox < W;
+            yv[j * 4 + q] = ok ? v : 0.f;
+            if (ok) {
+                a.out[(img + (size_t)oy * W + ox) * XN + co] = v;
+                s += v;
+                cnt += 1.f;
+            }
+        }
+    }
+    if (a.part != nullptr) {
+        s += __shfl_xor(s, 32);
+        cnt += __shfl_xor(cnt, 32);
+        const float mean = cnt > 0.f ? s / cnt : 0.f;
+        float m2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;
+            const int wy = row >> 3, wx = row & 7;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
+                const float dd = yv[j * 4 + q] - mean;
+                if (oy < H && ox < W) m2 = fmaf(dd, dd, m2);
+            }
+        }
+        m2 += __shfl_xor(m2, 32);
+        if (lh == 0) {
+            const int n_part = a.tiles_y * a.tiles_x;
+            a.part[((size_t)b * XN + co) * n_part + ty * a.tiles_x + tx] = make_float4(s, m2, cnt, 0.f);
+        }
+    }
+    XTL(3);
+}
+
+#ifdef X6_PROF
+// timeline summary of the most recent launch (tools/wino_x6_bench)
+void x6_timeline_print(int nwg) {
+    std::vector<unsigned long long> tl((size_t)X6_PROF * 16);
+    if (hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(x6_tl), tl.size() * 8) != hipSuccess) return;
+    if (nwg > X6_PROF) nwg = X6_PROF;
+    unsigned long long t0 = ~0ull, tend = 0, slast = 0;
+    double fill = 0, loop = 0, epi = 0;
+    for (int g = 0; g < nwg; ++g)
+        for (int w = 0; w < 4; ++w) {
+            const unsigned long long* q = &tl[((size_t)g * 4 + w) * 4];
+            t0 = q[0] < t0 ? q[0] : t0;
+            tend = q[3] > tend ? q[3] : tend;
+            slast = q[0] > slast ? q[0] : slast;
+            fill += (double)(q[1] - q[0]);
+            loop += (double)(q[2] - q[1]);
+            epi += (double)(q[3] - q[2]);
+        }
+    const double nw = nwg * 4.0;
+    printf("  timeline (us): first start -> last end %.2f, last start +%.2f; per wave: fill %.2f, loop %.2f, "
+           "epilogue %.2f\n", (tend - t0) * 0.01, (slast - t0) * 0.01, fill / nw * 0.01, loop / nw * 0.01,
+           epi / nw * 0.01);
+}
+#endif
+
+#ifdef X6_PROF2
+void x6_points_print(int nwg, int nchunks) {
+    std::vector<unsigned long long> pt((size_t)X6_PROF2 * 4 * 16 * 17);
+    if (hipMemcpyFromSymbol(pt.data(), HIP_SYMBOL(x6_pt), pt.size() * 8) != hipSuccess) return;
+    if (nwg > X6_PROF2) nwg = X6_PROF2;
+    double dur[17] = {0}, bar = 0;
+    int n = 0;
+    for (int g = 0; g < nwg; ++g)
+        for (int w = 0; w < 4; ++w)
+            for (int c = 1; c + 1 < nchunks && c < 16; ++c) {
+                const unsigned long long* q = &pt[(((size_t)g * 4 + w) * 16 + c) * 17];
+                for (int x = 0; x < 16; ++x) dur[x] += (double)(q[x + 1] - q[x]);
+                bar += (double)(q[17] - q[16]);   // next chunk's point 0 - this chunk's end (barrier)
+                ++n;
+            }
+    if (!n) return;
+    printf("  per-point s_memtime ticks (chunks 1..n-2, mean over %d wave-chunks):", n);
+    double tot = 0;
+    for (int x = 0; x < 16; ++x) { printf(" %.0f", dur[x] / n); tot += dur[x] / n; }
+    printf(" | barrier+top %.0f | chunk %.0f\n", bar / n, tot + bar / n);
+}
+#endif
+
+bool wino_x6_supported(int kh, int stride, int cin, int cout) {
+    return kh == 3 && stride == 1 && cout == XN && cin % XCK == 0 && cin <= XMAX_CIN;
+}
+
+static uint16_t bf16_rne_host(float x) {
+    uint32_t u;
+    std::memcpy(&u, &x, 4);
+    return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+static float bf16_val_host(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+// U pieces [chunk][xi][piece][co][16] bf16 (returned as the float-sized buffer holding the bits):
+// U = G g G^T in f64 rounded to f32 (bitwise wino_pack_weights' value), then split into three bf16 pieces
+// with round-to-nearest-even at each step (the device split of V does the same with v_cvt_pk_bf16_f32)
+std::vector<float> wino_x6_pack_weights(const float* kern, int cin) {
+#pragma clang fp contract(off)
+    static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    const size_t n16 = (size_t)cin / XCK * XXI * 3 * XN * XCK;
+    std::vector<uint16_t> U(n16);
+    for (int ci = 0; ci < cin; ++ci)
+        for (int co = 0; co < XN; ++co) {
+            double g[3][3];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) g[i][j] = kern[(((size_t)i * 3 + j) * cin + ci) * XN + co];
+            for (int p = 0; p < 4; ++p)
+                for (int q = 0; q < 4; ++q) {
+                    double u = 0.0;
+                    for (int i = 0; i < 3; ++i)
+                        for (int j = 0; j < 3; ++j) u += G[p][i] * g[i][j] * G[q][j];
+                    const float uf = (float)u;
+                    uint16_t pc[3];
+                    pc[0] = bf16_rne_host(uf);
+                    const float r = uf - bf16_val_host(pc[0]);
+                    pc[1] = bf16_rne_host(r);
+                    pc[2] = bf16_rne_host(r - bf16_val_host(pc[1]));
+                    const int chunk = ci / XCK, c = ci % XCK, xi = p * 4 + q;
+                    for (int k = 0; k < 3; ++k)
+                        U[((((size_t)chunk * XXI + xi) * 3 + k) * XN + co) * XCK + c] = pc[k];
+                }
+        }
+    std::vector<float> out((n16 + 1) / 2);
+    std::memcpy(out.data(), U.data(), n16 * 2);
+    return out;
+}
+
+hipError_t wino_x6_prepare() {
+    for (const void* k : {(const void*)wino_x6_kernel<PRO_NONE>, (const void*)wino_x6_kernel<PRO_AFF_RELU>,
+                          (const void*)wino_x6_kernel<PRO_AFF>, (const void*)wino_x6_kernel<PRO_AFF_RES>}) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)XLDS_BYTES);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
+    if (a.cin % XCK != 0 || a.cin > XMAX_CIN || a.tiles_y != (a.H + XTH - 1) / XTH ||
+        a.tiles_x != (a.W + XTW - 1) / XTW)
+        return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
+    switch (a.pro_mode) {
+        case PRO_NONE: hipLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
+        case PRO_AFF_RELU: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
+        case PRO_AFF: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
+        case PRO_AFF_RES: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RES>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rst

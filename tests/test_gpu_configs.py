@@ -22,7 +22,7 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32_winograd"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32_winograd", "winograd_bf16x6"])
 def test_config1_sdr_256x256_inference_model(precision):
     _need_gpu()
     from oracle import predictor_ref as PR

@@ -231,10 +231,15 @@ def test_split_bf16_precision_modes(precision, tol):
     assert err < tol, err   # bf16x3: the float64 simulation of the split gives ~2e-5 here; fp32 gives ~2e-6
 
 
-def test_winograd_residual_convs_match_oracle():
+WINO_MODES = {"fp32_winograd": 200, "winograd_bf16x6": 202}
+
+
+@pytest.mark.parametrize("precision", list(WINO_MODES))
+def test_winograd_residual_convs_match_oracle(precision):
     """RST_PRECISION_FP32_WINOGRAD: residual convs as fused Winograd F(2x2,3x3) and the 9x9 start conv as
     nine F(2x2,3x3) sub-convolutions on f32 MFMA vs float64, small geometry (production channel counts)
-    and odd sizes (partial 8x16 tiles)."""
+    and odd sizes (partial 8x16 tiles). RST_PRECISION_WINOGRAD_BF16X6: the same with the residual convs'
+    transform-domain products as exact 3-piece split-bf16 MFMA terms (fp32-level: same bounds)."""
     _need_gpu()
     from oracle import numpy_ref as R
     from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
@@ -246,9 +251,9 @@ def test_winograd_residual_convs_match_oracle():
         sp = synthetic_style_params(2, 1, plan.num_style_params, plan, seed=1)
         x = np.random.default_rng(0).random((2,) + ins).astype(np.float32)
         ref = R.transfer_forward(x, sp, w, ins, outs, br, bf)
-        m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision="fp32_winograd")
+        m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision=precision)
         ids = [m.layer_kernel_id(i) for i in range(m.num_layers())]
-        assert ids[0] == 201 and ids[3:13] == [200] * 10, ids   # 9x9 composite Winograd; residual Winograd
+        assert ids[0] == 201 and ids[3:13] == [WINO_MODES[precision]] * 10, ids   # 9x9 / residual Winograd
         inp = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}
         y = m(inp)
         err = float(np.abs(y.cpu().numpy() - ref).max())
@@ -268,7 +273,8 @@ def test_winograd_residual_convs_match_oracle():
             assert np.abs(g - r).max() / max(1.0, np.abs(r).max()) < 1e-4
 
 
-def test_winograd_full_size_matches_torch_oracle():
+@pytest.mark.parametrize("precision", list(WINO_MODES))
+def test_winograd_full_size_matches_torch_oracle(precision):
     _need_gpu()
     from oracle.torch_ref import TorchTransfer
     from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
@@ -279,7 +285,7 @@ def test_winograd_full_size_matches_torch_oracle():
     plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
     ws = init_weights(plan, seed=2)
     model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
-                                           weights=ws, max_batch=1, precision="fp32_winograd")
+                                           weights=ws, max_batch=1, precision=precision)
     x = np.random.default_rng(0).random((1,) + ins).astype(np.float32)
     sp = synthetic_style_params(1, 1, P, plan, seed=1)
     y = model({'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}).cpu().numpy()
@@ -287,7 +293,7 @@ def test_winograd_full_size_matches_torch_oracle():
     err = float(np.abs(y - ref).max())
     import json
     os.makedirs(OUT, exist_ok=True)
-    with open(os.path.join(OUT, 'winograd_parity.json'), 'w') as f:
+    with open(os.path.join(OUT, f'{precision}_parity.json'), 'w') as f:
         json.dump({'max_abs_full_size': err}, f)
     assert err < OUT_TOL, err
 
