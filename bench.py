@@ -59,6 +59,7 @@ KERNEL_NAMES = {
     113: "conv_bf3<3x3 s1 CK32 NT64 8x16 bf16x6>",
     200: "wino_conv<F(2x2,3x3) 8x16 N128 f32 MFMA>", 201: "wino9_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 f32 MFMA>",
     202: "wino_x6_conv<F(2x2,3x3) 8x16 N128 split-bf16 x6 MFMA>",
+    203: "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 split-bf16 x6 MFMA>",
 }
 
 
@@ -72,10 +73,10 @@ DTYPE_DESC = {
     "bf16x3": "fp32 via 2-piece split bf16 (3 product terms, 16 significant bits per operand), fp32 accumulate, "
               "on the residual convs; other layers fp32 MFMA",
     "bf16": "bf16 operands (8 significant bits), fp32 accumulate, on the residual convs; other layers fp32 MFMA",
-    "winograd_bf16x6": "fp32-level: the residual convs as fused Winograd F(2x2,3x3) whose transform-domain products "
-                       "are exact 3-piece split-bf16 MFMA terms (each fp32 operand = 3 bf16 pieces holding all 24 "
-                       "significant bits, 6 product terms, dropped terms <= 2^-25 of each product, fp32 "
-                       "accumulate); the 9x9 start conv as f32-MFMA composite Winograd; other layers f32 MFMA",
+    "winograd_bf16x6": "fp32-level: the residual convs and the 9x9 start conv (nine 3x3 sub-kernels) as fused Winograd "
+                       "F(2x2,3x3) whose transform-domain products are exact 3-piece split-bf16 MFMA terms (each "
+                       "fp32 operand = 3 bf16 pieces holding all 24 significant bits, 6 product terms, dropped "
+                       "terms <= 2^-25 of each product, fp32 accumulate); other layers f32 MFMA",
 }
 
 
@@ -97,6 +98,8 @@ def executed_mfma(model, plan, i: int, B: int):
         return 2.0 * tiles * 16 * 9 * 18 * l.cout, FP32_MFMA_PEAK_TFLOPS
     if kid == 202:
         return 6 * 2.0 * tiles * 16 * l.cin * l.cout, BF16_MFMA_PEAK_TFLOPS
+    if kid == 203:   # 9 sub-kernels x 16 channels + the gathered channel-16 K-step (16 wide), 6 terms
+        return 6 * 2.0 * tiles * 16 * (9 * 16 + 16) * l.cout, BF16_MFMA_PEAK_TFLOPS
     if 101 <= kid < 200:
         terms = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}.get(model.precision, 6)
         return terms * layer_flops(l) * B, BF16_MFMA_PEAK_TFLOPS

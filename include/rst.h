@@ -80,7 +80,7 @@ void rst_destroy(rst_handle* h);
  * WINOGRAD_BF16X6: as FP32_WINOGRAD, with the residual convs' transform-domain products (V = B^T d B times
  * U = G g G^T) computed as BF16X6 terms: each fp32 operand split exactly into three bf16 pieces, six
  * terms, fp32 accumulation (dropped terms <= 2^-25 of each product) — fp32-level products on the bf16
- * MFMA pipe; the start conv stays f32-MFMA Winograd.
+ * MFMA pipe; the 9x9 start conv likewise (its nine 3x3 sub-kernels' Winograd products as BF16X6 terms).
  * BF16: plain bf16 operands (round-to-nearest-even), fp32 accumulation — a Keras mixed_bfloat16
  * policy's arithmetic (BASELINE config 4 trains in bf16) — on the same layers as the split modes. */
 enum { RST_PRECISION_FP32 = 0, RST_PRECISION_BF16X3 = 1, RST_PRECISION_BF16X6 = 2, RST_PRECISION_FP32_WINOGRAD = 3,

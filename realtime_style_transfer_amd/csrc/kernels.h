@@ -112,6 +112,11 @@ std::vector<float> wino9_pack_weights(const float* kern, int cin);
 // wino9_pack_weights on the device (kern: HWIO [9][9][cin][32] on the device; U zero-initialised)
 hipError_t wino9_transform_launch(const float* kern, int cin, float* U, hipStream_t st);
 hipError_t wino9_launch(const Wino9Args& a, hipStream_t st);
+// The same layer with the transform-domain products as exact 3-piece split-bf16 MFMA terms (wino9_x6.hip);
+// U = wino9_x6_pack_weights (bf16 pieces [10][16][3][32][16]).
+std::vector<float> wino9_x6_pack_weights(const float* kern, int cin);
+hipError_t wino9_x6_prepare();
+hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st);
 int wino_tiles_y(int H);
 int wino_tiles_x(int W);
 std::vector<float> wino_pack_weights(const float* kern, int cin);

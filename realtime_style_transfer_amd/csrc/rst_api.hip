@@ -199,9 +199,11 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.n_part = e.tiles_y * e.tiles_x;
     } else if ((precision == RST_PRECISION_FP32_WINOGRAD || precision == RST_PRECISION_WINOGRAD_BF16X6) &&
                s.keras_kind == 0 && wino9_supported(s.k, s.stride, s.cin, s.cout) && s.norm == N_BN && s.conv_relu) {
-        // ---- first layer (9x9 conv + ReLU + BN + ReLU) as composite Winograd (wino9.hip)
-        e.kind = K_WINO9;
-        packed = wino9_pack_weights(kern, s.cin);
+        // ---- first layer (9x9 conv + ReLU + BN + ReLU) as composite Winograd: f32 MFMA (wino9.hip) or
+        // exact split-bf16 MFMA products (wino9_x6.hip)
+        const bool x6 = precision == RST_PRECISION_WINOGRAD_BF16X6;
+        e.kind = x6 ? K_WINO9X6 : K_WINO9;
+        packed = x6 ? wino9_x6_pack_weights(kern, s.cin) : wino9_pack_weights(kern, s.cin);
         bias_n.assign(bias, bias + s.cout);
         e.ntot = s.cout;
         e.pad_t = e.pad_l = 4;
@@ -432,7 +434,10 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     // kernels with > 64 KB of dynamic LDS need the attribute before any (graph-captured) launch
     for (auto& e : h->layers) {
         if (e.kind == K_SMALL || e.kind == K_WINO9) continue;
-        hipError_t pe = e.kind == K_WINO ? wino_prepare() : (e.kind == K_WINOX6 ? wino_x6_prepare() : conv_prepare(e.tile));
+        hipError_t pe = e.kind == K_WINO      ? wino_prepare()
+                        : e.kind == K_WINOX6  ? wino_x6_prepare()
+                        : e.kind == K_WINO9X6 ? wino9_x6_prepare()
+                                              : conv_prepare(e.tile);
         if (pe != hipSuccess) {
             delete h;
             return fail(RST_ERR_HIP, std::string("conv_prepare: ") + hipGetErrorString(pe));
@@ -484,7 +489,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         if (e.pro != PRO_AFF_RELU && e.pro != PRO_NONE)
             return fail(RST_ERR_UNSUPPORTED, "last layer prologue must be CIN+ReLU");
         HIP_TRY(small_conv_launch(a, st));
-    } else if (e.kind == K_WINO9) {
+    } else if (e.kind == K_WINO9 || e.kind == K_WINO9X6) {
         if (e.pro != PRO_NONE) return fail(RST_ERR_UNSUPPORTED, "9x9 Winograd conv reads the network input only");
         Wino9Args a{};
         a.in = in;
@@ -498,7 +503,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.cin = e.s.cin;
         a.tiles_y = e.tiles_y;
         a.tiles_x = e.tiles_x;
-        HIP_TRY(wino9_launch(a, st));
+        HIP_TRY(e.kind == K_WINO9X6 ? wino9_x6_launch(a, st) : wino9_launch(a, st));
     } else if (e.kind == K_WINO || e.kind == K_WINOX6) {
         WinoArgs a{};
         a.in = in;
@@ -647,8 +652,14 @@ int rst_precision(const rst_handle* h) { return h ? h->precision : -1; }
 int rst_layer_kernel_id(const rst_handle* h, int idx) {
     if (h == nullptr || idx < 0 || idx >= (int)h->layers.size()) return -1;
     const LayerExec& e = h->layers[idx];
-    return e.kind == K_SMALL ? 100
-                             : (e.kind == K_WINO ? 200 : (e.kind == K_WINO9 ? 201 : (e.kind == K_WINOX6 ? 202 : e.tile.id)));
+    switch (e.kind) {
+        case K_SMALL: return 100;
+        case K_WINO: return 200;
+        case K_WINO9: return 201;
+        case K_WINOX6: return 202;
+        case K_WINO9X6: return 203;
+        default: return e.tile.id;
+    }
 }
 
 int rst_layer_output_shape(const rst_handle* h, int idx, int batch, int* hwc3) {

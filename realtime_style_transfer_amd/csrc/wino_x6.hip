@@ -41,6 +41,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short short8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int XTH = 8, XTW = 16;                  // output pixels per workgroup
 constexpr int XPH = XTH + 2, XPW = XTW + 2;       // input patch 10 x 18
@@ -176,6 +177,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         sfor<0, XST>([&](auto K) __attribute__((always_inline)) { stage_one(chunk, pbuf, K); });
     };
 
+    // Per-thread staging descriptors (item k = float4 tid + 256k of a chunk's 720-float4 patch), computed
+    // once: global float offset of the clamped source pixel's channel quad at chunk 0; LDS float offset
+    // (items past 720 write a pad slot) | inside-image flag << 16; byte offset of the materialised block
+    // output at chunk 0 (past the buffer when the pixel is not interior: a buffer store drops it).
+    int sg_goff[XST], sg_lf[XST], sg_moff[XST];
+#pragma unroll
+    for (int k = 0; k < XST; ++k) {
+        const int it = tid + k * 256, itc = min(it, XPF4 - 1);
+        const int px = itc >> 2, q = itc & 3;
+        const int iy = y0 - 1 + px / XPW, ix = x0 - 1 + px % XPW;
+        const int cy = min(max(iy, 0), H - 1), cx = min(max(ix, 0), W - 1);
+        sg_goff[k] = (int)((img + (size_t)cy * W + cx) * Cin) + 4 * q;
+        const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
+        const int loff = it < XPF4 ? px * XPS + 4 * q : ((it - XPF4) >> 2) * XPS + XCK + 4 * (q & 1);
+        sg_lf[k] = loff | (inside ? 1 << 16 : 0);
+        const bool interior = it < XPF4 && inside && iy >= y0 && iy < y0 + XTH && ix >= x0 && ix < x0 + XTW;
+        sg_moff[k] = interior ? (int)(((img + (size_t)iy * W + ix) * Cin + 4 * q) * 4) : 0x7F000000;
+    }
+    const __amdgpu_buffer_rsrc_t msrd = __builtin_amdgcn_make_buffer_rsrc(
+        a.mat, 0, a.mat != nullptr ? (int)((size_t)a.batch * H * W * Cin * 4) : 0, 0x00020000);
+    const float bias_co = a.bias[wave * 32 + li];   // epilogue operand, fetched early
+
     // ---- U pieces: lane (li, lh) of wave w reads U[chunk][xi][piece][32w + li][8lh .. 8lh+7] -------
     const __amdgpu_buffer_rsrc_t usrd = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.U), 0, nchunks * XXI * 3 * XN * XVROW, 0x00020000);
@@ -275,6 +298,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     // A operands of point x: the three pieces of this lane's tile row, 16-B half lh (swizzled)
     const int varow = li * XVROW + 16 * (lh ^ ((li >> 3) & 1));
+    // Working state of the in-loop transform / staging, which is cut into pieces placed explicitly
+    // between the six MFMAs of a point (each MFMA of a point depends on the previous one, so whatever
+    // the scheduler clusters behind a run of MFMAs would run with the matrix pipe idle).
+    float w0x = 0.f, w0y = 0.f, w1x = 0.f, w1y = 0.f;
+    unsigned qa0 = 0, qa1 = 0, qa2 = 0, qb0 = 0, qb1 = 0, qb2 = 0;
+    f32x4 sp01 = f32x4{0.f, 0.f, 0.f, 0.f}, sp23 = sp01, sv = sp01;
+    // p = the bf16 pair nearest (x, y); (x, y) -= its value (exact in fp32)
+    auto piece = [&](float& x, float& y, unsigned& p) __attribute__((always_inline)) {
+        p = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
+        x = x - __uint_as_float(p << 16);
+        y = y - __uint_as_float(p & 0xFFFF0000u);
+    };
+    auto vwrite = [&](unsigned char* vbuf, int xi, unsigned p0, unsigned p1, unsigned p2) __attribute__((always_inline)) {
+        *reinterpret_cast<unsigned*>(vbuf + ((0 * XXI + xi) * 32) * XVROW + vwoff) = p0;
+        *reinterpret_cast<unsigned*>(vbuf + ((1 * XXI + xi) * 32) * XVROW + vwoff) = p1;
+        *reinterpret_cast<unsigned*>(vbuf + ((2 * XXI + xi) * 32) * XVROW + vwoff) = p2;
+    };
+
     // one chunk: P = chunk parity (V(c) in V[P], patch(c+1) in patch[1-P], patch[P] free)
     for (int c = 0; c < nchunks; ++c) {
         const int P = c & 1;
@@ -285,6 +326,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const unsigned char* va = vbytes + P * XV_BYTES + varow;
         unsigned char* const vnext = vbytes + (1 - P) * XV_BYTES;
         const float* const pnext = patch + (1 - P) * XPATCH_FL;
+        float* const pstage = patch + P * XPATCH_FL;
         short8 av[2][3];
         sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
             constexpr int p = decltype(Pc)::value;
@@ -295,42 +337,113 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             constexpr int x = decltype(X)::value;
             constexpr int s = x & (XRING - 1);
             XPT(c, x);
-            if constexpr (x + 1 < XXI) {
-                sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
-                    constexpr int p = decltype(Pc)::value;
-                    av[(x + 1) & 1][p] = *reinterpret_cast<const short8*>(va + (p * XXI + x + 1) * 32 * XVROW);
-                });
-            }
-            __builtin_amdgcn_sched_barrier(0);   // the reads of point x+1 issue before the MFMAs of x
-            const short8* A = av[x & 1];
-            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], ur[s][0], acc[x], 0, 0, 0);   // a0 b0
-            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], ur[s][1], acc[x], 0, 0, 0);   // a0 b1
-            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], ur[s][0], acc[x], 0, 0, 0);   // a1 b0
-            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], ur[s][2], acc[x], 0, 0, 0);   // a0 b2
-            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], ur[s][1], acc[x], 0, 0, 0);   // a1 b1
-            acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], ur[s][0], acc[x], 0, 0, 0);   // a2 b0
-            // refill the ring slot: point x + 8 of this chunk, or point x - 8 of the next (clamped:
-            // past the last chunk this re-reads U nobody uses)
-            if constexpr (!(X6_SKIP & 1)) {
-                if constexpr (x < XXI - XRING) load_u(c, std::integral_constant<int, x + XRING>{}, std::integral_constant<int, s>{});
-                else load_u(c1, std::integral_constant<int, x + XRING - XXI>{}, std::integral_constant<int, s>{});
-            }
-            // transform + split of chunk c+1 into V[1-P]
-            if constexpr (!(X6_SKIP & 2)) {
-                if constexpr (x == 0) tr_read(pnext);
-                if constexpr (x == 1 || x == 2) tr_rows(x - 1);
-                if constexpr (x >= 3 && x < 11) tr_cols(vnext, (x - 3) >> 1, ((x - 3) & 1) * 2);
-            }
-            // staging of chunk c+2 into patch[P] (free since chunk c's transform), loads of chunk c+3
-            if constexpr (!(X6_SKIP & 4) && x >= 11 && x < 11 + XST)
-                stage_one(c2, patch + P * XPATCH_FL, std::integral_constant<int, x - 11>{});
-            if constexpr (!(X6_SKIP & 4) && x == 11 + XST) load_patch(c3);
-            // interleave: each MFMA followed by up to 6 VALU / LDS / VMEM instructions of this point
-            sfor<0, 6>([&](auto) __attribute__((always_inline)) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x322, 6, 0);
+            sfor<0, 6>([&](auto K) __attribute__((always_inline)) {
+                constexpr int k = decltype(K)::value;
+                // the six terms (A piece, B piece): a0b0 a0b1 a1b0 a0b2 a1b1 a2b0; B2, B1, B0 are last read
+                // by MFMAs 3, 4, 5, so their ring registers are refilled right behind those
+                constexpr int ap = k == 2 || k == 4 ? 1 : (k == 5 ? 2 : 0);
+                constexpr int bp = k == 1 || k == 4 ? 1 : (k == 3 ? 2 : 0);
+                acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[x & 1][ap], ur[s][bp], acc[x], 0, 0, 0);
+                // A operands of point x + 1
+                if constexpr (k == 0 && x + 1 < XXI) {
+                    sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+                        constexpr int p = decltype(Pc)::value;
+                        av[(x + 1) & 1][p] = *reinterpret_cast<const short8*>(va + (p * XXI + x + 1) * 32 * XVROW);
+                    });
+                }
+                // U ring refill: point x + XRING of this chunk or point x + XRING - 16 of the next (clamped)
+                if constexpr (!(X6_SKIP & 1) && k >= 3) {
+                    constexpr int p = 5 - k;
+                    constexpr int xn = (x + XRING) & (XXI - 1);
+                    const int cn = x + XRING < XXI ? c : c1;
+                    ur[s][p] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             usrd, uvoff, ((cn * XXI + xn) * 3 + p) * (XN * XVROW), 0));
+                }
+                // input transform + split of chunk c+1 into V[1-P]
+                if constexpr (!(X6_SKIP & 2)) {
+                    if constexpr (x < 2 && k < 4) {              // patch reads: row 2x + k/2, columns 2(k&1), +1
+                        constexpr int r = 2 * x + (k >> 1);
+#pragma unroll
+                        for (int cc = 2 * (k & 1); cc < 2 * (k & 1) + 2; ++cc) {
+                            const f32x2 v = *reinterpret_cast<const f32x2*>(
+                                pnext + ((2 * twy + r) * XPW + 2 * twx + cc) * XPS + 2 * cp);
+                            dx[r][cc] = v.x;
+                            dy[r][cc] = v.y;
+                        }
+                    }
+                    if constexpr (x == 2 && k < 4) {             // B^T d, column k
+                        rows1(dx, k);
+                        rows1(dy, k);
+                    }
+                    if constexpr (x >= 3 && x < 11) {            // (B^T d) B: row r, points xi0, xi0 + 1
+                        constexpr int r = (x - 3) >> 1, q0 = ((x - 3) & 1) * 2, xi0 = r * 4 + q0;
+                        if constexpr (k == 0) {
+                            if constexpr (q0 == 0) {
+                                w0x = dx[r][0] - dx[r][2];
+                                w0y = dy[r][0] - dy[r][2];
+                                w1x = dx[r][1] + dx[r][2];
+                                w1y = dy[r][1] + dy[r][2];
+                            } else {
+                                w0x = dx[r][2] - dx[r][1];
+                                w0y = dy[r][2] - dy[r][1];
+                                w1x = dx[r][1] - dx[r][3];
+                                w1y = dy[r][1] - dy[r][3];
+                            }
+                        }
+                        if constexpr (k == 1) piece(w0x, w0y, qa0);
+                        if constexpr (k == 2) piece(w0x, w0y, qa1);
+                        if constexpr (k == 3) {
+                            piece(w0x, w0y, qa2);
+                            vwrite(vnext, xi0, qa0, qa1, qa2);
+                            piece(w1x, w1y, qb0);
+                        }
+                        if constexpr (k == 4) piece(w1x, w1y, qb1);
+                        if constexpr (k == 5) {
+                            piece(w1x, w1y, qb2);
+                            vwrite(vnext, xi0 + 1, qb0, qb1, qb2);
+                        }
+                    }
+                }
+                // staging of chunk c+2 into patch[P] (free since chunk c's transform): prologue affine reads,
+                // prologue math + materialised block output, patch write (branch-free: precomputed descriptors)
+                if constexpr (!(X6_SKIP & 4) && x >= 11 && x < 11 + XST) {
+                    constexpr int ks = x - 11;
+                    const int cch = c2 * XCK + 4 * (tid & 3);
+                    if constexpr (k == 0 && pro != PRO_NONE) {
+                        sp01 = *reinterpret_cast<const f32x4*>(pab + cch);
+                        sp23 = *reinterpret_cast<const f32x4*>(pab + cch + 2);
+                    }
+                    if constexpr (k == 2) {
+                        sv = xr[ks];
+                        if constexpr (pro != PRO_NONE) {
+                            const f32x4 r = rr[ks];
+                            sv.x = pro_apply(pro, sv.x, float2{sp01.x, sp01.y}, r.x);
+                            sv.y = pro_apply(pro, sv.y, float2{sp01.z, sp01.w}, r.y);
+                            sv.z = pro_apply(pro, sv.z, float2{sp23.x, sp23.y}, r.z);
+                            sv.w = pro_apply(pro, sv.w, float2{sp23.z, sp23.w}, r.w);
+                            if (a.mat != nullptr)
+                                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), msrd,
+                                                                       sg_moff[ks] + c2 * XCK * 4, 0, 0);
+                        }
+                    }
+                    if constexpr (k == 4) {
+                        const bool inside = (sg_lf[ks] >> 16) != 0;
+                        sv.x = inside ? sv.x : 0.f;
+                        sv.y = inside ? sv.y : 0.f;
+                        sv.z = inside ? sv.z : 0.f;
+                        sv.w = inside ? sv.w : 0.f;
+                        *reinterpret_cast<f32x4*>(pstage + (sg_lf[ks] & 0xFFFF)) = sv;
+                    }
+                }
+                // global loads of chunk c+3's patch (into the registers the staging above consumed)
+                if constexpr (!(X6_SKIP & 4) && x == 11 + XST && (k & 1) == 0 && k / 2 < XST) {
+                    constexpr int kk = k / 2;
+                    const int gi = sg_goff[kk] + c3 * XCK;
+                    xr[kk] = *reinterpret_cast<const f32x4*>(a.in + gi);
+                    if constexpr (pro == PRO_AFF_RES) rr[kk] = *reinterpret_cast<const f32x4*>(res_src + gi);
+                }
+                __builtin_amdgcn_sched_barrier(0);
             });
-            __builtin_amdgcn_sched_barrier(0);
         });
         XPT(c, 16);
         __syncthreads();
@@ -339,7 +452,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     // ---- epilogue: output transform, bias + ReLU, store, tile statistics -----------------------
     const int co = wave * 32 + li;
-    const float bias = a.bias[co];
+    const float bias = bias_co;
     float yv[64];
     float s = 0.f, cnt = 0.f;
 #pragma unroll
@@ -505,8 +618,8 @@ hipError_t wino_x6_prepare() {
 
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
     if (a.cin % XCK != 0 || a.cin > XMAX_CIN || a.tiles_y != (a.H + XTH - 1) / XTH ||
-        a.tiles_x != (a.W + XTW - 1) / XTW)
-        return hipErrorInvalidValue;
+        a.tiles_x != (a.W + XTW - 1) / XTW || (size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7F000000)
+        return hipErrorInvalidValue;   // 32-bit staging offsets; the out-of-range store offset must stay out of range
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
     switch (a.pro_mode) {
         case PRO_NONE: hipLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;

@@ -231,7 +231,7 @@ def test_split_bf16_precision_modes(precision, tol):
     assert err < tol, err   # bf16x3: the float64 simulation of the split gives ~2e-5 here; fp32 gives ~2e-6
 
 
-WINO_MODES = {"fp32_winograd": 200, "winograd_bf16x6": 202}
+WINO_MODES = {"fp32_winograd": (201, 200), "winograd_bf16x6": (203, 202)}   # (start conv, residual) kernel ids
 
 
 @pytest.mark.parametrize("precision", list(WINO_MODES))
@@ -253,7 +253,7 @@ def test_winograd_residual_convs_match_oracle(precision):
         ref = R.transfer_forward(x, sp, w, ins, outs, br, bf)
         m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision=precision)
         ids = [m.layer_kernel_id(i) for i in range(m.num_layers())]
-        assert ids[0] == 201 and ids[3:13] == [WINO_MODES[precision]] * 10, ids   # 9x9 / residual Winograd
+        assert ids[0] == WINO_MODES[precision][0] and ids[3:13] == [WINO_MODES[precision][1]] * 10, ids
         inp = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}
         y = m(inp)
         err = float(np.abs(y.cpu().numpy() - ref).max())
