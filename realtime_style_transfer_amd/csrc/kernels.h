@@ -9,6 +9,16 @@ namespace rst {
 enum ProMode { PRO_NONE = 0, PRO_AFF_RELU = 1, PRO_AFF = 2, PRO_AFF_RES = 3, PRO_MASK = 4 };
 enum EpiMode { EPI_NONE = 0, EPI_RELU_BN = 1, EPI_RELU_STATS = 2, EPI_STATS = 3 };
 
+// Workgroup barrier that orders LDS only: __syncthreads() is a workgroup-scope fence on all memory, which
+// on gfx950 waits for every outstanding global load and store of the wave (s_waitcnt vmcnt(0)) — the
+// prefetched operands still in flight and the epilogue's stores. Kernels whose global traffic is not
+// exchanged through the barrier use this one (s_waitcnt lgkmcnt(0); s_barrier).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Two-style blending (num_styles == 2, styleTransfer.py:36-44 with the weights completed as
 // [1 - w1, w1] at :297-302): w0*v0 + w1*v1 = v0 + w1*(v1 - v0). The one formula every blend site
 // uses (conv prologues, the standalone affine kernel, rst_style_param_map).
@@ -116,6 +126,8 @@ hipError_t wino9_launch(const Wino9Args& a, hipStream_t st);
 // U = wino9_x6_pack_weights (bf16 pieces [10][16][3][32][16]).
 std::vector<float> wino9_x6_pack_weights(const float* kern, int cin);
 hipError_t wino9_x6_prepare();
+int wino9_x6_tiles_y(int H);   // 16 x 16-pixel workgroup blocks
+int wino9_x6_tiles_x(int W);
 hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st);
 int wino_tiles_y(int H);
 int wino_tiles_x(int W);

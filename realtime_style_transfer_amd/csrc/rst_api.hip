@@ -209,8 +209,8 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.pad_t = e.pad_l = 4;
         e.gHo = s.Ho;
         e.gWo = s.Wo;
-        e.tiles_y = wino9_tiles_y(s.Ho);
-        e.tiles_x = wino9_tiles_x(s.Wo);
+        e.tiles_y = x6 ? wino9_x6_tiles_y(s.Ho) : wino9_tiles_y(s.Ho);
+        e.tiles_x = x6 ? wino9_x6_tiles_x(s.Wo) : wino9_tiles_x(s.Wo);
         e.n_part = 0;
     } else if ((precision == RST_PRECISION_FP32_WINOGRAD && wino_supported(s.k, s.stride, s.cin, s.cout) ||
                 precision == RST_PRECISION_WINOGRAD_BF16X6 && wino_x6_supported(s.k, s.stride, s.cin, s.cout)) &&

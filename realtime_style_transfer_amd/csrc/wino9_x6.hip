@@ -6,18 +6,18 @@
 // U_ab = G g_ab G^T) split exactly into three bf16 pieces, six product terms, fp32 accumulation
 // (dropped terms <= 2^-25 of each product; the scheme of wino_x6.hip).
 //
-// Workgroup = 4 waves, output block 8 x 16 pixels = 32 Winograd tiles x 32 output channels; wave w owns
-// the transform points 4w..4w+3 (= row p = w of the 4x4 point grid; 64 accumulator registers), two
-// workgroups per CU (75 KB of LDS each), so one workgroup's VALU-heavy transform + split phase runs
-// beside the other's MFMA phase and two waves share each SIMD's VALU issue.
-// K per sub-kernel: channels 0..15 are one K-step of the 32x32x16 MFMA (6 terms); channel 16 of all
-// nine sub-kernels is gathered into one more K-step (K index = ab, 9 of 16 used) at the end, its V values
-// kept in registers by the lanes that feed them to the MFMA. Per sub-kernel:
-//   transform (thread = tile x channel pair: 16 ds_read_b64, 64 adds, split, 48 ds_write_b32) -> barrier
-//   -> 24 MFMAs per wave (A: V pieces from LDS, B: U pieces from L2, prefetched one sub-kernel ahead)
-//   -> barrier.
-// Epilogue (as wino9.hip): M -> LDS, output transform per (tile, channel), bias -> ReLU -> BN (folded)
-// -> ReLU, or in training the raw ReLU output and per-tile {sum, M2, n}.
+// Workgroup = 8 waves (two per SIMD), output block 16 x 16 pixels = 8 x 8 = 64 Winograd tiles (two
+// 32-row MFMA M blocks) x 32 output channels. Wave w owns transform-point row p = w & 3 and the two
+// points q = 2(w >> 2), +1 of it (ξ = 4p + q), for both M blocks: four accumulators (64 registers).
+// The V operands never touch LDS: lane (li, lh) of a wave computes exactly the A-operand values it feeds
+// its MFMAs — row p of B^T d for tile 32h + li and channels 8lh..8lh+7 (two 32-B patch reads per point
+// of the 4x4 input tile, ds_read_b128), the two points' V, the exact 3-piece split, packed straight into
+// the short8 operands. K per sub-kernel: channels 0..15 = one K-step of the 32x32x16 MFMA (6 terms);
+// channel 16 of all nine sub-kernels is gathered into one more K-step at the end (K index = ab), its V
+// kept in registers by the lanes that feed it. The loop over the nine sub-kernels has no barrier.
+// Each U element (B operand, L2) is loaded by one wave and serves 64 tiles.
+// Epilogue, per M block: M -> LDS [xi][tile][co], output transform per (tile, channel), bias -> ReLU ->
+// BN (folded moving statistics) -> ReLU. Inference only (training keeps wino9.hip's f32 kernel).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstring>
@@ -31,24 +31,39 @@ namespace rst {
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short short8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int TH = 8, TW = 16;                 // output pixels per workgroup
-constexpr int PH = TH + 8, PW = TW + 8;        // input patch (pad 4 each side)
-constexpr int NPX = PH * PW;                   // 384 patch pixels
-constexpr int PS = 18;                         // patch pixel stride (floats): 17 channels + 1
+constexpr int TH = 16, TW = 16;                // output pixels per workgroup
+constexpr int PH = TH + 8, PW = TW + 8;        // input patch (pad 4 each side): 24 x 24
+constexpr int NPX = PH * PW;                   // 576 patch pixels
+constexpr int PS = 20;                         // patch pixel stride (floats): 17 channels + 3 (80 B, 16-B aligned)
+// A patch row holds the even pixels, then the odd ones (tiles step 2 pixels in x, so a wave's tiles read
+// consecutive pixels of one parity plane), padded to 496 floats: with that pitch the 16 lanes of every
+// ds_read_b128 lane group hit 16 distinct 4-bank groups (searched exhaustively; stride 2 x 80 B could use
+// only 8 of them)
+constexpr int PLANE = (PW / 2) * PS;           // 240 floats: one parity plane of a row
+constexpr int RP = 2 * PLANE + 16;             // 496 floats: row pitch
 constexpr int NT = 32;                         // output channels
 constexpr int NXI = 16;                        // transform points
-constexpr int VROW = 32;                       // bytes per (piece, xi, tile) row: 16 bf16
-constexpr int V_BYTES = 3 * NXI * 32 * VROW;   // 48 KB
-constexpr int PATCH_BYTES = NPX * PS * 4;      // 27 KB
+constexpr int VROW = 32;                       // bytes per (co, 16 channels) U row: 16 bf16
+constexpr int PATCH_FL = PH * RP;              // 11904 floats
 constexpr int MS = 33;                         // M exchange row stride (floats)
-constexpr int LDS_BYTES = PATCH_BYTES + V_BYTES;
-static_assert(NXI * 32 * MS * 4 <= LDS_BYTES, "M exchange fits in the patch + V space");
+constexpr int MEX_FL = NXI * 32 * MS;          // one M block: [16][32 tiles][33]
+constexpr int V16S = 12;                       // channel-16 V row: ab 0..8 + 3 pad (48 B)
+constexpr int V16_FL = NXI * 64 * V16S;        // [xi][tile][12] f32
+// LDS: [patch 0][v16][patch 1]. A tile computes from patch (t & 1) while the next tile's patch is staged
+// into the other one; the epilogue's M exchange uses the current patch + v16 (contiguous either way).
+constexpr int LDS_FL = 2 * PATCH_FL + V16_FL;
+constexpr int LDS_BYTES = LDS_FL * 4;          // 140 KB
+static_assert(MEX_FL <= PATCH_FL + V16_FL, "M exchange fits in one patch + v16");
 constexpr int UBLK = NT * VROW;                // bytes per (ab, xi, piece) U block: 32 co x 16 bf16
+constexpr int NTHR = 512;
+
+__host__ __device__ constexpr int pix_off(int r, int x) { return r * RP + (x & 1) * PLANE + (x >> 1) * PS; }
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -66,289 +81,353 @@ __device__ __forceinline__ unsigned piece(float& x, float& y) {
     return p;
 }
 
+// eight fp32 values -> the three short8 bf16 pieces (v = p0 + p1 + p2 exactly)
+__device__ __forceinline__ void split8(const float (&v)[8], short8 (&A)[3]) {
+    unsigned pk[3][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float x = v[2 * j], y = v[2 * j + 1];
+        pk[0][j] = piece(x, y);
+        pk[1][j] = piece(x, y);
+        pk[2][j] = piece(x, y);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) A[p] = __builtin_bit_cast(short8, (u32x4){pk[p][0], pk[p][1], pk[p][2], pk[p][3]});
+}
+
 }  // namespace
 
 // Experiment knobs (tools/wino9_x6_bench only; never set in the library build): W9_SKIP bit0 = no U loads
-// in the loop, bit1 = no transform / split, bit2 = no MFMAs
+// in the loop, bit1 = no transform (patch reads), bit2 = no MFMAs, bit3 = no split
 #ifndef W9_SKIP
 #define W9_SKIP 0
 #endif
+#ifdef W9_PROF
+// timeline per (workgroup, wave) on the constant 100 MHz clock: start, staged, loop done, end
+__device__ unsigned long long w9_tl[W9_PROF][8][9][4];   // [workgroup][wave][tile iteration][stamp]
+#define W9TL(k) \
+    if (blockIdx.x < W9_PROF && lane == 0 && w9_it < 9) w9_tl[blockIdx.x][wave][w9_it][(k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define W9TL(k)
+#endif
 
 template <int CINT>
-__global__ __launch_bounds__(256, 2) void wino9_x6_kernel(Wino9Args a) {
+__global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_tiles) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    __shared__ float red[2][4][NT];   // training statistics: per-wave partial sums
-    float* const patch = smem;                                                           // [384][18] f32
-    unsigned char* const vbytes = reinterpret_cast<unsigned char*>(smem) + PATCH_BYTES;  // [3][16][32][32 B]
-    float* const ms = smem;                                                              // [16][32][33] after
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar U offsets, no waterfall)
     const int li = lane & 31, lh = lane >> 5;
-    int bid = xcd_tile_order(blockIdx.x, gridDim.x);   // XCD-contiguous tile runs (halo reuse in L2)
-    const int tx = bid % a.tiles_x;
-    bid /= a.tiles_x;
-    const int ty = bid % a.tiles_y;
-    const int b = bid / a.tiles_y;
-    const int y0 = ty * TH, x0 = tx * TW;
+    const int p = wave & 3, qh = wave >> 2;   // point row p, points q = 2qh, 2qh + 1
+    int w9_it = 0;
+    (void)w9_it;
     const int H = a.H, W = a.W, Cin = CINT > 0 ? CINT : a.cin;
-    const size_t img = (size_t)b * H * W;
+    constexpr int ROW = PW * (CINT > 0 ? CINT : 17), TOTAL = PH * ROW, NIT = (TOTAL + NTHR - 1) / NTHR;
+    static_assert(CINT == 17 || CINT == 0, "");
 
-    // ---- U pieces: lane (li, lh) of wave w reads U[ab][4w + q][piece][co = li][8lh .. 8lh+7] ------
+    // ---- U pieces: lane (li, lh) reads U[ab][4p + q][piece][co = li][8lh .. 8lh+7] ------------------
     const __amdgpu_buffer_rsrc_t usrd =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, (9 + 1) * NXI * 3 * UBLK, 0x00020000);
     const int uvoff = li * VROW + 16 * lh;
-    short8 ub[2][4][3];
+    short8 ub[2][2][3];   // [buffer][q of the pair][piece]
     auto load_u = [&](auto BUF, int ab) __attribute__((always_inline)) {   // ab == 9: the channel-16 K-step
         constexpr int buf = decltype(BUF)::value;
-        sfor<0, 4>([&](auto Q) __attribute__((always_inline)) {
-            constexpr int q = decltype(Q)::value;
-            sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
-                constexpr int p = decltype(Pc)::value;
-                ub[buf][q][p] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                               usrd, uvoff, ((ab * NXI + 4 * wave + q) * 3 + p) * UBLK, 0));
+        if constexpr (!(W9_SKIP & 1)) {
+            sfor<0, 2>([&](auto Q) __attribute__((always_inline)) {
+                constexpr int q = decltype(Q)::value;
+                sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+                    constexpr int pc = decltype(Pc)::value;
+                    ub[buf][q][pc] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
+                        usrd, uvoff, ((ab * NXI + 4 * p + 2 * qh + q) * 3 + pc) * UBLK, 0));
+                });
             });
-        });
+        }
     };
+    if constexpr (W9_SKIP & 1) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) ub[0][q][pc] = ub[1][q][pc] = short8{};
+    }
     load_u(std::integral_constant<int, 0>{}, 0);
 
-    // ---- input patch (rows y0-4 .. y0+11, cols x0-4 .. x0+19) -> LDS [pixel][ch], zeros outside ----
-    if constexpr (CINT > 0) {
-        // all loads in flight before the first LDS write; clamped addresses, zeroed after the load
-        constexpr int ROW = PW * CINT, TOTAL = PH * ROW, NIT = (TOTAL + 255) / 256;
-        float v[NIT];
-        sfor<0, NIT>([&](auto K) __attribute__((always_inline)) {
+    // ---- persistent tile loop: workgroup g takes tiles g, g + G, ... The next tile's patch is staged into
+    // the other patch buffer in two halves during the current tile's sub-kernel loop (loads issued a few
+    // sub-kernels before their LDS stores, so their latency hides behind the MFMAs). ----
+    auto tile_coords = [&](int t, int& y0, int& x0, size_t& img) __attribute__((always_inline)) {
+        const int tx = t % a.tiles_x;
+        t /= a.tiles_x;
+        const int ty = t % a.tiles_y;
+        img = (size_t)(t / a.tiles_y) * H * W;
+        y0 = ty * TH;
+        x0 = tx * TW;
+    };
+    constexpr int NH = (NIT + 1) / 2;   // patch elements per thread per half
+    float pf[NH];
+    // (the staging index math is recomputed at every use from an opaque copy of tid: hoisted out of the
+    // tile loop it would pin ~3 registers per staged element)
+    auto load_half = [&](int t, auto HALF) __attribute__((always_inline)) {   // clamped addresses
+        constexpr int hf = decltype(HALF)::value;
+        int y0, x0;
+        size_t img;
+        tile_coords(t, y0, x0, img);
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        sfor<0, NH>([&](auto K) __attribute__((always_inline)) {
             constexpr int k = decltype(K)::value;
-            const int i = min(tid + k * 256, TOTAL - 1);
-            const int r = i / ROW, rem = i - r * ROW;
-            const int px = rem / CINT, c = rem - px * CINT;
+            const int i = min(tid + (hf * NH + k) * NTHR, PH * PW * Cin - 1);
+            const int r = i / (PW * Cin), rem = i - r * (PW * Cin);
+            const int px = rem / Cin, c = rem - px * Cin;
             const int gy = min(max(y0 - 4 + r, 0), H - 1), gx = min(max(x0 - 4 + px, 0), W - 1);
-            v[k] = a.in[(img + (size_t)gy * W + gx) * CINT + c];
+            pf[k] = a.in[(img + (size_t)gy * W + gx) * Cin + c];
         });
-        sfor<0, NIT>([&](auto K) __attribute__((always_inline)) {
+    };
+    auto store_half = [&](int t, float* pbuf, auto HALF) __attribute__((always_inline)) {   // zero outside
+        constexpr int hf = decltype(HALF)::value;
+        int y0, x0;
+        size_t img;
+        tile_coords(t, y0, x0, img);
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int total = PH * PW * Cin;
+        sfor<0, NH>([&](auto K) __attribute__((always_inline)) {
             constexpr int k = decltype(K)::value;
-            const int i = tid + k * 256;
-            if (TOTAL % 256 == 0 || (k + 1) * 256 <= TOTAL || i < TOTAL) {
-                const int r = i / ROW, rem = i - r * ROW;
-                const int px = rem / CINT, c = rem - px * CINT;
+            const int i = tid + (hf * NH + k) * NTHR;
+            if (hf * NH + k < NIT && ((hf * NH + k + 1) * NTHR <= TOTAL || i < total)) {
+                const int r = i / (PW * Cin), rem = i - r * (PW * Cin);
+                const int px = rem / Cin, c = rem - px * Cin;
                 const int gy = y0 - 4 + r, gx = x0 - 4 + px;
                 const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
-                patch[(r * PW + px) * PS + c] = inside ? v[k] : 0.f;
+                pbuf[pix_off(r, px) + c] = inside ? pf[k] : 0.f;
             }
         });
-    } else {
-        const int row_fl = PW * Cin, total = PH * row_fl;
-        for (int i = tid; i < total; i += 256) {
-            const int r = i / row_fl, rem = i - r * row_fl;
-            const int px = rem / Cin, c = rem - px * Cin;
-            const int gy = y0 - 4 + r, gx = x0 - 4 + px;
-            float v = 0.f;
-            if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = a.in[(img + (size_t)gy * W + gx) * Cin + c];
-            patch[(r * PW + px) * PS + c] = v;
-        }
-    }
-    for (int i = tid; i < NPX * (PS - Cin); i += 256) {   // channels cin..17 of every pixel: zero
-        const int px = i / (PS - Cin), c = Cin + i % (PS - Cin);
-        patch[px * PS + c] = 0.f;
-    }
-
-    floatx16 acc[4];
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
-
-    // transform role: tile tt (0..31), channel pair cp (channels 2cp, 2cp+1 of 0..15)
-    const int tt = tid >> 3, cp = tid & 7;
-    const int twy = tt >> 3, twx = tt & 7;
-    const int vwoff = tt * VROW + 16 * ((cp >> 2) ^ ((tt >> 3) & 1)) + 4 * (cp & 3);
-    auto vwrite = [&](int xi, unsigned p0, unsigned p1, unsigned p2) __attribute__((always_inline)) {
-        *reinterpret_cast<unsigned*>(vbytes + ((0 * NXI + xi) * 32) * VROW + vwoff) = p0;
-        *reinterpret_cast<unsigned*>(vbytes + ((1 * NXI + xi) * 32) * VROW + vwoff) = p1;
-        *reinterpret_cast<unsigned*>(vbytes + ((2 * NXI + xi) * 32) * VROW + vwoff) = p2;
-    };
-    auto transform = [&](int sa, int sb) __attribute__((always_inline)) {
-        const float* src = patch + ((2 * twy + 3 * sa) * PW + 2 * twx + 3 * sb) * PS + 2 * cp;
-        float dx[4][4], dy[4][4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const f32x2 v = *reinterpret_cast<const f32x2*>(src + (r * PW + c) * PS);
-                dx[r][c] = v.x;
-                dy[r][c] = v.y;
+        if constexpr (hf == 1)   // channels cin..19 (the previous M exchange overwrote them)
+            for (int i = tid; i < NPX * (PS - Cin); i += NTHR) {
+                const int px = i / (PS - Cin);
+                pbuf[pix_off(px / PW, px % PW) + Cin + i % (PS - Cin)] = 0.f;
             }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {   // B^T d
-            const float a0 = dx[0][c], a1 = dx[1][c], a2 = dx[2][c], a3 = dx[3][c];
-            dx[0][c] = a0 - a2; dx[1][c] = a1 + a2; dx[2][c] = a2 - a1; dx[3][c] = a1 - a3;
-            const float b0 = dy[0][c], b1 = dy[1][c], b2 = dy[2][c], b3 = dy[3][c];
-            dy[0][c] = b0 - b2; dy[1][c] = b1 + b2; dy[2][c] = b2 - b1; dy[3][c] = b1 - b3;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {   // (B^T d) B, split, write
-            float vx[4] = {dx[r][0] - dx[r][2], dx[r][1] + dx[r][2], dx[r][2] - dx[r][1], dx[r][1] - dx[r][3]};
-            float vy[4] = {dy[r][0] - dy[r][2], dy[r][1] + dy[r][2], dy[r][2] - dy[r][1], dy[r][1] - dy[r][3]};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const unsigned p0 = piece(vx[q], vy[q]);
-                const unsigned p1 = piece(vx[q], vy[q]);
-                const unsigned p2 = piece(vx[q], vy[q]);
-                vwrite(r * 4 + q, p0, p1, p2);
-            }
+    };
+    auto patch_buf = [&](int parity) __attribute__((always_inline)) { return smem + parity * (PATCH_FL + V16_FL); };
+    float* const v16s = smem + PATCH_FL;   // [16][64][12]: channel-16 V of every sub-kernel (K index ab)
+
+    // B^T d row p = Y + s X from the d rows (rY, rX), s = +-1 (one exact fma per element):
+    // p0: d0 - d2, p1: d1 + d2, p2: d2 - d1, p3: d1 - d3
+    const int rX = p == 0 ? 2 : (p == 1 ? 2 : (p == 2 ? 1 : 3));
+    const int rY = p == 0 ? 0 : (p == 2 ? 2 : 1);
+    const float sx = p == 1 ? 1.f : -1.f;
+    auto mfma6 = [&](floatx16& C, const short8 (&A)[3], const short8 (&B)[3]) __attribute__((always_inline)) {
+        if constexpr (!(W9_SKIP & 4)) {
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], C, 0, 0, 0);   // a0 b0
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], C, 0, 0, 0);   // a0 b1
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], C, 0, 0, 0);   // a1 b0
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], C, 0, 0, 0);   // a0 b2
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], C, 0, 0, 0);   // a1 b1
+            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], C, 0, 0, 0);   // a2 b0
+        } else {
+            C[0] += __builtin_bit_cast(float, (int)A[0][0] + (int)A[1][1] + (int)A[2][2] + (int)B[0][0] +
+                                                  (int)B[1][1] + (int)B[2][2]);
         }
     };
-    // channel 16: lane (li, lh) of wave w keeps V_ab[p = w][q][tile li][ch 16] for the K index ab = 8lh + j
-    float v16[4][8];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v16[q][j] = 0.f;
-    const int lwy = li >> 3, lwx = li & 7;
-    auto transform16 = [&](int ab, int sa, int sb) __attribute__((always_inline)) {
-        const float* src = patch + ((2 * lwy + 3 * sa) * PW + 2 * lwx + 3 * sb) * PS + 16;
-        float t[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {   // row p = wave of B^T d (wave-uniform branch)
-            const float d0 = src[(0 * PW + c) * PS], d1 = src[(1 * PW + c) * PS];
-            const float d2 = src[(2 * PW + c) * PS], d3 = src[(3 * PW + c) * PS];
-            t[c] = wave == 0 ? d0 - d2 : (wave == 1 ? d1 + d2 : (wave == 2 ? d2 - d1 : d1 - d3));
-        }
-        const float v[4] = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
-        const bool mine = (ab >> 3) == lh;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v16[q][ab & 7] = mine ? v[q] : v16[q][ab & 7];
-    };
-
-    // A operands of point 4w + q: the three pieces of this lane's tile row, 16-B half lh (swizzled)
-    const int varow = li * VROW + 16 * (lh ^ ((li >> 3) & 1));
-    auto mfma6 = [&](int q, const short8* A, const short8* B) __attribute__((always_inline)) {
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], acc[q], 0, 0, 0);   // a0 b0
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], acc[q], 0, 0, 0);   // a0 b1
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], acc[q], 0, 0, 0);   // a1 b0
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], acc[q], 0, 0, 0);   // a0 b2
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], acc[q], 0, 0, 0);   // a1 b1
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], acc[q], 0, 0, 0);   // a2 b0
-    };
-
-    __syncthreads();   // patch + zero pads visible
-    // sub-kernel loop fully unrolled: the U double buffer is indexed at compile time (registers)
-    sfor<0, 9>([&](auto AB) __attribute__((always_inline)) {
-        constexpr int ab = decltype(AB)::value, cur = ab & 1, sa = ab / 3, sb = ab % 3;
-        if constexpr (!(W9_SKIP & 2)) {
-            transform(sa, sb);
-            transform16(ab, sa, sb);
-        }
-        __syncthreads();   // V(ab) complete
-        if constexpr (!(W9_SKIP & 1)) load_u(std::integral_constant<int, cur ^ 1>{}, ab + 1);   // ab + 1 == 9: channel 16
-        sfor<0, 4>([&](auto Q) __attribute__((always_inline)) {
-            constexpr int q = decltype(Q)::value;
-            short8 A[3];
-            sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
-                constexpr int p = decltype(Pc)::value;
-                A[p] = *reinterpret_cast<const short8*>(vbytes + ((p * NXI + 4 * wave + q) * 32) * VROW + varow);
-            });
-            if constexpr (!(W9_SKIP & 4)) mfma6(q, A, ub[cur][q]);
-            else acc[q][0] += __builtin_bit_cast(float, (int)A[0][0] + (int)ub[cur][q][0][0]);
-        });
-        __syncthreads();   // V free for the next sub-kernel's transform
-    });
-    // channel-16 K-step: lane (li, lh) supplies K = 8lh .. 8lh+7 (ab; 9..15 are zero)
-    sfor<0, 4>([&](auto Q) __attribute__((always_inline)) {
-        constexpr int q = decltype(Q)::value;
-        unsigned pk[3][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float x = v16[q][2 * j], y = v16[q][2 * j + 1];
-            pk[0][j] = piece(x, y);
-            pk[1][j] = piece(x, y);
-            pk[2][j] = piece(x, y);
-        }
-        short8 A[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) A[p] = __builtin_bit_cast(short8, (u32x4){pk[p][0], pk[p][1], pk[p][2], pk[p][3]});
-        mfma6(q, A, ub[1][q]);   // 9 sub-kernels: the last load_u (ab + 1 == 9) went to buffer 9 & 1 = 1
-    });
-    __syncthreads();   // V / patch reads done before M overwrites them
-
-    // ---- M -> LDS [xi][tile][co]: accumulator j of lane (li, lh) is tile (j&3) + 8(j>>2) + 4lh, channel li
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;
-            ms[((wave * 4 + x) * 32 + row) * MS + li] = acc[x][j];
-        }
-    __syncthreads();
-
-    // ---- output transform + epilogue: thread = (channel co, tiles 4g..4g+3) ----------------------
-    const int co = tid & 31, g = tid >> 5;
+    const int co = tid & 31, g = tid >> 5;   // epilogue thread: output channel co, tiles 2g, 2g + 1 of a block
     const float bias = a.bias[co];
-    const bool train = a.part != nullptr;
-    const float2 bn = train ? make_float2(1.f, 0.f) : a.bn_ab[co];
-    float yv[16];
-    float s = 0.f, cnt = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int tile = g * 4 + k;
-        const int wy = tile >> 3, wx = tile & 7;
-        float m[16];
-#pragma unroll
-        for (int x = 0; x < NXI; ++x) m[x] = ms[(x * 32 + tile) * MS + co];
-        // T = A^T M (2 x 4), Y = T A (2 x 2); A^T = [[1,1,1,0],[0,1,-1,-1]]
-        float t0[4], t1[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            t0[c] = m[0 * 4 + c] + m[1 * 4 + c] + m[2 * 4 + c];
-            t1[c] = m[1 * 4 + c] - m[2 * 4 + c] - m[3 * 4 + c];
-        }
-        const float yy[4] = {t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3], t1[0] + t1[1] + t1[2],
-                             t1[1] - t1[2] - t1[3]};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
-            const bool ok = oy < H && ox < W;
-            const float v = fmaxf(yy[q] + bias, 0.f);                 // Conv2D(..., activation='relu')
-            yv[k * 4 + q] = ok ? v : 0.f;
-            if (ok) {
-                // inference: BN (folded moving statistics) -> ReLU; training: the raw ReLU output
-                a.out[(img + (size_t)oy * W + ox) * NT + co] = train ? v : fmaxf(fmaf(bn.x, v, bn.y), 0.f);
-                s += v;
-                cnt += 1.f;
-            }
-        }
+    const float2 bn = a.bn_ab[co];
+
+    int t = blockIdx.x;
+    if (t < n_tiles) {
+        load_half(t, std::integral_constant<int, 0>{});
+        store_half(t, patch_buf(0), std::integral_constant<int, 0>{});
+        load_half(t, std::integral_constant<int, 1>{});
+        store_half(t, patch_buf(0), std::integral_constant<int, 1>{});
     }
-    if (train) {   // per-tile {sum, M2, n} of channel co over the 128 pixels (two-pass, fixed order)
-        s += __shfl_xor(s, 32);
-        cnt += __shfl_xor(cnt, 32);
-        if (lane < 32) {
-            red[0][wave][co] = s;
-            red[1][wave][co] = cnt;
-        }
-        __syncthreads();
-        const float S = (red[0][0][co] + red[0][1][co]) + (red[0][2][co] + red[0][3][co]);
-        const float N = (red[1][0][co] + red[1][1][co]) + (red[1][2][co] + red[1][3][co]);
-        const float mean = N > 0.f ? S / N : 0.f;
-        float m2 = 0.f;
+    for (int it = 0; t < n_tiles; t += gridDim.x, ++it) {
+        w9_it = it;
+        W9TL(0);
+        const int tn = t + gridDim.x;
+        int y0, x0;
+        size_t img;
+        tile_coords(t, y0, x0, img);
+        float* const patch = patch_buf(it & 1);
+        float* const pnext = patch_buf((it & 1) ^ 1);
+        // patch element at the top-left of the epilogue's M exchange: the current patch + v16
+        float* const ms = (it & 1) ? smem + PATCH_FL : smem;   // [16][32][33], one M block at a time
+        // per-lane row pointers (tile li of block 0, rows rX / rY of the 4x4 input tile, channels 8lh..);
+        // every read below adds a compile-time offset (sub-kernel shift, block, column) to one of them
+        const float* const bx = patch + pix_off(2 * (li >> 3) + rX, 2 * (li & 7)) + 8 * lh;
+        const float* const by = patch + pix_off(2 * (li >> 3) + rY, 2 * (li & 7)) + 8 * lh;
+        const float* const bx16 = patch + pix_off(2 * (li >> 3) + rX, 2 * (li & 7)) + 16;
+        const float* const by16 = patch + pix_off(2 * (li >> 3) + rY, 2 * (li & 7)) + 16;
+        for (int i = tid; i < NXI * 64 * (V16S - 9); i += NTHR)   // channel-16 rows: ab 9..11 are zero
+            v16s[(i / (V16S - 9)) * V16S + 9 + i % (V16S - 9)] = 0.f;
+        floatx16 acc[2][2];   // [q of the pair][M block]
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int q = 0; q < 2; ++q)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int tile = g * 4 + k;
-                const int oy = y0 + 2 * (tile >> 3) + (q >> 1), ox = x0 + 2 * (tile & 7) + (q & 1);
-                const float d = yv[k * 4 + q] - mean;
-                if (oy < H && ox < W) m2 = fmaf(d, d, m2);
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[q][h][r] = 0.f;
+        lds_barrier();   // patch + pads visible
+        W9TL(1);
+        // The q pair is a compile-time parameter (one code path per wave-uniform value): pair 0 uses the
+        // columns 0..2 of B^T d (V0 = T0 - T2, V1 = T1 + T2), pair 1 the columns 1..3 (V2 = T2 - T1,
+        // V3 = T1 - T3).
+        auto main_loop = [&](auto QH) __attribute__((always_inline)) {
+            constexpr int QHC = decltype(QH)::value;
+            // sub-kernel loop fully unrolled (the U double buffer is indexed at compile time); no barriers
+            sfor<0, 9>([&](auto AB) __attribute__((always_inline)) {
+                constexpr int ab = decltype(AB)::value, cur = ab & 1, sa = ab / 3, sb = ab % 3;
+                load_u(std::integral_constant<int, cur ^ 1>{}, ab + 1);   // ab + 1 == 9: the channel-16 step's U
+                // the next tile's patch: loads at sub-kernels 1 and 4, LDS stores at 3 and 6
+                if constexpr (ab == 1 || ab == 4) {
+                    if (tn < n_tiles) load_half(tn, std::integral_constant<int, ab == 4>{});
+                }
+                if constexpr (ab == 3 || ab == 6) {
+                    if (tn < n_tiles) store_half(tn, pnext, std::integral_constant<int, ab == 6>{});
+                }
+                sfor<0, 2>([&](auto Hh) __attribute__((always_inline)) {
+                    constexpr int h = decltype(Hh)::value;
+                    const int tile = 32 * h + li;
+                    float tv[3][8], t16[3];
+                    if constexpr (!(W9_SKIP & 2)) {
+#pragma unroll
+                        for (int cc = 0; cc < 3; ++cc) {
+                            // pixel (8h + 3sa, 3sb + QHC + cc) relative to the lane's tile origin (even x)
+                            const int off = (8 * h + 3 * sa) * RP + ((3 * sb + QHC + cc) & 1) * PLANE +
+                                            ((3 * sb + QHC + cc) >> 1) * PS;
+                            const f32x4 x0v = *reinterpret_cast<const f32x4*>(bx + off);
+                            const f32x4 x1v = *reinterpret_cast<const f32x4*>(bx + off + 4);
+                            const f32x4 y0v = *reinterpret_cast<const f32x4*>(by + off);
+                            const f32x4 y1v = *reinterpret_cast<const f32x4*>(by + off + 4);
+                            const float xv[8] = {x0v.x, x0v.y, x0v.z, x0v.w, x1v.x, x1v.y, x1v.z, x1v.w};
+                            const float yv[8] = {y0v.x, y0v.y, y0v.z, y0v.w, y1v.x, y1v.y, y1v.z, y1v.w};
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) tv[cc][k] = fmaf(sx, xv[k], yv[k]);
+                            t16[cc] = fmaf(sx, bx16[off], by16[off]);   // channel 16 (the K-step gathered over ab)
+                        }
+                    } else {
+#pragma unroll
+                        for (int cc = 0; cc < 3; ++cc) {
+                            t16[cc] = bx[16 + cc];
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) tv[cc][k] = bx[k];
+                        }
+                    }
+                    float v0[8], v1[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        v0[k] = QHC == 0 ? tv[0][k] - tv[2][k] : tv[1][k] - tv[0][k];
+                        v1[k] = QHC == 0 ? tv[1][k] + tv[2][k] : tv[0][k] - tv[2][k];
+                    }
+                    // channel 16 -> LDS (lane half lh stores the point q = lh of the pair)
+                    {
+                        const float w0 = QHC == 0 ? t16[0] - t16[2] : t16[1] - t16[0];
+                        const float w1 = QHC == 0 ? t16[1] + t16[2] : t16[0] - t16[2];
+                        v16s[((4 * p + 2 * QHC + lh) * 64 + tile) * V16S + ab] = lh ? w1 : w0;
+                    }
+                    short8 A0[3], A1[3];
+                    if constexpr (!(W9_SKIP & 8)) {
+                        split8(v0, A0);
+                        split8(v1, A1);
+                    } else {
+#pragma unroll
+                        for (int pc = 0; pc < 3; ++pc) {
+                            A0[pc] = __builtin_bit_cast(short8, (f32x4){v0[pc], v0[pc + 1], v0[pc + 2], v0[pc + 3]});
+                            A1[pc] = __builtin_bit_cast(short8, (f32x4){v1[pc], v1[pc + 1], v1[pc + 2], v1[pc + 3]});
+                        }
+                    }
+                    mfma6(acc[0][h], A0, ub[cur][0]);
+                    mfma6(acc[1][h], A1, ub[cur][1]);
+                });
+            });
+        };
+        if (__builtin_amdgcn_readfirstlane(qh) == 0) main_loop(std::integral_constant<int, 0>{});
+        else main_loop(std::integral_constant<int, 1>{});
+        // channel-16 K-step: lane (li, lh) supplies K = 8lh .. 8lh+7 (ab; 9..15 are zero)
+        lds_barrier();   // every wave's channel-16 V in LDS
+        sfor<0, 2>([&](auto Hh) __attribute__((always_inline)) {
+            constexpr int h = decltype(Hh)::value;
+            float w[2][8];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float* r = v16s + ((4 * p + 2 * qh + q) * 64 + 32 * h + li) * V16S + 8 * lh;
+                const f32x4 r0 = *reinterpret_cast<const f32x4*>(r);
+                const f32x4 r1 = lh ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(r + 4);
+                w[q][0] = r0.x; w[q][1] = r0.y; w[q][2] = r0.z; w[q][3] = r0.w;
+                w[q][4] = r1.x; w[q][5] = r1.y; w[q][6] = r1.z; w[q][7] = r1.w;
             }
-        m2 += __shfl_xor(m2, 32);
-        __syncthreads();
-        if (lane < 32) red[0][wave][co] = m2;
-        __syncthreads();
-        if (tid < 32) {
-            const float M2 = (red[0][0][co] + red[0][1][co]) + (red[0][2][co] + red[0][3][co]);
-            const int n_part = a.tiles_y * a.tiles_x;
-            a.part[((size_t)b * NT + co) * n_part + ty * a.tiles_x + tx] = make_float4(S, M2, N, 0.f);
-        }
+            short8 A0[3], A1[3];
+            split8(w[0], A0);
+            split8(w[1], A1);
+            mfma6(acc[0][h], A0, ub[1][0]);   // 9 sub-kernels: the last load_u (ab + 1 == 9) went to buffer 1
+            mfma6(acc[1][h], A1, ub[1][1]);
+        });
+        if (tn < n_tiles) load_u(std::integral_constant<int, 0>{}, 0);   // the next tile's first U
+        W9TL(2);
+
+        // ---- epilogue, one M block at a time: M -> LDS [xi][tile][co], output transform, store -------
+        sfor<0, 2>([&](auto Hh) __attribute__((always_inline)) {
+            constexpr int h = decltype(Hh)::value;
+            lds_barrier();   // patch / v16 reads (h = 0) / the previous block's M reads (h = 1) done
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;   // accumulator j of lane (li, lh): tile row, co li
+                    ms[((4 * p + 2 * qh + q) * 32 + row) * MS + li] = acc[q][h][j];
+                }
+            lds_barrier();
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int tl = 2 * g + k, tile = 32 * h + tl;
+                const int wy = tile >> 3, wx = tile & 7;
+                float m[16];
+#pragma unroll
+                for (int x = 0; x < NXI; ++x) m[x] = ms[(x * 32 + tl) * MS + co];
+                // T = A^T M (2 x 4), Y = T A (2 x 2); A^T = [[1,1,1,0],[0,1,-1,-1]]
+                float t0[4], t1[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    t0[c] = m[0 * 4 + c] + m[1 * 4 + c] + m[2 * 4 + c];
+                    t1[c] = m[1 * 4 + c] - m[2 * 4 + c] - m[3 * 4 + c];
+                }
+                const float yy[4] = {t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3], t1[0] + t1[1] + t1[2],
+                                     t1[1] - t1[2] - t1[3]};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
+                    if (oy < H && ox < W) {
+                        const float v = fmaxf(yy[q] + bias, 0.f);                 // Conv2D(..., activation='relu')
+                        a.out[(img + (size_t)oy * W + ox) * NT + co] = fmaxf(fmaf(bn.x, v, bn.y), 0.f);   // BN -> ReLU
+                    }
+                }
+            }
+        });
+        lds_barrier();   // M reads done before the next tile's v16 pads / computations
+        W9TL(3);
     }
 }
+
+#ifdef W9_PROF
+void w9_timeline_print(int nwg) {
+    std::vector<unsigned long long> tl((size_t)W9_PROF * 8 * 9 * 4, 0);
+    if (hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(w9_tl), tl.size() * 8) != hipSuccess) return;
+    if (nwg > W9_PROF) nwg = W9_PROF;
+    double ph[4] = {0, 0, 0, 0};
+    int n = 0;
+    for (int g = 0; g < nwg; ++g)
+        for (int w = 0; w < 8; ++w)
+            for (int it = 0; it + 1 < 7; ++it) {
+                const unsigned long long* q = &tl[(((size_t)g * 8 + w) * 9 + it) * 4];
+                const unsigned long long nx = q[4];   // next iteration's stamp 0
+                ph[0] += (double)(q[1] - q[0]);
+                ph[1] += (double)(q[2] - q[1]);
+                ph[2] += (double)(q[3] - q[2]);
+                ph[3] += (double)(nx - q[3]);
+                ++n;
+            }
+    printf("  per tile (us, iterations 0..5): top %.2f, loop %.2f, epilogue %.2f, gap %.2f\n", ph[0] / n * 0.01,
+           ph[1] / n * 0.01, ph[2] / n * 0.01, ph[3] / n * 0.01);
+}
+#endif
 
 static uint16_t bf16_rne_host(float x) {
     uint32_t u;
@@ -410,14 +489,26 @@ hipError_t wino9_x6_prepare() {
     return hipSuccess;
 }
 
+int wino9_x6_tiles_y(int H) { return (H + TH - 1) / TH; }
+int wino9_x6_tiles_x(int W) { return (W + TW - 1) / TW; }
+
 hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st) {
-    if (a.cin > 17 || a.cin <= 0 || a.tiles_y != (a.H + TH - 1) / TH || a.tiles_x != (a.W + TW - 1) / TW)
-        return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
+    if (a.cin > 17 || a.cin <= 0 || a.tiles_y != (a.H + TH - 1) / TH || a.tiles_x != (a.W + TW - 1) / TW ||
+        a.part != nullptr || a.bn_ab == nullptr)
+        return hipErrorInvalidValue;   // inference only: training keeps wino9_launch (batch-statistics BN)
+    // persistent: one workgroup per CU (LDS and registers allow one), each looping over tiles
+    const int n_tiles = a.batch * a.tiles_y * a.tiles_x;
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            n_cu = 256;
+    }
+    const unsigned grid = (unsigned)(n_tiles < n_cu ? n_tiles : n_cu);
     if (a.cin == 17)
-        hipLaunchKernelGGL(wino9_x6_kernel<17>, dim3(grid), dim3(256), LDS_BYTES, st, a);
+        hipLaunchKernelGGL(wino9_x6_kernel<17>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_tiles);
     else
-        hipLaunchKernelGGL(wino9_x6_kernel<0>, dim3(grid), dim3(256), LDS_BYTES, st, a);
+        hipLaunchKernelGGL(wino9_x6_kernel<0>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_tiles);
     return hipGetLastError();
 }
 

@@ -275,12 +275,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
 
     // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..7) in flight --
-    if constexpr (pro != PRO_NONE) __syncthreads();   // pab visible before the first staging
+    if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging
     load_patch(0);
     sfor<0, XRING>([&](auto X) __attribute__((always_inline)) { load_u(0, X, X); });
     stage(0, patch);
     if (nchunks > 1) load_patch(1);
-    __syncthreads();
+    lds_barrier();
     tr_read(patch);
     tr_rows(0);
     tr_rows(1);
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         stage(1, patch + XPATCH_FL);
         if (nchunks > 2) load_patch(2);
     }
-    __syncthreads();
+    lds_barrier();
     XTL(1);
 
     // A operands of point x: the three pieces of this lane's tile row, 16-B half lh (swizzled)
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             });
         });
         XPT(c, 16);
-        __syncthreads();
+        lds_barrier();
     }
     XTL(2);
 

@@ -7,7 +7,7 @@ D=/tmp/w9b$$
 mkdir -p $D
 /opt/rocm/bin/hipcc $F -c realtime_style_transfer_amd/csrc/wino9.hip -o $D/wino9.o &
 /opt/rocm/bin/hipcc $F $W9FLAGS -fno-slp-vectorize -c realtime_style_transfer_amd/csrc/wino9_x6.hip -o $D/wino9_x6.o &
-/opt/rocm/bin/hipcc $F -c tools/wino9_x6_bench.hip -o $D/main.o &
+/opt/rocm/bin/hipcc $F $W9FLAGS -c tools/wino9_x6_bench.hip -o $D/main.o &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $D/wino9.o $D/wino9_x6.o $D/main.o -o tools/wino9_x6_bench${W9SUFFIX}
 rm -rf $D

@@ -8,6 +8,9 @@
 #include <cstdlib>
 #include <vector>
 #include "kernels.h"
+#ifdef W9_PROF
+namespace rst { void w9_timeline_print(int nwg); }
+#endif
 
 using namespace rst;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -41,6 +44,8 @@ int main(int argc, char** argv) {
     a.batch = B; a.H = H; a.W = W; a.cin = C; a.tiles_y = wino9_tiles_y(H); a.tiles_x = wino9_tiles_x(W);
     CK(wino9_x6_prepare());
     Wino9Args a32 = a, a6 = a;
+    a6.tiles_y = wino9_x6_tiles_y(H);
+    a6.tiles_x = wino9_x6_tiles_x(W);
     a32.U = U32; a32.out = o32;
     a6.U = U6; a6.out = o6;
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -54,6 +59,9 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         printf("%s B=%d: %.2f us/launch\n", v ? "wino9_x6" : "wino9   ", B, 1e3 * ms / iters);
+#ifdef W9_PROF
+        if (v) rst::w9_timeline_print(B * a6.tiles_y * a6.tiles_x);
+#endif
     }
     std::vector<float> h32(n_out), h6(n_out);
     CK(hipMemcpy(h32.data(), o32, n_out * 4, hipMemcpyDeviceToHost));
