@@ -59,7 +59,10 @@ KERNEL_NAMES = {
     113: "conv_bf3<3x3 s1 CK32 NT64 8x16 bf16x6>",
     200: "wino_conv<F(2x2,3x3) 8x16 N128 f32 MFMA>", 201: "wino9_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 f32 MFMA>",
     202: "wino_x6_conv<F(2x2,3x3) 8x16 N128 split-bf16 x6 MFMA>",
-    203: "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 split-bf16 x6 MFMA>",
+    301: "conv_lite<3x3 s2 Cin32 Cout16 f32 16x16x4 MFMA>", 302: "conv_lite<3x3 s2 Cin16 Cout32 f32 32x32x2 MFMA>",
+    303: "conv_lite<3x3 s2 transposed Cin128 Cout32 f32 32x32x2 MFMA>",
+    304: "conv_lite<3x3 s2 transposed Cin32 Cout16 f32 16x16x4 MFMA>",
+    203: "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 16x16 N32 split-bf16 x6 MFMA persistent>",
 }
 
 

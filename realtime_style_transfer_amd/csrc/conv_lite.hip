@@ -1,0 +1,593 @@
+// conv_lite.hip — the narrow-channel convolutions of the transfer network on f32 MFMA, exact f32:
+//   contract_0/1   Conv2D 3x3 s2 'same' + bias + ReLU -> BatchNorm -> ReLU     styleTransfer.py:194-203
+//   expand_0/1     Conv2DTranspose 3x3 s2 'same' + bias (+ CIN stats)         styleTransfer.py:115-119
+// (Cin 16..128, Cout 16 or 32). The general implicit-GEMM kernel (conv_mfma.hip) ran these at
+// 0.17-0.25 of their rooflines: 32-wide N tiles half empty for Cout = 16, and the 4-phase transposed
+// form issued all 16 (tap, phase) products of which 7 multiply structural zeros.
+//
+// Mapping (one workgroup = 4 waves = 4 rows of MS pixels of the GEMM grid; MS = Cout = MFMA M = N):
+//   * Cout 16 -> v_mfma_f32_16x16x4_f32, Cout 32 -> v_mfma_f32_32x32x2_f32: no idle columns;
+//   * the input halo of the tile (all channels of a Cin chunk) is staged once into LDS, stride-2
+//     columns split by parity so a wave's 16/32 pixels read consecutive 16-B slots, each pixel padded
+//     to an odd number of 16-B slots: every operand read is one conflict-free ds_read_b128 whose four
+//     channels feed four MFMAs;
+//   * weights are host-packed in the LDS image order [chunk][slot][r][kslot][n][4];
+//   * transposed conv: out[2p+py][2q+px] = sum over the taps of phase (py,px) of in[p+ty-1][q+tx-1] .
+//     w[py+2(1-ty)][px+2(1-tx)] — phase (0,0) has 4 taps, (0,1) and (1,0) two, (1,1) one: the nine
+//     (phase, tap) slots issue exactly the 9 x Cin x Cout MACs per input pixel, and the four operand
+//     positions (ty, tx) are read once and shared by the phases that use them;
+//   * the CIN statistics {sum, M2, n} of a tile merge its four phases (finalize sees one partial per
+//     tile and channel), two-pass inside the tile, fixed order: deterministic.
+// Multi-chunk layers (expand_0, Cin 128 in 4 chunks of 32) double-buffer the halo + weight image:
+// chunk c+1 is loaded into registers while chunk c's MFMAs run and written to the other buffer after.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+#include <vector>
+
+#include "kernels.h"
+
+#ifndef LITE_SKIP
+#define LITE_SKIP 0   // tools/lite_bench knobs: 1 no halo loads, 2 no MFMAs, 4 no weight loads
+#endif
+
+namespace rst {
+
+#ifdef LITE_PROF
+// s_memtime per (workgroup < 64, wave, step < 16, point): 0 step top, 1 after staging + barrier,
+// 2 after the MFMAs, 3 after the epilogue (tools/lite_bench)
+__device__ unsigned long long lite_tl[64][4][16][4];
+#define LTL(st, pt) \
+    if (blockIdx.x < 64 && lane == 0 && (st) < 16) lite_tl[blockIdx.x][wave][(st)][(pt)] = __builtin_amdgcn_s_memtime()
+#else
+#define LTL(st, pt)
+#endif
+
+namespace lite {
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int MODE, int CIN, int NC, int CKC>
+struct Cfg {
+    static constexpr int MS = NC;                           // MFMA M = N = Cout
+    static constexpr int TW = MS, TH = 4;                   // GEMM-grid tile: 4 rows x MS pixels
+    static constexpr int KS = 64 / MS;                      // k slots per MFMA (lane groups)
+    static constexpr int NCH = CIN / CKC;                   // Cin chunks
+    static constexpr int QC = CKC / 4;                      // channel quads per pixel and chunk
+    static constexpr int R = QC / KS;                       // operand reads per slot and chunk
+    static constexpr int HR = MODE == 0 ? 2 * TH + 1 : TH + 1;
+    static constexpr int HC = MODE == 0 ? 2 * TW + 1 : TW + 1;
+    static constexpr int CS = CKC + 4;                      // floats per halo pixel (odd 16-B slots)
+    static constexpr int HALO = HR * HC * CS;               // floats per halo buffer
+    static constexpr int WCH = 9 * CKC * NC;                // weight floats per chunk
+        static constexpr int HITEMS = HR * HC * QC;             // float4 items per halo chunk
+    static constexpr int HREG = (HITEMS + 255) / 256;
+    static constexpr int WITEMS = WCH / 4;
+    static constexpr int WREG = (WITEMS + 255) / 256;
+    static constexpr int NACC = MS == 16 ? 4 : 16;          // accumulator floats per MFMA tile and lane
+    static constexpr int NPH = MODE == 0 ? 1 : 4;           // output phases
+    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 + 8 * NC * 4;
+    static_assert(CIN % CKC == 0 && CKC % (4 * KS) == 0, "chunking");
+    static_assert(MS == 16 || MS == 32, "MFMA shape");
+    static_assert(((CS / 4) & 1) == 1, "odd 16-B slots per halo pixel");
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+};
+
+template <int MS>
+struct Mfma;
+template <>
+struct Mfma<16> {
+    typedef f32x4 acc_t;
+    static __device__ __forceinline__ acc_t op(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // accumulator entry j of lane l: row (pixel) and column (channel)
+    static __device__ __forceinline__ int row(int j, int lane) { return 4 * (lane >> 4) + j; }
+    static __device__ __forceinline__ int col(int lane) { return lane & 15; }
+};
+template <>
+struct Mfma<32> {
+    typedef f32x16 acc_t;
+    static __device__ __forceinline__ acc_t op(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int j, int lane) { return (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5); }
+    static __device__ __forceinline__ int col(int lane) { return lane & 31; }
+};
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        sfor<I + 1, N>(f);
+    }
+}
+
+// transposed-conv slots: (phase, operand position ty*2+tx); the kernel tap is ky = py + 2(1-ty), kx = px + 2(1-tx)
+__host__ __device__ constexpr int t_phase(int s) { return s < 4 ? 0 : (s < 6 ? 1 : (s < 8 ? 2 : 3)); }
+__host__ __device__ constexpr int t_pos(int s) {
+    return s < 4 ? s : (s == 4 ? 1 : (s == 5 ? 3 : (s == 6 ? 2 : 3)));
+}
+}  // namespace lite
+
+template <int MODE, int CIN, int NC, int CKC, int PRO>
+__global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles) {
+    using namespace lite;
+    using C = Cfg<MODE, CIN, NC, CKC>;
+    using M = Mfma<C::MS>;
+    typedef typename M::acc_t acc_t;
+    constexpr int MS = C::MS, TW = C::TW, TH = C::TH, KS = C::KS, CS = C::CS, HC = C::HC, HR = C::HR, R = C::R;
+    constexpr int QC = C::QC, NCH = C::NCH;
+
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* const halo = smem;                  // [HALO]   one Cin chunk of the tile's input halo
+    float* const wts = smem + C::HALO;         // [WCH]    one Cin chunk of the weights
+    float* const red = wts + C::WCH;           // [8][NC]  statistics scratch
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int H = a.H, W = a.W;
+    auto halo_off = [&](int hy, int hx) __attribute__((always_inline)) {
+        if constexpr (MODE == 0) return (hy * HC + (hx & 1) * (TW + 1) + (hx >> 1)) * CS;
+        else return (hy * HC + hx) * CS;
+    };
+
+    // ---- persistent schedule: this workgroup's k-th tile is xcd_tile_order(blockIdx.x + k grid) (the
+    // grid is a multiple of 8, so every tile of a workgroup stays on its XCD's contiguous range) ------
+    struct Tile { int b, ty, tx, y0, x0, iy0, ix0; };
+    auto tile_of = [&](int k) __attribute__((always_inline)) {
+        Tile T;
+        int t = xcd_tile_order(blockIdx.x + k * gridDim.x, n_tiles);
+        T.tx = t % a.tiles_x;
+        t /= a.tiles_x;
+        T.ty = t % a.tiles_y;
+        T.b = t / a.tiles_y;
+        T.y0 = T.ty * TH;
+        T.x0 = T.tx * TW;
+        T.iy0 = MODE == 0 ? 2 * T.y0 - a.pad_t : T.y0 - 1;
+        T.ix0 = MODE == 0 ? 2 * T.x0 - a.pad_l : T.x0 - 1;
+        return T;
+    };
+
+    // ---- staging map -----------------------------------------------------------------------------
+    // Thread t stages channel quad q = t % QC of main column col = (t / QC) % (HC - 1) in rows
+    // rsub + RPP k, and (t < HR QC) the last halo column in row t / QC: the global and LDS offsets
+    // advance by a constant per row (a per-item (pixel, quad) decode cost as much VALU as the MFMAs).
+    constexpr int HCM = HC - 1, TPR = HCM * QC, RPP = 256 / TPR, NMAIN = (HR + RPP - 1) / RPP;
+    constexpr int NEXTRA = HR * QC;
+    static_assert(256 % TPR == 0 && NEXTRA <= 256, "staging map");
+    const int q = tid % QC, col = (tid / QC) % HCM, rsub = tid / TPR, ehy = min(tid / QC, HR - 1);
+    const int lcm = halo_off(0, col) + 4 * q, lce = halo_off(0, HCM) + 4 * q;
+    f32x4 hreg[NMAIN + 1], rreg[NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01, pa23;
+    auto load_step = [&](const Tile& T, int ch) __attribute__((always_inline)) {
+        const int co = ch * CKC;
+        const int ixm = min(max(T.ix0 + col, 0), W - 1), ixe = min(max(T.ix0 + HCM, 0), W - 1);
+        const int rb = T.b * H;
+        sfor<0, NMAIN + 1>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int hy = k < NMAIN ? min(rsub + RPP * k, HR - 1) : ehy;
+            const int gi = ((rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)) * CIN + co + 4 * q;
+#if LITE_SKIP & 1
+            hreg[k] = f32x4{(float)gi, 0.f, 0.f, 0.f};
+#else
+            hreg[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
+            if constexpr (PRO == PRO_AFF_RES) rreg[k] = *reinterpret_cast<const f32x4*>(a.res + gi);
+#endif
+        });
+        if constexpr (PRO != PRO_NONE) {
+            const f32x4* pa = reinterpret_cast<const f32x4*>(a.pro_ab + (size_t)T.b * CIN + co + 4 * q);
+            pa01 = pa[0];
+            pa23 = pa[1];
+        }
+        if constexpr (NCH > 1) {
+            sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
+                constexpr int k = decltype(K)::value;
+                const int it = min(tid + 256 * k, C::WITEMS - 1);
+                wreg[k] = reinterpret_cast<const f32x4*>(a.wpk)[(size_t)ch * C::WITEMS + it];
+            });
+        }
+    };
+    auto xform = [&](f32x4 v, f32x4 r) __attribute__((always_inline)) {
+        if constexpr (PRO != PRO_NONE) {
+            v.x = fmaf(pa01.x, v.x, pa01.y);
+            v.y = fmaf(pa01.z, v.y, pa01.w);
+            v.z = fmaf(pa23.x, v.z, pa23.y);
+            v.w = fmaf(pa23.z, v.w, pa23.w);
+            if constexpr (PRO == PRO_AFF_RELU) {
+                v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+            } else if constexpr (PRO == PRO_AFF_RES) {
+                v += r;
+            }
+        }
+        return v;
+    };
+    auto store_step = [&](const Tile& T) __attribute__((always_inline)) {
+        const bool okm = T.ix0 + col >= 0 && T.ix0 + col < W;
+        const bool oke = T.ix0 + HCM >= 0 && T.ix0 + HCM < W;
+        auto row_ok = [&](int hy) __attribute__((always_inline)) { return T.iy0 + hy >= 0 && T.iy0 + hy < H; };
+        sfor<0, NMAIN>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int hy = rsub + RPP * k;
+            if (HR % RPP == 0 || k < NMAIN - 1 || hy < HR) {
+                const f32x4 v = okm && row_ok(hy) ? xform(hreg[k], rreg[k]) : f32x4{0.f, 0.f, 0.f, 0.f};
+                *reinterpret_cast<f32x4*>(halo + lcm + hy * (HC * CS)) = v;
+            }
+        });
+        if (tid < NEXTRA) {
+            const f32x4 v = oke && row_ok(ehy) ? xform(hreg[NMAIN], rreg[NMAIN]) : f32x4{0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<f32x4*>(halo + lce + ehy * (HC * CS)) = v;
+        }
+        if constexpr (NCH > 1) {
+            sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
+                constexpr int k = decltype(K)::value;
+                const int it = tid + 256 * k;
+                if (C::WITEMS % 256 == 0 || it < C::WITEMS) reinterpret_cast<f32x4*>(wts)[it] = wreg[k];
+            });
+        }
+    };
+
+    // ---- operands: A = pixel m of this wave's row, quad g + KS r; B = row (slot, r, g), column m ------
+    const int m = lane % MS, g = lane / MS;
+    auto a_off = [&](int pos) __attribute__((always_inline)) {   // pos: tap (MODE 0) / operand position (MODE 1)
+        if constexpr (MODE == 0) return halo_off(2 * wave + pos / 3, 2 * m + pos % 3);
+        else return halo_off(wave + (pos >> 1), m + (pos & 1));
+    };
+    // software pipeline: the operands of step u+1 are read before the MFMAs of step u issue. Steps:
+    // MODE 0 one (r, kernel row) = 3 taps, 12 MFMAs into 3 accumulators (one per kx: no back-to-back
+    // dependent MFMAs); MODE 1 one r = 4 operand positions x 9 slots, 36 MFMAs into the 4 phase
+    // accumulators (phase 0's four slots alternate between two).
+    constexpr int NA = MODE == 0 ? 3 : 4, NB = MODE == 0 ? 3 : 9, NSTEP = MODE == 0 ? 3 * R : R;
+    constexpr int NACCS = MODE == 0 ? 3 : 5;
+    acc_t acc[NACCS];
+    auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int p = 0; p < NACCS; ++p)
+#pragma unroll
+            for (int j = 0; j < C::NACC; ++j) acc[p][j] = 0.f;
+    };
+    auto read_step = [&](auto U, f32x4 (&A)[NA], f32x4 (&Bv)[NB]) __attribute__((always_inline)) {
+        constexpr int u = decltype(U)::value;
+        if constexpr (MODE == 0) {
+            constexpr int r = u / 3, ky = u % 3;
+            const int qo = 4 * (g + KS * r);
+            sfor<0, 3>([&](auto X) __attribute__((always_inline)) {
+                constexpr int kx = decltype(X)::value, t = ky * 3 + kx;
+                A[kx] = *reinterpret_cast<const f32x4*>(halo + a_off(t) + qo);
+                Bv[kx] = *reinterpret_cast<const f32x4*>(wts + (((t * R + r) * KS + g) * MS + m) * 4);
+            });
+        } else {
+            constexpr int r = u;
+            const int qo = 4 * (g + KS * r);
+            sfor<0, 4>([&](auto P) __attribute__((always_inline)) {
+                constexpr int pos = decltype(P)::value;
+                A[pos] = *reinterpret_cast<const f32x4*>(halo + a_off(pos) + qo);
+            });
+            sfor<0, 9>([&](auto S) __attribute__((always_inline)) {
+                constexpr int sl = decltype(S)::value;
+                Bv[sl] = *reinterpret_cast<const f32x4*>(wts + (((sl * R + r) * KS + g) * MS + m) * 4);
+            });
+        }
+    };
+    auto mfma_step = [&](const f32x4 (&A)[NA], const f32x4 (&Bv)[NB]) __attribute__((always_inline)) {
+        sfor<0, 4>([&](auto I) __attribute__((always_inline)) {
+            constexpr int i = decltype(I)::value;
+            if constexpr (MODE == 0) {
+                sfor<0, 3>([&](auto X) __attribute__((always_inline)) {
+                    constexpr int kx = decltype(X)::value;
+                    acc[kx] = M::op(A[kx][i], Bv[kx][i], acc[kx]);
+                });
+            } else {
+                constexpr int order[9] = {0, 4, 6, 8, 1, 5, 7, 2, 3};
+                sfor<0, 9>([&](auto S) __attribute__((always_inline)) {
+                    constexpr int sl = order[decltype(S)::value];
+                    constexpr int ai = (sl == 1 || sl == 3) ? 4 : t_phase(sl);
+                    acc[ai] = M::op(A[t_pos(sl)][i], Bv[sl][i], acc[ai]);
+                });
+            }
+        });
+    };
+    auto compute = [&]() __attribute__((always_inline)) {
+        if constexpr ((LITE_SKIP & 2) == 0) {
+            f32x4 A0[NA], B0[NB], A1[NA], B1[NB];
+            read_step(std::integral_constant<int, 0>{}, A0, B0);
+            sfor<0, NSTEP>([&](auto U) __attribute__((always_inline)) {
+                constexpr int u = decltype(U)::value;
+                if constexpr (u + 1 < NSTEP) {
+                    if constexpr (((u + 1) & 1) == 0) read_step(std::integral_constant<int, u + 1>{}, A0, B0);
+                    else read_step(std::integral_constant<int, u + 1>{}, A1, B1);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr ((u & 1) == 0) mfma_step(A0, B0);
+                else mfma_step(A1, B1);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        }
+    };
+
+    // ---- epilogue of one tile ----------------------------------------------------------------------
+    const int n = M::col(lane);
+    const float bias = a.bias[n];
+    const float2 bn = MODE == 0 ? a.bn_ab[n] : float2{1.f, 0.f};
+    auto epilogue = [&](const Tile& T) __attribute__((always_inline)) {
+        if constexpr (MODE == 0) {   // bias + ReLU -> BatchNorm (inference affine) -> ReLU, NHWC store
+            const acc_t y = (acc[0] + acc[1]) + acc[2];
+            const int oy = T.y0 + wave;
+            const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
+            float* const orow = a.out + ((size_t)(T.b * a.Ho + oy) * a.Wo) * NC + n;
+#pragma unroll
+            for (int j = 0; j < C::NACC; ++j) {
+                const int ox = T.x0 + M::row(j, lane);
+                float v = fmaxf(y[j] + bias, 0.f);
+                v = fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                if (full || (oy < a.Ho && ox < a.Wo)) orow[(size_t)ox * NC] = v;
+            }
+        } else {   // bias, pixel-shuffle store, per-tile CIN statistics over the four phases
+            acc[0] = acc[0] + acc[4];
+            const int p = T.y0 + wave;
+            const int Ho2 = 2 * a.Ho, Wo2 = 2 * a.Wo;
+            float s = 0.f, cnt = 0.f;
+            // interior tiles (every pixel inside) store without per-element guards
+            const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
+            float* const orow = a.out + ((size_t)(T.b * Ho2 + 2 * p) * Wo2) * NC + n;
+            if (full) {
+#pragma unroll
+                for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+                    for (int j = 0; j < C::NACC; ++j) {
+                        const int qq = T.x0 + M::row(j, lane);
+                        const float v = acc[ph][j] + bias;
+                        acc[ph][j] = v;
+                        orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
+                        s += v;
+                    }
+                cnt = 4.f * C::NACC;
+            } else {
+#pragma unroll
+                for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+                    for (int j = 0; j < C::NACC; ++j) {
+                        const int qq = T.x0 + M::row(j, lane);
+                        const float v = acc[ph][j] + bias;
+                        acc[ph][j] = v;
+                        if (p < a.Ho && qq < a.Wo) {
+                            orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
+                            s += v;
+                            cnt += 1.f;
+                        }
+                    }
+            }
+            if (a.part != nullptr) {
+                // lanes n, n + MS, ... hold column n: reduce over them, then over the 4 waves (fixed order)
+#pragma unroll
+                for (int o = MS; o < 64; o <<= 1) {
+                    s += __shfl_xor(s, o);
+                    cnt += __shfl_xor(cnt, o);
+                }
+                if (lane < MS) {
+                    red[wave * NC + n] = s;
+                    red[4 * NC + wave * NC + n] = cnt;
+                }
+                lds_barrier();
+                const float S = (red[n] + red[NC + n]) + (red[2 * NC + n] + red[3 * NC + n]);
+                const float N = (red[4 * NC + n] + red[5 * NC + n]) + (red[6 * NC + n] + red[7 * NC + n]);
+                const float mean = N > 0.f ? S / N : 0.f;
+                float m2 = 0.f;
+#pragma unroll
+                for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+                    for (int j = 0; j < C::NACC; ++j) {
+                        const int qq = T.x0 + M::row(j, lane);
+                        const float d = acc[ph][j] - mean;
+                        if (full || (p < a.Ho && qq < a.Wo)) m2 = fmaf(d, d, m2);
+                    }
+#pragma unroll
+                for (int o = MS; o < 64; o <<= 1) m2 += __shfl_xor(m2, o);
+                lds_barrier();
+                if (lane < MS) red[wave * NC + n] = m2;
+                lds_barrier();
+                if (tid < NC) {   // lane tid < NC holds column tid
+                    const float M2 = (red[tid] + red[NC + tid]) + (red[2 * NC + tid] + red[3 * NC + tid]);
+                    const int n_part = a.tiles_y * a.tiles_x;
+                    a.part[((size_t)T.b * NC + tid) * n_part + T.ty * a.tiles_x + T.tx] = make_float4(S, M2, N, 0.f);
+                }
+            }
+        }
+    };
+
+    // ---- main loop over (tile, chunk) steps: step s+1's global loads are in flight while step s
+    // computes and (last chunk) stores its tile ---------------------------------------------------------
+    if constexpr (NCH == 1) {   // one weight image for every tile: staged once
+        for (int it = tid; it < C::WITEMS; it += 256)
+            reinterpret_cast<f32x4*>(wts)[it] = reinterpret_cast<const f32x4*>(a.wpk)[it];
+    }
+    const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int n_steps = my_tiles * NCH;
+    Tile cur = tile_of(0);
+    load_step(cur, 0);
+    zero_acc();
+    for (int s = 0; s < n_steps; ++s) {
+        const int ch = s % NCH;
+        LTL(s, 0);
+        if (s > 0) lds_barrier();        // the previous step's operand reads are done
+        store_step(cur);
+        lds_barrier();
+        LTL(s, 1);
+        Tile nxt = cur;
+        if (s + 1 < n_steps) {
+            const int ch1 = (s + 1) % NCH;
+            if (ch1 == 0) nxt = tile_of((s + 1) / NCH);
+            load_step(nxt, ch1);
+        }
+        compute();
+        LTL(s, 2);
+        if (ch == NCH - 1) {
+            epilogue(cur);
+            zero_acc();
+        }
+        LTL(s, 3);
+        cur = nxt;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side: the instantiated layer shapes
+// ------------------------------------------------------------------------------------------------
+#define RST_LITE_CONFIGS(X)        \
+    X(1, 0, 32, 16, 32)            \
+    X(2, 0, 16, 32, 16)            \
+    X(3, 1, 128, 32, 32)           \
+    X(4, 1, 32, 16, 32)
+
+bool conv_lite_select(int keras_kind, int k, int stride, int cin, int cout, LiteTile* t) {
+    if (k != 3 || stride != 2) return false;
+#define X(ID, MODE, CIN, NC, CKC)                                                  \
+    if (keras_kind == MODE && cin == CIN && cout == NC) {                          \
+        using C = lite::Cfg<MODE, CIN, NC, CKC>;                                   \
+        t->id = ID; t->mode = MODE; t->cin = CIN; t->nc = NC; t->ckc = CKC;        \
+        t->th = C::TH; t->tw = C::TW; t->lds_bytes = (int)C::LDS_BYTES;            \
+        return true;                                                               \
+    }
+    RST_LITE_CONFIGS(X)
+#undef X
+    return false;
+}
+
+// weights: Conv2D HWIO [ky][kx][ci][co]; Conv2DTranspose [ky][kx][co][ci] (Keras layouts) ->
+// [chunk][slot][r][kslot][n][4], the LDS image of one chunk
+std::vector<float> conv_lite_pack_weights(const LiteTile& t, const float* kern) {
+    const int ks = 64 / t.nc, nch = t.cin / t.ckc, R = t.ckc / 4 / ks;
+    std::vector<float> out((size_t)nch * 9 * t.ckc * t.nc);
+    size_t idx = 0;
+    for (int ch = 0; ch < nch; ++ch)
+        for (int s = 0; s < 9; ++s)
+            for (int r = 0; r < R; ++r)
+                for (int g = 0; g < ks; ++g)
+                    for (int n = 0; n < t.nc; ++n)
+                        for (int i = 0; i < 4; ++i) {
+                            const int ci = ch * t.ckc + 4 * (g + ks * r) + i;
+                            if (t.mode == 0) {
+                                out[idx++] = kern[((size_t)s * t.cin + ci) * t.nc + n];
+                            } else {
+                                const int ph = lite::t_phase(s), pos = lite::t_pos(s);
+                                const int py = ph >> 1, px = ph & 1, tyy = pos >> 1, txx = pos & 1;
+                                const int ky = py + 2 * (1 - tyy), kx = px + 2 * (1 - txx);
+                                out[idx++] = kern[(((size_t)ky * 3 + kx) * t.nc + n) * t.cin + ci];
+                            }
+                        }
+    return out;
+}
+
+#ifdef LITE_PROF
+void lite_timeline_print(int nsteps) {
+    std::vector<unsigned long long> tl((size_t)64 * 4 * 16 * 4);
+    if (hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(lite_tl), tl.size() * 8) != hipSuccess) return;
+    double d[3] = {0, 0, 0}, gap = 0;
+    int n = 0, ng = 0;
+    for (int g = 0; g < 64; ++g)
+        for (int w = 0; w < 4; ++w)
+            for (int st = 0; st < nsteps && st < 16; ++st) {
+                const unsigned long long* q = &tl[(((size_t)g * 4 + w) * 16 + st) * 4];
+                if (q[0] == 0 || q[3] < q[0]) continue;
+                for (int k = 0; k < 3; ++k) d[k] += (double)(q[k + 1] - q[k]);
+                ++n;
+                if (st + 1 < nsteps && st + 1 < 16) {
+                    const unsigned long long* q1 = q + 4;
+                    if (q1[0] >= q[3] && q1[0] != 0) { gap += (double)(q1[0] - q[3]); ++ng; }
+                }
+            }
+    if (n) printf("    per step (us): staging+barrier %.2f, MFMA %.2f, epilogue %.2f (n=%d)\n", d[0] / n * 0.01,
+                  d[1] / n * 0.01, d[2] / n * 0.01, n);
+    hipMemset(tl.data(), 0, 0);
+    std::vector<unsigned long long> z(tl.size(), 0);
+    hipMemcpyToSymbol(HIP_SYMBOL(lite_tl), z.data(), z.size() * 8);
+}
+#endif
+
+// persistent grid: every CU holds as many workgroups as LDS and registers allow (queried once per
+// instantiation at prepare time), rounded to a multiple of the 8 XCDs; never more than the tiles
+static int lite_cu_count() {
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            n_cu = 256;
+    }
+    return n_cu;
+}
+
+template <int MODE, int CIN, int NC, int CKC, int PRO>
+static int lite_slots() {
+    static int slots = 0;
+    if (slots == 0) {
+        using C = lite::Cfg<MODE, CIN, NC, CKC>;
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_lite_kernel<MODE, CIN, NC, CKC, PRO>, 256,
+                                                         C::LDS_BYTES) != hipSuccess || per_cu <= 0)
+            per_cu = 1;
+        slots = ((lite_cu_count() * per_cu) / 8) * 8;
+        if (slots <= 0) slots = 8;
+    }
+    return slots;
+}
+
+template <int MODE, int CIN, int NC, int CKC, int PRO>
+static void lite_launch_pro(const ConvArgs& a, int n_tiles, hipStream_t st) {
+    using C = lite::Cfg<MODE, CIN, NC, CKC>;
+    const int grid = std::min(n_tiles, lite_slots<MODE, CIN, NC, CKC, PRO>());
+    hipLaunchKernelGGL((conv_lite_kernel<MODE, CIN, NC, CKC, PRO>), dim3(grid), dim3(256), C::LDS_BYTES, st, a, n_tiles);
+}
+
+template <int MODE, int CIN, int NC, int CKC>
+static hipError_t lite_launch_cfg(const ConvArgs& a, hipStream_t st) {
+    using C = lite::Cfg<MODE, CIN, NC, CKC>;
+    if (a.cin != CIN || a.cout != NC || a.tiles_y != (a.Ho + C::TH - 1) / C::TH ||
+        a.tiles_x != (a.Wo + C::TW - 1) / C::TW || (size_t)a.batch * a.H * a.W * CIN >= ((size_t)1 << 31))
+        return hipErrorInvalidValue;   // 32-bit staging offsets
+    const int n_tiles = a.batch * a.tiles_y * a.tiles_x;
+    switch (a.pro_mode) {
+        case PRO_NONE: lite_launch_pro<MODE, CIN, NC, CKC, PRO_NONE>(a, n_tiles, st); break;
+        case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU>(a, n_tiles, st); break;
+        case PRO_AFF_RES: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES>(a, n_tiles, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int MODE, int CIN, int NC, int CKC>
+static hipError_t lite_prepare_cfg() {
+    using C = lite::Cfg<MODE, CIN, NC, CKC>;
+    for (const void* k : {(const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_NONE>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES>}) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES);
+        if (e != hipSuccess) return e;
+    }
+    // occupancy queries outside any graph capture
+    lite_slots<MODE, CIN, NC, CKC, PRO_NONE>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES>();
+    return hipSuccess;
+}
+
+hipError_t conv_lite_launch(const LiteTile& t, const ConvArgs& a, hipStream_t st) {
+    switch (t.id) {
+#define X(ID, MODE, CIN, NC, CKC) \
+    case ID: return lite_launch_cfg<MODE, CIN, NC, CKC>(a, st);
+        RST_LITE_CONFIGS(X)
+#undef X
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t conv_lite_prepare(const LiteTile& t) {
+    switch (t.id) {
+#define X(ID, MODE, CIN, NC, CKC) \
+    case ID: return lite_prepare_cfg<MODE, CIN, NC, CKC>();
+        RST_LITE_CONFIGS(X)
+#undef X
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace rst

@@ -159,6 +159,18 @@ int small_conv_tiles_y(int H);
 int small_conv_tiles_x(int W);
 int small_conv_weight_stride();
 
+// Narrow-channel 3x3 stride-2 convs (contract_0/1) and 3x3 s2 transposed convs (expand_0/1) on f32
+// MFMA with no idle columns and no zero-tap products (conv_lite.hip). Reuses ConvArgs: Ho/Wo are the
+// GEMM grid (conv: output dims; transposed: input dims), cout the stored channels, pro_mode/part as
+// for conv_mfma; the transposed form writes one {sum, M2, n} per (tile, channel), phases merged.
+struct LiteTile {
+    int id, mode, cin, nc, ckc, th, tw, lds_bytes;
+};
+bool conv_lite_select(int keras_kind, int k, int stride, int cin, int cout, LiteTile* t);
+std::vector<float> conv_lite_pack_weights(const LiteTile& t, const float* kern);
+hipError_t conv_lite_launch(const LiteTile& t, const ConvArgs& a, hipStream_t st);
+hipError_t conv_lite_prepare(const LiteTile& t);
+
 // CIN statistics finalize: merge per-tile {sum, M2, n} (Chan, f64) -> per-(b,c) affine.
 struct FinalizeArgs {
     const float4* part;      // [B][ntot][n_part]

@@ -176,7 +176,7 @@ namespace rst {
 // point at the layer's Keras weights; passing an array of (index + 1) values instead yields the
 // gather map from canonical weights to the packed image (training re-packs after each update).
 int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const float* bias, std::vector<float>& packed,
-                  std::vector<float>& bias_n, int precision) {
+                  std::vector<float>& bias_n, int precision, bool allow_lite) {
     const size_t kcount = (size_t)s.k * s.k * s.cin * s.cout;
     (void)kcount;
     if (s.keras_kind == 1 && s.k == 9 && s.stride == 1) {
@@ -227,6 +227,26 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.gWo = s.Wo;
         e.tiles_y = wino_tiles_y(s.Ho);
         e.tiles_x = wino_tiles_x(s.Wo);
+        e.n_part = e.tiles_y * e.tiles_x;
+    } else if (allow_lite && conv_lite_select(s.keras_kind, s.k, s.stride, s.cin, s.cout, &e.lite) &&
+               (s.keras_kind == 0 ? (s.norm == N_BN && s.conv_relu) : (s.norm == N_CIN && !s.conv_relu))) {
+        // ---- narrow 3x3 s2 conv / transposed conv: exact f32 MFMA, no idle columns, no zero taps
+        e.kind = K_LITE;
+        packed = conv_lite_pack_weights(e.lite, kern);
+        bias_n.assign(bias, bias + s.cout);
+        e.ntot = s.cout;
+        if (s.keras_kind == 0) {
+            const int pt = std::max((s.Ho - 1) * 2 + 3 - s.H, 0), pl = std::max((s.Wo - 1) * 2 + 3 - s.W, 0);
+            e.pad_t = pt / 2;
+            e.pad_l = pl / 2;
+            e.gHo = s.Ho;
+            e.gWo = s.Wo;
+        } else {
+            e.gHo = s.H;
+            e.gWo = s.W;
+        }
+        e.tiles_y = (e.gHo + e.lite.th - 1) / e.lite.th;
+        e.tiles_x = (e.gWo + e.lite.tw - 1) / e.lite.tw;
         e.n_part = e.tiles_y * e.tiles_x;
     } else {
         int taps, ntot, kh;
@@ -352,7 +372,8 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         // the Winograd kernel has no two-style blend prologue: those layers keep the direct kernel
         const bool wino_mode = precision == RST_PRECISION_FP32_WINOGRAD || precision == RST_PRECISION_WINOGRAD_BF16X6;
         const int lp = (wino_mode && shape->num_styles == 2) ? RST_PRECISION_FP32 : precision;
-        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp)) != RST_OK) { delete h; return st; }
+        // the narrow-conv kernel has no two-style blend prologue either
+        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, shape->num_styles == 1)) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
         if (s.norm == N_BN) {
@@ -437,6 +458,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         hipError_t pe = e.kind == K_WINO      ? wino_prepare()
                         : e.kind == K_WINOX6  ? wino_x6_prepare()
                         : e.kind == K_WINO9X6 ? wino9_x6_prepare()
+                        : e.kind == K_LITE    ? conv_lite_prepare(e.lite)
                                               : conv_prepare(e.tile);
         if (pe != hipSuccess) {
             delete h;
@@ -556,7 +578,12 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.pro_mode = e.pro;
         a.epi_mode = e.s.norm == N_BN ? EPI_RELU_BN : (e.s.conv_relu ? EPI_RELU_STATS : EPI_STATS);
         a.shuffle = e.kind == K_CONVT2 ? 1 : 0;
-        HIP_TRY(conv_launch(e.tile, a, st));
+        if (e.kind == K_LITE) {
+            if (blend) return fail(RST_ERR_UNSUPPORTED, "narrow conv kernel has no two-style blend prologue");
+            HIP_TRY(conv_lite_launch(e.lite, a, st));
+        } else {
+            HIP_TRY(conv_launch(e.tile, a, st));
+        }
     }
     if (ev) HIP_TRY(hipEventRecord(ev[1], st));
     if (e.s.norm == N_CIN) {
@@ -658,6 +685,7 @@ int rst_layer_kernel_id(const rst_handle* h, int idx) {
         case K_WINO9: return 201;
         case K_WINOX6: return 202;
         case K_WINO9X6: return 203;
+        case K_LITE: return 300 + e.lite.id;
         default: return e.tile.id;
     }
 }

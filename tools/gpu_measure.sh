@@ -33,8 +33,8 @@ fi
 if want pmc; then
     rm -rf gpurun_out/pmc_f gpurun_out/pmc_w
     timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f -o run -- \
-        python tools/wino_probe.py fp32_winograd 3 > gpurun_out/pmc_f.log 2>&1 || { tail -20 gpurun_out/pmc_f.log; exit 1; }
+        python tools/wino_probe.py winograd_bf16x6 3 > gpurun_out/pmc_f.log 2>&1 || { tail -20 gpurun_out/pmc_f.log; exit 1; }
     timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w -o run -- \
-        python tools/wino_probe.py fp32_winograd 3 > gpurun_out/pmc_w.log 2>&1 || { tail -20 gpurun_out/pmc_w.log; exit 1; }
+        python tools/wino_probe.py winograd_bf16x6 3 > gpurun_out/pmc_w.log 2>&1 || { tail -20 gpurun_out/pmc_w.log; exit 1; }
     echo "pmc ok"
 fi

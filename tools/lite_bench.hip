@@ -1,0 +1,97 @@
+// lite_bench.hip — standalone timing of the narrow-conv kernels (conv_lite.hip) on the headline shapes
+// (rst-960-120-128-17, B = 1 and 8): contract_0 480x960x32 -> 16, contract_1 240x480x16 -> 32,
+// expand_0 120x240x128 -> 32 (x4 phases), expand_1 240x480x32 -> 16 (x4 phases).
+// Build: bash tools/build_lite_bench.sh   Run: ./tools/lite_bench [iters]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../realtime_style_transfer_amd/csrc/conv_lite.hip"
+
+using namespace rst;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+static float* dev_rand(size_t n, float lo, float hi, unsigned seed) {
+    std::vector<float> h(n);
+    srand(seed);
+    for (auto& v : h) v = lo + (hi - lo) * (rand() / (float)RAND_MAX);
+    float* d;
+    CK(hipMalloc(&d, n * 4));
+    CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+    return d;
+}
+
+struct Shape { const char* name; int kind, H, W, cin, cout, pro; };
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 200;
+    const Shape shapes[] = {{"contract_0", 0, 480, 960, 32, 16, PRO_NONE},
+                            {"contract_1", 0, 240, 480, 16, 32, PRO_NONE},
+                            {"expand_0", 1, 120, 240, 128, 32, PRO_AFF_RES},
+                            {"expand_1", 1, 240, 480, 32, 16, PRO_AFF_RELU}};
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int B : {1, 8})
+        for (const Shape& s : shapes) {
+            LiteTile t{};
+            if (!conv_lite_select(s.kind, 3, 2, s.cin, s.cout, &t)) { printf("no tile for %s\n", s.name); return 1; }
+            CK(conv_lite_prepare(t));
+            const int Ho = s.kind == 0 ? (s.H + 1) / 2 : s.H, Wo = s.kind == 0 ? (s.W + 1) / 2 : s.W;
+            const size_t nin = (size_t)B * s.H * s.W * s.cin;
+            const size_t nout = (size_t)B * (s.kind == 0 ? Ho * Wo : 4 * Ho * Wo) * s.cout;
+            float* in = dev_rand(nin, -1.f, 1.f, 1);
+            float* res = dev_rand(nin, -1.f, 1.f, 2);
+            float* w = dev_rand((size_t)9 * s.cin * s.cout, -0.1f, 0.1f, 3);
+            float* bias = dev_rand(s.cout, -0.1f, 0.1f, 4);
+            float* ab = dev_rand((size_t)2 * B * s.cin, 0.5f, 1.f, 5);
+            float* out;
+            CK(hipMalloc(&out, nout * 4));
+            const int tiles_y = (Ho + t.th - 1) / t.th, tiles_x = (Wo + t.tw - 1) / t.tw;
+            float4* part;
+            CK(hipMalloc(&part, (size_t)B * s.cout * tiles_y * tiles_x * 16));
+            ConvArgs a{};
+            a.in = in;
+            a.res = res;
+            a.pro_ab = reinterpret_cast<const float2*>(ab);
+            a.wpk = w;
+            a.bias = bias;
+            a.bn_ab = reinterpret_cast<const float2*>(ab);
+            a.out = out;
+            a.part = s.kind == 1 ? part : nullptr;
+            a.batch = B;
+            a.H = s.H;
+            a.W = s.W;
+            a.cin = s.cin;
+            a.Ho = Ho;
+            a.Wo = Wo;
+            a.ntot = s.cout;
+            a.cout = s.cout;
+            a.pad_t = a.pad_l = 0;
+            a.tiles_y = tiles_y;
+            a.tiles_x = tiles_x;
+            a.pro_mode = s.pro;
+            for (int i = 0; i < 5; ++i) CK(conv_lite_launch(t, a, st));
+            CK(hipEventRecord(e0, st));
+            for (int i = 0; i < iters; ++i) CK(conv_lite_launch(t, a, st));
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const double us = ms * 1e3 / iters;
+            const double flops = 2.0 * B * (s.kind == 0 ? (double)Ho * Wo : (double)s.H * s.W) * 9 * s.cin * s.cout;
+            const double bytes = 4.0 * (nin * (s.pro == PRO_AFF_RES ? 2 : 1) + nout);
+#ifdef LITE_PROF
+            lite_timeline_print(16);
+#endif
+            printf("B=%d %-11s %8.2f us   %6.1f TFLOP/s (%.2f of f32 MFMA)   %7.1f GB/s (%.2f of HBM)   grid %d\n", B,
+                   s.name, us, flops / us * 1e-6, flops / us * 1e-6 / 157.3, bytes / us * 1e-3,
+                   bytes / us * 1e-3 / 8000.0, B * tiles_y * tiles_x);
+            CK(hipFree(in)); CK(hipFree(res)); CK(hipFree(w)); CK(hipFree(bias)); CK(hipFree(ab));
+            CK(hipFree(out)); CK(hipFree(part));
+        }
+    return 0;
+}

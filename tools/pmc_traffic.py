@@ -32,6 +32,15 @@ def short_name(k: str) -> str:
     if m:
         args = tuple(int(v) for v in m.group(1).split(","))
         return CONFIG_NAMES.get(args[:5], "conv_mfma<" + ",".join(map(str, args)) + ">")
+    m = re.search(r"conv_lite_kernel<([^>]*)>", k)
+    if m:
+        mode, cin, nc = (int(v) for v in m.group(1).split(",")[:3])
+        shape = "16x16x4" if nc == 16 else "32x32x2"
+        return f"conv_lite<3x3 s2 {'transposed ' if mode else ''}Cin{cin} Cout{nc} f32 {shape} MFMA>"
+    if "wino9_x6_kernel" in k:
+        return "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 16x16 N32 split-bf16 x6 MFMA persistent>"
+    if "wino_x6_kernel" in k:
+        return "wino_x6_conv<F(2x2,3x3) 8x16 N128 split-bf16 x6 MFMA>"
     if "wino9_conv_kernel" in k:
         return "wino9_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 f32 MFMA>"
     if "wino_conv" in k:
