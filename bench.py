@@ -59,6 +59,7 @@ KERNEL_NAMES = {
     113: "conv_bf3<3x3 s1 CK32 NT64 8x16 bf16x6>",
     200: "wino_conv<F(2x2,3x3) 8x16 N128 f32 MFMA>", 201: "wino9_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 f32 MFMA>",
     202: "wino_x6_conv<F(2x2,3x3) 8x16 N128 split-bf16 x6 MFMA>",
+    204: "last_x6<9x9 transposed Cin16 Cout3 as N=(kx,co) split-bf16 x6 MFMA>",
     301: "conv_lite<3x3 s2 Cin32 Cout16 f32 16x16x4 MFMA>", 302: "conv_lite<3x3 s2 Cin16 Cout32 f32 32x32x2 MFMA>",
     303: "conv_lite<3x3 s2 transposed Cin128 Cout32 f32 32x32x2 MFMA>",
     304: "conv_lite<3x3 s2 transposed Cin32 Cout16 f32 16x16x4 MFMA>",
@@ -79,7 +80,8 @@ DTYPE_DESC = {
     "winograd_bf16x6": "fp32-level: the residual convs and the 9x9 start conv (nine 3x3 sub-kernels) as fused Winograd "
                        "F(2x2,3x3) whose transform-domain products are exact 3-piece split-bf16 MFMA terms (each "
                        "fp32 operand = 3 bf16 pieces holding all 24 significant bits, 6 product terms, dropped "
-                       "terms <= 2^-25 of each product, fp32 accumulate); other layers f32 MFMA",
+                       "terms <= 2^-25 of each product, fp32 accumulate); the final 9x9 transposed conv as a GEMM "
+                       "over (kx, co) columns with the same exact split-bf16 products; other layers f32 MFMA",
 }
 
 
@@ -103,6 +105,9 @@ def executed_mfma(model, plan, i: int, B: int):
         return 6 * 2.0 * tiles * 16 * l.cin * l.cout, BF16_MFMA_PEAK_TFLOPS
     if kid == 203:   # 9 sub-kernels x 16 channels + the gathered channel-16 K-step (16 wide), 6 terms
         return 6 * 2.0 * tiles * 16 * (9 * 16 + 16) * l.cout, BF16_MFMA_PEAK_TFLOPS
+    if kid == 204:   # 4 output rows x 128 x' per workgroup tile, N = 32 columns (27 used), K = 9 x 16, 6 terms
+        wg = B * (-(-Ho // 4)) * (-(-Wo // 120))
+        return 6 * 2.0 * wg * 4 * 128 * 32 * 144, BF16_MFMA_PEAK_TFLOPS
     if 101 <= kid < 200:
         terms = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}.get(model.precision, 6)
         return terms * layer_flops(l) * B, BF16_MFMA_PEAK_TFLOPS

@@ -171,6 +171,22 @@ std::vector<float> conv_lite_pack_weights(const LiteTile& t, const float* kern);
 hipError_t conv_lite_launch(const LiteTile& t, const ConvArgs& a, hipStream_t st);
 hipError_t conv_lite_prepare(const LiteTile& t);
 
+// Final 9x9 Conv2DTranspose (16 -> 3) on the bf16 MFMA pipe with exact split-bf16 products (conv_last.hip)
+struct LastArgs {
+    const float* in;        // [B][H][W][16] raw expand output
+    const float2* pro_ab;   // [B][16] CIN affine of the input (+ ReLU), or null (input already applied)
+    const float* w;         // last_x6_pack_weights image
+    const float* bias;      // [3]
+    float* out;             // [B][H][W][3] raw conv output
+    float4* part;           // [B][3][tiles_y * tiles_x] {sum, M2, n}
+    int batch, H, W, cin, tiles_y, tiles_x;
+};
+std::vector<float> last_x6_pack_weights(const float* kern, int cin);
+int last_x6_tiles_y(int H);
+int last_x6_tiles_x(int W);
+hipError_t last_x6_prepare();
+hipError_t last_x6_launch(const LastArgs& a, hipStream_t st);
+
 // CIN statistics finalize: merge per-tile {sum, M2, n} (Chan, f64) -> per-(b,c) affine.
 struct FinalizeArgs {
     const float4* part;      // [B][ntot][n_part]

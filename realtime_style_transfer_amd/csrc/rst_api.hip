@@ -182,6 +182,17 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
     if (s.keras_kind == 1 && s.k == 9 && s.stride == 1) {
         // ---- final 9x9 transposed conv: flip -> correlation, pack [ky][ci][kx][co]
         if (s.cout != 3) return fail(RST_ERR_UNSUPPORTED, "last layer must have 3 channels");
+        if (allow_lite && precision == RST_PRECISION_WINOGRAD_BF16X6 && s.cin == 16) {
+            // bf16 MFMA with exact split products (conv_last.hip)
+            e.kind = K_LASTX6;
+            packed = last_x6_pack_weights(kern, s.cin);
+            bias_n.assign(bias, bias + 3);
+            e.ntot = 3;
+            e.tiles_y = last_x6_tiles_y(s.Ho);
+            e.tiles_x = last_x6_tiles_x(s.Wo);
+            e.n_part = e.tiles_y * e.tiles_x;
+            return RST_OK;
+        }
         e.kind = K_SMALL;
         const int ws = small_conv_weight_stride();
         std::vector<float> w((size_t)9 * s.cin * ws, 0.f);
@@ -455,6 +466,14 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     // kernels with > 64 KB of dynamic LDS need the attribute before any (graph-captured) launch
     for (auto& e : h->layers) {
         if (e.kind == K_SMALL || e.kind == K_WINO9) continue;
+        if (e.kind == K_LASTX6) {
+            const hipError_t pe = last_x6_prepare();
+            if (pe != hipSuccess) {
+                delete h;
+                return fail(RST_ERR_HIP, std::string("last_x6_prepare: ") + hipGetErrorString(pe));
+            }
+            continue;
+        }
         hipError_t pe = e.kind == K_WINO      ? wino_prepare()
                         : e.kind == K_WINOX6  ? wino_x6_prepare()
                         : e.kind == K_WINO9X6 ? wino9_x6_prepare()
@@ -488,7 +507,30 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
     const float2* pro_ab = (e.pro_src >= 0 && e.pro != PRO_NONE) ? h->layers[e.pro_src].d_ab : nullptr;
     const bool blend = two && pro_ab != nullptr;
     const LayerExec* src = e.pro_src >= 0 ? &h->layers[e.pro_src] : nullptr;
-    if (e.kind == K_SMALL) {
+    if (e.kind == K_LASTX6) {
+        LastArgs a{};
+        a.in = in;
+        a.pro_ab = pro_ab;
+        if (blend) {   // no blend prologue: materialise the blended input first (as for the VALU kernel)
+            HIP_TRY(affine_act_blend_launch(in, pro_ab, src->d_ab1, mip_ptr(h, src->out_mip, sw), nullptr, h->d_xlast,
+                                            B, (long)e.s.H * e.s.W, e.s.cin, 1, st));
+            a.in = h->d_xlast;
+            a.pro_ab = nullptr;
+        }
+        if (e.pro != PRO_AFF_RELU && e.pro != PRO_NONE)
+            return fail(RST_ERR_UNSUPPORTED, "last layer prologue must be CIN+ReLU");
+        a.w = e.d_w;
+        a.bias = e.d_bias;
+        a.out = e.d_out;
+        a.part = e.d_part;
+        a.batch = B;
+        a.H = e.s.H;
+        a.W = e.s.W;
+        a.cin = e.s.cin;
+        a.tiles_y = e.tiles_y;
+        a.tiles_x = e.tiles_x;
+        HIP_TRY(last_x6_launch(a, st));
+    } else if (e.kind == K_SMALL) {
         SmallConvArgs a{};
         a.in = in;
         a.pro_ab = pro_ab;
@@ -686,6 +728,7 @@ int rst_layer_kernel_id(const rst_handle* h, int idx) {
         case K_WINOX6: return 202;
         case K_WINO9X6: return 203;
         case K_LITE: return 300 + e.lite.id;
+        case K_LASTX6: return 204;
         default: return e.tile.id;
     }
 }

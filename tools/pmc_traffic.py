@@ -37,6 +37,8 @@ def short_name(k: str) -> str:
         mode, cin, nc = (int(v) for v in m.group(1).split(",")[:3])
         shape = "16x16x4" if nc == 16 else "32x32x2"
         return f"conv_lite<3x3 s2 {'transposed ' if mode else ''}Cin{cin} Cout{nc} f32 {shape} MFMA>"
+    if "last_x6_kernel" in k:
+        return "last_x6<9x9 transposed Cin16 Cout3 as N=(kx,co) split-bf16 x6 MFMA>"
     if "wino9_x6_kernel" in k:
         return "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 16x16 N32 split-bf16 x6 MFMA persistent>"
     if "wino_x6_kernel" in k:
