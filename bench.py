@@ -105,9 +105,8 @@ def executed_mfma(model, plan, i: int, B: int):
         return 6 * 2.0 * tiles * 16 * l.cin * l.cout, BF16_MFMA_PEAK_TFLOPS
     if kid == 203:   # 9 sub-kernels x 16 channels + the gathered channel-16 K-step (16 wide), 6 terms
         return 6 * 2.0 * tiles * 16 * (9 * 16 + 16) * l.cout, BF16_MFMA_PEAK_TFLOPS
-    if kid == 204:   # 4 output rows x 128 x' per workgroup tile, N = 32 columns (27 used), K = 9 x 16, 6 terms
-        wg = B * (-(-Ho // 4)) * (-(-Wo // 120))
-        return 6 * 2.0 * wg * 4 * 128 * 32 * 144, BF16_MFMA_PEAK_TFLOPS
+    if kid == 204:   # per output row and 88-column strip: 3 x' tiles of 32, N = 32 columns (27 used), K = 9 x 16
+        return 6 * 2.0 * B * Ho * (-(-Wo // 88)) * 3 * 32 * 32 * 144, BF16_MFMA_PEAK_TFLOPS
     if 101 <= kid < 200:
         terms = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}.get(model.precision, 6)
         return terms * layer_flops(l) * B, BF16_MFMA_PEAK_TFLOPS

@@ -86,7 +86,12 @@ def _pool_route(tr, B):
 
 # precision: arithmetic of the VGG16 3x3 convs (forward and input gradient) — BASELINE config 4 trains
 # in bf16; "bf16x6" is the exact 3-piece bf16 split (fp32-level products: same errors as fp32, L2 <= 1e-4),
-# "bf16x3" the 2-piece split (16-bit operands: median gradient L2 error 1.5e-3, worst 2.3e-2 measured)
+# "bf16x3" the 2-piece split (16-bit operands). Round 1 measured a 2.26 % L2 deviation on
+# residual_block_0_conv1 and loosened this bound to 5e-2; the cause was not bf16x3 rounding but ReLU
+# routing: a VGG16 pre-activation within rounding distance of 0 was active in the GPU's float32 forward
+# and inactive in the float64 oracle's, which moves every upstream gradient by ~1 %. With the oracle
+# taking its ReLU masks from the GPU activations (relu_route) the worst bf16x3 gradient is 1.4e-4
+# relative L2 (profiles/r02/train_parity_A_bf16x3.json), so the bound is back to 1e-3.
 # "bf16": plain bf16 operands of the VGG16 convs, checked against the float64 oracle run with the same
 # bf16 rounding of every VGG conv's input/kernel (forward) and output gradient/kernel (input gradient).
 # That simulation matches block1_conv2 to 1e-6; beyond it the fp32-vs-float64 activation differences
@@ -98,7 +103,7 @@ def _pool_route(tr, B):
 # (residual-block convs, forward + input gradient, as Winograd F(2x2,3x3): ~1e-6 relative per conv)
 @pytest.mark.parametrize("name,precision,gtol,transfer", [
     ("A", "fp32", 2e-3, "fp32"), ("B", "fp32", 2e-3, "fp32"), ("A", "bf16x6", 2e-3, "fp32"),
-    ("A", "bf16x3", 5e-2, "fp32"), ("A", "bf16", 0.05, "fp32"),
+    ("A", "bf16x3", 1e-3, "fp32"), ("A", "bf16", 0.05, "fp32"),
     ("A", "fp32", 2e-3, "fp32_winograd"), ("B", "fp32", 2e-3, "fp32_winograd"), ("A", "bf16", 0.05, "fp32_winograd")])
 def test_training_step_matches_oracle(name, precision, gtol, transfer):
     _need_gpu()
