@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -46,9 +47,21 @@ __device__ unsigned long long lite_tl[64][4][16][4];
 
 namespace lite {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-template <int MODE, int CIN, int NC, int CKC>
+// (x, y) -> three packed bf16 pairs, x = x0 + x1 + x2 exactly (round-to-nearest-even at each step)
+__device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned& p1, unsigned& p2) {
+    p0 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
+    const float rx = x - __uint_as_float(p0 << 16), ry = y - __uint_as_float(p0 & 0xFFFF0000u);
+    p1 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){rx, ry}, bf16x2));
+    const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xFFFF0000u);
+    p2 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){sx, sy}, bf16x2));
+}
+
+template <int MODE, int CIN, int NC, int CKC, int X6 = 0>
 struct Cfg {
     static constexpr int MS = NC;                           // MFMA M = N = Cout
     static constexpr int TW = MS, TH = 4;                   // GEMM-grid tile: 4 rows x MS pixels
@@ -58,10 +71,14 @@ struct Cfg {
     static constexpr int R = QC / KS;                       // operand reads per slot and chunk
     static constexpr int HR = MODE == 0 ? 2 * TH + 1 : TH + 1;
     static constexpr int HC = MODE == 0 ? 2 * TW + 1 : TW + 1;
+    static constexpr int NPIX = HR * HC;
     static constexpr int CS = CKC + 4;                      // floats per halo pixel (odd 16-B slots)
-    static constexpr int HALO = HR * HC * CS;               // floats per halo buffer
-    static constexpr int WCH = 9 * CKC * NC;                // weight floats per chunk
-        static constexpr int HITEMS = HR * HC * QC;             // float4 items per halo chunk
+    // split-bf16 x6 (MODE 1, Cout 32): halo [piece][16-ch step][k half][pixel][8 bf16], weights
+    // [slot][16-ch step][piece][k half][n][8 bf16] — the 32x32x16 bf16 operand layouts, no padding
+    static constexpr int KS2 = CKC / 16;                    // 16-channel K steps per chunk (x6)
+    static constexpr int HALO = X6 ? 3 * KS2 * 2 * NPIX * 4 : NPIX * CS;   // floats per halo buffer
+    static constexpr int WCH = X6 ? 9 * CKC * NC * 3 / 2 : 9 * CKC * NC;   // floats per chunk of weights
+    static constexpr int HITEMS = HR * HC * QC;             // float4 items per halo chunk
     static constexpr int HREG = (HITEMS + 255) / 256;
     static constexpr int WITEMS = WCH / 4;
     static constexpr int WREG = (WITEMS + 255) / 256;
@@ -71,6 +88,7 @@ struct Cfg {
     static_assert(CIN % CKC == 0 && CKC % (4 * KS) == 0, "chunking");
     static_assert(MS == 16 || MS == 32, "MFMA shape");
     static_assert(((CS / 4) & 1) == 1, "odd 16-B slots per halo pixel");
+    static_assert(!X6 || (MODE == 1 && NC == 32 && CKC % 16 == 0), "x6: transposed, Cout 32");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
@@ -111,10 +129,10 @@ __host__ __device__ constexpr int t_pos(int s) {
 }
 }  // namespace lite
 
-template <int MODE, int CIN, int NC, int CKC, int PRO>
+template <int MODE, int CIN, int NC, int CKC, int PRO, int X6>
 __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles) {
     using namespace lite;
-    using C = Cfg<MODE, CIN, NC, CKC>;
+    using C = Cfg<MODE, CIN, NC, CKC, X6>;
     using M = Mfma<C::MS>;
     typedef typename M::acc_t acc_t;
     constexpr int MS = C::MS, TW = C::TW, TH = C::TH, KS = C::KS, CS = C::CS, HC = C::HC, HR = C::HR, R = C::R;
@@ -201,6 +219,23 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         }
         return v;
     };
+    // x6: channel quad q of the chunk = 16-ch step q >> 2, k half (q >> 1) & 1, bf16 slots 4 (q & 1) .. +3
+    unsigned char* const hbytes = reinterpret_cast<unsigned char*>(halo);
+    const int xq = (((q >> 2) * 2 + ((q >> 1) & 1)) * C::NPIX) * 16 + (q & 1) * 8;   // + piece + pixel
+    constexpr int XPIECE = C::KS2 * 2 * C::NPIX * 16;                                 // bytes per piece plane
+    auto put = [&](int hy, int hx, int lf, f32x4 v) __attribute__((always_inline)) {
+        if constexpr (X6) {
+            unsigned p0[2], p1[2], p2[2];
+            split3(v.x, v.y, p0[0], p1[0], p2[0]);
+            split3(v.z, v.w, p0[1], p1[1], p2[1]);
+            unsigned char* dst = hbytes + xq + (hy * HC + hx) * 16;
+            *reinterpret_cast<uint2*>(dst) = make_uint2(p0[0], p0[1]);
+            *reinterpret_cast<uint2*>(dst + XPIECE) = make_uint2(p1[0], p1[1]);
+            *reinterpret_cast<uint2*>(dst + 2 * XPIECE) = make_uint2(p2[0], p2[1]);
+        } else {
+            *reinterpret_cast<f32x4*>(halo + lf + hy * (HC * CS)) = v;
+        }
+    };
     auto store_step = [&](const Tile& T) __attribute__((always_inline)) {
         const bool okm = T.ix0 + col >= 0 && T.ix0 + col < W;
         const bool oke = T.ix0 + HCM >= 0 && T.ix0 + HCM < W;
@@ -210,12 +245,12 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             const int hy = rsub + RPP * k;
             if (HR % RPP == 0 || k < NMAIN - 1 || hy < HR) {
                 const f32x4 v = okm && row_ok(hy) ? xform(hreg[k], rreg[k]) : f32x4{0.f, 0.f, 0.f, 0.f};
-                *reinterpret_cast<f32x4*>(halo + lcm + hy * (HC * CS)) = v;
+                put(hy, col, lcm, v);
             }
         });
         if (tid < NEXTRA) {
             const f32x4 v = oke && row_ok(ehy) ? xform(hreg[NMAIN], rreg[NMAIN]) : f32x4{0.f, 0.f, 0.f, 0.f};
-            *reinterpret_cast<f32x4*>(halo + lce + ehy * (HC * CS)) = v;
+            put(ehy, HCM, lce, v);
         }
         if constexpr (NCH > 1) {
             sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
@@ -286,8 +321,58 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
         });
     };
+    // x6 (MODE 1, Cout 32): per 16-channel step the 4 operand positions x 3 pieces of A are read once;
+    // the slots walk in phase-interleaved order with B (3 pieces) read one slot ahead; 6 terms per slot
+    auto compute_x6 = [&]() __attribute__((always_inline)) {
+      if constexpr (X6) {   // discarded (not instantiated) for the f32 configurations
+        const unsigned char* wbytes = reinterpret_cast<const unsigned char*>(wts);
+        const int kh = lane >> 5;
+        constexpr int order[9] = {0, 4, 6, 8, 1, 5, 7, 2, 3};
+        constexpr int ap[6] = {0, 0, 1, 0, 1, 2}, bp[6] = {0, 1, 0, 2, 1, 0};
+        sfor<0, C::KS2>([&](auto KSI) __attribute__((always_inline)) {
+            constexpr int ks = decltype(KSI)::value;
+            short8 A[4][3];
+            sfor<0, 4>([&](auto P) __attribute__((always_inline)) {
+                constexpr int pos = decltype(P)::value;
+                const int pix = (wave + (pos >> 1)) * HC + m + (pos & 1);
+                sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
+                    constexpr int pc = decltype(PC)::value;
+                    A[pos][pc] = *reinterpret_cast<const short8*>(hbytes + pc * XPIECE +
+                                                                  ((ks * 2 + kh) * C::NPIX + pix) * 16);
+                });
+            });
+            auto readB = [&](int sl, short8 (&Bv)[3]) __attribute__((always_inline)) {
+                sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
+                    constexpr int pc = decltype(PC)::value;
+                    Bv[pc] = *reinterpret_cast<const short8*>(wbytes + ((((sl * C::KS2 + ks) * 3 + pc) * 2 + kh) * 32 + m) * 16);
+                });
+            };
+            short8 B0[3], B1[3];
+            readB(order[0], B0);
+            sfor<0, 9>([&](auto J) __attribute__((always_inline)) {
+                constexpr int j = decltype(J)::value, sl = order[j];
+                constexpr int ai = (sl == 1 || sl == 3) ? 4 : t_phase(sl), pos = t_pos(sl);
+                if constexpr (j + 1 < 9) {
+                    if constexpr ((j & 1) == 0) readB(order[j + 1], B1);
+                    else readB(order[j + 1], B0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                sfor<0, 6>([&](auto T6) __attribute__((always_inline)) {
+                    constexpr int t6 = decltype(T6)::value;
+                    if constexpr ((j & 1) == 0)
+                        acc[ai] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[pos][ap[t6]], B0[bp[t6]], acc[ai], 0, 0, 0);
+                    else
+                        acc[ai] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[pos][ap[t6]], B1[bp[t6]], acc[ai], 0, 0, 0);
+                });
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        });
+      }
+    };
     auto compute = [&]() __attribute__((always_inline)) {
-        if constexpr ((LITE_SKIP & 2) == 0) {
+        if constexpr (X6) {
+            if constexpr ((LITE_SKIP & 2) == 0) compute_x6();
+        } else if constexpr ((LITE_SKIP & 2) == 0) {
             f32x4 A0[NA], B0[NB], A1[NA], B1[NB];
             read_step(std::integral_constant<int, 0>{}, A0, B0);
             sfor<0, NSTEP>([&](auto U) __attribute__((always_inline)) {
@@ -433,28 +518,74 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
 // host side: the instantiated layer shapes
 // ------------------------------------------------------------------------------------------------
 #define RST_LITE_CONFIGS(X)        \
-    X(1, 0, 32, 16, 32)            \
-    X(2, 0, 16, 32, 16)            \
-    X(3, 1, 128, 32, 32)           \
-    X(4, 1, 32, 16, 32)
+    X(1, 0, 32, 16, 32, 0)         \
+    X(2, 0, 16, 32, 16, 0)         \
+    X(3, 1, 128, 32, 32, 0)        \
+    X(4, 1, 32, 16, 32, 0)         \
+    X(5, 1, 128, 32, 32, 1)
 
-bool conv_lite_select(int keras_kind, int k, int stride, int cin, int cout, LiteTile* t) {
+bool conv_lite_select(int keras_kind, int k, int stride, int cin, int cout, bool x6, LiteTile* t) {
     if (k != 3 || stride != 2) return false;
-#define X(ID, MODE, CIN, NC, CKC)                                                  \
-    if (keras_kind == MODE && cin == CIN && cout == NC) {                          \
-        using C = lite::Cfg<MODE, CIN, NC, CKC>;                                   \
-        t->id = ID; t->mode = MODE; t->cin = CIN; t->nc = NC; t->ckc = CKC;        \
-        t->th = C::TH; t->tw = C::TW; t->lds_bytes = (int)C::LDS_BYTES;            \
-        return true;                                                               \
-    }
-    RST_LITE_CONFIGS(X)
+    // split-bf16 x6 where an instantiation exists (expand_0), the f32 form otherwise
+    for (int pass = x6 ? 1 : 0; pass >= 0; --pass) {
+#define X(ID, MODE, CIN, NC, CKC, X6)                                              \
+        if (X6 == pass && keras_kind == MODE && cin == CIN && cout == NC) {            \
+            using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;                               \
+            t->id = ID; t->mode = MODE; t->cin = CIN; t->nc = NC; t->ckc = CKC;        \
+            t->th = C::TH; t->tw = C::TW; t->lds_bytes = (int)C::LDS_BYTES; t->x6 = X6; \
+            return true;                                                               \
+        }
+        RST_LITE_CONFIGS(X)
 #undef X
+    }
     return false;
 }
 
 // weights: Conv2D HWIO [ky][kx][ci][co]; Conv2DTranspose [ky][kx][co][ci] (Keras layouts) ->
 // [chunk][slot][r][kslot][n][4], the LDS image of one chunk
+static uint16_t lite_bf16_rne(float x) {
+    uint32_t u;
+    std::memcpy(&u, &x, 4);
+    return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+static float lite_bf16_val(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+static float lite_slot_weight(const LiteTile& t, const float* kern, int s, int ci, int n) {
+    if (t.mode == 0) return kern[((size_t)s * t.cin + ci) * t.nc + n];
+    const int ph = lite::t_phase(s), pos = lite::t_pos(s);
+    const int py = ph >> 1, px = ph & 1, tyy = pos >> 1, txx = pos & 1;
+    const int ky = py + 2 * (1 - tyy), kx = px + 2 * (1 - txx);
+    return kern[(((size_t)ky * 3 + kx) * t.nc + n) * t.cin + ci];
+}
+
 std::vector<float> conv_lite_pack_weights(const LiteTile& t, const float* kern) {
+    if (t.x6) {   // [chunk][slot][16-ch step][piece][k half][n][8] bf16, each weight split into 3 RNE pieces
+        const int nch = t.cin / t.ckc, ks2 = t.ckc / 16;
+        std::vector<uint16_t> img((size_t)nch * 9 * ks2 * 3 * 2 * t.nc * 8);
+        size_t idx = 0;
+        for (int ch = 0; ch < nch; ++ch)
+            for (int s = 0; s < 9; ++s)
+                for (int k2 = 0; k2 < ks2; ++k2)
+                    for (int pc = 0; pc < 3; ++pc)
+                        for (int kh = 0; kh < 2; ++kh)
+                            for (int n = 0; n < t.nc; ++n)
+                                for (int e = 0; e < 8; ++e) {
+                                    const float v = lite_slot_weight(t, kern, s, ch * t.ckc + k2 * 16 + kh * 8 + e, n);
+                                    uint16_t p[3];
+                                    p[0] = lite_bf16_rne(v);
+                                    const float r = v - lite_bf16_val(p[0]);
+                                    p[1] = lite_bf16_rne(r);
+                                    p[2] = lite_bf16_rne(r - lite_bf16_val(p[1]));
+                                    img[idx++] = p[pc];
+                                }
+        std::vector<float> out(img.size() / 2);
+        std::memcpy(out.data(), img.data(), img.size() * 2);
+        return out;
+    }
     const int ks = 64 / t.nc, nch = t.cin / t.ckc, R = t.ckc / 4 / ks;
     std::vector<float> out((size_t)nch * 9 * t.ckc * t.nc);
     size_t idx = 0;
@@ -516,13 +647,13 @@ static int lite_cu_count() {
     return n_cu;
 }
 
-template <int MODE, int CIN, int NC, int CKC, int PRO>
+template <int MODE, int CIN, int NC, int CKC, int PRO, int X6>
 static int lite_slots() {
     static int slots = 0;
     if (slots == 0) {
-        using C = lite::Cfg<MODE, CIN, NC, CKC>;
+        using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_lite_kernel<MODE, CIN, NC, CKC, PRO>, 256,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6>, 256,
                                                          C::LDS_BYTES) != hipSuccess || per_cu <= 0)
             per_cu = 1;
         slots = ((lite_cu_count() * per_cu) / 8) * 8;
@@ -531,49 +662,50 @@ static int lite_slots() {
     return slots;
 }
 
-template <int MODE, int CIN, int NC, int CKC, int PRO>
+template <int MODE, int CIN, int NC, int CKC, int PRO, int X6>
 static void lite_launch_pro(const ConvArgs& a, int n_tiles, hipStream_t st) {
-    using C = lite::Cfg<MODE, CIN, NC, CKC>;
-    const int grid = std::min(n_tiles, lite_slots<MODE, CIN, NC, CKC, PRO>());
-    hipLaunchKernelGGL((conv_lite_kernel<MODE, CIN, NC, CKC, PRO>), dim3(grid), dim3(256), C::LDS_BYTES, st, a, n_tiles);
+    using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
+    const int grid = std::min(n_tiles, lite_slots<MODE, CIN, NC, CKC, PRO, X6>());
+    hipLaunchKernelGGL((conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6>), dim3(grid), dim3(256), C::LDS_BYTES, st, a,
+                       n_tiles);
 }
 
-template <int MODE, int CIN, int NC, int CKC>
+template <int MODE, int CIN, int NC, int CKC, int X6>
 static hipError_t lite_launch_cfg(const ConvArgs& a, hipStream_t st) {
-    using C = lite::Cfg<MODE, CIN, NC, CKC>;
+    using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
     if (a.cin != CIN || a.cout != NC || a.tiles_y != (a.Ho + C::TH - 1) / C::TH ||
         a.tiles_x != (a.Wo + C::TW - 1) / C::TW || (size_t)a.batch * a.H * a.W * CIN >= ((size_t)1 << 31))
         return hipErrorInvalidValue;   // 32-bit staging offsets
     const int n_tiles = a.batch * a.tiles_y * a.tiles_x;
     switch (a.pro_mode) {
-        case PRO_NONE: lite_launch_pro<MODE, CIN, NC, CKC, PRO_NONE>(a, n_tiles, st); break;
-        case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU>(a, n_tiles, st); break;
-        case PRO_AFF_RES: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES>(a, n_tiles, st); break;
+        case PRO_NONE: lite_launch_pro<MODE, CIN, NC, CKC, PRO_NONE, X6>(a, n_tiles, st); break;
+        case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>(a, n_tiles, st); break;
+        case PRO_AFF_RES: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>(a, n_tiles, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-template <int MODE, int CIN, int NC, int CKC>
+template <int MODE, int CIN, int NC, int CKC, int X6>
 static hipError_t lite_prepare_cfg() {
-    using C = lite::Cfg<MODE, CIN, NC, CKC>;
-    for (const void* k : {(const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_NONE>,
-                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU>,
-                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES>}) {
+    using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
+    for (const void* k : {(const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_NONE, X6>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES);
         if (e != hipSuccess) return e;
     }
     // occupancy queries outside any graph capture
-    lite_slots<MODE, CIN, NC, CKC, PRO_NONE>();
-    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU>();
-    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_NONE, X6>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>();
     return hipSuccess;
 }
 
 hipError_t conv_lite_launch(const LiteTile& t, const ConvArgs& a, hipStream_t st) {
     switch (t.id) {
-#define X(ID, MODE, CIN, NC, CKC) \
-    case ID: return lite_launch_cfg<MODE, CIN, NC, CKC>(a, st);
+#define X(ID, MODE, CIN, NC, CKC, X6) \
+    case ID: return lite_launch_cfg<MODE, CIN, NC, CKC, X6>(a, st);
         RST_LITE_CONFIGS(X)
 #undef X
         default: return hipErrorInvalidValue;
@@ -582,8 +714,8 @@ hipError_t conv_lite_launch(const LiteTile& t, const ConvArgs& a, hipStream_t st
 
 hipError_t conv_lite_prepare(const LiteTile& t) {
     switch (t.id) {
-#define X(ID, MODE, CIN, NC, CKC) \
-    case ID: return lite_prepare_cfg<MODE, CIN, NC, CKC>();
+#define X(ID, MODE, CIN, NC, CKC, X6) \
+    case ID: return lite_prepare_cfg<MODE, CIN, NC, CKC, X6>();
         RST_LITE_CONFIGS(X)
 #undef X
         default: return hipErrorInvalidValue;

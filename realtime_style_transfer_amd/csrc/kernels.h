@@ -165,8 +165,9 @@ int small_conv_weight_stride();
 // for conv_mfma; the transposed form writes one {sum, M2, n} per (tile, channel), phases merged.
 struct LiteTile {
     int id, mode, cin, nc, ckc, th, tw, lds_bytes;
+    int x6;                 // 1: split-bf16 x6 operands on the bf16 MFMA pipe (fp32-level products)
 };
-bool conv_lite_select(int keras_kind, int k, int stride, int cin, int cout, LiteTile* t);
+bool conv_lite_select(int keras_kind, int k, int stride, int cin, int cout, bool x6, LiteTile* t);
 std::vector<float> conv_lite_pack_weights(const LiteTile& t, const float* kern);
 hipError_t conv_lite_launch(const LiteTile& t, const ConvArgs& a, hipStream_t st);
 hipError_t conv_lite_prepare(const LiteTile& t);

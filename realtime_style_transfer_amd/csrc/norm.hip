@@ -15,10 +15,41 @@ namespace rst {
 
 constexpr int FIN_THREADS = 512;
 
+// Sum over the 64 lanes of a wave, every lane ends with the same value, fixed order (deterministic):
+// DPP butterflies inside each 16-lane row (quad xor 1, xor 2, half-row mirror, row mirror) on each
+// 32-bit half, then the four row sums read out of lanes 0/16/32/48. VALU only: the ds_bpermute chain of
+// __shfl_xor (6 dependent LDS round trips per value) was most of a residual finalize's 3.6 us.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xFFFFFFFFll), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ float lane_read(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double lane_read(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFFll), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+    v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_f<0x141>(v);   // row_half_mirror
+    v += dpp_f<0x140>(v);   // row_mirror
+    return (lane_read(v, 0) + lane_read(v, 16)) + (lane_read(v, 32) + lane_read(v, 48));
+}
+
 template <int NT, typename T>
 __device__ __forceinline__ T block_sum(T v, T* scratch) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);   // a + b == b + a: every lane ends equal
+    v = wave_sum(v);
     if constexpr (NT == 64) {
         return v;
     } else {

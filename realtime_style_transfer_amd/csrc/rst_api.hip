@@ -239,7 +239,8 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         e.tiles_y = wino_tiles_y(s.Ho);
         e.tiles_x = wino_tiles_x(s.Wo);
         e.n_part = e.tiles_y * e.tiles_x;
-    } else if (allow_lite && conv_lite_select(s.keras_kind, s.k, s.stride, s.cin, s.cout, &e.lite) &&
+    } else if (allow_lite && conv_lite_select(s.keras_kind, s.k, s.stride, s.cin, s.cout,
+                                              precision == RST_PRECISION_WINOGRAD_BF16X6, &e.lite) &&
                (s.keras_kind == 0 ? (s.norm == N_BN && s.conv_relu) : (s.norm == N_CIN && !s.conv_relu))) {
         // ---- narrow 3x3 s2 conv / transposed conv: exact f32 MFMA, no idle columns, no zero taps
         e.kind = K_LITE;
@@ -727,7 +728,7 @@ int rst_layer_kernel_id(const rst_handle* h, int idx) {
         case K_WINO9: return 201;
         case K_WINOX6: return 202;
         case K_WINO9X6: return 203;
-        case K_LITE: return 300 + e.lite.id;
+        case K_LITE: return 300 + e.lite.id;   // 305: the x6 expand_0 form
         case K_LASTX6: return 204;
         default: return e.tile.id;
     }

@@ -7,6 +7,9 @@
 #include <cstdlib>
 #include <vector>
 
+#ifndef LITE_X6
+#define LITE_X6 0
+#endif
 #include "../realtime_style_transfer_amd/csrc/conv_lite.hip"
 
 using namespace rst;
@@ -38,7 +41,7 @@ int main(int argc, char** argv) {
     for (int B : {1, 8})
         for (const Shape& s : shapes) {
             LiteTile t{};
-            if (!conv_lite_select(s.kind, 3, 2, s.cin, s.cout, &t)) { printf("no tile for %s\n", s.name); return 1; }
+            if (!conv_lite_select(s.kind, 3, 2, s.cin, s.cout, LITE_X6 != 0, &t)) { printf("no tile for %s\n", s.name); return 1; }
             CK(conv_lite_prepare(t));
             const int Ho = s.kind == 0 ? (s.H + 1) / 2 : s.H, Wo = s.kind == 0 ? (s.W + 1) / 2 : s.W;
             const size_t nin = (size_t)B * s.H * s.W * s.cin;

@@ -34,7 +34,10 @@ def short_name(k: str) -> str:
         return CONFIG_NAMES.get(args[:5], "conv_mfma<" + ",".join(map(str, args)) + ">")
     m = re.search(r"conv_lite_kernel<([^>]*)>", k)
     if m:
-        mode, cin, nc = (int(v) for v in m.group(1).split(",")[:3])
+        f = [int(v) for v in m.group(1).split(",")]
+        mode, cin, nc = f[:3]
+        if len(f) > 5 and f[5]:
+            return f"conv_lite<3x3 s2 transposed Cin{cin} Cout{nc} split-bf16 x6 32x32x16 MFMA>"
         shape = "16x16x4" if nc == 16 else "32x32x2"
         return f"conv_lite<3x3 s2 {'transposed ' if mode else ''}Cin{cin} Cout{nc} f32 {shape} MFMA>"
     if "last_x6_kernel" in k:
