@@ -30,7 +30,7 @@
 #include "kernels.h"
 
 #ifndef LITE_SKIP
-#define LITE_SKIP 0   // tools/lite_bench knobs: 1 no halo loads, 2 no MFMAs, 4 no weight loads
+#define LITE_SKIP 0   // tools/lite_bench knobs: 1 no halo loads, 2 no MFMAs, 8 no output stores, 32 no statistics
 #endif
 
 namespace rst {
@@ -176,8 +176,12 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     static_assert(256 % TPR == 0 && NEXTRA <= 256, "staging map");
     const int q = tid % QC, col = (tid / QC) % HCM, rsub = tid / TPR, ehy = min(tid / QC, HR - 1);
     const int lcm = halo_off(0, col) + 4 * q, lce = halo_off(0, HCM) + 4 * q;
-    f32x4 hreg[NMAIN + 1], rreg[NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01, pa23;
-    auto load_step = [&](const Tile& T, int ch) __attribute__((always_inline)) {
+    // two register sets of staged input (single-chunk layers prefetch two tiles ahead: the HBM latency
+    // under load exceeds one tile's MFMAs); multi-chunk layers use set 0 only
+    constexpr int NSET = NCH == 1 ? 2 : 1;
+    f32x4 hreg[NSET][NMAIN + 1], rreg[NSET][NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01[NSET], pa23[NSET];
+    auto load_step = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {
+        constexpr int st = decltype(SET)::value;
         const int co = ch * CKC;
         const int ixm = min(max(T.ix0 + col, 0), W - 1), ixe = min(max(T.ix0 + HCM, 0), W - 1);
         const int rb = T.b * H;
@@ -186,16 +190,16 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             const int hy = k < NMAIN ? min(rsub + RPP * k, HR - 1) : ehy;
             const int gi = ((rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)) * CIN + co + 4 * q;
 #if LITE_SKIP & 1
-            hreg[k] = f32x4{(float)gi, 0.f, 0.f, 0.f};
+            hreg[st][k] = f32x4{(float)gi, 0.f, 0.f, 0.f};
 #else
-            hreg[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
-            if constexpr (PRO == PRO_AFF_RES) rreg[k] = *reinterpret_cast<const f32x4*>(a.res + gi);
+            hreg[st][k] = *reinterpret_cast<const f32x4*>(a.in + gi);
+            if constexpr (PRO == PRO_AFF_RES) rreg[st][k] = *reinterpret_cast<const f32x4*>(a.res + gi);
 #endif
         });
         if constexpr (PRO != PRO_NONE) {
             const f32x4* pa = reinterpret_cast<const f32x4*>(a.pro_ab + (size_t)T.b * CIN + co + 4 * q);
-            pa01 = pa[0];
-            pa23 = pa[1];
+            pa01[st] = pa[0];
+            pa23[st] = pa[1];
         }
         if constexpr (NCH > 1) {
             sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
@@ -205,12 +209,12 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             });
         }
     };
-    auto xform = [&](f32x4 v, f32x4 r) __attribute__((always_inline)) {
+    auto xform = [&](f32x4 v, f32x4 r, const f32x4& p01, const f32x4& p23) __attribute__((always_inline)) {
         if constexpr (PRO != PRO_NONE) {
-            v.x = fmaf(pa01.x, v.x, pa01.y);
-            v.y = fmaf(pa01.z, v.y, pa01.w);
-            v.z = fmaf(pa23.x, v.z, pa23.y);
-            v.w = fmaf(pa23.z, v.w, pa23.w);
+            v.x = fmaf(p01.x, v.x, p01.y);
+            v.y = fmaf(p01.z, v.y, p01.w);
+            v.z = fmaf(p23.x, v.z, p23.y);
+            v.w = fmaf(p23.z, v.w, p23.w);
             if constexpr (PRO == PRO_AFF_RELU) {
                 v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
             } else if constexpr (PRO == PRO_AFF_RES) {
@@ -236,7 +240,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             *reinterpret_cast<f32x4*>(halo + lf + hy * (HC * CS)) = v;
         }
     };
-    auto store_step = [&](const Tile& T) __attribute__((always_inline)) {
+    auto store_step = [&](const Tile& T, auto SET) __attribute__((always_inline)) {
+        constexpr int st = decltype(SET)::value;
         const bool okm = T.ix0 + col >= 0 && T.ix0 + col < W;
         const bool oke = T.ix0 + HCM >= 0 && T.ix0 + HCM < W;
         auto row_ok = [&](int hy) __attribute__((always_inline)) { return T.iy0 + hy >= 0 && T.iy0 + hy < H; };
@@ -244,12 +249,14 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             constexpr int k = decltype(K)::value;
             const int hy = rsub + RPP * k;
             if (HR % RPP == 0 || k < NMAIN - 1 || hy < HR) {
-                const f32x4 v = okm && row_ok(hy) ? xform(hreg[k], rreg[k]) : f32x4{0.f, 0.f, 0.f, 0.f};
+                const f32x4 v = okm && row_ok(hy) ? xform(hreg[st][k], rreg[st][k], pa01[st], pa23[st])
+                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
                 put(hy, col, lcm, v);
             }
         });
         if (tid < NEXTRA) {
-            const f32x4 v = oke && row_ok(ehy) ? xform(hreg[NMAIN], rreg[NMAIN]) : f32x4{0.f, 0.f, 0.f, 0.f};
+            const f32x4 v = oke && row_ok(ehy) ? xform(hreg[st][NMAIN], rreg[st][NMAIN], pa01[st], pa23[st])
+                                               : f32x4{0.f, 0.f, 0.f, 0.f};
             put(ehy, HCM, lce, v);
         }
         if constexpr (NCH > 1) {
@@ -422,7 +429,9 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         const int qq = T.x0 + M::row(j, lane);
                         const float v = acc[ph][j] + bias;
                         acc[ph][j] = v;
+#if (LITE_SKIP & 8) == 0
                         orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
+#endif
                         s += v;
                     }
                 cnt = 4.f * C::NACC;
@@ -441,7 +450,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         }
                     }
             }
-            if (a.part != nullptr) {
+            if (a.part != nullptr && (LITE_SKIP & 32) == 0) {
                 // lanes n, n + MS, ... hold column n: reduce over them, then over the 4 waves (fixed order)
 #pragma unroll
                 for (int o = MS; o < 64; o <<= 1) {
@@ -486,31 +495,75 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             reinterpret_cast<f32x4*>(wts)[it] = reinterpret_cast<const f32x4*>(a.wpk)[it];
     }
     const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int n_steps = my_tiles * NCH;
-    Tile cur = tile_of(0);
-    load_step(cur, 0);
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, NSET - 1>;
     zero_acc();
-    for (int s = 0; s < n_steps; ++s) {
-        const int ch = s % NCH;
-        LTL(s, 0);
-        if (s > 0) lds_barrier();        // the previous step's operand reads are done
-        store_step(cur);
-        lds_barrier();
-        LTL(s, 1);
-        Tile nxt = cur;
-        if (s + 1 < n_steps) {
-            const int ch1 = (s + 1) % NCH;
-            if (ch1 == 0) nxt = tile_of((s + 1) / NCH);
-            load_step(nxt, ch1);
+    if constexpr (NCH == 1) {
+        // tile k's input sits in register set k & 1, loaded two tiles ahead
+        Tile T0 = tile_of(0), T1 = T0;
+        load_step(T0, 0, S0{});
+        if (my_tiles > 1) {
+            T1 = tile_of(1);
+            load_step(T1, 0, S1{});
         }
-        compute();
-        LTL(s, 2);
-        if (ch == NCH - 1) {
-            epilogue(cur);
+        for (int k = 0; k < my_tiles; k += 2) {
+            LTL(k, 0);
+            if (k > 0) lds_barrier();
+            store_step(T0, S0{});
+            lds_barrier();
+            LTL(k, 1);
+            Tile T2 = T0;
+            if (k + 2 < my_tiles) {
+                T2 = tile_of(k + 2);
+                load_step(T2, 0, S0{});
+            }
+            compute();
+            LTL(k, 2);
+            epilogue(T0);
             zero_acc();
+            LTL(k, 3);
+            if (k + 1 < my_tiles) {
+                lds_barrier();
+                store_step(T1, S1{});
+                lds_barrier();
+                Tile T3 = T1;
+                if (k + 3 < my_tiles) {
+                    T3 = tile_of(k + 3);
+                    load_step(T3, 0, S1{});
+                }
+                compute();
+                epilogue(T1);
+                zero_acc();
+                T1 = T3;
+            }
+            T0 = T2;
         }
-        LTL(s, 3);
-        cur = nxt;
+    } else {
+        const int n_steps = my_tiles * NCH;
+        Tile cur = tile_of(0);
+        load_step(cur, 0, S0{});
+        for (int s = 0; s < n_steps; ++s) {
+            const int ch = s % NCH;
+            LTL(s, 0);
+            if (s > 0) lds_barrier();        // the previous step's operand reads are done
+            store_step(cur, S0{});
+            lds_barrier();
+            LTL(s, 1);
+            Tile nxt = cur;
+            if (s + 1 < n_steps) {
+                const int ch1 = (s + 1) % NCH;
+                if (ch1 == 0) nxt = tile_of((s + 1) / NCH);
+                load_step(nxt, ch1, S0{});
+            }
+            compute();
+            LTL(s, 2);
+            if (ch == NCH - 1) {
+                epilogue(cur);
+                zero_acc();
+            }
+            LTL(s, 3);
+            cur = nxt;
+        }
     }
 }
 

@@ -92,7 +92,7 @@ __device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned&
 #endif
 #ifdef X6_PROF
 // timeline per (workgroup, wave) on the constant 100 MHz clock: start, pipeline filled, chunk loop done, end
-__device__ unsigned long long x6_tl[X6_PROF][4][4];
+__device__ unsigned long long x6_tl[X6_PROF][8][4];
 #define XTL(k) \
     if (blockIdx.x < X6_PROF && lane == 0) x6_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -511,15 +511,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 #ifdef X6_PROF
 // timeline summary of the most recent launch (tools/wino_x6_bench)
-void x6_timeline_print(int nwg) {
-    std::vector<unsigned long long> tl((size_t)X6_PROF * 16);
+void x6_timeline_print(int nwg, int nwave) {
+    std::vector<unsigned long long> tl((size_t)X6_PROF * 32);
     if (hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(x6_tl), tl.size() * 8) != hipSuccess) return;
     if (nwg > X6_PROF) nwg = X6_PROF;
     unsigned long long t0 = ~0ull, tend = 0, slast = 0;
     double fill = 0, loop = 0, epi = 0;
     for (int g = 0; g < nwg; ++g)
-        for (int w = 0; w < 4; ++w) {
-            const unsigned long long* q = &tl[((size_t)g * 4 + w) * 4];
+        for (int w = 0; w < nwave; ++w) {
+            const unsigned long long* q = &tl[((size_t)g * 8 + w) * 4];
             t0 = q[0] < t0 ? q[0] : t0;
             tend = q[3] > tend ? q[3] : tend;
             slast = q[0] > slast ? q[0] : slast;
@@ -527,7 +527,7 @@ void x6_timeline_print(int nwg) {
             loop += (double)(q[2] - q[1]);
             epi += (double)(q[3] - q[2]);
         }
-    const double nw = nwg * 4.0;
+    const double nw = nwg * (double)nwave;
     printf("  timeline (us): first start -> last end %.2f, last start +%.2f; per wave: fill %.2f, loop %.2f, "
            "epilogue %.2f\n", (tend - t0) * 0.01, (slast - t0) * 0.01, fill / nw * 0.01, loop / nw * 0.01,
            epi / nw * 0.01);
@@ -556,6 +556,382 @@ void x6_points_print(int nwg, int nchunks) {
     printf(" | barrier+top %.0f | chunk %.0f\n", bar / n, tot + bar / n);
 }
 #endif
+
+// ============================================================================================================
+// Two-waves-per-SIMD form (the launched one). The single-wave kernel above keeps every transform point of a
+// 32-channel slice in one wave (256 accumulator registers, one wave per SIMD), so the transform / split VALU
+// of the next chunk can only fill the gaps of that same wave's MFMA chain and its dependent VALU chains
+// stall the matrix pipe (per-point stamps: the transform points ran 405 vs 240 ticks without it). Here a
+// workgroup has 8 waves: wave (g, h) owns output channels [32g, 32g+32) and the transform points of rows
+// p = 2h, 2h+1 (points 8h .. 8h+7, 128 accumulator registers), so the two waves of a SIMD interleave and one
+// wave's VALU issues while the other's MFMAs run. The input transform is split the same way (thread half h
+// computes rows 2h, 2h+1 of B^T d, from three of the four patch rows). Epilogue: each half forms its partial
+// output transform (Y = A^T M A is linear in the points) into an LDS image [pixel][channel], then all 512
+// threads add the two halves, apply bias + ReLU and store whole pixels' channel quads (1 KB per wave
+// instruction instead of 64 scattered 4-B stores per lane), and reduce the per-channel statistics.
+#ifndef X6W_RING
+#define X6W_RING 2
+#endif
+
+constexpr int YT = 512;                             // threads per workgroup (8 waves)
+constexpr int YPT = 8;                              // transform points per wave
+constexpr int YST = (XPF4 + YT - 1) / YT;           // 2 staging float4 per thread
+constexpr int YRING = X6W_RING;                     // U register ring (points in flight), divides 8
+constexpr int YSTR = 132;                           // epilogue image row stride (floats): lh halves 32 banks apart
+constexpr size_t YIMG_BYTES = (size_t)2 * 128 * YSTR * 4;
+constexpr size_t YEPI_BYTES = YIMG_BYTES + 2 * 8 * 32 * 16;
+constexpr size_t YLDS_BYTES = XLDS_BYTES > YEPI_BYTES ? XLDS_BYTES : YEPI_BYTES;
+static_assert(8 % YRING == 0, "ring must divide the points per wave");
+
+template <int PRO>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_x6w_kernel(WinoArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* const patch = smem;                                            // [2][180][24] f32
+    unsigned char* const vbytes = reinterpret_cast<unsigned char*>(smem + 2 * XPATCH_FL);   // [2][3][16][32][32 B]
+    float2* const pab = reinterpret_cast<float2*>(vbytes + 2 * XV_BYTES);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    const int g = wave & 3, h = wave >> 2;   // output channel group, transform-point half
+    XTL(0);
+    int bid = xcd_tile_order(blockIdx.x, gridDim.x);
+    const int tx = bid % a.tiles_x;
+    bid /= a.tiles_x;
+    const int ty = bid % a.tiles_y;
+    const int b = bid / a.tiles_y;
+    const int y0 = ty * XTH, x0 = tx * XTW;
+    const int H = a.H, W = a.W, Cin = a.cin;
+    constexpr int pro = PRO;
+    const size_t img = (size_t)b * H * W;
+    const float* res_src = pro == PRO_AFF_RES ? a.res : a.in;
+    const int nchunks = Cin / XCK;
+
+    if constexpr (pro != PRO_NONE) {
+        for (int c = tid; c < Cin; c += YT) pab[c] = a.pro_ab[(size_t)b * Cin + c];
+    }
+
+    // ---- staging descriptors (item k = float4 tid + 512k of a chunk's 720-float4 patch), as above --------
+    int sg_goff[YST], sg_lf[YST], sg_moff[YST];
+#pragma unroll
+    for (int k = 0; k < YST; ++k) {
+        const int it = tid + k * YT, itc = min(it, XPF4 - 1);
+        const int px = itc >> 2, q = itc & 3;
+        const int iy = y0 - 1 + px / XPW, ix = x0 - 1 + px % XPW;
+        const int cy = min(max(iy, 0), H - 1), cx = min(max(ix, 0), W - 1);
+        sg_goff[k] = (int)((img + (size_t)cy * W + cx) * Cin) + 4 * q;
+        const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
+        const int loff = it < XPF4 ? px * XPS + 4 * q : ((it - XPF4) >> 2) * XPS + XCK + 4 * (q & 1);
+        sg_lf[k] = loff | (inside ? 1 << 16 : 0);
+        const bool interior = it < XPF4 && inside && iy >= y0 && iy < y0 + XTH && ix >= x0 && ix < x0 + XTW;
+        sg_moff[k] = interior ? (int)(((img + (size_t)iy * W + ix) * Cin + 4 * q) * 4) : 0x7F000000;
+    }
+    const __amdgpu_buffer_rsrc_t msrd = __builtin_amdgcn_make_buffer_rsrc(
+        a.mat, 0, a.mat != nullptr ? (int)((size_t)a.batch * H * W * Cin * 4) : 0, 0x00020000);
+    f32x4 xr[YST], rr[YST];
+#pragma unroll
+    for (int k = 0; k < YST; ++k) rr[k] = xr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int k, int chunk) __attribute__((always_inline)) {
+        const int gi = sg_goff[k] + chunk * XCK;
+        xr[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
+        if constexpr (pro == PRO_AFF_RES) rr[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
+    };
+    // prologue of the staged value (affine [+ ReLU | + residual]) and the materialised block output
+    auto stage_math = [&](int k, int chunk, f32x4 p01, f32x4 p23) __attribute__((always_inline)) {
+        f32x4 v = xr[k];
+        if constexpr (pro != PRO_NONE) {
+            const f32x4 r = rr[k];
+            v.x = pro_apply(pro, v.x, float2{p01.x, p01.y}, r.x);
+            v.y = pro_apply(pro, v.y, float2{p01.z, p01.w}, r.y);
+            v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
+            v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
+            if (a.mat != nullptr)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd,
+                                                       sg_moff[k] + chunk * XCK * 4, 0, 0);
+        }
+        return v;
+    };
+    auto stage_write = [&](int k, float* pbuf, f32x4 v) __attribute__((always_inline)) {
+        const bool inside = (sg_lf[k] >> 16) != 0;
+        v.x = inside ? v.x : 0.f;
+        v.y = inside ? v.y : 0.f;
+        v.z = inside ? v.z : 0.f;
+        v.w = inside ? v.w : 0.f;
+        *reinterpret_cast<f32x4*>(pbuf + (sg_lf[k] & 0xFFFF)) = v;
+    };
+    const int cq4 = 4 * (tid & 3);   // channel quad of every staging item of this thread
+    auto stage_all = [&](int chunk, float* pbuf) __attribute__((always_inline)) {
+        sfor<0, YST>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            f32x4 p01 = f32x4{0.f, 0.f, 0.f, 0.f}, p23 = p01;
+            if constexpr (pro != PRO_NONE) {
+                p01 = *reinterpret_cast<const f32x4*>(pab + chunk * XCK + cq4);
+                p23 = *reinterpret_cast<const f32x4*>(pab + chunk * XCK + cq4 + 2);
+            }
+            stage_write(k, pbuf, stage_math(k, chunk, p01, p23));
+        });
+    };
+
+    // ---- U pieces: lane (li, lh) of wave (g, h) reads U[chunk][8h + x][piece][32g + li][8lh .. 8lh+7] ------
+    const __amdgpu_buffer_rsrc_t usrd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.U), 0, nchunks * XXI * 3 * XN * XVROW, 0x00020000);
+    const int uvoff = (g * 32 + li) * XVROW + 16 * lh;
+    short8 ur[YRING][3];
+    auto load_u1 = [&](int chunk, int x, int s, int p) __attribute__((always_inline)) {
+        ur[s][p] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 usrd, uvoff, ((chunk * XXI + 8 * h + x) * 3 + p) * (XN * XVROW), 0));
+    };
+
+    // ---- input transform + split: thread = (half h, tile tt, channel pair cp) --------------------------
+    // Rows 2h, 2h+1 of B^T d from patch rows f0, f1, f2 = (d0, d2, d1) for h = 0, (d2, d1, d3) for h = 1:
+    // row 2h = f0 - f1, row 2h+1 = f1 + sgn f2 (sgn = +1 / -1; an fma with a +-1 factor rounds as the add).
+    const int tt = (tid >> 3) & 31, cp = tid & 7;
+    const int twy = tt >> 3, twx = tt & 7;
+    const int rd0 = ((2 * twy) * XPW + 2 * twx) * XPS + 2 * cp;
+    const int rofs0 = (2 * h) * XPW * XPS, rofs1 = (2 - h) * XPW * XPS, rofs2 = (1 + 2 * h) * XPW * XPS;
+    const float sgn = h ? -1.f : 1.f;
+    const int vwoff = tt * XVROW + 16 * ((cp >> 2) ^ ((tt >> 3) & 1)) + 4 * (cp & 3) + 8 * h * 32 * XVROW;
+    float fx[3][4], fy[3][4];
+    auto tr_read_col = [&](const float* pbuf, int c) __attribute__((always_inline)) {
+        const f32x2 v0 = *reinterpret_cast<const f32x2*>(pbuf + rd0 + rofs0 + c * XPS);
+        const f32x2 v1 = *reinterpret_cast<const f32x2*>(pbuf + rd0 + rofs1 + c * XPS);
+        const f32x2 v2 = *reinterpret_cast<const f32x2*>(pbuf + rd0 + rofs2 + c * XPS);
+        fx[0][c] = v0.x; fy[0][c] = v0.y;
+        fx[1][c] = v1.x; fy[1][c] = v1.y;
+        fx[2][c] = v2.x; fy[2][c] = v2.y;
+    };
+    auto tr_rows_col = [&](int c) __attribute__((always_inline)) {   // row 2h -> f0, row 2h+1 -> f2
+        fx[2][c] = fmaf(sgn, fx[2][c], fx[1][c]);
+        fy[2][c] = fmaf(sgn, fy[2][c], fy[1][c]);
+        fx[0][c] = fx[0][c] - fx[1][c];
+        fy[0][c] = fy[0][c] - fy[1][c];
+    };
+    auto piece = [&](float& x, float& y, unsigned& p) __attribute__((always_inline)) {
+        p = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
+        x = x - __uint_as_float(p << 16);
+        y = y - __uint_as_float(p & 0xFFFF0000u);
+    };
+    auto last_piece = [&](float x, float y) __attribute__((always_inline)) {
+        return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
+    };
+    auto vwrite = [&](unsigned char* vbuf, int lx, unsigned p0, unsigned p1, unsigned p2) __attribute__((always_inline)) {
+        *reinterpret_cast<unsigned*>(vbuf + ((0 * XXI + lx) * 32) * XVROW + vwoff) = p0;
+        *reinterpret_cast<unsigned*>(vbuf + ((1 * XXI + lx) * 32) * XVROW + vwoff) = p1;
+        *reinterpret_cast<unsigned*>(vbuf + ((2 * XXI + lx) * 32) * XVROW + vwoff) = p2;
+    };
+    // (B^T d) B of row rs (0: f0, 1: f2), points q0, q0 + 1 (local points lx = 4 rs + q0, + 1)
+    float w0x = 0.f, w0y = 0.f, w1x = 0.f, w1y = 0.f;
+    auto cols = [&](int rs, int q0) __attribute__((always_inline)) {
+        const float* rx = rs ? fx[2] : fx[0];
+        const float* ry = rs ? fy[2] : fy[0];
+        if (q0 == 0) {
+            w0x = rx[0] - rx[2];
+            w0y = ry[0] - ry[2];
+            w1x = rx[1] + rx[2];
+            w1y = ry[1] + ry[2];
+        } else {
+            w0x = rx[2] - rx[1];
+            w0y = ry[2] - ry[1];
+            w1x = rx[1] - rx[3];
+            w1y = ry[1] - ry[3];
+        }
+    };
+    auto transform_all = [&](const float* pbuf, unsigned char* vbuf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) tr_read_col(pbuf, c);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) tr_rows_col(c);
+#pragma unroll
+        for (int rs = 0; rs < 2; ++rs)
+#pragma unroll
+            for (int q0 = 0; q0 < 4; q0 += 2) {
+                cols(rs, q0);
+                unsigned p0, p1;
+                piece(w0x, w0y, p0);
+                piece(w0x, w0y, p1);
+                vwrite(vbuf, 4 * rs + q0, p0, p1, last_piece(w0x, w0y));
+                piece(w1x, w1y, p0);
+                piece(w1x, w1y, p1);
+                vwrite(vbuf, 4 * rs + q0 + 1, p0, p1, last_piece(w1x, w1y));
+            }
+    };
+
+    floatx16 acc[YPT];
+#pragma unroll
+    for (int x = 0; x < YPT; ++x)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+
+    // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..R-1) in flight ----
+    if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging
+    sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 0); });
+    sfor<0, YRING>([&](auto X) __attribute__((always_inline)) {
+        sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+            load_u1(0, decltype(X)::value, decltype(X)::value, decltype(Pc)::value);
+        });
+    });
+    stage_all(0, patch);
+    if (nchunks > 1) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 1); });
+    lds_barrier();
+    transform_all(patch, vbytes);
+    if (nchunks > 1) {
+        stage_all(1, patch + XPATCH_FL);
+        if (nchunks > 2) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 2); });
+    }
+    lds_barrier();
+
+    XTL(1);
+    const int varow = li * XVROW + 16 * (lh ^ ((li >> 3) & 1)) + 8 * h * 32 * XVROW;
+    unsigned qa0 = 0, qa1 = 0, qb0 = 0, qb1 = 0;
+    f32x4 sp01 = f32x4{0.f, 0.f, 0.f, 0.f}, sp23 = sp01, sv = sp01;
+
+    for (int c = 0; c < nchunks; ++c) {
+        const int P = c & 1;
+        const int c1 = min(c + 1, nchunks - 1), c2 = min(c + 2, nchunks - 1), c3 = min(c + 3, nchunks - 1);
+        const unsigned char* va = vbytes + P * XV_BYTES + varow;
+        unsigned char* const vnext = vbytes + (1 - P) * XV_BYTES;
+        const float* const pnext = patch + (1 - P) * XPATCH_FL;
+        float* const pstage = patch + P * XPATCH_FL;
+        short8 av[2][3];
+        sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+            constexpr int p = decltype(Pc)::value;
+            av[0][p] = *reinterpret_cast<const short8*>(va + (p * XXI) * 32 * XVROW);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        sfor<0, YPT>([&](auto X) __attribute__((always_inline)) {
+            constexpr int x = decltype(X)::value;
+            constexpr int s = x % YRING;
+            sfor<0, 6>([&](auto K) __attribute__((always_inline)) {
+                constexpr int k = decltype(K)::value;
+                constexpr int ap = k == 2 || k == 4 ? 1 : (k == 5 ? 2 : 0);
+                constexpr int bp = k == 1 || k == 4 ? 1 : (k == 3 ? 2 : 0);
+                acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[x & 1][ap], ur[s][bp], acc[x], 0, 0, 0);
+                if constexpr (k == 0 && x + 1 < YPT) {
+                    sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+                        constexpr int p = decltype(Pc)::value;
+                        av[(x + 1) & 1][p] = *reinterpret_cast<const short8*>(va + (p * XXI + x + 1) * 32 * XVROW);
+                    });
+                }
+                if constexpr (!(X6_SKIP & 1) && k >= 3) {   // U ring refill (B2, B1, B0 last read by MFMAs 3, 4, 5)
+                    constexpr int xn = (x + YRING) % YPT;
+                    load_u1(x + YRING < YPT ? c : c1, xn, s, 5 - k);
+                }
+                // transform + split of chunk c+1 into V[1-P]
+                if constexpr (!(X6_SKIP & 2) && x == 0 && k < 4) tr_read_col(pnext, k);
+                if constexpr (!(X6_SKIP & 2) && x == 1 && k < 4) tr_rows_col(k);
+                if constexpr (!(X6_SKIP & 2) && x >= 2 && x < 6) {
+                    constexpr int rs = (x - 2) >> 1, q0 = ((x - 2) & 1) * 2, lx0 = 4 * rs + q0;
+                    if constexpr (k == 0) cols(rs, q0);
+                    if constexpr (k == 1) piece(w0x, w0y, qa0);
+                    if constexpr (k == 2) piece(w0x, w0y, qa1);
+                    if constexpr (k == 3) {
+                        vwrite(vnext, lx0, qa0, qa1, last_piece(w0x, w0y));
+                        piece(w1x, w1y, qb0);
+                    }
+                    if constexpr (k == 4) piece(w1x, w1y, qb1);
+                    if constexpr (k == 5) vwrite(vnext, lx0 + 1, qb0, qb1, last_piece(w1x, w1y));
+                }
+                // staging of chunk c+2 into patch[P], then the loads of chunk c+3 into the freed registers
+                if constexpr (!(X6_SKIP & 4) && x >= 6) {
+                    constexpr int ks = x - 6;
+                    if constexpr (k == 0 && pro != PRO_NONE) {
+                        sp01 = *reinterpret_cast<const f32x4*>(pab + c2 * XCK + cq4);
+                        sp23 = *reinterpret_cast<const f32x4*>(pab + c2 * XCK + cq4 + 2);
+                    }
+                    if constexpr (k == 2) sv = stage_math(ks, c2, sp01, sp23);
+                    if constexpr (k == 4) stage_write(ks, pstage, sv);
+                    if constexpr (k == 5) gload(ks, c3);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        });
+        lds_barrier();
+    }
+
+    XTL(2);
+    // ---- epilogue: partial output transform per half -> LDS image, then sum + bias + ReLU + store + stats --
+    float* const yimg = smem + h * (128 * YSTR);
+    {
+        const int co = g * 32 + li;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;   // Winograd tile of this accumulator row
+            const int wy = row >> 3, wx = row & 7;
+            float t0[4], t1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {   // T = A^T M over this half's two rows of M
+                const float ma = acc[q][j], mb = acc[4 + q][j];
+                t0[q] = h == 0 ? ma + mb : ma;
+                t1[q] = h == 0 ? mb : -ma - mb;
+            }
+            const float yy[4] = {t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3], t1[0] + t1[1] + t1[2],
+                                 t1[1] - t1[2] - t1[3]};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) yimg[((2 * wy + (q >> 1)) * XTW + 2 * wx + (q & 1)) * YSTR + co] = yy[q];
+        }
+    }
+    lds_barrier();
+    // thread = (pixel column pr, channel quad cq); rows 0..7 of the tile
+    const int cq = tid & 31, pr = tid >> 5;
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + 4 * cq);
+    const bool col_ok = x0 + pr < W;
+    f32x4 yv[XTH];
+    f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < XTH; ++i) {
+        const int off = (i * XTW + pr) * YSTR + 4 * cq;
+        f32x4 v = *reinterpret_cast<const f32x4*>(smem + off) + *reinterpret_cast<const f32x4*>(smem + 128 * YSTR + off) + b4;
+        if (!a.linear) {
+            v.x = fmaxf(v.x, 0.f);
+            v.y = fmaxf(v.y, 0.f);
+            v.z = fmaxf(v.z, 0.f);
+            v.w = fmaxf(v.w, 0.f);
+        }
+        const bool ok = col_ok && y0 + i < H;
+        if (ok) *reinterpret_cast<f32x4*>(a.out + (img + (size_t)(y0 + i) * W + x0 + pr) * XN + 4 * cq) = v;
+        yv[i] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+        s4 += yv[i];
+    }
+    if (a.part != nullptr) {
+        f32x4* const red = reinterpret_cast<f32x4*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES);   // [2][8][32]
+        const float cnt = (float)(min(XTH, H - y0) * min(XTW, W - x0));
+        auto xsum = [&](f32x4 v) __attribute__((always_inline)) {
+            v.x += __shfl_xor(v.x, 32);
+            v.y += __shfl_xor(v.y, 32);
+            v.z += __shfl_xor(v.z, 32);
+            v.w += __shfl_xor(v.w, 32);
+            return v;
+        };
+        s4 = xsum(s4);
+        if (lh == 0) red[wave * 32 + cq] = s4;
+        lds_barrier();
+        f32x4 S = red[cq];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) S += red[w * 32 + cq];
+        const f32x4 mean = S / cnt;
+        f32x4 m2 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < XTH; ++i) {
+            const bool ok = col_ok && y0 + i < H;
+            const f32x4 d = yv[i] - mean;
+            if (ok) m2 += d * d;
+        }
+        m2 = xsum(m2);
+        if (lh == 0) red[256 + wave * 32 + cq] = m2;
+        lds_barrier();
+        if (tid < 32) {
+            f32x4 M = red[256 + cq];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) M += red[256 + w * 32 + cq];
+            const int n_part = a.tiles_y * a.tiles_x;
+            float4* const dst = a.part + ((size_t)b * XN + 4 * cq) * n_part + ty * a.tiles_x + tx;
+            dst[0] = make_float4(S.x, M.x, cnt, 0.f);
+            dst[n_part] = make_float4(S.y, M.y, cnt, 0.f);
+            dst[2 * n_part] = make_float4(S.z, M.z, cnt, 0.f);
+            dst[3 * n_part] = make_float4(S.w, M.w, cnt, 0.f);
+        }
+    }
+    XTL(3);
+}
 
 bool wino_x6_supported(int kh, int stride, int cin, int cout) {
     return kh == 3 && stride == 1 && cout == XN && cin % XCK == 0 && cin <= XMAX_CIN;
@@ -613,14 +989,33 @@ hipError_t wino_x6_prepare() {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)XLDS_BYTES);
         if (e != hipSuccess) return e;
     }
+    for (const void* k : {(const void*)wino_x6w_kernel<PRO_NONE>, (const void*)wino_x6w_kernel<PRO_AFF_RELU>,
+                          (const void*)wino_x6w_kernel<PRO_AFF>, (const void*)wino_x6w_kernel<PRO_AFF_RES>}) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)YLDS_BYTES);
+        if (e != hipSuccess) return e;
+    }
     return hipSuccess;
 }
+
+// 1 = the two-waves-per-SIMD kernel (default), 0 = the single-wave kernel (tools/wino_x6_bench comparisons)
+static int g_x6_variant = 1;
+void wino_x6_set_variant(int v) { g_x6_variant = v; }
 
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
     if (a.cin % XCK != 0 || a.cin > XMAX_CIN || a.tiles_y != (a.H + XTH - 1) / XTH ||
         a.tiles_x != (a.W + XTW - 1) / XTW || (size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7F000000)
         return hipErrorInvalidValue;   // 32-bit staging offsets; the out-of-range store offset must stay out of range
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
+    if (g_x6_variant == 1) {
+        switch (a.pro_mode) {
+            case PRO_NONE: hipLaunchKernelGGL(wino_x6w_kernel<PRO_NONE>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
+            case PRO_AFF_RELU: hipLaunchKernelGGL(wino_x6w_kernel<PRO_AFF_RELU>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
+            case PRO_AFF: hipLaunchKernelGGL(wino_x6w_kernel<PRO_AFF>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
+            case PRO_AFF_RES: hipLaunchKernelGGL(wino_x6w_kernel<PRO_AFF_RES>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (a.pro_mode) {
         case PRO_NONE: hipLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
         case PRO_AFF_RELU: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
