@@ -142,7 +142,6 @@ bool wino_x6_supported(int kh, int stride, int cin, int cout);
 std::vector<float> wino_x6_pack_weights(const float* kern, int cin);
 hipError_t wino_x6_prepare();
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st);
-void wino_x6_set_variant(int v);   // 1 = two waves per SIMD (default), 0 = single-wave kernel (bench tool)
 
 // Final 9x9 transposed conv with Cout = 3 on the VALU (conv_small.hip).
 struct SmallConvArgs {

@@ -12,18 +12,25 @@
 // carry fp32 precision at 6/16 of the f32-MFMA cost. U is formed on the host in f64, rounded once to
 // f32 (as wino.hip) and split on the host; V is split by the input-transform threads as they write it.
 //
-// Workgroup = 4 waves, output tile 8 x 16 pixels = 32 Winograd tiles (one 32-row MFMA M tile) x 128
-// output channels; wave w owns channels [32w, 32w+32) for all 16 transform points (16 accumulators,
-// 256 AGPRs; one wave per SIMD). Input channels go in chunks of 16 = the MFMA K: per chunk and point
-// the six terms are six MFMAs whose A operands are the V pieces (LDS, [piece][xi][tile][16 ch] bf16,
-// one ds_read_b128 per lane per piece) and B operands the U pieces (L2, packed on the host in MFMA
-// B-operand order, one 16-B load per lane per piece, kept in an 8-point register ring).
-// Per chunk c one software-pipelined step with one barrier: the 96 MFMAs on V(c) interleave with the
-// input transform + split of chunk c+1 (thread = (tile, channel pair): 16 ds_read_b64, 64 adds,
-// 3 v_cvt_pk_bf16_f32 per channel pair and point, 48 ds_write_b32), the staging of chunk c+2
-// (CIN affine [+ ReLU | + residual] prologue, materialised block output) and the loads of chunk c+3.
-// Epilogue (as wino.hip): output transform, conv bias + ReLU, store, per-(workgroup, channel) two-pass
-// {sum, M2, n} for the conditional instance norm that follows.
+// Workgroup = 8 waves (two per SIMD), output tile 8 x 16 pixels = 32 Winograd tiles (one 32-row MFMA M
+// tile) x 128 output channels. Wave (g, h) owns channels [32g, 32g+32) and the transform points of rows
+// p = 2h, 2h+1 (points 8h .. 8h+7: 8 accumulators, 128 registers), so the two waves of a SIMD interleave
+// and one wave's transform VALU issues while the other's MFMAs run (a single-wave-per-SIMD form holding
+// all 16 points, 256 accumulator registers, left that VALU in the gaps of its own dependent MFMA chain:
+// 34.8 vs 32.4 us at B=1). Input channels go in chunks of 16 = the MFMA K: per chunk and point the six
+// terms are six MFMAs whose A operands are the V pieces (LDS, [piece][xi][tile][16 ch] bf16, one
+// ds_read_b128 per lane per piece) and B operands the U pieces (L2, packed on the host in MFMA B-operand
+// order, one 16-B load per lane per piece, a 2-point register ring). Per chunk c one software-pipelined
+// step with one barrier: the 48 MFMAs of each wave on V(c) interleave with the input transform + split of
+// chunk c+1 (thread = (half h, tile, channel pair): rows 2h, 2h+1 of B^T d from three patch rows, 12
+// ds_read_b64, 32 adds, 3 v_cvt_pk_bf16_f32 per channel pair and point, 24 ds_write_b32), the staging of
+// chunk c+2 (CIN affine [+ ReLU | + residual] prologue, materialised block output) and the loads of c+3.
+// The loop is bound by the U stream (196 KB per workgroup and chunk from L2: 72-80 GB/s per CU, the
+// L2-served rate MI355X_MICROARCH.md measures for shared rows); without the U reloads it runs 27 us.
+// Epilogue: each half forms its partial output transform (Y = A^T M A is linear in the points) into an
+// LDS image [pixel][channel]; all 512 threads add the halves, apply bias + ReLU, store whole pixels'
+// channel quads (1 KB per wave instruction) and reduce the per-(workgroup, channel) two-pass {sum, M2, n}
+// for the conditional instance norm that follows.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstring>
@@ -51,13 +58,11 @@ constexpr int XPS = 24;                           // patch pixel stride (floats)
 constexpr int XN = 128;                           // output channels (4 waves x 32)
 constexpr int XXI = 16;                           // transform points
 constexpr int XPF4 = XNP * XCK / 4;               // 720 float4 per chunk patch
-constexpr int XST = (XPF4 + 255) / 256;           // 3 staging float4 per thread
 constexpr int XMAX_CIN = 256;
 constexpr int XPATCH_FL = XNP * XPS;              // one patch buffer (floats)
 constexpr int XVROW = 32;                         // bytes per (piece, xi, tile) row: 16 bf16
 constexpr int XV_BYTES = 3 * XXI * 32 * XVROW;    // one V buffer: 48 KB
-constexpr int XRING = 4;                          // U register ring (points in flight)
-constexpr size_t XLDS_BYTES = (size_t)2 * XPATCH_FL * 4 + 2 * XV_BYTES + XMAX_CIN * sizeof(float2);
+constexpr size_t XLDS_BYTES = (size_t)2 * XPATCH_FL * 4 + 2 * XV_BYTES + XMAX_CIN * sizeof(float2);   // loop
 
 template <int I, int N, typename F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -74,15 +79,6 @@ __device__ __forceinline__ float pro_apply(int mode, float x, float2 ab, float r
     return y;
 }
 
-// (x, y) -> three packed bf16 pairs (lo half: x's piece, hi half: y's piece), x = x0 + x1 + x2 exactly
-__device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned& p1, unsigned& p2) {
-    p0 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
-    const float rx = x - __uint_as_float(p0 << 16), ry = y - __uint_as_float(p0 & 0xFFFF0000u);
-    p1 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){rx, ry}, bf16x2));
-    const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xFFFF0000u);
-    p2 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){sx, sy}, bf16x2));
-}
-
 }  // namespace
 
 // Experiment knobs (tools/wino_x6_bench only; never set in the library build): X6_SKIP bit0 = no U reloads
@@ -91,423 +87,13 @@ __device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned&
 #define X6_SKIP 0
 #endif
 #ifdef X6_PROF
-// timeline per (workgroup, wave) on the constant 100 MHz clock: start, pipeline filled, chunk loop done, end
+// timeline per (workgroup, wave < 8) on the constant 100 MHz clock: start, pipeline filled, chunk loop done, end
 __device__ unsigned long long x6_tl[X6_PROF][8][4];
 #define XTL(k) \
     if (blockIdx.x < X6_PROF && lane == 0) x6_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define XTL(k)
 #endif
-#ifdef X6_PROF2
-// s_memtime at the start of every point of every chunk, per (workgroup < X6_PROF2, wave)
-__device__ unsigned long long x6_pt[X6_PROF2][4][16][17];
-#define XPT(cc, pp) \
-    if (blockIdx.x < X6_PROF2 && lane == 0 && (cc) < 16) x6_pt[blockIdx.x][wave][(cc)][(pp)] = __builtin_amdgcn_s_memtime()
-#else
-#define XPT(cc, pp)
-#endif
-
-template <int PRO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino_x6_kernel(WinoArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* const patch = smem;                                            // [2][180][24] f32
-    unsigned char* const vbytes = reinterpret_cast<unsigned char*>(smem + 2 * XPATCH_FL);   // [2][3][16][32][32 B]
-    float2* const pab = reinterpret_cast<float2*>(vbytes + 2 * XV_BYTES);
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int li = lane & 31, lh = lane >> 5;
-    XTL(0);
-    int bid = xcd_tile_order(blockIdx.x, gridDim.x);   // XCD-contiguous tile runs (halo reuse in L2)
-    const int tx = bid % a.tiles_x;
-    bid /= a.tiles_x;
-    const int ty = bid % a.tiles_y;
-    const int b = bid / a.tiles_y;
-    const int y0 = ty * XTH, x0 = tx * XTW;
-    const int H = a.H, W = a.W, Cin = a.cin;
-    constexpr int pro = PRO;
-    const size_t img = (size_t)b * H * W;
-    const float* res_src = pro == PRO_AFF_RES ? a.res : a.in;
-    const int nchunks = Cin / XCK;
-
-    if constexpr (pro != PRO_NONE) {
-        for (int c = tid; c < Cin; c += 256) pab[c] = a.pro_ab[(size_t)b * Cin + c];
-    }
-
-    // ---- patch staging: global -> registers (clamped, branch-free) -> prologue -> LDS ----------
-    f32x4 xr[XST], rr[XST];
-#pragma unroll
-    for (int k = 0; k < XST; ++k) rr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto load_patch = [&](int chunk) __attribute__((always_inline)) {
-        const int c0 = chunk * XCK;
-        sfor<0, XST>([&](auto K) __attribute__((always_inline)) {
-            constexpr int k = decltype(K)::value;
-            const int it = min(tid + k * 256, XPF4 - 1);
-            const int px = it >> 2, q = it & 3;
-            const int iy = min(max(y0 - 1 + px / XPW, 0), H - 1), ix = min(max(x0 - 1 + px % XPW, 0), W - 1);
-            const size_t gi = (img + (size_t)iy * W + ix) * Cin + c0 + 4 * q;
-            xr[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
-            if constexpr (pro == PRO_AFF_RES) rr[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
-        });
-    };
-    auto stage_one = [&](int chunk, float* pbuf, auto K) __attribute__((always_inline)) {
-        constexpr int k = decltype(K)::value;
-        const int it = tid + k * 256;
-        if (k < XST - 1 || it < XPF4) {
-            const int px = it >> 2, q = it & 3;
-            const int iy = y0 - 1 + px / XPW, ix = x0 - 1 + px % XPW;
-            const int c = chunk * XCK + 4 * q;
-            f32x4 v = xr[k];
-            const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
-            if constexpr (pro != PRO_NONE) {
-                const f32x4 r = rr[k];
-                const f32x4 p01 = *reinterpret_cast<const f32x4*>(pab + c);       // (a,b) of c, c+1
-                const f32x4 p23 = *reinterpret_cast<const f32x4*>(pab + c + 2);   // (a,b) of c+2, c+3
-                v.x = pro_apply(pro, v.x, float2{p01.x, p01.y}, r.x);
-                v.y = pro_apply(pro, v.y, float2{p01.z, p01.w}, r.y);
-                v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
-                v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
-                if (a.mat != nullptr && inside && iy >= y0 && iy < y0 + XTH && ix >= x0 && ix < x0 + XTW)
-                    *reinterpret_cast<f32x4*>(a.mat + (img + (size_t)iy * W + ix) * Cin + c) = v;
-            }
-            if (!inside) v = f32x4{0.f, 0.f, 0.f, 0.f};
-            *reinterpret_cast<f32x4*>(pbuf + px * XPS + 4 * q) = v;
-        }
-    };
-    auto stage = [&](int chunk, float* pbuf) __attribute__((always_inline)) {
-        sfor<0, XST>([&](auto K) __attribute__((always_inline)) { stage_one(chunk, pbuf, K); });
-    };
-
-    // Per-thread staging descriptors (item k = float4 tid + 256k of a chunk's 720-float4 patch), computed
-    // once: global float offset of the clamped source pixel's channel quad at chunk 0; LDS float offset
-    // (items past 720 write a pad slot) | inside-image flag << 16; byte offset of the materialised block
-    // output at chunk 0 (past the buffer when the pixel is not interior: a buffer store drops it).
-    int sg_goff[XST], sg_lf[XST], sg_moff[XST];
-#pragma unroll
-    for (int k = 0; k < XST; ++k) {
-        const int it = tid + k * 256, itc = min(it, XPF4 - 1);
-        const int px = itc >> 2, q = itc & 3;
-        const int iy = y0 - 1 + px / XPW, ix = x0 - 1 + px % XPW;
-        const int cy = min(max(iy, 0), H - 1), cx = min(max(ix, 0), W - 1);
-        sg_goff[k] = (int)((img + (size_t)cy * W + cx) * Cin) + 4 * q;
-        const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
-        const int loff = it < XPF4 ? px * XPS + 4 * q : ((it - XPF4) >> 2) * XPS + XCK + 4 * (q & 1);
-        sg_lf[k] = loff | (inside ? 1 << 16 : 0);
-        const bool interior = it < XPF4 && inside && iy >= y0 && iy < y0 + XTH && ix >= x0 && ix < x0 + XTW;
-        sg_moff[k] = interior ? (int)(((img + (size_t)iy * W + ix) * Cin + 4 * q) * 4) : 0x7F000000;
-    }
-    const __amdgpu_buffer_rsrc_t msrd = __builtin_amdgcn_make_buffer_rsrc(
-        a.mat, 0, a.mat != nullptr ? (int)((size_t)a.batch * H * W * Cin * 4) : 0, 0x00020000);
-    const float bias_co = a.bias[wave * 32 + li];   // epilogue operand, fetched early
-
-    // ---- U pieces: lane (li, lh) of wave w reads U[chunk][xi][piece][32w + li][8lh .. 8lh+7] -------
-    const __amdgpu_buffer_rsrc_t usrd = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.U), 0, nchunks * XXI * 3 * XN * XVROW, 0x00020000);
-    const int uvoff = (wave * 32 + li) * XVROW + 16 * lh;
-    short8 ur[XRING][3];
-    auto load_u = [&](int chunk, auto X, auto S) __attribute__((always_inline)) {
-        constexpr int x = decltype(X)::value, s = decltype(S)::value;
-        sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
-            constexpr int p = decltype(Pc)::value;
-            ur[s][p] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     usrd, uvoff, ((chunk * XXI + x) * 3 + p) * (XN * XVROW), 0));
-        });
-    };
-
-    // ---- input transform + split, one thread per (tile tt, channel pair cp) ---------------------
-    const int tt = tid >> 3, cp = tid & 7;
-    const int twy = tt >> 3, twx = tt & 7;
-    // byte offset of this thread's bf16 pair inside a V row: 16-B halves swapped for odd tile groups
-    const int vwoff = tt * XVROW + 16 * ((cp >> 2) ^ ((tt >> 3) & 1)) + 4 * (cp & 3);
-    float dx[4][4], dy[4][4];   // the tile of channels 2cp (x) and 2cp + 1 (y); scalar f32 ops only
-    auto tr_read = [&](const float* pbuf) __attribute__((always_inline)) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const f32x2 v = *reinterpret_cast<const f32x2*>(pbuf + ((2 * twy + r) * XPW + 2 * twx + c) * XPS + 2 * cp);
-                dx[r][c] = v.x;
-                dy[r][c] = v.y;
-            }
-    };
-    auto rows1 = [&](float (&d)[4][4], int c) __attribute__((always_inline)) {   // B^T d, column c, in place
-        const float a0 = d[0][c], a1 = d[1][c], a2 = d[2][c], a3 = d[3][c];
-        d[0][c] = a0 - a2;
-        d[1][c] = a1 + a2;
-        d[2][c] = a2 - a1;
-        d[3][c] = a1 - a3;
-    };
-    auto tr_rows = [&](int half) __attribute__((always_inline)) {   // columns 2 half, 2 half + 1
-        rows1(dx, 2 * half);
-        rows1(dx, 2 * half + 1);
-        rows1(dy, 2 * half);
-        rows1(dy, 2 * half + 1);
-    };
-    // (B^T d) B for row r, points q0 and q0 + 1 (q0 = 0 or 2), split and written to vbuf
-    auto tr_cols = [&](unsigned char* vbuf, int r, int q0) __attribute__((always_inline)) {
-        float v0x, v0y, v1x, v1y;
-        if (q0 == 0) {
-            v0x = dx[r][0] - dx[r][2];
-            v0y = dy[r][0] - dy[r][2];
-            v1x = dx[r][1] + dx[r][2];
-            v1y = dy[r][1] + dy[r][2];
-        } else {
-            v0x = dx[r][2] - dx[r][1];
-            v0y = dy[r][2] - dy[r][1];
-            v1x = dx[r][1] - dx[r][3];
-            v1y = dy[r][1] - dy[r][3];
-        }
-        unsigned p0, p1, p2;
-        const int xi0 = r * 4 + q0;
-        split3(v0x, v0y, p0, p1, p2);
-        *reinterpret_cast<unsigned*>(vbuf + ((0 * XXI + xi0) * 32) * XVROW + vwoff) = p0;
-        *reinterpret_cast<unsigned*>(vbuf + ((1 * XXI + xi0) * 32) * XVROW + vwoff) = p1;
-        *reinterpret_cast<unsigned*>(vbuf + ((2 * XXI + xi0) * 32) * XVROW + vwoff) = p2;
-        split3(v1x, v1y, p0, p1, p2);
-        *reinterpret_cast<unsigned*>(vbuf + ((0 * XXI + xi0 + 1) * 32) * XVROW + vwoff) = p0;
-        *reinterpret_cast<unsigned*>(vbuf + ((1 * XXI + xi0 + 1) * 32) * XVROW + vwoff) = p1;
-        *reinterpret_cast<unsigned*>(vbuf + ((2 * XXI + xi0 + 1) * 32) * XVROW + vwoff) = p2;
-    };
-
-    floatx16 acc[XXI];
-#pragma unroll
-    for (int x = 0; x < XXI; ++x)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
-
-    // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..7) in flight --
-    if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging
-    load_patch(0);
-    sfor<0, XRING>([&](auto X) __attribute__((always_inline)) { load_u(0, X, X); });
-    stage(0, patch);
-    if (nchunks > 1) load_patch(1);
-    lds_barrier();
-    tr_read(patch);
-    tr_rows(0);
-    tr_rows(1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        tr_cols(vbytes, r, 0);
-        tr_cols(vbytes, r, 2);
-    }
-    if (nchunks > 1) {
-        stage(1, patch + XPATCH_FL);
-        if (nchunks > 2) load_patch(2);
-    }
-    lds_barrier();
-    XTL(1);
-
-    // A operands of point x: the three pieces of this lane's tile row, 16-B half lh (swizzled)
-    const int varow = li * XVROW + 16 * (lh ^ ((li >> 3) & 1));
-    // Working state of the in-loop transform / staging, which is cut into pieces placed explicitly
-    // between the six MFMAs of a point (each MFMA of a point depends on the previous one, so whatever
-    // the scheduler clusters behind a run of MFMAs would run with the matrix pipe idle).
-    float w0x = 0.f, w0y = 0.f, w1x = 0.f, w1y = 0.f;
-    unsigned qa0 = 0, qa1 = 0, qa2 = 0, qb0 = 0, qb1 = 0, qb2 = 0;
-    f32x4 sp01 = f32x4{0.f, 0.f, 0.f, 0.f}, sp23 = sp01, sv = sp01;
-    // p = the bf16 pair nearest (x, y); (x, y) -= its value (exact in fp32)
-    auto piece = [&](float& x, float& y, unsigned& p) __attribute__((always_inline)) {
-        p = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
-        x = x - __uint_as_float(p << 16);
-        y = y - __uint_as_float(p & 0xFFFF0000u);
-    };
-    auto vwrite = [&](unsigned char* vbuf, int xi, unsigned p0, unsigned p1, unsigned p2) __attribute__((always_inline)) {
-        *reinterpret_cast<unsigned*>(vbuf + ((0 * XXI + xi) * 32) * XVROW + vwoff) = p0;
-        *reinterpret_cast<unsigned*>(vbuf + ((1 * XXI + xi) * 32) * XVROW + vwoff) = p1;
-        *reinterpret_cast<unsigned*>(vbuf + ((2 * XXI + xi) * 32) * XVROW + vwoff) = p2;
-    };
-
-    // one chunk: P = chunk parity (V(c) in V[P], patch(c+1) in patch[1-P], patch[P] free)
-    for (int c = 0; c < nchunks; ++c) {
-        const int P = c & 1;
-        // past the last chunk the pipeline repeats the last chunk's work into buffers nobody reads (branch-
-        // free, so the transform / staging instructions can interleave with the MFMAs); restaging a chunk
-        // writes the same materialised values again
-        const int c1 = min(c + 1, nchunks - 1), c2 = min(c + 2, nchunks - 1), c3 = min(c + 3, nchunks - 1);
-        const unsigned char* va = vbytes + P * XV_BYTES + varow;
-        unsigned char* const vnext = vbytes + (1 - P) * XV_BYTES;
-        const float* const pnext = patch + (1 - P) * XPATCH_FL;
-        float* const pstage = patch + P * XPATCH_FL;
-        short8 av[2][3];
-        sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
-            constexpr int p = decltype(Pc)::value;
-            av[0][p] = *reinterpret_cast<const short8*>(va + (p * XXI) * 32 * XVROW);
-        });
-        __builtin_amdgcn_sched_barrier(0);
-        sfor<0, XXI>([&](auto X) __attribute__((always_inline)) {
-            constexpr int x = decltype(X)::value;
-            constexpr int s = x & (XRING - 1);
-            XPT(c, x);
-            sfor<0, 6>([&](auto K) __attribute__((always_inline)) {
-                constexpr int k = decltype(K)::value;
-                // the six terms (A piece, B piece): a0b0 a0b1 a1b0 a0b2 a1b1 a2b0; B2, B1, B0 are last read
-                // by MFMAs 3, 4, 5, so their ring registers are refilled right behind those
-                constexpr int ap = k == 2 || k == 4 ? 1 : (k == 5 ? 2 : 0);
-                constexpr int bp = k == 1 || k == 4 ? 1 : (k == 3 ? 2 : 0);
-                acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[x & 1][ap], ur[s][bp], acc[x], 0, 0, 0);
-                // A operands of point x + 1
-                if constexpr (k == 0 && x + 1 < XXI) {
-                    sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
-                        constexpr int p = decltype(Pc)::value;
-                        av[(x + 1) & 1][p] = *reinterpret_cast<const short8*>(va + (p * XXI + x + 1) * 32 * XVROW);
-                    });
-                }
-                // U ring refill: point x + XRING of this chunk or point x + XRING - 16 of the next (clamped)
-                if constexpr (!(X6_SKIP & 1) && k >= 3) {
-                    constexpr int p = 5 - k;
-                    constexpr int xn = (x + XRING) & (XXI - 1);
-                    const int cn = x + XRING < XXI ? c : c1;
-                    ur[s][p] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                             usrd, uvoff, ((cn * XXI + xn) * 3 + p) * (XN * XVROW), 0));
-                }
-                // input transform + split of chunk c+1 into V[1-P]
-                if constexpr (!(X6_SKIP & 2)) {
-                    if constexpr (x < 2 && k < 4) {              // patch reads: row 2x + k/2, columns 2(k&1), +1
-                        constexpr int r = 2 * x + (k >> 1);
-#pragma unroll
-                        for (int cc = 2 * (k & 1); cc < 2 * (k & 1) + 2; ++cc) {
-                            const f32x2 v = *reinterpret_cast<const f32x2*>(
-                                pnext + ((2 * twy + r) * XPW + 2 * twx + cc) * XPS + 2 * cp);
-                            dx[r][cc] = v.x;
-                            dy[r][cc] = v.y;
-                        }
-                    }
-                    if constexpr (x == 2 && k < 4) {             // B^T d, column k
-                        rows1(dx, k);
-                        rows1(dy, k);
-                    }
-                    if constexpr (x >= 3 && x < 11) {            // (B^T d) B: row r, points xi0, xi0 + 1
-                        constexpr int r = (x - 3) >> 1, q0 = ((x - 3) & 1) * 2, xi0 = r * 4 + q0;
-                        if constexpr (k == 0) {
-                            if constexpr (q0 == 0) {
-                                w0x = dx[r][0] - dx[r][2];
-                                w0y = dy[r][0] - dy[r][2];
-                                w1x = dx[r][1] + dx[r][2];
-                                w1y = dy[r][1] + dy[r][2];
-                            } else {
-                                w0x = dx[r][2] - dx[r][1];
-                                w0y = dy[r][2] - dy[r][1];
-                                w1x = dx[r][1] - dx[r][3];
-                                w1y = dy[r][1] - dy[r][3];
-                            }
-                        }
-                        if constexpr (k == 1) piece(w0x, w0y, qa0);
-                        if constexpr (k == 2) piece(w0x, w0y, qa1);
-                        if constexpr (k == 3) {
-                            piece(w0x, w0y, qa2);
-                            vwrite(vnext, xi0, qa0, qa1, qa2);
-                            piece(w1x, w1y, qb0);
-                        }
-                        if constexpr (k == 4) piece(w1x, w1y, qb1);
-                        if constexpr (k == 5) {
-                            piece(w1x, w1y, qb2);
-                            vwrite(vnext, xi0 + 1, qb0, qb1, qb2);
-                        }
-                    }
-                }
-                // staging of chunk c+2 into patch[P] (free since chunk c's transform): prologue affine reads,
-                // prologue math + materialised block output, patch write (branch-free: precomputed descriptors)
-                if constexpr (!(X6_SKIP & 4) && x >= 11 && x < 11 + XST) {
-                    constexpr int ks = x - 11;
-                    const int cch = c2 * XCK + 4 * (tid & 3);
-                    if constexpr (k == 0 && pro != PRO_NONE) {
-                        sp01 = *reinterpret_cast<const f32x4*>(pab + cch);
-                        sp23 = *reinterpret_cast<const f32x4*>(pab + cch + 2);
-                    }
-                    if constexpr (k == 2) {
-                        sv = xr[ks];
-                        if constexpr (pro != PRO_NONE) {
-                            const f32x4 r = rr[ks];
-                            sv.x = pro_apply(pro, sv.x, float2{sp01.x, sp01.y}, r.x);
-                            sv.y = pro_apply(pro, sv.y, float2{sp01.z, sp01.w}, r.y);
-                            sv.z = pro_apply(pro, sv.z, float2{sp23.x, sp23.y}, r.z);
-                            sv.w = pro_apply(pro, sv.w, float2{sp23.z, sp23.w}, r.w);
-                            if (a.mat != nullptr)
-                                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sv), msrd,
-                                                                       sg_moff[ks] + c2 * XCK * 4, 0, 0);
-                        }
-                    }
-                    if constexpr (k == 4) {
-                        const bool inside = (sg_lf[ks] >> 16) != 0;
-                        sv.x = inside ? sv.x : 0.f;
-                        sv.y = inside ? sv.y : 0.f;
-                        sv.z = inside ? sv.z : 0.f;
-                        sv.w = inside ? sv.w : 0.f;
-                        *reinterpret_cast<f32x4*>(pstage + (sg_lf[ks] & 0xFFFF)) = sv;
-                    }
-                }
-                // global loads of chunk c+3's patch (into the registers the staging above consumed)
-                if constexpr (!(X6_SKIP & 4) && x == 11 + XST && (k & 1) == 0 && k / 2 < XST) {
-                    constexpr int kk = k / 2;
-                    const int gi = sg_goff[kk] + c3 * XCK;
-                    xr[kk] = *reinterpret_cast<const f32x4*>(a.in + gi);
-                    if constexpr (pro == PRO_AFF_RES) rr[kk] = *reinterpret_cast<const f32x4*>(res_src + gi);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            });
-        });
-        XPT(c, 16);
-        lds_barrier();
-    }
-    XTL(2);
-
-    // ---- epilogue: output transform, bias + ReLU, store, tile statistics -----------------------
-    const int co = wave * 32 + li;
-    const float bias = bias_co;
-    float yv[64];
-    float s = 0.f, cnt = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;   // Winograd tile of this accumulator row
-        const int wy = row >> 3, wx = row & 7;
-        float m[16];
-#pragma unroll
-        for (int x = 0; x < XXI; ++x) m[x] = acc[x][j];
-        // T = A^T M (2 x 4), Y = T A (2 x 2); A^T = [[1,1,1,0],[0,1,-1,-1]]
-        float t0[4], t1[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            t0[c] = m[0 * 4 + c] + m[1 * 4 + c] + m[2 * 4 + c];
-            t1[c] = m[1 * 4 + c] - m[2 * 4 + c] - m[3 * 4 + c];
-        }
-        const float yy[4] = {t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3], t1[0] + t1[1] + t1[2],
-                             t1[1] - t1[2] - t1[3]};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
-            const float v = a.linear ? yy[q] + bias : fmaxf(yy[q] + bias, 0.f);
-            const bool ok = oy < H && ox < W;
-            yv[j * 4 + q] = ok ? v : 0.f;
-            if (ok) {
-                a.out[(img + (size_t)oy * W + ox) * XN + co] = v;
-                s += v;
-                cnt += 1.f;
-            }
-        }
-    }
-    if (a.part != nullptr) {
-        s += __shfl_xor(s, 32);
-        cnt += __shfl_xor(cnt, 32);
-        const float mean = cnt > 0.f ? s / cnt : 0.f;
-        float m2 = 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int row = (j & 3) + 8 * (j >> 2) + 4 * lh;
-            const int wy = row >> 3, wx = row & 7;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
-                const float dd = yv[j * 4 + q] - mean;
-                if (oy < H && ox < W) m2 = fmaf(dd, dd, m2);
-            }
-        }
-        m2 += __shfl_xor(m2, 32);
-        if (lh == 0) {
-            const int n_part = a.tiles_y * a.tiles_x;
-            a.part[((size_t)b * XN + co) * n_part + ty * a.tiles_x + tx] = make_float4(s, m2, cnt, 0.f);
-        }
-    }
-    XTL(3);
-}
 
 #ifdef X6_PROF
 // timeline summary of the most recent launch (tools/wino_x6_bench)
@@ -534,41 +120,6 @@ void x6_timeline_print(int nwg, int nwave) {
 }
 #endif
 
-#ifdef X6_PROF2
-void x6_points_print(int nwg, int nchunks) {
-    std::vector<unsigned long long> pt((size_t)X6_PROF2 * 4 * 16 * 17);
-    if (hipMemcpyFromSymbol(pt.data(), HIP_SYMBOL(x6_pt), pt.size() * 8) != hipSuccess) return;
-    if (nwg > X6_PROF2) nwg = X6_PROF2;
-    double dur[17] = {0}, bar = 0;
-    int n = 0;
-    for (int g = 0; g < nwg; ++g)
-        for (int w = 0; w < 4; ++w)
-            for (int c = 1; c + 1 < nchunks && c < 16; ++c) {
-                const unsigned long long* q = &pt[(((size_t)g * 4 + w) * 16 + c) * 17];
-                for (int x = 0; x < 16; ++x) dur[x] += (double)(q[x + 1] - q[x]);
-                bar += (double)(q[17] - q[16]);   // next chunk's point 0 - this chunk's end (barrier)
-                ++n;
-            }
-    if (!n) return;
-    printf("  per-point s_memtime ticks (chunks 1..n-2, mean over %d wave-chunks):", n);
-    double tot = 0;
-    for (int x = 0; x < 16; ++x) { printf(" %.0f", dur[x] / n); tot += dur[x] / n; }
-    printf(" | barrier+top %.0f | chunk %.0f\n", bar / n, tot + bar / n);
-}
-#endif
-
-// ============================================================================================================
-// Two-waves-per-SIMD form (the launched one). The single-wave kernel above keeps every transform point of a
-// 32-channel slice in one wave (256 accumulator registers, one wave per SIMD), so the transform / split VALU
-// of the next chunk can only fill the gaps of that same wave's MFMA chain and its dependent VALU chains
-// stall the matrix pipe (per-point stamps: the transform points ran 405 vs 240 ticks without it). Here a
-// workgroup has 8 waves: wave (g, h) owns output channels [32g, 32g+32) and the transform points of rows
-// p = 2h, 2h+1 (points 8h .. 8h+7, 128 accumulator registers), so the two waves of a SIMD interleave and one
-// wave's VALU issues while the other's MFMAs run. The input transform is split the same way (thread half h
-// computes rows 2h, 2h+1 of B^T d, from three of the four patch rows). Epilogue: each half forms its partial
-// output transform (Y = A^T M A is linear in the points) into an LDS image [pixel][channel], then all 512
-// threads add the two halves, apply bias + ReLU and store whole pixels' channel quads (1 KB per wave
-// instruction instead of 64 scattered 4-B stores per lane), and reduce the per-channel statistics.
 #ifndef X6W_RING
 #define X6W_RING 2
 #endif
@@ -578,13 +129,13 @@ constexpr int YPT = 8;                              // transform points per wave
 constexpr int YST = (XPF4 + YT - 1) / YT;           // 2 staging float4 per thread
 constexpr int YRING = X6W_RING;                     // U register ring (points in flight), divides 8
 constexpr int YSTR = 132;                           // epilogue image row stride (floats): lh halves 32 banks apart
-constexpr size_t YIMG_BYTES = (size_t)2 * 128 * YSTR * 4;
-constexpr size_t YEPI_BYTES = YIMG_BYTES + 2 * 8 * 32 * 16;
+constexpr size_t YIMG_BYTES = (size_t)2 * 128 * YSTR * 4;       // epilogue: two halves' partial Y [pixel][channel]
+constexpr size_t YEPI_BYTES = YIMG_BYTES + 2 * 8 * 32 * 16;     // + statistics reduction [2][8 waves][32] float4
 constexpr size_t YLDS_BYTES = XLDS_BYTES > YEPI_BYTES ? XLDS_BYTES : YEPI_BYTES;
 static_assert(8 % YRING == 0, "ring must divide the points per wave");
 
 template <int PRO>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_x6w_kernel(WinoArgs a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_x6_kernel(WinoArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* const patch = smem;                                            // [2][180][24] f32
     unsigned char* const vbytes = reinterpret_cast<unsigned char*>(smem + 2 * XPATCH_FL);   // [2][3][16][32][32 B]
@@ -986,41 +537,22 @@ std::vector<float> wino_x6_pack_weights(const float* kern, int cin) {
 hipError_t wino_x6_prepare() {
     for (const void* k : {(const void*)wino_x6_kernel<PRO_NONE>, (const void*)wino_x6_kernel<PRO_AFF_RELU>,
                           (const void*)wino_x6_kernel<PRO_AFF>, (const void*)wino_x6_kernel<PRO_AFF_RES>}) {
-        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)XLDS_BYTES);
-        if (e != hipSuccess) return e;
-    }
-    for (const void* k : {(const void*)wino_x6w_kernel<PRO_NONE>, (const void*)wino_x6w_kernel<PRO_AFF_RELU>,
-                          (const void*)wino_x6w_kernel<PRO_AFF>, (const void*)wino_x6w_kernel<PRO_AFF_RES>}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)YLDS_BYTES);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
 
-// 1 = the two-waves-per-SIMD kernel (default), 0 = the single-wave kernel (tools/wino_x6_bench comparisons)
-static int g_x6_variant = 1;
-void wino_x6_set_variant(int v) { g_x6_variant = v; }
-
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
     if (a.cin % XCK != 0 || a.cin > XMAX_CIN || a.tiles_y != (a.H + XTH - 1) / XTH ||
         a.tiles_x != (a.W + XTW - 1) / XTW || (size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7F000000)
         return hipErrorInvalidValue;   // 32-bit staging offsets; the out-of-range store offset must stay out of range
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
-    if (g_x6_variant == 1) {
-        switch (a.pro_mode) {
-            case PRO_NONE: hipLaunchKernelGGL(wino_x6w_kernel<PRO_NONE>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
-            case PRO_AFF_RELU: hipLaunchKernelGGL(wino_x6w_kernel<PRO_AFF_RELU>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
-            case PRO_AFF: hipLaunchKernelGGL(wino_x6w_kernel<PRO_AFF>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
-            case PRO_AFF_RES: hipLaunchKernelGGL(wino_x6w_kernel<PRO_AFF_RES>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
     switch (a.pro_mode) {
-        case PRO_NONE: hipLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
-        case PRO_AFF_RELU: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
-        case PRO_AFF: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
-        case PRO_AFF_RES: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RES>, dim3(grid), dim3(256), XLDS_BYTES, st, a); break;
+        case PRO_NONE: hipLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
+        case PRO_AFF_RELU: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
+        case PRO_AFF: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
+        case PRO_AFF_RES: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RES>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -44,7 +44,7 @@ def short_name(k: str) -> str:
         return "last_x6<9x9 transposed Cin16 Cout3 as N=(kx,co) split-bf16 x6 MFMA>"
     if "wino9_x6_kernel" in k:
         return "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 16x16 N32 split-bf16 x6 MFMA persistent>"
-    if "wino_x6_kernel" in k:
+    if "wino_x6_kernel" in k or "wino_x6w_kernel" in k:
         return "wino_x6_conv<F(2x2,3x3) 8x16 N128 split-bf16 x6 MFMA>"
     if "wino9_conv_kernel" in k:
         return "wino9_conv<9x9 as 9 x F(2x2,3x3) 8x16 N32 f32 MFMA>"
