@@ -112,7 +112,10 @@ __device__ unsigned long long w9_tl[W9_PROF][8][9][4];   // [workgroup][wave][ti
 #endif
 
 template <int CINT>
-__global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_tiles) {
+// Work units: units 0 .. n_full-1 are whole tiles; the n_tiles - n_full tiles of the last, partial round
+// are split into two units each (one 32-tile M block, i.e. 8 output rows), so that round occupies twice
+// as many CUs for about half as long (1800 tiles on 256 CUs: 7 full rounds + 8 tiles -> 16 half units).
+__global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_units, int n_full) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -154,7 +157,10 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_ti
     // ---- persistent tile loop: workgroup g takes tiles g, g + G, ... The next tile's patch is staged into
     // the other patch buffer in two halves during the current tile's sub-kernel loop (loads issued a few
     // sub-kernels before their LDS stores, so their latency hides behind the MFMAs). ----
-    auto tile_coords = [&](int t, int& y0, int& x0, size_t& img) __attribute__((always_inline)) {
+    auto unit_tile = [&](int u) __attribute__((always_inline)) { return u < n_full ? u : n_full + ((u - n_full) >> 1); };
+    auto unit_mask = [&](int u) __attribute__((always_inline)) { return u < n_full ? 3 : 1 << ((u - n_full) & 1); };
+    auto tile_coords = [&](int u, int& y0, int& x0, size_t& img) __attribute__((always_inline)) {
+        int t = unit_tile(u);
         const int tx = t % a.tiles_x;
         t /= a.tiles_x;
         const int ty = t % a.tiles_y;
@@ -232,17 +238,18 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_ti
     const float bias = a.bias[co];
     const float2 bn = a.bn_ab[co];
 
-    int t = blockIdx.x;
-    if (t < n_tiles) {
+    int t = blockIdx.x;   // work unit
+    if (t < n_units) {
         load_half(t, std::integral_constant<int, 0>{});
         store_half(t, patch_buf(0), std::integral_constant<int, 0>{});
         load_half(t, std::integral_constant<int, 1>{});
         store_half(t, patch_buf(0), std::integral_constant<int, 1>{});
     }
-    for (int it = 0; t < n_tiles; t += gridDim.x, ++it) {
+    for (int it = 0; t < n_units; t += gridDim.x, ++it) {
         w9_it = it;
         W9TL(0);
         const int tn = t + gridDim.x;
+        const int hmask = __builtin_amdgcn_readfirstlane(unit_mask(t));   // M blocks of this unit
         int y0, x0;
         size_t img;
         tile_coords(t, y0, x0, img);
@@ -270,21 +277,24 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_ti
         // The q pair is a compile-time parameter (one code path per wave-uniform value): pair 0 uses the
         // columns 0..2 of B^T d (V0 = T0 - T2, V1 = T1 + T2), pair 1 the columns 1..3 (V2 = T2 - T1,
         // V3 = T1 - T3).
-        auto main_loop = [&](auto QH) __attribute__((always_inline)) {
-            constexpr int QHC = decltype(QH)::value;
+        // MASK (compile time: a runtime branch per block stops the scheduler from overlapping one block's
+        // MFMAs with the next block's transform): the M blocks this unit computes
+        auto main_loop = [&](auto QH, auto MK) __attribute__((always_inline)) {
+            constexpr int QHC = decltype(QH)::value, MASK = decltype(MK)::value;
             // sub-kernel loop fully unrolled (the U double buffer is indexed at compile time); no barriers
             sfor<0, 9>([&](auto AB) __attribute__((always_inline)) {
                 constexpr int ab = decltype(AB)::value, cur = ab & 1, sa = ab / 3, sb = ab % 3;
                 load_u(std::integral_constant<int, cur ^ 1>{}, ab + 1);   // ab + 1 == 9: the channel-16 step's U
                 // the next tile's patch: loads at sub-kernels 1 and 4, LDS stores at 3 and 6
                 if constexpr (ab == 1 || ab == 4) {
-                    if (tn < n_tiles) load_half(tn, std::integral_constant<int, ab == 4>{});
+                    if (tn < n_units) load_half(tn, std::integral_constant<int, ab == 4>{});
                 }
                 if constexpr (ab == 3 || ab == 6) {
-                    if (tn < n_tiles) store_half(tn, pnext, std::integral_constant<int, ab == 6>{});
+                    if (tn < n_units) store_half(tn, pnext, std::integral_constant<int, ab == 6>{});
                 }
                 sfor<0, 2>([&](auto Hh) __attribute__((always_inline)) {
                     constexpr int h = decltype(Hh)::value;
+                    if constexpr (!(MASK & (1 << h))) return;   // half unit: the other M block only
                     const int tile = 32 * h + li;
                     float tv[3][8], t16[3];
                     if constexpr (!(W9_SKIP & 2)) {
@@ -339,12 +349,18 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_ti
                 });
             });
         };
-        if (__builtin_amdgcn_readfirstlane(qh) == 0) main_loop(std::integral_constant<int, 0>{});
-        else main_loop(std::integral_constant<int, 1>{});
+        auto main_loop_q = [&](auto MK) __attribute__((always_inline)) {
+            if (__builtin_amdgcn_readfirstlane(qh) == 0) main_loop(std::integral_constant<int, 0>{}, MK);
+            else main_loop(std::integral_constant<int, 1>{}, MK);
+        };
+        if (hmask == 3) main_loop_q(std::integral_constant<int, 3>{});
+        else if (hmask == 1) main_loop_q(std::integral_constant<int, 1>{});
+        else main_loop_q(std::integral_constant<int, 2>{});
         // channel-16 K-step: lane (li, lh) supplies K = 8lh .. 8lh+7 (ab; 9..15 are zero)
         lds_barrier();   // every wave's channel-16 V in LDS
         sfor<0, 2>([&](auto Hh) __attribute__((always_inline)) {
             constexpr int h = decltype(Hh)::value;
+            if (!(hmask & (1 << h))) return;
             float w[2][8];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
@@ -360,12 +376,13 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_ti
             mfma6(acc[0][h], A0, ub[1][0]);   // 9 sub-kernels: the last load_u (ab + 1 == 9) went to buffer 1
             mfma6(acc[1][h], A1, ub[1][1]);
         });
-        if (tn < n_tiles) load_u(std::integral_constant<int, 0>{}, 0);   // the next tile's first U
+        if (tn < n_units) load_u(std::integral_constant<int, 0>{}, 0);   // the next tile's first U
         W9TL(2);
 
         // ---- epilogue, one M block at a time: M -> LDS [xi][tile][co], output transform, store -------
         sfor<0, 2>([&](auto Hh) __attribute__((always_inline)) {
             constexpr int h = decltype(Hh)::value;
+            if (!(hmask & (1 << h))) return;   // uniform over the workgroup (barriers inside)
             lds_barrier();   // patch / v16 reads (h = 0) / the previous block's M reads (h = 1) done
 #pragma unroll
             for (int q = 0; q < 2; ++q)
@@ -426,6 +443,24 @@ void w9_timeline_print(int nwg) {
             }
     printf("  per tile (us, iterations 0..5): top %.2f, loop %.2f, epilogue %.2f, gap %.2f\n", ph[0] / n * 0.01,
            ph[1] / n * 0.01, ph[2] / n * 0.01, ph[3] / n * 0.01);
+    // per workgroup (wave 0): first stamp, end of its last unit; the span of the whole grid
+    unsigned long long t0 = ~0ull, tmax = 0;
+    for (int g = 0; g < nwg; ++g) {
+        const unsigned long long* q = &tl[((size_t)g * 8) * 9 * 4];
+        if (q[0] && q[0] < t0) t0 = q[0];
+    }
+    int gmax = -1;
+    for (int g = 0; g < nwg; ++g) {
+        const unsigned long long* q = &tl[((size_t)g * 8) * 9 * 4];
+        unsigned long long e = 0;
+        int last = -1;
+        for (int it = 0; it < 9; ++it)
+            if (q[it * 4 + 3]) { e = q[it * 4 + 3]; last = it; }
+        if (g < 20 || g % 32 == 0)
+            printf("    wg %3d: start +%.2f, %d units, end +%.2f us\n", g, (q[0] - t0) * 0.01, last + 1, (e - t0) * 0.01);
+        if (e > tmax) { tmax = e; gmax = g; }
+    }
+    printf("  grid span %.2f us (last workgroup to finish: %d)\n", (tmax - t0) * 0.01, gmax);
 }
 #endif
 
@@ -498,17 +533,21 @@ hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st) {
         return hipErrorInvalidValue;   // inference only: training keeps wino9_launch (batch-statistics BN)
     // persistent: one workgroup per CU (LDS and registers allow one), each looping over tiles
     const int n_tiles = a.batch * a.tiles_y * a.tiles_x;
-    static int n_cu = 0;
+    static int n_cu = 0;   // queried once (not per launch: graph capture replays the recorded arguments)
     if (n_cu == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
     }
     const unsigned grid = (unsigned)(n_tiles < n_cu ? n_tiles : n_cu);
+    // a last round that fills at most half the grid runs as half-tile units (see the kernel)
+    const int tail = n_tiles % (int)grid;
+    const int n_full = (tail > 0 && 2 * tail <= (int)grid) ? n_tiles - tail : n_tiles;
+    const int n_units = n_full + 2 * (n_tiles - n_full);
     if (a.cin == 17)
-        hipLaunchKernelGGL(wino9_x6_kernel<17>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_tiles);
+        hipLaunchKernelGGL(wino9_x6_kernel<17>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_units, n_full);
     else
-        hipLaunchKernelGGL(wino9_x6_kernel<0>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_tiles);
+        hipLaunchKernelGGL(wino9_x6_kernel<0>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_units, n_full);
     return hipGetLastError();
 }
 

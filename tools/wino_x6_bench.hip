@@ -41,15 +41,20 @@ int main(int argc, char** argv) {
     // zm = 1: zero-mean inputs and prologue bias 0 (a ReLU prologue then zeroes about half the patch, as the
     // CIN + ReLU inputs of the frame's conv1 layers)
     const int zm = argc > 5 ? atoi(argv[5]) : 0;
+    // chain = 1: each timed launch reads the output the previous launch wrote (ping-pong, Cin = 128), as the
+    // frame's residual convs do; chain = 2: the chain's zero-mean weights without the chaining
+    const int chain = argc > 6 ? atoi(argv[6]) : 0;
     auto hin = host_rand((size_t)B * H * W * C, zm ? -2.f : -1.f, zm ? 2.f : 3.f, 1);
     auto hres = host_rand((size_t)B * H * W * C, -1, 1, 5);
-    auto hk = host_rand((size_t)9 * C * 128, 0.f, 0.05f, 2);          // residual init U(0, 0.05)
+    // residual init U(0, 0.05); zero-mean in chain mode (a gain near 1 per layer keeps the chained values finite)
+    auto hk = host_rand((size_t)9 * C * 128, chain ? -0.05f : 0.f, 0.05f, 2);
     auto hb = host_rand(128, -0.1f, 0.1f, 3);
     auto hab = host_rand((size_t)B * C * 2, 0.5f, 1.f, 4);
     if (zm)
         for (size_t i = 1; i < hab.size(); i += 2) hab[i] = 0.f;
     float* in = dev(hin);
     float* res = dev(hres);
+    float* pp[2] = {dev(hin), dev(hin)};   // chain ping-pong buffers (B x H x W x 128)
     float* U32 = dev(wino_pack_weights(hk.data(), C));
     float* U6 = dev(wino_x6_pack_weights(hk.data(), C));
     float* bias = dev(hb);
@@ -97,6 +102,10 @@ int main(int argc, char** argv) {
                 x.in = cin_[j]; x.res = cres[j]; x.out = cout_[j]; x.mat = cmat[j];
                 x.U = v ? cu6[j] : cu32[j];
             }
+            if (chain == 1 && C == 128) {
+                x.in = pp[i & 1];
+                x.out = pp[(i + 1) & 1];
+            }
             CK(launch());
         }
         x.in = in; x.res = res; x.out = outs[v]; x.mat = mats[v]; x.U = v ? U6 : U32;
@@ -108,9 +117,9 @@ int main(int argc, char** argv) {
         if (v) rst::x6_timeline_print(B * a.tiles_y * a.tiles_x, 8);
 #endif
         if (v) printf("%s B=%d Cin=%d pro=%d%s: %.2f us/launch, bf16 pipe %.3f (6 terms), direct-equivalent %.1f TF/s\n",
-                      names[v], B, C, pro, cold ? " cold" : "", us, 6 * exec / (us * 1e-6) / 2.5e15, direct / (us * 1e-6) / 1e12);
+                      names[v], B, C, pro, cold ? " cold" : (chain == 1 ? " chain" : (chain == 2 ? " zero-mean weights" : "")), us, 6 * exec / (us * 1e-6) / 2.5e15, direct / (us * 1e-6) / 1e12);
         else printf("%s B=%d Cin=%d pro=%d%s: %.2f us/launch, f32 pipe %.3f, direct-equivalent %.1f TF/s\n", names[v], B,
-                    C, pro, cold ? " cold" : "", us, exec / (us * 1e-6) / 157.3e12, direct / (us * 1e-6) / 1e12);
+                    C, pro, cold ? " cold" : (chain == 1 ? " chain" : (chain == 2 ? " zero-mean weights" : "")), us, exec / (us * 1e-6) / 157.3e12, direct / (us * 1e-6) / 1e12);
     }
     const auto h32 = host(outs[0], n_out), h6 = host(outs[1], n_out);
     double md = 0, mx = 0;
