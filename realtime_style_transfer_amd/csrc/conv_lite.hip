@@ -681,9 +681,8 @@ void lite_timeline_print(int nsteps) {
             }
     if (n) printf("    per step (us): staging+barrier %.2f, MFMA %.2f, epilogue %.2f (n=%d)\n", d[0] / n * 0.01,
                   d[1] / n * 0.01, d[2] / n * 0.01, n);
-    hipMemset(tl.data(), 0, 0);
-    std::vector<unsigned long long> z(tl.size(), 0);
-    hipMemcpyToSymbol(HIP_SYMBOL(lite_tl), z.data(), z.size() * 8);
+    std::vector<unsigned long long> z(tl.size(), 0);   // clear for the next measured launch
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(lite_tl), z.data(), z.size() * 8);
 }
 #endif
 

@@ -142,6 +142,8 @@ bool wino_x6_supported(int kh, int stride, int cin, int cout);
 std::vector<float> wino_x6_pack_weights(const float* kern, int cin);
 hipError_t wino_x6_prepare();
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st);
+// kernel-execution timestamps (hipExtLaunchKernel events) for the next wino_x6_launch on this thread
+void wino_x6_set_timing_events(hipEvent_t start, hipEvent_t stop);
 
 // Final 9x9 transposed conv with Cout = 3 on the VALU (conv_small.hip).
 struct SmallConvArgs {

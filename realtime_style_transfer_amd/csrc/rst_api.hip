@@ -503,7 +503,9 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
     hipEvent_t* ev = nullptr;
     if (h->prof_on && h->prof_step < h->prof_max_steps)
         ev = &h->prof_events[((size_t)h->prof_step * h->layers.size() + li) * 3];
-    if (ev) HIP_TRY(hipEventRecord(ev[0], st));
+    // the split-bf16 residual conv (the dominant kernel) records its own execution interval into ev[0..1]
+    const bool ext_ev = ev != nullptr && e.kind == K_WINOX6;
+    if (ev && !ext_ev) HIP_TRY(hipEventRecord(ev[0], st));
     const float* in = (e.pro_src < 0) ? content : h->layers[e.pro_src].d_out;
     const float2* pro_ab = (e.pro_src >= 0 && e.pro != PRO_NONE) ? h->layers[e.pro_src].d_ab : nullptr;
     const bool blend = two && pro_ab != nullptr;
@@ -588,6 +590,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.pro_mode = e.pro;
         a.linear = e.s.conv_relu ? 0 : 1;
         if (blend) return fail(RST_ERR_UNSUPPORTED, "Winograd conv has no two-style blend prologue");
+        if (ext_ev) wino_x6_set_timing_events(ev[0], ev[1]);
         HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
     } else {
         ConvArgs a{};
@@ -628,7 +631,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             HIP_TRY(conv_launch(e.tile, a, st));
         }
     }
-    if (ev) HIP_TRY(hipEventRecord(ev[1], st));
+    if (ev && !ext_ev) HIP_TRY(hipEventRecord(ev[1], st));
     if (e.s.norm == N_CIN) {
         FinalizeArgs f{};
         f.part = e.d_part;

@@ -31,6 +31,7 @@
 // LDS image [pixel][channel]; all 512 threads add the halves, apply bias + ReLU, store whole pixels'
 // channel quads (1 KB per wave instruction) and reduce the per-(workgroup, channel) two-pass {sum, M2, n}
 // for the conditional instance norm that follows.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstring>
@@ -543,16 +544,26 @@ hipError_t wino_x6_prepare() {
     return hipSuccess;
 }
 
+// Optional kernel-execution timestamps for the next launch (rst_profile: the dominant kernel's duration
+// measured by the dispatch itself, as rocprofv3 does, instead of marker events around the launch)
+static thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
+void wino_x6_set_timing_events(hipEvent_t start, hipEvent_t stop) {
+    g_ev_start = start;
+    g_ev_stop = stop;
+}
+
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
     if (a.cin % XCK != 0 || a.cin > XMAX_CIN || a.tiles_y != (a.H + XTH - 1) / XTH ||
         a.tiles_x != (a.W + XTW - 1) / XTW || (size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7F000000)
         return hipErrorInvalidValue;   // 32-bit staging offsets; the out-of-range store offset must stay out of range
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
+    const hipEvent_t e0 = g_ev_start, e1 = g_ev_stop;
+    g_ev_start = g_ev_stop = nullptr;
     switch (a.pro_mode) {
-        case PRO_NONE: hipLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
-        case PRO_AFF_RELU: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
-        case PRO_AFF: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
-        case PRO_AFF_RES: hipLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RES>, dim3(grid), dim3(YT), YLDS_BYTES, st, a); break;
+        case PRO_NONE: hipExtLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(YT), YLDS_BYTES, st, e0, e1, 0, a); break;
+        case PRO_AFF_RELU: hipExtLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(YT), YLDS_BYTES, st, e0, e1, 0, a); break;
+        case PRO_AFF: hipExtLaunchKernelGGL(wino_x6_kernel<PRO_AFF>, dim3(grid), dim3(YT), YLDS_BYTES, st, e0, e1, 0, a); break;
+        case PRO_AFF_RES: hipExtLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RES>, dim3(grid), dim3(YT), YLDS_BYTES, st, e0, e1, 0, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
