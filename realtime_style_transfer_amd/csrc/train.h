@@ -39,6 +39,7 @@ struct WgradArgs {
     int transposed;
     int nsplit;
     long span;               // set by wgrad_launch
+    int x6;                  // 1: residual-conv shape on the split-bf16 x6 kernel (fp32-level products)
 };
 int wgrad_choose_splits(const WgradArgs& a);
 size_t wgrad_slab_bytes(const WgradArgs& a);

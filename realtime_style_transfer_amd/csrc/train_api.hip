@@ -415,6 +415,9 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
         w.D = t->d_dz;
         w.slab = t->d_slab;
         w.dW = grad + T.woff;
+        // residual convs in the Winograd mode: weight gradient on the split-bf16 x6 kernel (fp32-level
+        // products, wgrad.hip); the other layers and the exact-f32 mode keep the f32-MFMA kernel
+        w.x6 = T.wino_fwd && s.res_block >= 0 ? 1 : 0;
         w.nsplit = wgrad_choose_splits(w);
         RST_HIP_TRY(wgrad_launch(w, st));
         if (!T.has_dgrad) continue;

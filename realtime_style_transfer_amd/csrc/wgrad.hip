@@ -180,6 +180,200 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradArgs a) {
             }
 }
 
+// ---- residual convs (3x3 s1, 128 -> 128): the same GEMM with exact split-bf16 products ----------------
+// Both operands are split exactly into three bf16 pieces when a stage is written to LDS (x = x0 + x1 + x2,
+// round-to-nearest-even at each step) and every 32x32 output tile accumulates the six terms a0b0 a0b1
+// a1b0 a0b2 a1b1 a2b0 on v_mfma_f32_32x32x16_bf16 (dropped terms <= 2^-25 of each product; the scheme of
+// wino_x6.hip): 6 bf16 MFMAs of 32 cycles per 16 pixels instead of 8 f32 ones of 64. LDS holds one stage
+// of KP = 32 pixels as [piece][row or column][pixel] bf16, rows padded to 80 B (odd 16-B slots: the
+// ds_read_b128 of 32 consecutive rows hit distinct bank groups); a staging thread owns 4 consecutive rows
+// (or columns) x 4 consecutive pixels, so its f32x4 loads (4 channels of one pixel) transpose into
+// pixel-pair bf16 words. Register prefetch of the next stage as in wgrad_mfma_kernel; slabs and the
+// fixed-order reduction are shared with it.
+namespace wx6 {
+constexpr int TR = 128, TC = 128, KP = 32;
+constexpr int RSB = 80;                       // bytes per LDS row (32 bf16 + 16 B pad)
+constexpr int PLANE = TR * RSB;               // bytes per piece plane (TR == TC)
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned piece(float& x, float& y) {   // nearest bf16 pair; (x, y) -= it (exact)
+    const unsigned p = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
+    x = x - __uint_as_float(p << 16);
+    y = y - __uint_as_float(p & 0xFFFF0000u);
+    return p;
+}
+}  // namespace wx6
+
+__global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs a) {
+    using namespace wx6;
+    __shared__ __attribute__((aligned(16))) unsigned char la[3 * PLANE], lb[3 * PLANE];
+    const WgradGeom g = wgrad_geom(a);
+    const int nr = (g.R + TR - 1) / TR, nc = (g.Cu + TC - 1) / TC;
+    int bid = blockIdx.x;
+    const int split = bid % a.nsplit;
+    bid /= a.nsplit;
+    const int tc = bid % nc;
+    const int trw = bid / nc;
+    const int r0 = trw * TR, c0 = tc * TC;
+    const long qhw = (long)a.Qh * a.Qw;
+    const long total = (long)a.batch * qhw;
+    const long q_begin = (long)split * a.span;
+    const long q_end = min(total, q_begin + a.span);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int li = lane & 31, lh = lane >> 5;
+
+    // staging: rows r0 + 4 rg .. +3 (one tap: Cs % 4 == 0) and columns c0 + 4 rg .. +3, pixels 4 pq .. +3
+    const int rg = tid >> 3, pq = tid & 7;   // pixel quad fastest: 8 lanes write 64 contiguous LDS bytes
+    const int r = r0 + 4 * rg;
+    const bool rvalid = r < g.R;
+    const int tap = rvalid ? r / g.Cs : 0;
+    const int ch = rvalid ? r - tap * g.Cs : 0;
+    const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+    const int dy = ky - a.pad_t, dx = kx - a.pad_l;
+    const int c = c0 + 4 * rg;
+    const bool cvalid = c < g.Cu;
+    f32x4 sreg[2][4], ureg[2][4];   // two stages in flight (one stage of MFMAs is shorter than the load latency)
+    // the thread's first pixel q0 + 4 pq as (image, row, column), advanced by KP per stage without
+    // divisions (the per-load decode cost as much VALU as the split)
+    int pb = 0, py = 0, px = 0;
+    {
+        const int qi = (int)(q_begin + 4 * pq), qhw_i = (int)qhw;
+        pb = qi / qhw_i;
+        const int rem = qi - pb * qhw_i;
+        py = rem / a.Qw;
+        px = rem - py * a.Qw;
+    }
+    auto advance = [&](int d) __attribute__((always_inline)) {
+        px += d;
+        while (px >= a.Qw) {
+            px -= a.Qw;
+            if (++py == a.Qh) {
+                py = 0;
+                ++pb;
+            }
+        }
+    };
+    auto load_stage = [&](long q0, auto SET) __attribute__((always_inline)) {
+        constexpr int st = decltype(SET)::value;
+        int b = pb, qy = py, qx = px;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const long q = q0 + 4 * pq + k;
+            f32x4 v = f32x4(0.f), u = f32x4(0.f);
+            if (q < q_end) {
+                const int sy = qy * a.stride + dy, sx = qx * a.stride + dx;
+                if (rvalid && sy >= 0 && sy < g.SH && sx >= 0 && sx < g.SW)
+                    v = *reinterpret_cast<const f32x4*>(g.S + (((size_t)b * g.SH + sy) * g.SW + sx) * g.Cs + ch);
+                if (cvalid) u = *reinterpret_cast<const f32x4*>(g.U + (size_t)q * g.Cu + c);
+            }
+            sreg[st][k] = v;
+            ureg[st][k] = u;
+            if (++qx == a.Qw) {
+                qx = 0;
+                if (++qy == a.Qh) {
+                    qy = 0;
+                    ++b;
+                }
+            }
+        }
+        advance(KP);
+    };
+    // f32x4 x 4 pixels -> rows 4rg + j, pixels 4pq .. 4pq+3 of the three piece planes (8 B per row and piece)
+    auto put = [&](unsigned char* base, const f32x4 (&v)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float x0 = v[0][j], y0 = v[1][j], x1 = v[2][j], y1 = v[3][j];
+            unsigned p[3][2];
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+                p[pc][0] = piece(x0, y0);
+                p[pc][1] = piece(x1, y1);
+            }
+            unsigned char* dst = base + (4 * rg + j) * RSB + 8 * pq;
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<uint2*>(dst + pc * PLANE) = make_uint2(p[pc][0], p[pc][1]);
+        }
+    };
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
+
+    auto mfma_stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int ks = 0; ks < KP / 16; ++ks) {
+            short8 A[2][3], B[2][3];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc) {
+                    A[m][pc] = *reinterpret_cast<const short8*>(la + pc * PLANE + (wr * 64 + m * 32 + li) * RSB +
+                                                                (16 * ks + 8 * lh) * 2);
+                    B[m][pc] = *reinterpret_cast<const short8*>(lb + pc * PLANE + (wc * 64 + m * 32 + li) * RSB +
+                                                                (16 * ks + 8 * lh) * 2);
+                }
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n) {
+                    floatx16& C = acc[m][n];
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[m][0], B[n][0], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[m][0], B[n][1], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[m][1], B[n][0], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[m][0], B[n][2], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[m][1], B[n][1], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[m][2], B[n][0], C, 0, 0, 0);
+                }
+        }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    const int nst = q_begin < q_end ? (int)((q_end - q_begin + KP - 1) / KP) : 0;
+    // stage k sits in register set k & 1: loaded two stages ahead, written to LDS one stage ahead
+    if (nst > 0) {
+        load_stage(q_begin, S0{});
+        if (nst > 1) load_stage(q_begin + KP, S1{});
+        put(la, sreg[0]);
+        put(lb, ureg[0]);
+        __syncthreads();
+    }
+    for (int k = 0; k < nst; k += 2) {
+        if (k + 2 < nst) load_stage(q_begin + (long)(k + 2) * KP, S0{});
+        mfma_stage();
+        __syncthreads();
+        if (k + 1 < nst) {
+            put(la, sreg[1]);
+            put(lb, ureg[1]);
+            __syncthreads();
+            if (k + 3 < nst) load_stage(q_begin + (long)(k + 3) * KP, S1{});
+            mfma_stage();
+            __syncthreads();
+            if (k + 2 < nst) {
+                put(la, sreg[0]);
+                put(lb, ureg[0]);
+                __syncthreads();
+            }
+        }
+    }
+    const int Rp = nr * TR, Cp = nc * TC;
+    float* out = a.slab + (size_t)split * Rp * Cp;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = (i & 3) + 8 * (i >> 2) + 4 * lh;
+                out[(size_t)(r0 + wr * 64 + m * 32 + row) * Cp + c0 + wc * 64 + n * 32 + li] = acc[m][n][i];
+            }
+}
+
 // ---- contract_start (9x9 s1 SAME, cin <= 17 -> 32): LDS-patch weight gradient --------------------------
 // The generic kernel above reads its S operand (the shifted input, R = 81 taps x 17 channels = 1377
 // rows) straight from global memory with 4-byte loads (17 channels: no 16-B vectors): every input
@@ -394,7 +588,9 @@ hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
     const int nr = (R + t.tr - 1) / t.tr, nc = (Cu + t.tc - 1) / t.tc;
     const dim3 grid((unsigned)(nr * nc * a.nsplit));
     const bool vs = Cs % 4 == 0;
-    if (t.tr == 128) {
+    if (a.x6 && !a.transposed && vs && t.tr == 128 && t.tc == 128 && wx6::KP == wg::KP) {
+        hipLaunchKernelGGL(wgrad_x6_kernel, grid, dim3(256), 0, st, a);
+    } else if (t.tr == 128) {
         if (vs) hipLaunchKernelGGL((wgrad_mfma_kernel<128, 128, 2, 2, true>), grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((wgrad_mfma_kernel<128, 128, 2, 2, false>), grid, dim3(256), 0, st, a);
     } else {
