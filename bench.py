@@ -232,7 +232,8 @@ def train_executed_work(plan, H, W, vgg_precision: str, transfer_precision: str)
     and the prediction's input gradient; the 3x3 convs after the first on bf16 with `terms` products per fp32
     product (bf16: 1, bf16x3: 3, bf16x6: 6), the 3-channel first conv and fp32 mode on f32. Gram: forward of
     two images and one backward on f32 MFMA."""
-    wino = transfer_precision == "fp32_winograd"
+    wino = transfer_precision in ("fp32_winograd", "winograd_bf16x6")
+    x6 = transfer_precision == "winograd_bf16x6"   # residual convs: 6 bf16 terms per product, on the bf16 pipe
 
     def conv_exec(i, l):
         Ho, Wo = l.out_hw
@@ -242,9 +243,13 @@ def train_executed_work(plan, H, W, vgg_precision: str, transfer_precision: str)
         if wino and l.block.startswith('residual'):
             return 2.0 * tiles * 16 * l.cin * l.cout
         return layer_flops(l)
-    t_fwd = sum(conv_exec(i, l) for i, l in enumerate(plan.layers))
-    t_wgrad = sum(layer_flops(l) for l in plan.layers)
-    t_dgrad = sum(conv_exec(i, l) for i, l in enumerate(plan.layers) if i > 0)
+    t_f32, t_bf16 = 0.0, 0.0
+    for i, l in enumerate(plan.layers):
+        work = conv_exec(i, l) + layer_flops(l) + (conv_exec(i, l) if i > 0 else 0.0)   # fwd + wgrad + dgrad
+        if x6 and l.block.startswith('residual'):
+            t_bf16 += 6 * work
+        else:
+            t_f32 += work
     terms = {"bf16": 1, "bf16x3": 3, "bf16x6": 6}.get(vgg_precision, 0)
     chans = [64, 64, 128, 128, 256, 256, 256, 512, 512, 512, 512, 512, 512]
     pools = {1, 3, 6, 9}
@@ -259,10 +264,10 @@ def train_executed_work(plan, H, W, vgg_precision: str, transfer_precision: str)
             gram += 3 * 2.0 * h * w * c * c
             h, w = h // 2, w // 2
         cin = c
-    return {"transfer_f32": t_fwd + t_wgrad + t_dgrad, "vgg_f32": vgg_f32, "vgg_bf16": vgg_bf16, "gram_f32": gram}
+    return {"transfer_f32": t_f32, "transfer_bf16": t_bf16, "vgg_f32": vgg_f32, "vgg_bf16": vgg_bf16, "gram_f32": gram}
 
 
-def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"):
+def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32", transfer="winograd_bf16x6"):
     from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
     from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
     dev = ctx.device
@@ -273,7 +278,7 @@ def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"
     # train_network.py fits the MobileNetV3Small style predictor jointly (stylePrediction.py:25-75)
     pr = StylePredictionTrainer(sins, cfg.style_feature_extractor_type, P, max_batch=TB, device=dev)
     tr = StyleTransferTrainingModel(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, loss_model=lm,
-                                    weights=weights, max_batch=TB, device=dev, style_predictor=pr)
+                                    weights=weights, max_batch=TB, device=dev, style_predictor=pr, precision=transfer)
     rng = np.random.default_rng(3000 + ctx.rank)
     x = {'content': torch.from_numpy(rng.random((TB,) + ins, dtype=np.float32)).to(dev),
          'style': torch.from_numpy(rng.random((TB, 1) + sins, dtype=np.float32)).to(dev)}
@@ -289,7 +294,7 @@ def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"
     ms = el * 1e3 / args.train_steps
     tfs = per_sample * TB / (ms * 1e-3) / 1e12
     ex = train_executed_work(plan, outs[0], outs[1], precision, tr.precision)
-    ideal_ms = TB * ((ex["vgg_bf16"]) / (BF16_MFMA_PEAK_TFLOPS * 1e12) +
+    ideal_ms = TB * ((ex["vgg_bf16"] + ex["transfer_bf16"]) / (BF16_MFMA_PEAK_TFLOPS * 1e12) +
                      (ex["transfer_f32"] + ex["vgg_f32"] + ex["gram_f32"]) / (FP32_MFMA_PEAK_TFLOPS * 1e12)) * 1e3
     return {"workload": f"{SPEC} train_network.py step (BASELINE config 4): MobileNetV3Small style predictor + "
                         f"transfer net, training-mode forward, VGG16/Gram loss (no depth term), backward of both, " +
@@ -299,15 +304,19 @@ def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"
             "frames_per_s": round(ctx.world * TB * args.train_steps / el, 3),
             "dtype": {"fp32": "fp32 (f32 MFMA)",
                       "bf16x6": "VGG16 3x3 convs: exact 3-piece split bf16 MFMA (fp32-level products, fp32 accumulate); "
-                                "transfer net and the rest fp32 (transfer_precision)",
+                                "transfer net and the rest fp32-level (see transfer_precision)",
                       "bf16x3": "VGG16 3x3 convs: 2-piece split bf16 MFMA (16-bit operands, fp32 accumulate); "
-                                "transfer net and the rest fp32 (transfer_precision)",
+                                "transfer net and the rest fp32-level (see transfer_precision)",
                       "bf16": "VGG16 3x3 convs: bf16 operands, fp32 accumulate (mixed_bfloat16 arithmetic); "
-                              "transfer net and the rest fp32 (transfer_precision)"}[precision],
+                              "transfer net and the rest fp32-level (see transfer_precision)"}[precision],
             "transfer_precision": {"fp32": "exact f32 MFMA",
                                    "fp32_winograd": "residual 3x3 convs (forward + input gradient) and the 9x9 start "
                                                     "conv (forward) as Winograd F(2x2,3x3) on f32 MFMA, the other "
-                                                    "transfer convs exact f32"}[tr.precision],
+                                                    "transfer convs exact f32",
+                                   "winograd_bf16x6": "residual 3x3 convs (forward, input gradient, weight gradient) on "
+                                                      "exact 3-piece split-bf16 MFMA products (fp32-level), the 9x9 start "
+                                                      "conv (forward) as Winograd F(2x2,3x3) on f32 MFMA, the other "
+                                                      "transfer convs exact f32"}[tr.precision],
             "tflop_per_sample": round(per_sample / 1e12, 4),
             "algorithmic_tflops_per_gpu": round(tfs, 2),
             "roofline": {"bound": "mfma (mixed)", "ideal_ms": round(ideal_ms, 3), "achieved_ms": round(ms, 3),

@@ -172,9 +172,11 @@ int rst_trainer_create(const rst_shape* shape, const float* weights_host, size_t
                        const rst_loss_shape* loss, const float* vgg_weights_host, size_t num_vgg_weights,
                        rst_trainer** out);
 /* As rst_trainer_create with the transfer network's conv arithmetic: RST_PRECISION_FP32 (exact-f32
- * MFMA, what rst_trainer_create uses) or RST_PRECISION_FP32_WINOGRAD (the residual-block 3x3 convs,
- * forward and input gradient, as Winograd F(2x2,3x3) on f32 MFMA; weight images re-transformed on
- * the device after every update). Same training loop as train_network.py:128-138 (Keras fit). */
+ * MFMA, what rst_trainer_create uses), RST_PRECISION_FP32_WINOGRAD (the residual-block 3x3 convs,
+ * forward and input gradient, and the 9x9 start conv forward as Winograd F(2x2,3x3) on f32 MFMA; weight
+ * images re-transformed on the device after every update) or RST_PRECISION_WINOGRAD_BF16X6 (as
+ * FP32_WINOGRAD with the residual convs' forward, input gradient and weight gradient on exact 3-piece
+ * split-bf16 MFMA products, fp32-level). Same training loop as train_network.py:128-138 (Keras fit). */
 int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, size_t num_weights,
                           const rst_loss_shape* loss, const float* vgg_weights_host, size_t num_vgg_weights,
                           int precision, rst_trainer** out);

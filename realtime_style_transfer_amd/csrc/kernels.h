@@ -140,6 +140,8 @@ hipError_t wino_launch(const WinoArgs& a, hipStream_t st);
 // MFMA terms (wino_x6.hip); same WinoArgs, U = wino_x6_pack_weights (bf16 pieces [cin/16][16][3][128][16]).
 bool wino_x6_supported(int kh, int stride, int cin, int cout);
 std::vector<float> wino_x6_pack_weights(const float* kern, int cin);
+// wino_x6_pack_weights on the device (kern: HWIO [3][3][cin][128] on the device; bitwise the host image)
+hipError_t wino_x6_transform_launch(const float* kern, int cin, float* U, hipStream_t st);
 hipError_t wino_x6_prepare();
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st);
 // kernel-execution timestamps (hipExtLaunchKernel events) for the next wino_x6_launch on this thread

@@ -175,12 +175,14 @@ namespace {
 int repack(rst_trainer* t, hipStream_t st) {
     for (TLayer& T : t->L) {
         if (T.e.kind == K_WINO9) RST_HIP_TRY(wino9_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
+        else if (T.e.kind == K_WINOX6) RST_HIP_TRY(wino_x6_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
         else if (T.wino_fwd) RST_HIP_TRY(wino_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
         else RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_w, T.e.d_w, T.n_w, st));
         RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_b, T.e.d_bias, T.n_b, st));
         if (T.has_dgrad && T.wino_dg) {
             RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_dg, T.d_kflip, T.n_dg, st));
-            RST_HIP_TRY(wino_transform_launch(T.d_kflip, T.dg.s.cin, T.d_wdg, st));
+            RST_HIP_TRY(T.dg.kind == K_WINOX6 ? wino_x6_transform_launch(T.d_kflip, T.dg.s.cin, T.d_wdg, st)
+                                              : wino_transform_launch(T.d_kflip, T.dg.s.cin, T.d_wdg, st));
         } else if (T.has_dgrad) {
             RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_dg, T.d_wdg, T.n_dg, st));
         }
@@ -226,7 +228,7 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.tiles_y = e.tiles_y;
             a.tiles_x = e.tiles_x;
             RST_HIP_TRY(wino9_launch(a, st));
-        } else if (e.kind == K_WINO) {
+        } else if (e.kind == K_WINO || e.kind == K_WINOX6) {
             WinoArgs a{};
             a.in = Pv->e.d_out;
             a.res = e.pro_res;
@@ -244,7 +246,7 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.tiles_x = e.tiles_x;
             a.pro_mode = e.pro;
             a.linear = e.s.conv_relu ? 0 : 1;
-            RST_HIP_TRY(wino_launch(a, st));
+            RST_HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
         } else {
             ConvArgs a = conv_geometry(e, B);
             a.in = Pv ? Pv->e.d_out : content;
@@ -415,9 +417,9 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
         w.D = t->d_dz;
         w.slab = t->d_slab;
         w.dW = grad + T.woff;
-        // residual convs in the Winograd mode: weight gradient on the split-bf16 x6 kernel (fp32-level
-        // products, wgrad.hip); the other layers and the exact-f32 mode keep the f32-MFMA kernel
-        w.x6 = T.wino_fwd && s.res_block >= 0 ? 1 : 0;
+        // WINOGRAD_BF16X6: the residual convs' weight gradient on the split-bf16 x6 kernel (fp32-level
+        // products, wgrad.hip); the other layers and modes keep the f32-MFMA kernel
+        w.x6 = T.e.kind == K_WINOX6 ? 1 : 0;
         w.nsplit = wgrad_choose_splits(w);
         RST_HIP_TRY(wgrad_launch(w, st));
         if (!T.has_dgrad) continue;
@@ -440,7 +442,7 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
             a.tiles_x = T.dg.tiles_x;
             a.pro_mode = PRO_NONE;
             a.linear = 1;
-            RST_HIP_TRY(wino_launch(a, st));
+            RST_HIP_TRY(T.dg.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
         } else {
             ConvArgs a = conv_geometry(T.dg, B);
             a.in = t->d_dz;
@@ -482,9 +484,10 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
     if (!shape || !weights_host || !loss || !vgg_weights_host || !out)
         return set_error(RST_ERR_INVALID, "rst_trainer_create: null argument");
     *out = nullptr;
-    if (precision != RST_PRECISION_FP32 && precision != RST_PRECISION_FP32_WINOGRAD)
-        return set_error(RST_ERR_INVALID, "rst_trainer_create_ex: transfer-network precision must be FP32 or "
-                                          "FP32_WINOGRAD");
+    if (precision != RST_PRECISION_FP32 && precision != RST_PRECISION_FP32_WINOGRAD &&
+        precision != RST_PRECISION_WINOGRAD_BF16X6)
+        return set_error(RST_ERR_INVALID, "rst_trainer_create_ex: transfer-network precision must be FP32, "
+                                          "FP32_WINOGRAD or WINOGRAD_BF16X6");
     if (shape->num_styles != 1)
         return set_error(RST_ERR_UNSUPPORTED, "rst_trainer_create: num_styles must be 1 (train_network.py:55)");
     if (shape->max_batch <= 0) return set_error(RST_ERR_INVALID, "rst_trainer_create: max_batch must be positive");
@@ -535,11 +538,14 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
         std::vector<float> packed, bias_n;
         // residual convs on Winograd when asked (their prologue always materialises the input for wgrad)
         // and the 9x9 start conv on the composite Winograd kernel (training mode: raw ReLU output + tile stats)
-        const int lp = (precision == RST_PRECISION_FP32_WINOGRAD && (s.res_block >= 0 || li == 0))
-                           ? precision : RST_PRECISION_FP32;
+        // WINOGRAD_BF16X6: residual convs (forward, input gradient, weight gradient) on the split-bf16 x6
+        // kernels; the start conv keeps the f32 composite Winograd (its x6 kernel is inference-only)
+        const bool wmode = precision == RST_PRECISION_FP32_WINOGRAD || precision == RST_PRECISION_WINOGRAD_BF16X6;
+        const int lp = !wmode || (s.res_block < 0 && li != 0) ? RST_PRECISION_FP32
+                       : (li == 0 ? RST_PRECISION_FP32_WINOGRAD : precision);
         if ((st = prepare_layer(T.e, s, kidx.data(), bidx.data(), packed, bias_n, lp)) != RST_OK)
             return fail_delete(t, st);
-        T.wino_fwd = T.e.kind == K_WINO || T.e.kind == K_WINO9;
+        T.wino_fwd = T.e.kind == K_WINO || T.e.kind == K_WINOX6 || T.e.kind == K_WINO9;
         if (T.e.kind == K_WINO9) T.e.n_part = T.e.tiles_y * T.e.tiles_x;   // batch statistics per tile
         std::vector<int> mw = T.wino_fwd ? std::vector<int>() : to_map(packed), mb = to_map(bias_n);
         T.n_w = packed.size();
@@ -594,7 +600,7 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
             if ((st = prepare_layer(T.dg, ds, kd.data(), zb.data(), pdg, bdg, lp)) != RST_OK) return fail_delete(t, st);
             if (T.dg.kind == K_SMALL) return fail_delete(t, set_error(RST_ERR_UNSUPPORTED, "dgrad kind"));
             T.dg.s = ds;
-            T.wino_dg = T.dg.kind == K_WINO;
+            T.wino_dg = T.dg.kind == K_WINO || T.dg.kind == K_WINOX6;
             std::vector<int> md = to_map(T.wino_dg ? kd : pdg);   // Winograd: canonical -> flipped HWIO
             T.n_dg = md.size();
             if ((st = t->alloc(&T.d_map_dg, md.size() * 4, md.data())) != RST_OK) return fail_delete(t, st);
@@ -626,11 +632,14 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
     }
     for (auto& T : t->L) {
         if (T.e.kind != K_SMALL) {
-            hipError_t pe = T.e.kind == K_WINO9 ? hipSuccess : (T.wino_fwd ? wino_prepare() : conv_prepare(T.e.tile));
+            hipError_t pe = T.e.kind == K_WINO9    ? hipSuccess
+                            : T.e.kind == K_WINOX6 ? wino_x6_prepare()
+                            : T.wino_fwd           ? wino_prepare()
+                                                   : conv_prepare(T.e.tile);
             if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));
         }
         if (T.has_dgrad) {
-            hipError_t pe = T.wino_dg ? wino_prepare() : conv_prepare(T.dg.tile);
+            hipError_t pe = T.dg.kind == K_WINOX6 ? wino_x6_prepare() : T.wino_dg ? wino_prepare() : conv_prepare(T.dg.tile);
             if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));
         }
     }

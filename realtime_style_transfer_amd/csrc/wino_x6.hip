@@ -535,6 +535,51 @@ std::vector<float> wino_x6_pack_weights(const float* kern, int cin) {
     return out;
 }
 
+// Device form of wino_x6_pack_weights (training re-packs after every optimizer step): one thread per
+// (ci, co), U = G g G^T in float64 with the host's operation order and no contraction, rounded to f32,
+// then split into three bf16 pieces with round-to-nearest-even at each step — bitwise the host image.
+__global__ __launch_bounds__(256) void wino_x6_transform_kernel(const float* __restrict__ kern, int cin,
+                                                                unsigned short* __restrict__ U) {
+#pragma clang fp contract(off)
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= cin * XN) return;
+    const int ci = idx / XN, co = idx - (idx / XN) * XN;
+    const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    double g[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) g[i][j] = kern[(((size_t)i * 3 + j) * cin + ci) * XN + co];
+    const int chunk = ci / XCK, c = ci % XCK;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double u = 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) u = u + G[p][i] * g[i][j] * G[q][j];
+            const float uf = (float)u;
+            // pieces as the host computes them: RNE to bf16, remainder exact in f32
+            const unsigned b0 = __builtin_bit_cast(unsigned short, (__bf16)uf);
+            const float r = uf - __uint_as_float(b0 << 16);
+            const unsigned b1 = __builtin_bit_cast(unsigned short, (__bf16)r);
+            const unsigned b2 = __builtin_bit_cast(unsigned short, (__bf16)(r - __uint_as_float(b1 << 16)));
+            const size_t base = ((size_t)chunk * XXI + p * 4 + q) * 3;
+            U[((base + 0) * XN + co) * XCK + c] = (unsigned short)b0;
+            U[((base + 1) * XN + co) * XCK + c] = (unsigned short)b1;
+            U[((base + 2) * XN + co) * XCK + c] = (unsigned short)b2;
+        }
+}
+
+hipError_t wino_x6_transform_launch(const float* kern, int cin, float* U, hipStream_t st) {
+    if (cin % XCK != 0 || cin > XMAX_CIN) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wino_x6_transform_kernel, dim3((unsigned)((cin * XN + 255) / 256)), dim3(256), 0, st, kern, cin,
+                       reinterpret_cast<unsigned short*>(U));
+    return hipGetLastError();
+}
+
 hipError_t wino_x6_prepare() {
     for (const void* k : {(const void*)wino_x6_kernel<PRO_NONE>, (const void*)wino_x6_kernel<PRO_AFF_RELU>,
                           (const void*)wino_x6_kernel<PRO_AFF>, (const void*)wino_x6_kernel<PRO_AFF_RES>}) {

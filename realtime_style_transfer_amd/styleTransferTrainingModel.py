@@ -107,8 +107,9 @@ class StyleTransferTrainingModel:
                  seed: int = 2, max_batch: int = 4, optimizer: Optional[RMSprop] = None, process_group=None,
                  device=None, name: str = "StyleTransferTrainingModel", style_predictor=None,
                  precision: str = "fp32_winograd"):
-        if precision not in ("fp32", "fp32_winograd"):
-            raise ValueError(f"transfer-network training precision must be 'fp32' or 'fp32_winograd', got {precision!r}")
+        if precision not in ("fp32", "fp32_winograd", "winograd_bf16x6"):
+            raise ValueError("transfer-network training precision must be 'fp32', 'fp32_winograd' or "
+                             f"'winograd_bf16x6', got {precision!r}")
         self.name = name
         self.precision = precision
         self.plan: Plan = network_plan(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, 1)

@@ -99,12 +99,15 @@ def _pool_route(tr, B):
 # the first pool, 5.7e-3 at block5_conv3), so the transfer-net gradients carry bf16 noise (with the
 # ReLU masks aligned: worst layer 1.8 % L2, loss terms 9e-4 / 1.8e-3 relative with the exact-f32 /
 # Winograd transfer convs, measured)
-# transfer: arithmetic of the transfer network's convs — "fp32" (exact-f32 MFMA) or "fp32_winograd"
-# (residual-block convs, forward + input gradient, as Winograd F(2x2,3x3): ~1e-6 relative per conv)
+# transfer: arithmetic of the transfer network's convs — "fp32" (exact-f32 MFMA), "fp32_winograd"
+# (residual-block convs, forward + input gradient, as Winograd F(2x2,3x3): ~1e-6 relative per conv) or
+# "winograd_bf16x6" (those residual convs and their weight gradient on exact 3-piece split-bf16 MFMA
+# products: dropped terms <= 2^-25 per product, the same 2e-3 bound)
 @pytest.mark.parametrize("name,precision,gtol,transfer", [
     ("A", "fp32", 2e-3, "fp32"), ("B", "fp32", 2e-3, "fp32"), ("A", "bf16x6", 2e-3, "fp32"),
     ("A", "bf16x3", 1e-3, "fp32"), ("A", "bf16", 0.05, "fp32"),
-    ("A", "fp32", 2e-3, "fp32_winograd"), ("B", "fp32", 2e-3, "fp32_winograd"), ("A", "bf16", 0.05, "fp32_winograd")])
+    ("A", "fp32", 2e-3, "fp32_winograd"), ("B", "fp32", 2e-3, "fp32_winograd"), ("A", "bf16", 0.05, "fp32_winograd"),
+    ("A", "fp32", 2e-3, "winograd_bf16x6"), ("B", "fp32", 2e-3, "winograd_bf16x6"), ("A", "bf16", 0.05, "winograd_bf16x6")])
 def test_training_step_matches_oracle(name, precision, gtol, transfer):
     _need_gpu()
     from oracle import torch_train as T
@@ -192,7 +195,7 @@ def test_training_step_matches_oracle(name, precision, gtol, transfer):
     assert gerr < gtol, gerr
 
 
-@pytest.mark.parametrize("transfer", ["fp32", "fp32_winograd"])
+@pytest.mark.parametrize("transfer", ["fp32", "fp32_winograd", "winograd_bf16x6"])
 def test_training_step_is_deterministic_and_learns(transfer):
     _need_gpu()
     cfg = CONFIGS['A']
