@@ -44,6 +44,9 @@ int main(int argc, char** argv) {
     // chain = 1: each timed launch reads the output the previous launch wrote (ping-pong, Cin = 128), as the
     // frame's residual convs do; chain = 2: the chain's zero-mean weights without the chaining
     const int chain = argc > 6 ? atoi(argv[6]) : 0;
+    // fin = 1: a CIN finalize launch (norm.hip) after every conv launch, as in the frame; the time reported
+    // is per (conv + finalize) pair, and a finalize-only loop is timed beside it
+    const int fin = argc > 7 ? atoi(argv[7]) : 0;
     auto hin = host_rand((size_t)B * H * W * C, zm ? -2.f : -1.f, zm ? 2.f : 3.f, 1);
     auto hres = host_rand((size_t)B * H * W * C, -1, 1, 5);
     // residual init U(0, 0.05); zero-mean in chain mode (a gain near 1 per layer keeps the chained values finite)
@@ -87,6 +90,30 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(cu6[i], U6, nu6 * 4, hipMemcpyDeviceToDevice));
     }
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    float2* fab;
+    CK(hipMalloc(&fab, (size_t)B * 128 * sizeof(float2)));
+    auto fin_args = [&](const float4* part) {
+        FinalizeArgs f{};
+        f.part = part;
+        f.ab = fab;
+        f.batch = B;
+        f.C = 128;
+        f.ntot = 128;
+        f.n_part = a.tiles_y * a.tiles_x;
+        f.phases = 1;
+        f.eps = 1e-5f;
+        return f;
+    };
+    if (fin) {
+        const FinalizeArgs f = fin_args(parts[1]);
+        for (int i = 0; i < 20; ++i) CK(finalize_launch(f, 0));
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < 200; ++i) CK(finalize_launch(f, 0));
+        CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("finalize alone: %.2f us/launch\n", ms * 1e3 / 200);
+    }
     const int iters = 200;
     const char* names[2] = {"wino   ", "wino_x6"};
     for (int v = 0; v < 2; ++v) {
@@ -107,6 +134,7 @@ int main(int argc, char** argv) {
                 x.out = pp[(i + 1) & 1];
             }
             CK(launch());
+            if (fin) CK(finalize_launch(fin_args(x.part), 0));
         }
         x.in = in; x.res = res; x.out = outs[v]; x.mat = mats[v]; x.U = v ? U6 : U32;
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
