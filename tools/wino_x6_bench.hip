@@ -47,6 +47,8 @@ int main(int argc, char** argv) {
     // fin = 1: a CIN finalize launch (norm.hip) after every conv launch, as in the frame; the time reported
     // is per (conv + finalize) pair, and a finalize-only loop is timed beside it
     const int fin = argc > 7 ? atoi(argv[7]) : 0;
+    // nomat = 1: no materialised block output (the frame's conv1 layers: a.mat == nullptr)
+    const int nomat = argc > 8 ? atoi(argv[8]) : 0;
     auto hin = host_rand((size_t)B * H * W * C, zm ? -2.f : -1.f, zm ? 2.f : 3.f, 1);
     auto hres = host_rand((size_t)B * H * W * C, -1, 1, 5);
     // residual init U(0, 0.05); zero-mean in chain mode (a gain near 1 per layer keeps the chained values finite)
@@ -118,7 +120,7 @@ int main(int argc, char** argv) {
     const char* names[2] = {"wino   ", "wino_x6"};
     for (int v = 0; v < 2; ++v) {
         WinoArgs x = a;
-        x.U = v ? U6 : U32; x.out = outs[v]; x.mat = mats[v]; x.part = parts[v];
+        x.U = v ? U6 : U32; x.out = outs[v]; x.mat = nomat ? nullptr : mats[v]; x.part = parts[v];
         auto launch = [&]() { return v ? wino_x6_launch(x, 0) : wino_launch(x, 0); };
         for (int i = 0; i < 20; ++i) CK(launch());
         CK(hipDeviceSynchronize());
@@ -126,7 +128,7 @@ int main(int argc, char** argv) {
         for (int i = 0; i < iters; ++i) {
             if (cold) {
                 const int j = i % cold;
-                x.in = cin_[j]; x.res = cres[j]; x.out = cout_[j]; x.mat = cmat[j];
+                x.in = cin_[j]; x.res = cres[j]; x.out = cout_[j]; x.mat = nomat ? nullptr : cmat[j];
                 x.U = v ? cu6[j] : cu32[j];
             }
             if (chain == 1 && C == 128) {
@@ -136,7 +138,7 @@ int main(int argc, char** argv) {
             CK(launch());
             if (fin) CK(finalize_launch(fin_args(x.part), 0));
         }
-        x.in = in; x.res = res; x.out = outs[v]; x.mat = mats[v]; x.U = v ? U6 : U32;
+        x.in = in; x.res = res; x.out = outs[v]; x.mat = nomat ? nullptr : mats[v]; x.U = v ? U6 : U32;
         CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = 1e3 * ms / iters;
