@@ -122,33 +122,6 @@ __device__ __forceinline__ void sfor(F&& f) {
     }
 }
 
-// 4x4 transpose inside each quad of lanes: lane i of a quad holds v[j] = (row j, channel 4c + i) of an
-// accumulator group; afterwards it holds (row i, channels 4c .. 4c+3), one 16-B store per lane. Two DPP
-// exchange stages (lane ^ 2 on register bit 1, lane ^ 1 on register bit 0), no LDS.
-__device__ __forceinline__ f32x4 quad_transpose(f32x4 v, int lane) {
-    auto xch = [](float x, auto CTRL) __attribute__((always_inline)) {
-        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), decltype(CTRL)::value, 0xF, 0xF, true));
-    };
-    using X2 = std::integral_constant<int, 0x4E>;   // quad_perm [2,3,0,1]: lane ^ 2
-    using X1 = std::integral_constant<int, 0xB1>;   // quad_perm [1,0,3,2]: lane ^ 1
-    const bool b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
-    // stage A: t[j] = in[lane ^ 2][j ^ 2] where lane bit 1 != j bit 1
-    const float s0 = xch(v.z, X2{}), s1 = xch(v.w, X2{}), s2 = xch(v.x, X2{}), s3 = xch(v.y, X2{});
-    f32x4 t;
-    t.x = b1 ? s0 : v.x;
-    t.y = b1 ? s1 : v.y;
-    t.z = b1 ? v.z : s2;
-    t.w = b1 ? v.w : s3;
-    // stage B: out[j] = t[lane ^ 1][j ^ 1] where lane bit 0 != j bit 0
-    const float u0 = xch(t.y, X1{}), u1 = xch(t.x, X1{}), u2 = xch(t.w, X1{}), u3 = xch(t.z, X1{});
-    f32x4 o;
-    o.x = b0 ? u0 : t.x;
-    o.y = b0 ? t.y : u1;
-    o.z = b0 ? u2 : t.z;
-    o.w = b0 ? t.w : u3;
-    return o;
-}
-
 // transposed-conv slots: (phase, operand position ty*2+tx); the kernel tap is ky = py + 2(1-ty), kx = px + 2(1-tx)
 __host__ __device__ constexpr int t_phase(int s) { return s < 4 ? 0 : (s < 6 ? 1 : (s < 8 ? 2 : 3)); }
 __host__ __device__ constexpr int t_pos(int s) {
@@ -425,35 +398,21 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
 
     // ---- epilogue of one tile ----------------------------------------------------------------------
     const int n = M::col(lane);
-    const int nq = n & ~3;   // channel quad of this lane's quad after the transpose
     const float bias = a.bias[n];
     const float2 bn = MODE == 0 ? a.bn_ab[n] : float2{1.f, 0.f};
-    // Stores: the accumulator holds one channel per lane; each group of 4 registers is transposed inside
-    // the lane quad (quad_transpose) so a lane stores one pixel's 4 channels as one 16-B write — a wave
-    // instruction writes 16 (Cout 16) or 8 (Cout 32) whole pixels instead of 64 scattered dwords (the
-    // dword-store epilogue was store-issue-bound: expand_1 spent more cycles in it than in its MFMAs).
-    auto store_group = [&](const acc_t& v, int g, auto&& addr_ok) __attribute__((always_inline)) {
-        const f32x4 q = quad_transpose(f32x4{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]}, lane);
-        const int row = M::row(4 * g + (lane & 3), lane);
-        addr_ok(row, q);
-    };
     auto epilogue = [&](const Tile& T) __attribute__((always_inline)) {
         if constexpr (MODE == 0) {   // bias + ReLU -> BatchNorm (inference affine) -> ReLU, NHWC store
-            acc_t y = (acc[0] + acc[1]) + acc[2];
+            const acc_t y = (acc[0] + acc[1]) + acc[2];
             const int oy = T.y0 + wave;
             const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
-            float* const orow = a.out + ((size_t)(T.b * a.Ho + oy) * a.Wo) * NC + nq;
+            float* const orow = a.out + ((size_t)(T.b * a.Ho + oy) * a.Wo) * NC + n;
 #pragma unroll
             for (int j = 0; j < C::NACC; ++j) {
-                const float v = fmaxf(y[j] + bias, 0.f);
-                y[j] = fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                const int ox = T.x0 + M::row(j, lane);
+                float v = fmaxf(y[j] + bias, 0.f);
+                v = fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                if (full || (oy < a.Ho && ox < a.Wo)) orow[(size_t)ox * NC] = v;
             }
-#pragma unroll
-            for (int g = 0; g < C::NACC / 4; ++g)
-                store_group(y, g, [&](int row, const f32x4& q) __attribute__((always_inline)) {
-                    const int ox = T.x0 + row;
-                    if (full || (oy < a.Ho && ox < a.Wo)) *reinterpret_cast<f32x4*>(orow + (size_t)ox * NC) = q;
-                });
         } else {   // bias, pixel-shuffle store, per-tile CIN statistics over the four phases
             acc[0] = acc[0] + acc[4];
             const int p = T.y0 + wave;
@@ -461,14 +420,18 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             float s = 0.f, cnt = 0.f;
             // interior tiles (every pixel inside) store without per-element guards
             const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
-            float* const orow = a.out + ((size_t)(T.b * Ho2 + 2 * p) * Wo2) * NC + nq;
+            float* const orow = a.out + ((size_t)(T.b * Ho2 + 2 * p) * Wo2) * NC + n;
             if (full) {
 #pragma unroll
                 for (int ph = 0; ph < 4; ++ph)
 #pragma unroll
                     for (int j = 0; j < C::NACC; ++j) {
+                        const int qq = T.x0 + M::row(j, lane);
                         const float v = acc[ph][j] + bias;
                         acc[ph][j] = v;
+#if (LITE_SKIP & 8) == 0
+                        orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
+#endif
                         s += v;
                     }
                 cnt = 4.f * C::NACC;
@@ -481,22 +444,12 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         const float v = acc[ph][j] + bias;
                         acc[ph][j] = v;
                         if (p < a.Ho && qq < a.Wo) {
+                            orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
                             s += v;
                             cnt += 1.f;
                         }
                     }
             }
-#if (LITE_SKIP & 8) == 0
-#pragma unroll
-            for (int ph = 0; ph < 4; ++ph)
-#pragma unroll
-                for (int g = 0; g < C::NACC / 4; ++g)
-                    store_group(acc[ph], g, [&](int row, const f32x4& q) __attribute__((always_inline)) {
-                        const int qq = T.x0 + row;
-                        if (full || (p < a.Ho && qq < a.Wo))
-                            *reinterpret_cast<f32x4*>(orow + ((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC) = q;
-                    });
-#endif
             if (a.part != nullptr && (LITE_SKIP & 32) == 0) {
                 // lanes n, n + MS, ... hold column n: reduce over them, then over the 4 waves (fixed order)
 #pragma unroll
