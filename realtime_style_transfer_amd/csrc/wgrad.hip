@@ -481,6 +481,109 @@ static bool wgrad9_applies(const WgradArgs& a) {
            a.pad_t == 4 && a.pad_l == 4 && a.Qh == a.XH && a.Qw == a.XW;
 }
 
+// ---- expand_last (9x9 s1 SAME Conv2DTranspose, 16 -> 3): LDS-patch weight gradient ---------------------
+// The generic kernel's shifted operand here is dZ with 3 channels (no 16-B vectors: 4-byte global loads,
+// every element fetched once per tap) and its 256 x 32 tile idles half of N (Cu = 16): 1.1 ms per B=4
+// step for 14 GFLOP. As wgrad9 for the start conv: a workgroup walks 8 x 16 pixel tiles, stages the
+// 16 x 24 x 3 dZ patch (planar [co][row][col]) and the 128-pixel X tile transposed to [ci][pixel] once, and
+//   dW[(tap, co)][ci] += sum_p X[p][ci] dZ[p + tap - pad][co]
+// runs on v_mfma_f32_16x16x4_f32 with M = the 16 input channels (A = X^T, one ds_read_b128 per 4 k-steps),
+// N = the 243 (tap, co) columns (16 tiles of 16, 4 per wave; column decode once per kernel), K = pixels:
+// k-step s of lane group kg is pixel 32 kg + s, so a lane's 4 consecutive k-steps are 4 consecutive pixels
+// of one tile row. Each workgroup writes one [256][16] slab; wgrad_reduce_kernel sums them in a fixed order.
+namespace wt9 {
+constexpr int TH = 8, TW = 16, NPX = TH * TW;         // pixels per tile
+constexpr int PR = TH + 8, PC = TW + 8, PRS = 25;     // dZ patch rows / cols / row stride (floats)
+constexpr int PL = PR * PRS;                          // plane stride (400 floats)
+constexpr int CS = 3, CU = 16, NCOL = 81 * CS, NTW = 4;   // 243 columns: 16 tiles of 16, 4 per wave
+constexpr int RP = 16 * 16, CP = CU;                  // slab rows (padded columns) x slab columns
+constexpr int XS = NPX + 4;                           // X^T row stride (floats)
+constexpr int ZERO = CS * PL;                         // zero words after the planes (padding columns)
+constexpr int XOFF = CS * PL + 8;                     // X^T offset (16-B aligned)
+constexpr int LDS_FL = XOFF + CU * XS;
+}  // namespace wt9
+
+__global__ __launch_bounds__(256, 2) void wgradT9_kernel(WgradArgs a) {
+    using namespace wt9;
+    __shared__ __attribute__((aligned(16))) float lds[LDS_FL];
+    float* const patch = lds;           // [co][PR][PRS] + zero words
+    float* const xt = lds + XOFF;       // [ci][XS]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, kg = lane >> 4;
+    const int tiles_x = (a.Qw + TW - 1) / TW, tiles_y = (a.Qh + TH - 1) / TH;
+    const int ntiles = a.batch * tiles_x * tiles_y;
+
+    int coff[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = (wave + 4 * j) * 16 + l16;   // wave w owns column tiles w, w+4, w+8, w+12
+        if (n < NCOL) {
+            const int tap = n / CS, co = n % CS;
+            coff[j] = co * PL + (tap / 9) * PRS + tap % 9;
+        } else {
+            coff[j] = -1;
+        }
+    }
+    f32x4 acc[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (tid < 8) patch[ZERO + tid] = 0.f;
+
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int b = t / (tiles_x * tiles_y), rem = t % (tiles_x * tiles_y);
+        const int y0 = (rem / tiles_x) * TH, x0 = (rem % tiles_x) * TW;
+        __syncthreads();   // previous tile's operands consumed
+        for (int i = tid; i < PR * PC * CS; i += 256) {
+            const int c = i % CS, px = i / CS;
+            const int r = px / PC, q = px % PC;
+            const int gy = y0 - a.pad_t + r, gx = x0 - a.pad_l + q;
+            float v = 0.f;
+            if (gy >= 0 && gy < a.DH && gx >= 0 && gx < a.DW) v = a.D[(((size_t)b * a.DH + gy) * a.DW + gx) * CS + c];
+            patch[c * PL + r * PRS + q] = v;
+        }
+        for (int i = tid; i < NPX * (CU / 4); i += 256) {   // X tile, one float4 (4 channels) per item
+            const int cq = i & 3, p = i >> 2;
+            const int oy = y0 + p / TW, ox = x0 + p % TW;
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (oy < a.Qh && ox < a.Qw)
+                v = *reinterpret_cast<const f32x4*>(a.X + (((size_t)b * a.XH + oy) * a.XW + ox) * CU + 4 * cq);
+            xt[(4 * cq + 0) * XS + p] = v.x;
+            xt[(4 * cq + 1) * XS + p] = v.y;
+            xt[(4 * cq + 2) * XS + p] = v.z;
+            xt[(4 * cq + 3) * XS + p] = v.w;
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int g = 0; g < 8; ++g) {
+            const int p0 = 32 * kg + 4 * g;
+            const f32x4 a4 = *reinterpret_cast<const f32x4*>(xt + l16 * XS + p0);
+            const int pixoff = (p0 / TW) * PRS + p0 % TW;
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                const float* src = patch + (coff[j] >= 0 ? coff[j] + pixoff : ZERO);
+                const int st = coff[j] >= 0 ? 1 : 0;
+                const float b0 = src[0], b1 = src[st], b2 = src[2 * st], b3 = src[3 * st];
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b0, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b1, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b2, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b3, acc[j], 0, 0, 0);
+            }
+        }
+    }
+    // slab [blockIdx][row n = (tap, co)][ci]: accumulator i of lane (l16, kg) is ci = 4 kg + i, n = tile*16 + l16
+    float* slab = a.slab + (size_t)blockIdx.x * RP * CP;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = (wave + 4 * j) * 16 + l16;
+        *reinterpret_cast<f32x4*>(slab + (size_t)n * CP + 4 * kg) = acc[j];
+    }
+}
+
+static bool wgradT9_applies(const WgradArgs& a) {
+    return a.transposed && a.kh == 9 && a.kw == 9 && a.stride == 1 && a.C2 == wt9::CS && a.C1 == wt9::CU &&
+           a.Qh == a.XH && a.Qw == a.XW && a.DH == a.XH && a.DW == a.XW;
+}
+
 // dW[r][c] = sum over splits (fixed order)
 // dW = sum over the nsplit slabs, in a fixed order: a workgroup owns 64 float4 columns of dW; its four
 // waves sum contiguous quarters of the slab range (8 loads in flight per lane), then wave 0 adds the
@@ -546,7 +649,7 @@ void wgrad_dims(const WgradArgs& a, int& R, int& Cu, int& Cs) {
 constexpr int W9_BLOCKS = 512;   // two workgroups per CU, each a persistent walk over the pixel tiles
 
 int wgrad_choose_splits(const WgradArgs& a) {
-    if (wgrad9_applies(a)) return W9_BLOCKS;
+    if (wgrad9_applies(a) || wgradT9_applies(a)) return W9_BLOCKS;
     int R, Cu, Cs;
     wgrad_dims(a, R, Cu, Cs);
     const WTile t = wgrad_tile(a);
@@ -560,6 +663,7 @@ int wgrad_choose_splits(const WgradArgs& a) {
 
 size_t wgrad_slab_bytes(const WgradArgs& a) {
     if (wgrad9_applies(a)) return (size_t)a.nsplit * w9::NCOLP * 32 * sizeof(float);
+    if (wgradT9_applies(a)) return (size_t)a.nsplit * wt9::RP * wt9::CP * sizeof(float);
     int R, Cu, Cs;
     wgrad_dims(a, R, Cu, Cs);
     const WTile t = wgrad_tile(a);
@@ -577,6 +681,15 @@ hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
         if (e != hipSuccess) return e;
         const size_t n4 = (size_t)R * Cu / 4;
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, a, w9::NCOLP, 32);
+        return hipGetLastError();
+    }
+    if (wgradT9_applies(a)) {
+        if (a.nsplit < 1) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(wgradT9_kernel, dim3((unsigned)a.nsplit), dim3(256), 0, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const size_t n4 = (size_t)R * Cu / 4;
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, a, wt9::RP, wt9::CP);
         return hipGetLastError();
     }
     if (Cu % 4 != 0) return hipErrorInvalidValue;
