@@ -520,7 +520,8 @@ static ConvTile tile_of() {
     X(16, 2, 2, 1, 4, 32, 8, 16, 4, 1, 4, 1)         \
     X(17, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 1)         \
     X(18, 1, 1, 1, 32, 64, 8, 16, 2, 2, 1, 1)         \
-    X(19, 1, 1, 1, 32, 128, 4, 16, 2, 2, 1, 1)
+    X(19, 1, 1, 1, 32, 128, 4, 16, 2, 2, 1, 1)        \
+    X(20, 1, 1, 1, 32, 32, 8, 16, 4, 1, 1, 1)
 
 bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
     // pick CK (Cin chunk) and NT (output columns per workgroup)

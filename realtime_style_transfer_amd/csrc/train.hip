@@ -224,6 +224,60 @@ hipError_t scaled_diff_launch(const float* a, const float* b, float scale, float
     return hipGetLastError();
 }
 
+// VGG16 conv0 input gradient, second half (train_api.hip vgg_backward): the 3x3 conv 64 -> 3 runs as a
+// 1x1 conv 64 -> 27 (+5 zero) columns P[q][(tap, c)] on conv_mfma (a 3-column output tile idled 29 of the
+// MFMA's 32 columns: 681 us per B=4 step), and out[y][x][c] = sum over the 9 taps (ky, kx) of
+// P[y + ky - 1][x + kx - 1][(3 ky + kx) 3 + c] (SAME, pad 1; zero outside), fixed tap order.
+// Workgroup = 4 output rows x 64 columns (one pixel per thread): the (4+2) x (64+2) x 32 source rows of
+// P are staged into LDS with coalesced 16-B loads (a pixel-per-thread gather of 12 B from each of nine
+// 128-B rows ran at 274 us per B=4 step for 240 MB), then each thread sums its 9 taps from LDS.
+constexpr int T3_TH = 4, T3_TW = 64, T3_SH = T3_TH + 2, T3_SW = T3_TW + 2, T3_PS = 33;   // pixel stride (floats)
+__global__ __launch_bounds__(256) void tap3_sum_kernel(const float* __restrict__ p, float* __restrict__ out, int B,
+                                                       int H, int W) {
+    __shared__ float tile[T3_SH * T3_SW * T3_PS];
+    const int tiles_x = (W + T3_TW - 1) / T3_TW, tiles_y = (H + T3_TH - 1) / T3_TH;
+    const int t = blockIdx.x;
+    const int b = t / (tiles_x * tiles_y), rem = t % (tiles_x * tiles_y);
+    const int y0 = (rem / tiles_x) * T3_TH, x0 = (rem % tiles_x) * T3_TW;
+    for (int i = threadIdx.x; i < T3_SH * T3_SW * 8; i += 256) {
+        const int q = i & 7, px = i >> 3;
+        const int r = px / T3_SW, c = px % T3_SW;
+        const int gy = y0 - 1 + r, gx = x0 - 1 + c;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W)
+            v = *reinterpret_cast<const float4*>(p + (((size_t)b * H + gy) * W + gx) * 32 + 4 * q);
+        float* d = tile + px * T3_PS + 4 * q;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+    }
+    __syncthreads();
+    const int ty = threadIdx.x / T3_TW, tx = threadIdx.x % T3_TW;
+    const int y = y0 + ty, x = x0 + tx;
+    if (y >= H || x >= W) return;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {   // zero-padded halo: out-of-image taps add 0
+            const float* q = tile + ((ty + ky) * T3_SW + tx + kx) * T3_PS + (3 * ky + kx) * 3;
+            s0 += q[0];
+            s1 += q[1];
+            s2 += q[2];
+        }
+    const size_t o = (((size_t)b * H + y) * W + x) * 3;
+    out[o + 0] = s0;
+    out[o + 1] = s1;
+    out[o + 2] = s2;
+}
+
+hipError_t tap3_sum_launch(const float* p, float* out, int B, int H, int W, hipStream_t st) {
+    const long n = (long)B * ((H + T3_TH - 1) / T3_TH) * ((W + T3_TW - 1) / T3_TW);
+    hipLaunchKernelGGL(tap3_sum_kernel, dim3((unsigned)n), dim3(256), 0, st, p, out, B, H, W);
+    return hipGetLastError();
+}
+
 // total variation backward: d/dx of factor * (sum |x[y+1]-x[y]| + sum |x[:,x+1]-x[:,x]|), added to g
 __global__ __launch_bounds__(256) void tv_bwd_kernel(const float* __restrict__ x, float factor, float* __restrict__ g,
                                                      int B, int H, int W, int C) {

@@ -141,6 +141,7 @@ struct rst_trainer {
     std::vector<TLayer> L;
     rst_loss_handle* loss = nullptr;
     ConvBwd vgg[13];
+    ConvBwd vgg0p;   // VGG conv0 input gradient as a 1x1 conv 64 -> (tap, c) columns + tap3_sum
     ConvBwd gram[4];
     std::vector<void*> allocs;
     float* d_wc = nullptr;        // canonical weights (Keras order)
@@ -309,7 +310,35 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
             RST_HIP_TRY(hipMemcpyAsync(t->d_vgg_dbg[i], g, (size_t)B * c.H * c.W * c.cout * 4, hipMemcpyDeviceToDevice,
                                        st));
         const bool pooled = i > 0 && VGG_POOL[i - 1];
-        float* dst = i == 0 ? gimg : (pooled ? t->d_vpool : t->d_vg[which ^ 1]);
+        if (i == 0) {   // 64 -> 3: 1x1 conv to the 27 (tap, c) columns (into the free gradient buffer), tap sum
+            const ConvBwd& pb = t->vgg0p;
+            float* pbuf = t->d_vg[which ^ 1];
+            ConvArgs a{};
+            a.in = g;
+            a.res = c.d_out;              // ReLU mask from the forward output
+            a.wpk = pb.d_w;
+            a.bias = t->d_zero;
+            a.out = pbuf;
+            a.batch = B;
+            a.H = c.H;
+            a.W = c.W;
+            a.cin = c.cout;
+            a.Ho = c.H;
+            a.Wo = c.W;
+            a.ntot = 32;
+            a.cout = 32;
+            a.pad_t = a.pad_l = 0;
+            a.tiles_y = pb.tiles_y;
+            a.tiles_x = pb.tiles_x;
+            a.n_blocks = pb.n_blocks;
+            a.nchunks = pb.nchunks;
+            a.pro_mode = PRO_MASK;
+            a.epi_mode = EPI_NONE;
+            RST_HIP_TRY(conv_launch(pb.tile, a, st));
+            RST_HIP_TRY(tap3_sum_launch(pbuf, gimg, B, c.H, c.W, st));
+            break;
+        }
+        float* dst = pooled ? t->d_vpool : t->d_vg[which ^ 1];
         ConvArgs a{};
         a.in = g;
         a.res = c.d_out;                  // ReLU mask from the forward output
@@ -676,6 +705,23 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
             if ((st = t->alloc(&vb.d_w, pk.size() * 4, pk.data())) != RST_OK) return fail_delete(t, st);
             hipError_t pe = conv_prepare(vb.tile);
             if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));
+            if (i == 0) {   // the 1x1 form used by vgg_backward: W1[ci][(tap, c)] = wd[tap][ci][c], 27 of 32 columns
+                ConvBwd& pb = t->vgg0p;
+                if (cin != 3 || !conv_select(1, 1, cout, 32, &pb.tile))
+                    return fail_delete(t, set_error(RST_ERR_UNSUPPORTED, "no 1x1 tile for the VGG conv0 input gradient"));
+                std::vector<float> w1((size_t)cout * 32, 0.f);
+                for (int tp = 0; tp < 9; ++tp)
+                    for (int co = 0; co < cout; ++co)
+                        for (int ci = 0; ci < 3; ++ci) w1[(size_t)co * 32 + tp * 3 + ci] = wd[((size_t)tp * cout + co) * 3 + ci];
+                pb.tiles_y = (c.H + pb.tile.th - 1) / pb.tile.th;
+                pb.tiles_x = (c.W + pb.tile.tw - 1) / pb.tile.tw;
+                pb.n_blocks = (32 + pb.tile.nt - 1) / pb.tile.nt;
+                pb.nchunks = (cout + pb.tile.ck - 1) / pb.tile.ck;
+                std::vector<float> pk1 = pack_conv_tiles(w1, 1, cout, 32, pb.tile);
+                if ((st = t->alloc(&pb.d_w, pk1.size() * 4, pk1.data())) != RST_OK) return fail_delete(t, st);
+                pe = conv_prepare(pb.tile);
+                if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));
+            }
             cin = cout;
         }
         size_t max_packed = 0;

@@ -17,4 +17,10 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_train -o run -- \
     python tools/train_step_run.py --steps 5 --transfer winograd_bf16x6 > gpurun_out/train_prof.log 2>&1 || { tail -30 gpurun_out/train_prof.log; exit 1; }
 tail -3 gpurun_out/train_prof.log
-echo "measure ok"
+
+rm -rf gpurun_out/pmc_f gpurun_out/pmc_w
+timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_f -o run -- \
+    python tools/wino_probe.py winograd_bf16x6 3 > gpurun_out/pmc_f.log 2>&1 || { tail -20 gpurun_out/pmc_f.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_w -o run -- \
+    python tools/wino_probe.py winograd_bf16x6 3 > gpurun_out/pmc_w.log 2>&1 || { tail -20 gpurun_out/pmc_w.log; exit 1; }
+echo "pmc ok"
