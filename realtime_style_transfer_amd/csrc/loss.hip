@@ -16,14 +16,15 @@ namespace rst {
 __global__ __launch_bounds__(256) void maxpool2_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
                                                        int H, int W, int C) {
     const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
-    const long total = (long)B * Ho * Wo * C4;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256L) {
-        const int c4 = (int)(i % C4);
-        long p = i / C4;
-        const int ox = (int)(p % Wo);
+    const int total = B * Ho * Wo * C4;   // < 2^31 (maxpool2_launch): 32-bit index math (a 64-bit division
+                                          // chain per element cost more than the loads)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        const int c4 = i % C4;
+        int p = i / C4;
+        const int ox = p % Wo;
         p /= Wo;
-        const int oy = (int)(p % Ho);
-        const int b = (int)(p / Ho);
+        const int oy = p % Ho;
+        const int b = p / Ho;
         const float4* base = reinterpret_cast<const float4*>(x + (((size_t)b * H + 2 * oy) * W + 2 * ox) * C) + c4;
         const float4 a0 = base[0], a1 = base[C4], a2 = base[(size_t)W * C4], a3 = base[(size_t)W * C4 + C4];
         float4 m;
@@ -36,7 +37,7 @@ __global__ __launch_bounds__(256) void maxpool2_kernel(const float* __restrict__
 }
 
 hipError_t maxpool2_launch(const float* x, float* y, int B, int H, int W, int C, hipStream_t st) {
-    if (C % 4 != 0) return hipErrorInvalidValue;
+    if (C % 4 != 0 || (long)B * (H / 2) * (W / 2) * (C / 4) >= (1L << 31)) return hipErrorInvalidValue;
     const long total = (long)B * (H / 2) * (W / 2) * (C / 4);
     long blocks = (total + 255) / 256;
     if (blocks > 16384) blocks = 16384;
