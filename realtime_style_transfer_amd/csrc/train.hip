@@ -63,6 +63,98 @@ __global__ __launch_bounds__(256) void norm_bwd_reduce_kernel(NormBwdArgs a) {
     }
 }
 
+// The same two passes with 16-B vectors (C % 4 == 0: every layer but expand_last): thread = (pixel lane,
+// channel quad), 32-bit pixel indices; per channel the partial sums keep a fixed order (deterministic).
+// The scalar forms above spent more issue on 64-bit index math than on their loads.
+typedef float nf4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void norm_bwd_reduce4_kernel(NormBwdArgs a) {
+    __shared__ float2 red[256 * 4];
+    const int tile = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int C = a.C, C4 = C / 4;
+    const int R = 256 / C4;
+    const int c4 = tid % C4, r = tid / C4;
+    nf4 s1 = nf4{0.f, 0.f, 0.f, 0.f}, s2 = s1;
+    if (r < R) {
+        float2 ab[4], mr[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ab[k] = a.ab[b * C + 4 * c4 + k];
+            mr[k] = a.mr[b * C + 4 * c4 + k];
+        }
+        const int p0 = tile * a.tile, p1 = min(a.hw, p0 + a.tile);
+        const float* zb = a.z + (size_t)b * a.hw * C + 4 * c4;
+        const float* gb = a.g + (size_t)b * a.hw * C + 4 * c4;
+        for (int p = p0 + r; p < p1; p += R) {
+            const nf4 z = *reinterpret_cast<const nf4*>(zb + (size_t)p * C);
+            const nf4 g = *reinterpret_cast<const nf4*>(gb + (size_t)p * C);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float dn = post_grad(a.post, g[k], z[k], ab[k]);
+                s1[k] += dn;
+                s2[k] = fmaf(dn, (z[k] - mr[k].x) * mr[k].y, s2[k]);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[tid * 4 + k] = make_float2(s1[k], s2[k]);
+    __syncthreads();
+    if (tid < C) {
+        const int q4 = tid / 4, k = tid % 4;
+        float t1 = 0.f, t2 = 0.f;
+        for (int q = 0; q < R; ++q) {
+            const float2 v = red[(q * C4 + q4) * 4 + k];
+            t1 += v.x;
+            t2 += v.y;
+        }
+        a.part[((size_t)b * C + tid) * a.n_tiles + tile] = make_float2(t1, t2);
+    }
+}
+
+__global__ __launch_bounds__(256) void norm_bwd_apply4_kernel(NormBwdArgs a) {
+    __shared__ float red[256 * 4];
+    const int tile = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int C = a.C, C4 = C / 4;
+    const int R = 256 / C4;
+    const int c4 = tid % C4, r = tid / C4;
+    nf4 sdz = nf4{0.f, 0.f, 0.f, 0.f};
+    if (r < R) {
+        float2 ab[4], mr[4], kk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ab[k] = a.ab[b * C + 4 * c4 + k];
+            mr[k] = a.mr[b * C + 4 * c4 + k];
+            kk[k] = a.consts[b * C + 4 * c4 + k];
+        }
+        const int p0 = tile * a.tile, p1 = min(a.hw, p0 + a.tile);
+        const size_t base = (size_t)b * a.hw * C + 4 * c4;
+        for (int p = p0 + r; p < p1; p += R) {
+            const size_t i = base + (size_t)p * C;
+            const nf4 z = *reinterpret_cast<const nf4*>(a.z + i);
+            const nf4 g = *reinterpret_cast<const nf4*>(a.g + i);
+            nf4 dz;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float dn = post_grad(a.post, g[k], z[k], ab[k]);
+                const float xh = (z[k] - mr[k].x) * mr[k].y;
+                float d = ab[k].x * (dn - kk[k].x - xh * kk[k].y);
+                if (a.conv_relu && !(z[k] > 0.f)) d = 0.f;
+                dz[k] = d;
+            }
+            *reinterpret_cast<nf4*>(a.dz + i) = dz;
+            sdz += dz;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[tid * 4 + k] = sdz[k];
+    __syncthreads();
+    if (tid < C) {
+        const int q4 = tid / 4, k = tid % 4;
+        float t = 0.f;
+        for (int q = 0; q < R; ++q) t += red[(q * C4 + q4) * 4 + k];
+        a.part[((size_t)b * C + tid) * a.n_tiles + tile].x = t;
+    }
+}
+
 // per (b, c) [per c when merge_images]: S1, S2 in f64 -> consts (S1/N, S2/N), and the parameter grads
 __global__ __launch_bounds__(64) void norm_bwd_finalize_kernel(NormBwdArgs a) {
     const int c = blockIdx.x, b = blockIdx.y;
@@ -142,12 +234,15 @@ __global__ __launch_bounds__(64) void norm_bwd_bias_kernel(NormBwdArgs a) {
 hipError_t norm_bwd_launch(const NormBwdArgs& a0, hipStream_t st) {
     NormBwdArgs a = a0;
     if (a.C > 256) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(norm_bwd_reduce_kernel, dim3(a.n_tiles, a.batch), dim3(256), 0, st, a);
+    const bool v4 = a.C % 4 == 0 && (size_t)a.hw * a.C < ((size_t)1 << 31);
+    if (v4) hipLaunchKernelGGL(norm_bwd_reduce4_kernel, dim3(a.n_tiles, a.batch), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(norm_bwd_reduce_kernel, dim3(a.n_tiles, a.batch), dim3(256), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3(a.C, a.batch), dim3(64), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(a.n_tiles, a.batch), dim3(256), 0, st, a);
+    if (v4) hipLaunchKernelGGL(norm_bwd_apply4_kernel, dim3(a.n_tiles, a.batch), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(a.n_tiles, a.batch), dim3(256), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (a.dconv_bias != nullptr) {
         hipLaunchKernelGGL(norm_bwd_bias_kernel, dim3(a.C), dim3(64), 0, st, a);
