@@ -591,8 +591,20 @@ __global__ __launch_bounds__(FCT) void se_bwd_kernel(const float* __restrict__ p
     const int b = blockIdx.x, t = threadIdx.x;
     // dse[c] = sum over tiles (fixed order), then ds2
     for (int c = t; c < C; c += FCT) {
-        float s = 0.f;
-        for (int k = 0; k < n_part; ++k) s += part[((size_t)b * n_part + k) * C + c];
+        // four accumulators (partial k -> k mod 4), combined in a fixed order: deterministic, and 8 loads in
+        // flight per lane instead of one dependent add chain over the tiles (58 us per call at B=4)
+        const float* pc = part + (size_t)b * n_part * C + c;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int k = 0;
+#pragma unroll 2
+        for (; k + 4 <= n_part; k += 4) {
+            a0 += pc[(size_t)k * C];
+            a1 += pc[(size_t)(k + 1) * C];
+            a2 += pc[(size_t)(k + 2) * C];
+            a3 += pc[(size_t)(k + 3) * C];
+        }
+        for (; k < n_part; ++k) a0 += pc[(size_t)k * C];
+        const float s = (a0 + a1) + (a2 + a3);
         const float u = s2[(size_t)b * C + c] + 3.f;
         const float d = (u > 0.f && u < 6.f) ? s * (1.f / 6.f) : 0.f;
         v_c[c] = d;
