@@ -89,6 +89,30 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
     }
 }
 
+// Sum over the 64 lanes of a wave in f64, the same value in every lane, fixed order (deterministic): DPP
+// butterflies inside each 16-lane row (quad xor 1, xor 2, half-row mirror, row mirror) on both 32-bit
+// halves, then the four row sums read from lanes 0/16/32/48 (as norm.hip's wave_sum; the ds_bpermute chain
+// of a double __shfl_xor butterfly was most of these small finalize kernels).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xFFFFFFFFll), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double lane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFFll), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    v += dpp_d<0x141>(v);
+    v += dpp_d<0x140>(v);
+    return (lane_d(v, 0) + lane_d(v, 16)) + (lane_d(v, 32) + lane_d(v, 48));
+}
+
 // one block (64 threads) per channel: Chan merge over all tiles of all images
 __global__ __launch_bounds__(64) void bn_finalize_kernel(const float4* __restrict__ part, int n_tiles, int B, int HW,
                                                          int C, int ppw, float* __restrict__ gamma_beta_mm_mv,
@@ -101,8 +125,7 @@ __global__ __launch_bounds__(64) void bn_finalize_kernel(const float4* __restric
         const float4 v = part[(size_t)i * cg * 2 + 2 * q];
         s += (double)(l == 0 ? v.x : l == 1 ? v.y : l == 2 ? v.z : v.w);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_sum_d(s);
     const double N = (double)B * HW;
     const double mean = s / N;
     double m2 = 0.0;
@@ -117,8 +140,7 @@ __global__ __launch_bounds__(64) void bn_finalize_kernel(const float4* __restric
         const double d = ts / n - mean;
         m2 += tm + n * d * d;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m2 += __shfl_xor(m2, o);
+    m2 = wave_sum_d(m2);
     if (t == 0) {
         const double var = m2 / N;
         const double rstd = 1.0 / sqrt(var + (double)eps);
@@ -220,11 +242,8 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(BnBwdArgs a) {
         s1 += (double)(l == 0 ? v1.x : l == 1 ? v1.y : l == 2 ? v1.z : v1.w);
         s2 += (double)(l == 0 ? v2.x : l == 1 ? v2.y : l == 2 ? v2.z : v2.w);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        s1 += __shfl_xor(s1, o);
-        s2 += __shfl_xor(s2, o);
-    }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
     if (t == 0) {
         const double N = (double)a.B * a.HW;
         a.consts[c] = make_float2((float)(s1 / N), (float)(s2 / N));
