@@ -142,6 +142,16 @@ bool wino_x6_supported(int kh, int stride, int cin, int cout);
 std::vector<float> wino_x6_pack_weights(const float* kern, int cin);
 // wino_x6_pack_weights on the device (kern: HWIO [3][3][cin][128] on the device; bitwise the host image)
 hipError_t wino_x6_transform_launch(const float* kern, int cin, float* U, hipStream_t st);
+// Several layers' x6 transforms in one launch (training re-pack after every optimizer step): job k maps
+// kern[k] (HWIO, cin[k] -> 128) to U[k]; at most X6_MAX_JOBS jobs per call.
+constexpr int X6_MAX_JOBS = 24;
+struct X6TransformJobs {
+    const float* kern[X6_MAX_JOBS];
+    float* U[X6_MAX_JOBS];
+    int cin[X6_MAX_JOBS];
+    int n;
+};
+hipError_t wino_x6_transform_batch_launch(const X6TransformJobs& jobs, hipStream_t st);
 hipError_t wino_x6_prepare();
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st);
 // kernel-execution timestamps (hipExtLaunchKernel events) for the next wino_x6_launch on this thread

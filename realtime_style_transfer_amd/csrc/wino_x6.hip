@@ -538,10 +538,9 @@ std::vector<float> wino_x6_pack_weights(const float* kern, int cin) {
 // Device form of wino_x6_pack_weights (training re-packs after every optimizer step): one thread per
 // (ci, co), U = G g G^T in float64 with the host's operation order and no contraction, rounded to f32,
 // then split into three bf16 pieces with round-to-nearest-even at each step — bitwise the host image.
-__global__ __launch_bounds__(256) void wino_x6_transform_kernel(const float* __restrict__ kern, int cin,
-                                                                unsigned short* __restrict__ U) {
+__device__ __forceinline__ void x6_transform_one(const float* __restrict__ kern, int cin, unsigned short* __restrict__ U,
+                                                 int idx) {
 #pragma clang fp contract(off)
-    const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= cin * XN) return;
     const int ci = idx / XN, co = idx - (idx / XN) * XN;
     const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
@@ -571,6 +570,32 @@ __global__ __launch_bounds__(256) void wino_x6_transform_kernel(const float* __r
             U[((base + 1) * XN + co) * XCK + c] = (unsigned short)b1;
             U[((base + 2) * XN + co) * XCK + c] = (unsigned short)b2;
         }
+}
+
+__global__ __launch_bounds__(256) void wino_x6_transform_kernel(const float* __restrict__ kern, int cin,
+                                                                unsigned short* __restrict__ U) {
+    x6_transform_one(kern, cin, U, blockIdx.x * 256 + threadIdx.x);
+}
+
+// batched form: job = blockIdx.x / blocks_per_job (jobs with a smaller cin leave their last blocks idle)
+__global__ __launch_bounds__(256) void wino_x6_transform_batch_kernel(X6TransformJobs jobs, int blocks_per_job) {
+    const int job = blockIdx.x / blocks_per_job, blk = blockIdx.x - job * blocks_per_job;
+    if (job >= jobs.n) return;
+    x6_transform_one(jobs.kern[job], jobs.cin[job], reinterpret_cast<unsigned short*>(jobs.U[job]),
+                     blk * 256 + threadIdx.x);
+}
+
+hipError_t wino_x6_transform_batch_launch(const X6TransformJobs& jobs, hipStream_t st) {
+    if (jobs.n <= 0) return hipSuccess;
+    if (jobs.n > X6_MAX_JOBS) return hipErrorInvalidValue;
+    int max_cin = 0;
+    for (int k = 0; k < jobs.n; ++k) {
+        if (jobs.cin[k] % XCK != 0 || jobs.cin[k] > XMAX_CIN) return hipErrorInvalidValue;
+        max_cin = jobs.cin[k] > max_cin ? jobs.cin[k] : max_cin;
+    }
+    const int bpj = (max_cin * XN + 255) / 256;
+    hipLaunchKernelGGL(wino_x6_transform_batch_kernel, dim3((unsigned)(bpj * jobs.n)), dim3(256), 0, st, jobs, bpj);
+    return hipGetLastError();
 }
 
 hipError_t wino_x6_transform_launch(const float* kern, int cin, float* U, hipStream_t st) {
