@@ -298,7 +298,7 @@ def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"
                      (ex["transfer_f32"] + ex["vgg_f32"] + ex["gram_f32"]) / (FP32_MFMA_PEAK_TFLOPS * 1e12)) * 1e3
     return {"workload": f"{SPEC} train_network.py step (BASELINE config 4): MobileNetV3Small style predictor + "
                         f"transfer net, training-mode forward, VGG16/Gram loss (no depth term), backward of both, " +
-                        ("RCCL gradient all-reduce (SUM, one bucket) + BN moving-statistics average, "
+                        ("one all-reduce per step (SUM, one bucket: gradients + BN moving statistics, the latter then / world), "
                          if ctx.world > 1 else "") + "RMSprop on both", "batch_per_gpu": TB, "steps": args.train_steps,
             "ms_per_step": round(ms, 3),
             "frames_per_s": round(ctx.world * TB * args.train_steps / el, 3),
@@ -467,9 +467,12 @@ def parse_args(argv=None):
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
     ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--train-modes", default="bf16,bf16x3,bf16x6,fp32",
+                    help="VGG16 precisions of the training line, comma-separated; the first is the headline")
     ap.add_argument("--precision", default=DEFAULT_PRECISION,
-                    help="headline precision mode: fp32_winograd (default: fp32 arithmetic, residual convs as "
-                         "fused Winograd F(2x2,3x3)), fp32 (all direct), bf16x6, bf16x3")
+                    help="headline transfer precision mode (default winograd_bf16x6: fp32-level Winograd F(2x2,3x3) "
+                         "with exact split-bf16 MFMA products); also fp32, fp32_winograd, bf16x6, bf16x3 and bf16 "
+                         "(bf16 is not fp32-level)")
     ap.add_argument("--no-bf16x3", action="store_true", help="skip the other precision-mode measurements")
     ap.add_argument("--no-predictor", action="store_true", help="skip the style-predictor measurement")
     ap.add_argument("--no-ingest", action="store_true", help="skip the G-buffer ingest measurement")
@@ -696,11 +699,12 @@ def run(args, ctx):
     if args.train_batch > 0:
         # BASELINE config 4 trains in bf16: the headline training figure runs the VGG16 3x3 convs with bf16
         # operands and fp32 accumulation; the split-bf16 (bf16x3, bf16x6) and fp32 runs are reported beside it
-        train = bench_training(args, ctx, cfg, ins, outs, plan, weights, P, "bf16")
+        modes = [m for m in args.train_modes.split(",") if m]
+        train = bench_training(args, ctx, cfg, ins, outs, plan, weights, P, modes[0])
         keep = ("ms_per_step", "frames_per_s", "algorithmic_tflops_per_gpu", "dtype", "roofline")
         train["other_precisions"] = {p: {k: v for k, v in bench_training(args, ctx, cfg, ins, outs, plan, weights, P,
                                                                           p).items() if k in keep}
-                                     for p in ("bf16x3", "bf16x6", "fp32")}
+                                     for p in modes[1:]}
 
     # ---------------- parity + CPU baseline (rank 0 at N=1 only, bounded sample) ----------------
     max_abs = None

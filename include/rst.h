@@ -199,6 +199,16 @@ int rst_trainer_apply_gradients(rst_trainer* t, const float* grad, float learnin
 int rst_trainer_copy_weights(rst_trainer* t, float* dst, size_t count, void* stream);
 int rst_trainer_copy_slots(rst_trainer* t, float* dst, size_t count, void* stream);
 int rst_trainer_set_weights(rst_trainer* t, const float* src, size_t count, void* stream);
+/* Data parallel: the BatchNormalization moving statistics (every BN layer's moving_mean then
+ * moving_variance, get_weights() order), which each rank updates from its own batch. get copies them
+ * into dst (e.g. the tail of the gradient bucket, so ONE all-reduce carries both); set writes
+ * src[i] / divisor back (divisor = world size after a SUM all-reduce: tf.distribute.MirroredStrategy's
+ * MEAN aggregation of the moving-average assignments, styleTransfer.py:201, train_network.py:61) without
+ * re-packing any kernel image (no training kernel reads them). Replaces the reference's implicit
+ * MirroredStrategy sync; the reference itself trains on one GPU (train_network.py:14-23). */
+size_t rst_trainer_num_moving_statistics(const rst_trainer* t);
+int rst_trainer_get_moving_statistics(rst_trainer* t, float* dst, size_t count, void* stream);
+int rst_trainer_set_moving_statistics(rst_trainer* t, const float* src, size_t count, float divisor, void* stream);
 /* Debug: gradient of the batch loss w.r.t. conv layer `layer`'s activated output (before any skip
  * add; the last layer's is d loss / d prediction) from the most recent compute_gradients. */
 int rst_trainer_copy_output_gradient(rst_trainer* t, int layer, float* dst, size_t count, int batch, void* stream);
@@ -258,6 +268,11 @@ int rst_predictor_trainer_apply_gradients(rst_predictor_trainer* t, const float*
 int rst_predictor_trainer_copy_weights(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
 int rst_predictor_trainer_set_weights(rst_predictor_trainer* t, const float* src, size_t count, void* stream);
 int rst_predictor_trainer_copy_slots(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
+/* As rst_trainer_*_moving_statistics for the predictor's BatchNormalization layers (MobileNetV3Small). */
+size_t rst_predictor_trainer_num_moving_statistics(const rst_predictor_trainer* t);
+int rst_predictor_trainer_get_moving_statistics(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
+int rst_predictor_trainer_set_moving_statistics(rst_predictor_trainer* t, const float* src, size_t count, float divisor,
+                                                void* stream);
 
 /* ---- G-buffer ingest ----
  * Replaces the host-side numpy/TF preprocessing of an Unreal HDR screenshot:

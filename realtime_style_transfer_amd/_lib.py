@@ -11,6 +11,7 @@ import ctypes
 import os
 from pathlib import Path
 
+import numpy as np
 import torch  # noqa: F401  (must precede loading librst, see module docstring)
 
 _PKG = Path(__file__).resolve().parent
@@ -29,12 +30,15 @@ EXPORTED_SYMBOLS = [
     "rst_trainer_create", "rst_trainer_create_ex", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
     "rst_trainer_compute_gradients", "rst_trainer_apply_gradients", "rst_trainer_copy_weights",
     "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_copy_output_gradient",
-    "rst_trainer_debug_vgg_gradient", "rst_trainer_loss",
+    "rst_trainer_debug_vgg_gradient", "rst_trainer_loss", "rst_trainer_num_moving_statistics",
+    "rst_trainer_get_moving_statistics", "rst_trainer_set_moving_statistics",
     "rst_predictor_num_weights", "rst_predictor_create", "rst_predictor_destroy", "rst_predictor_forward",
     "rst_predictor_num_stages", "rst_predictor_stage_shape", "rst_predictor_copy_stage",
     "rst_predictor_trainer_create", "rst_predictor_trainer_destroy", "rst_predictor_trainer_num_weights",
     "rst_predictor_trainer_forward", "rst_predictor_trainer_backward", "rst_predictor_trainer_apply_gradients",
     "rst_predictor_trainer_copy_weights", "rst_predictor_trainer_set_weights", "rst_predictor_trainer_copy_slots",
+    "rst_predictor_trainer_num_moving_statistics", "rst_predictor_trainer_get_moving_statistics",
+    "rst_predictor_trainer_set_moving_statistics",
     "rst_gbuffer_resized_size", "rst_gbuffer_preprocess", "rst_crc32c_extend",
 ]
 EXTRACTORS = {"DUMMY": 0, "MOBILE_NET": 1}   # include/rst.h RST_EXTRACTOR_*
@@ -147,6 +151,13 @@ def load() -> ctypes.CDLL:
     lib.rst_trainer_copy_output_gradient.restype = i
     lib.rst_trainer_debug_vgg_gradient.argtypes = [vp, i, vp, sz, i, vp]
     lib.rst_trainer_debug_vgg_gradient.restype = i
+    for pre in ("rst_trainer", "rst_predictor_trainer"):
+        getattr(lib, pre + "_num_moving_statistics").argtypes = [vp]
+        getattr(lib, pre + "_num_moving_statistics").restype = sz
+        getattr(lib, pre + "_get_moving_statistics").argtypes = [vp, vp, sz, vp]
+        getattr(lib, pre + "_get_moving_statistics").restype = i
+        getattr(lib, pre + "_set_moving_statistics").argtypes = [vp, vp, sz, fp, vp]
+        getattr(lib, pre + "_set_moving_statistics").restype = i
     lib.rst_trainer_loss.argtypes = [vp]
     lib.rst_trainer_loss.restype = vp
     lib.rst_predictor_num_weights.argtypes = [ctypes.POINTER(RstPredictorShape)]
@@ -205,6 +216,16 @@ def check(code: int):
 def stream_ptr(stream=None) -> int:
     s = torch.cuda.current_stream() if stream is None else stream
     return int(s.cuda_stream)
+
+
+def as_device(x, device) -> torch.Tensor:
+    """Keras-call input convenience: numpy arrays and host tensors are copied to ``device`` as float32 (the
+    H2D copy Keras does for host inputs); device tensors pass through untouched."""
+    if not isinstance(x, torch.Tensor):
+        x = torch.from_numpy(np.ascontiguousarray(x, np.float32))
+    if not x.is_cuda:
+        x = x.to(device=device, dtype=torch.float32)
+    return x
 
 
 def dev_ptr(t: torch.Tensor) -> int:

@@ -55,6 +55,8 @@ struct rst_predictor_trainer {
     float2* consts = nullptr;
     float* slab = nullptr;
     float* wt = nullptr;                    // transposed 1x1 weights (dgrad)
+    int* stat_index = nullptr;              // weight index of every BN moving_mean / moving_variance entry
+    size_t n_stat = 0;
     std::vector<void*> allocs;
     ~rst_predictor_trainer() {
         for (void* p : allocs) (void)hipFree(p);
@@ -112,6 +114,20 @@ int rst_predictor_trainer_create(const rst_predictor_shape* shape, const float* 
             hipMemset(t->d_zeros, 0, 1024 * 4) != hipSuccess) {
             delete t;
             return set_error(RST_ERR_HIP, "rst_predictor_trainer_create: upload failed");
+        }
+    }
+    {   // BN moving statistics in get_weights() order (the units are laid out in weight order)
+        std::vector<int> idx;
+        for (const PUnit& u : P.units)
+            if (u.kind != PU_DUMMY)
+                for (int i = 0; i < 2 * u.cout; ++i) idx.push_back((int)(u.goff + 2 * (size_t)u.cout + i));
+        t->n_stat = idx.size();
+        if (!idx.empty()) {
+            TRY(t->alloc(&t->stat_index, idx.size() * 4));
+            if (hipMemcpy(t->stat_index, idx.data(), idx.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+                delete t;
+                return set_error(RST_ERR_HIP, "rst_predictor_trainer_create: upload failed");
+            }
         }
     }
     const size_t nu = P.units.size();
@@ -356,6 +372,23 @@ int rst_predictor_trainer_copy_weights(rst_predictor_trainer* t, float* dst, siz
 int rst_predictor_trainer_set_weights(rst_predictor_trainer* t, const float* src, size_t count, void* stream) {
     if (!t || !src || count != t->plan.total) return set_error(RST_ERR_INVALID, "rst_predictor_trainer_set_weights");
     RST_HIP_TRY(hipMemcpyAsync(t->d_wc, src, count * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return RST_OK;
+}
+
+size_t rst_predictor_trainer_num_moving_statistics(const rst_predictor_trainer* t) { return t ? t->n_stat : 0; }
+
+int rst_predictor_trainer_get_moving_statistics(rst_predictor_trainer* t, float* dst, size_t count, void* stream) {
+    if (!t || !dst || count != t->n_stat)
+        return set_error(RST_ERR_INVALID, "rst_predictor_trainer_get_moving_statistics: bad argument");
+    if (count) RST_HIP_TRY(gather_launch(t->d_wc, t->stat_index, dst, count, (hipStream_t)stream));
+    return RST_OK;
+}
+
+int rst_predictor_trainer_set_moving_statistics(rst_predictor_trainer* t, const float* src, size_t count, float divisor,
+                                                void* stream) {
+    if (!t || !src || count != t->n_stat || !(divisor > 0.f))
+        return set_error(RST_ERR_INVALID, "rst_predictor_trainer_set_moving_statistics: bad argument");
+    RST_HIP_TRY(scatter_div_launch(src, t->stat_index, t->d_wc, count, divisor, (hipStream_t)stream));
     return RST_OK;
 }
 

@@ -56,5 +56,6 @@ hipError_t gram_bwd_weights_launch(const float* gp, const float* gs, const int* 
 hipError_t preprocess_bwd_launch(const float* gpre, float* gx, size_t pixels, int accumulate, hipStream_t st);
 hipError_t rmsprop_launch(float* w, float* ms, const float* g, size_t n, float lr, float rho, float eps, hipStream_t st);
 hipError_t gather_launch(const float* src, const int* map, float* dst, size_t n, hipStream_t st);
+hipError_t scatter_div_launch(const float* src, const int* index, float* dst, size_t n, float divisor, hipStream_t st);
 
 }  // namespace rst

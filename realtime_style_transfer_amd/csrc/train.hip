@@ -515,6 +515,21 @@ hipError_t rmsprop_launch(float* w, float* ms, const float* g, size_t n, float l
     return hipGetLastError();
 }
 
+// dst[index[i]] = src[i] / divisor: writes a few canonical weight entries (the cross-rank average of the BN
+// moving statistics) without touching the packed kernel images that are derived from the others
+__global__ __launch_bounds__(256) void scatter_div_kernel(const float* __restrict__ src, const int* __restrict__ index,
+                                                          float* __restrict__ dst, size_t n, float divisor) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[index[i]] = src[i] / divisor;
+}
+
+hipError_t scatter_div_launch(const float* src, const int* index, float* dst, size_t n, float divisor, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(scatter_div_kernel, dim3(blocks), dim3(256), 0, st, src, index, dst, n, divisor);
+    return hipGetLastError();
+}
+
 // packed[i] = map[i] < 0 ? 0 : src[map[i]]  (re-pack canonical weights into kernel stage images)
 __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ src, const int* __restrict__ map,
                                                      float* __restrict__ dst, size_t n) {

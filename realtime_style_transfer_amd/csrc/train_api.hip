@@ -157,6 +157,8 @@ struct rst_trainer {
     float* d_vpool = nullptr;
     float* d_gram_packed = nullptr;
     float* d_vgg_dbg[13] = {};    // debug: d loss / d (VGG conv i output), when enabled
+    int* d_stat_index = nullptr;  // canonical index of every BN moving_mean / moving_variance entry
+    size_t n_stat = 0;
     ~rst_trainer() {
         if (loss) rst_loss_destroy(loss);
         for (void* p : allocs) (void)hipFree(p);
@@ -776,6 +778,15 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
     if ((st = t->alloc(&t->d_nb_consts, (size_t)B * 256 * sizeof(float2))) != RST_OK) return fail_delete(t, st);
     if ((st = t->alloc(&t->d_slab, slab)) != RST_OK) return fail_delete(t, st);
     if ((st = t->alloc(&t->d_gstyle, (size_t)B * P * 4)) != RST_OK) return fail_delete(t, st);
+    {   // BN moving statistics in get_weights() order: per BN layer moving_mean[cout], moving_variance[cout]
+        std::vector<int> idx;
+        for (const TLayer& T : t->L)
+            if (T.goff)
+                for (int i = 0; i < 2 * T.e.s.cout; ++i) idx.push_back((int)(T.goff + 2 * T.e.s.cout + i));
+        t->n_stat = idx.size();
+        if (!idx.empty() && (st = t->alloc(&t->d_stat_index, idx.size() * 4, idx.data())) != RST_OK)
+            return fail_delete(t, st);
+    }
     // the last layer's output gradient is d(loss)/d(prediction), written by the VGG backward
     if ((st = repack(t, nullptr)) != RST_OK) return fail_delete(t, st);
     if (hipDeviceSynchronize() != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, "rst_trainer_create sync"));
@@ -849,6 +860,22 @@ int rst_trainer_debug_vgg_gradient(rst_trainer* t, int layer, float* dst, size_t
     const size_t n = (size_t)batch * c.H * c.W * c.cout;
     if (!dst || count != n) return set_error(RST_ERR_INVALID, "rst_trainer_debug_vgg_gradient: count mismatch");
     RST_HIP_TRY(hipMemcpyAsync(dst, t->d_vgg_dbg[layer], n * 4, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    return RST_OK;
+}
+
+size_t rst_trainer_num_moving_statistics(const rst_trainer* t) { return t ? t->n_stat : 0; }
+
+int rst_trainer_get_moving_statistics(rst_trainer* t, float* dst, size_t count, void* stream) {
+    if (!t || !dst || count != t->n_stat) return set_error(RST_ERR_INVALID, "rst_trainer_get_moving_statistics: bad argument");
+    if (count) RST_HIP_TRY(gather_launch(t->d_wc, t->d_stat_index, dst, count, static_cast<hipStream_t>(stream)));
+    return RST_OK;
+}
+
+int rst_trainer_set_moving_statistics(rst_trainer* t, const float* src, size_t count, float divisor, void* stream) {
+    if (!t || !src || count != t->n_stat || !(divisor > 0.f))
+        return set_error(RST_ERR_INVALID, "rst_trainer_set_moving_statistics: bad argument");
+    // no re-pack: no packed kernel image is derived from the moving statistics in training mode
+    RST_HIP_TRY(scatter_div_launch(src, t->d_stat_index, t->d_wc, count, divisor, static_cast<hipStream_t>(stream)));
     return RST_OK;
 }
 

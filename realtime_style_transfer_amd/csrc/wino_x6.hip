@@ -623,12 +623,13 @@ void wino_x6_set_timing_events(hipEvent_t start, hipEvent_t stop) {
 }
 
 hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
+    // the timing events belong to this launch only, also when it is refused below
+    const hipEvent_t e0 = g_ev_start, e1 = g_ev_stop;
+    g_ev_start = g_ev_stop = nullptr;
     if (a.cin % XCK != 0 || a.cin > XMAX_CIN || a.tiles_y != (a.H + XTH - 1) / XTH ||
         a.tiles_x != (a.W + XTW - 1) / XTW || (size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7F000000)
         return hipErrorInvalidValue;   // 32-bit staging offsets; the out-of-range store offset must stay out of range
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
-    const hipEvent_t e0 = g_ev_start, e1 = g_ev_stop;
-    g_ev_start = g_ev_stop = nullptr;
     switch (a.pro_mode) {
         case PRO_NONE: hipExtLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(YT), YLDS_BYTES, st, e0, e1, 0, a); break;
         case PRO_AFF_RELU: hipExtLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(YT), YLDS_BYTES, st, e0, e1, 0, a); break;

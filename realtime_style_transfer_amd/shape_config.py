@@ -16,7 +16,7 @@ import json
 
 
 class StyleFeatureExtractor:
-    """Mirror of ``models/stylePrediction.py:186-189`` (string enum)."""
+    """Mirror of ``models/stylePrediction.py:19-22`` (string enum)."""
     DUMMY = 'DUMMY'
     EFFICIENT_NET = 'EFFICIENT_NET'
     MOBILE_NET = 'MOBILE_NET'

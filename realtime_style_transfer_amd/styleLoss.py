@@ -9,7 +9,15 @@
 * ``make_style_loss_function(loss_model, output_shape, num_styles, with_depth_loss)`` — returns
   ``(compute_loss, model)`` like styleLoss.py:295-369; ``compute_loss(y_pred, y_true)`` returns the
   per-image ``(B,)`` loss dict. The MiDaS depth term needs a TF-Hub download (styleLoss.py:254) and
-  is not available: ``with_depth_loss=True`` raises.
+  is not available: ``with_depth_loss=True`` (ShapeConfig's default, shape_config.py:30) is accepted
+  at construction, as the reference's inference/export scripts build the loss without evaluating it
+  (predict_video_using_checkpoint.py:53-57, save_using_checkpoint.py:49-52), and raises
+  ``NotImplementedError`` when a loss that needs the depth term is computed.
+* ``StyleLossModelMobileNet(input_shape)`` (styleLoss.py:155-193) — its layer choice and factors, so the
+  scripts that construct it and never evaluate it (predict_using_checkpoint.py:55,
+  predict_video_using_checkpoint.py:43, save_using_checkpoint.py:39) run; evaluating it raises
+  ``NotImplementedError`` (the MobileNetV3Small loss trunk is not built: ImageNet weights are a download
+  and no training entry point of the reference uses it).
 """
 from __future__ import annotations
 
@@ -114,6 +122,31 @@ class StyleLossModelVGG:
         return t
 
 
+class StyleLossModelMobileNet:
+    """styleLoss.py:155-193: constructible with the reference's layer names and factors; not evaluable."""
+
+    def __init__(self, input_shape, name: str = "StyleLossModelMobileNet"):
+        self.name = name
+        self.input_shape = tuple(int(v) for v in input_shape)
+        self.style_layers = ['expanded_conv_2/Add', 'expanded_conv_4/Add', 'expanded_conv_5/Add',
+                             'expanded_conv_7/Add']
+        self.content_layers = ['expanded_conv_9/Add', 'expanded_conv_10/Add']
+        self.num_style_layers = len(self.style_layers)
+        self.content_loss_factor = 1e-3
+        self.style_loss_factor = 1
+        self.total_variation_loss_factor = 1e-3
+        self.depth_loss_factor = 1e-4
+        self.trainable = False
+
+    def _unavailable(self, *args, **kwargs):
+        raise NotImplementedError(
+            "StyleLossModelMobileNet is construct-only on MI355X: the MobileNetV3Small loss trunk (ImageNet weights, a "
+            "network download) is not built; train with StyleLossModelVGG as train_network.py:85 does")
+
+    __call__ = _unavailable
+    losses = _unavailable
+
+
 def gram_matrix(input_tensor: torch.Tensor) -> torch.Tensor:
     """styleLoss.py:21-37: einsum('bijc,bijd->bcd') / (H*W) on the device (channels % 64 == 0)."""
     lib = _lib.load()
@@ -125,18 +158,43 @@ def gram_matrix(input_tensor: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def make_style_loss_function(loss_feature_extractor_model: StyleLossModelVGG, output_shape, num_styles,
-                             with_depth_loss=True):
-    """styleLoss.py:295-369 (without the MiDaS depth term)."""
-    if with_depth_loss:
-        raise NotImplementedError("depth loss needs the TF-Hub MiDaS model (styleLoss.py:254), which is a network "
-                                  "download; pass with_depth_loss=False")
-    if tuple(output_shape) != loss_feature_extractor_model.input_shape:
-        raise ValueError(f"output_shape {output_shape} != loss model input {loss_feature_extractor_model.input_shape}")
-    model = loss_feature_extractor_model
+DEPTH_LOSS_UNAVAILABLE = ("the depth loss term needs the TF-Hub MiDaS model (styleLoss.py:250-288), a network "
+                          "download that is not available here; build the loss with with_depth_loss=False")
 
-    def compute_loss(y_pred: torch.Tensor, y_true: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
-        t = model.losses(y_pred, y_true['content'], y_true['style'])
+
+class StyleLoss:
+    """The Keras ``StyleLoss`` model make_style_loss_function returns (styleLoss.py:360-361): called with
+    ``(inputs, ground_truth)`` or ``{'prediction', 'ground_truth'}`` it returns the per-image loss dict."""
+
+    def __init__(self, feature_model, with_depth_loss: bool):
+        self.feature_model = feature_model
+        self.with_depth_loss = bool(with_depth_loss)
+        self.trainable = False
+        self.name = "StyleLoss"
+
+    def compute(self, y_pred: torch.Tensor, y_true: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        if self.with_depth_loss:
+            raise NotImplementedError(DEPTH_LOSS_UNAVAILABLE)
+        t = self.feature_model.losses(y_pred, y_true['content'], y_true['style'])
         return {"loss": t[:, 0], "feature_loss": t[:, 1], "style_loss": t[:, 2], "total_variation_loss": t[:, 3]}
 
+    def __call__(self, inputs):
+        if isinstance(inputs, dict):
+            return self.compute(inputs['prediction'], inputs['ground_truth'])
+        raise NotImplementedError("StyleLoss takes {'prediction', 'ground_truth'}; the (inputs, ground_truth) form of "
+                                  "StyleTransferModels.loss_model runs the inference model first — use "
+                                  "StyleTransferTrainingModel.train_step")
+
+
+def make_style_loss_function(loss_feature_extractor_model, output_shape, num_styles, with_depth_loss=True):
+    """styleLoss.py:295-369 -> (compute_loss, model). The MiDaS depth term is not available: a loss built with
+    ``with_depth_loss=True`` constructs, and raises NotImplementedError when it is computed."""
+    if tuple(output_shape) != tuple(loss_feature_extractor_model.input_shape):
+        raise ValueError(f"output_shape {output_shape} != loss model input {loss_feature_extractor_model.input_shape}")
+    model = StyleLoss(loss_feature_extractor_model, with_depth_loss)
+
+    def compute_loss(y_pred: torch.Tensor, y_true: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        return model.compute(y_pred, y_true)
+
+    compute_loss.with_depth_loss = model.with_depth_loss
     return compute_loss, model

@@ -204,7 +204,13 @@ class StylePredictionModel:
         self._weights = [np.ascontiguousarray(w, np.float32) for w in weights]
         self._build()
 
+    def compile(self, run_eagerly=False, **kwargs):
+        """Keras Model.compile: nothing to compile (kernels built ahead of time)."""
+
+    trainable = False
+
     def __call__(self, style: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        style = _lib.as_device(style, self.device)
         if style.dim() != 4 or tuple(style.shape[1:]) != self.input_shape:
             raise ValueError(f"style must be (B,{','.join(map(str, self.input_shape))}), got {tuple(style.shape)}")
         B = style.shape[0]
@@ -219,7 +225,9 @@ class StylePredictionModel:
                                                      _lib.stream_ptr(stream)))
         return out
 
-    predict = __call__
+    def predict(self, style, batch_size=None, verbose=0) -> np.ndarray:
+        """Keras Model.predict: the style parameters as a host numpy array."""
+        return self(style).cpu().numpy()
 
     # ------------------------------------------------------------------ debugging
     def num_stages(self) -> int:

@@ -35,7 +35,8 @@ class StyleTransferModel:
 
     def __init__(self, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, num_styles=1,
                  name="StyleTransferModel", weights: Optional[Sequence[np.ndarray]] = None, seed: int = 2,
-                 max_batch: int = 8, device=None, precision: str = "fp32", allow_reduced_precision: bool = False):
+                 max_batch: int = 8, device=None, precision: str = "winograd_bf16x6",
+                 allow_reduced_precision: bool = False):
         self.name = name
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"precision must be one of {list(_lib.PRECISIONS)}, got {precision!r}")
@@ -100,6 +101,12 @@ class StyleTransferModel:
         self._weights = [np.ascontiguousarray(w, np.float32) for w in weights]
         self._build()
 
+    def compile(self, run_eagerly=False, **kwargs):
+        """Keras Model.compile (predict_*_using_checkpoint.py setup_model): nothing to compile — the kernels are
+        built ahead of time and the forward is graph-capturable."""
+
+    trainable = False
+
     def keras_layer_attributes(self) -> List[List[str]]:
         """Variables per weighted Keras layer, in model order: each Conv2D/Conv2DTranspose owns
         (kernel, bias); the BatchNormalization after a contract conv (styleTransfer.py:194-203) is its
@@ -152,10 +159,12 @@ class StyleTransferModel:
 
     def __call__(self, inputs: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None,
                  stream=None) -> torch.Tensor:
-        content = inputs['content']
-        style_params = self._check_inputs(content, inputs['style_params'])
+        content = _lib.as_device(inputs['content'], self.device)
+        style_params = self._check_inputs(content, _lib.as_device(inputs['style_params'], self.device))
         B = content.shape[0]
         sw = inputs.get('style_weights')
+        if sw is not None:
+            sw = _lib.as_device(sw, self.device)
         if sw is not None and self.num_styles == 1:
             raise ValueError("style_weights given but num_styles == 1")
         if self.num_styles > 1:
@@ -174,7 +183,9 @@ class StyleTransferModel:
                                            _lib.stream_ptr(stream)))
         return out
 
-    predict = __call__
+    def predict(self, inputs: Dict[str, torch.Tensor], batch_size=None, verbose=0) -> np.ndarray:
+        """Keras Model.predict: the output as a host numpy array (predict_video_using_checkpoint.py:96-98)."""
+        return self(inputs).cpu().numpy()
 
     # ------------------------------------------------------------------ profiling
     def profile_begin(self, max_steps: int):
@@ -226,8 +237,13 @@ def apply_style_weights(style_weights: torch.Tensor, style_params: torch.Tensor)
         raise ValueError(f"style_params must be (B,1,S,n) = ({B},1,{S},n), got {tuple(style_params.shape)}")
     if S != 2:
         return style_params
-    n = style_params.shape[-1]
+    # the device blend takes w0 as 1 - w1 (the model always completes the weights so, :297-302); refuse weights
+    # that are not completed rather than return w0*p0 + w1*p1 computed with a different w0
     w1 = style_weights[..., 1].contiguous()
+    if not torch.allclose(style_weights[..., 0], 1.0 - w1, rtol=0.0, atol=1e-6):
+        raise ValueError("style_weights[..., 0] must equal 1 - style_weights[..., 1] (the completed [1 - sum(w), w] "
+                         "form of styleTransfer.py:297-302)")
+    n = style_params.shape[-1]
     p = style_params.reshape(B, 2, n).contiguous()
     out = torch.empty((B, H, W, n), dtype=torch.float32, device=style_weights.device)
     _lib.check(_lib.load().rst_style_param_map(_lib.dev_ptr(w1), _lib.dev_ptr(p), B, H * W, S, n, _lib.dev_ptr(out),

@@ -16,6 +16,8 @@ from typing import Callable, Dict, Optional
 
 import torch
 
+from . import _lib
+
 log = logging.getLogger(__name__)
 
 
@@ -51,14 +53,21 @@ class StyleTransferInference:
         flat = style.reshape((B * S,) + tuple(style.shape[2:]))
         return self.style_predictor(flat).view(B, S, -1)
 
+    def compile(self, run_eagerly=False, **kwargs):
+        """Keras Model.compile: nothing to compile (kernels built ahead of time)."""
+
+    trainable = False
+
     def __call__(self, inputs: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        sp = self.predict_style_params(inputs['style'])
+        sp = self.predict_style_params(_lib.as_device(inputs['style'], self.transfer.device))
         transfer_input = {'content': inputs['content'], 'style_params': sp}
         if 'style_weights' in inputs:
             transfer_input['style_weights'] = inputs['style_weights']
         return self.transfer(transfer_input, out=out)
 
-    predict = __call__
+    def predict(self, inputs: Dict[str, torch.Tensor], batch_size=None, verbose=0):
+        """Keras Model.predict: the output as a host numpy array (predict_using_checkpoint.py:99)."""
+        return self(inputs).cpu().numpy()
 
 
 def make_style_transfer_inference_model(num_styles, style_predictor_factory_func: Callable[[int], object],

@@ -13,14 +13,15 @@ weight sets take an RMSprop step. Without one, ``style_params`` are an input (``
 'style_params'}``) and their gradient is returned.
 
 * ``compute_loss`` returns the per-image ``(B,)`` loss; Keras minimises its sum, and so does this.
-* Data parallel: under an initialised process group, the gradients (transfer and predictor in ONE
-  flat bucket) are all-reduced (SUM, RCCL over xGMI) before the update, which equals one step on the
-  concatenated global batch except that each rank normalises with its own BatchNorm batch statistics
-  (TF without SyncBatchNorm does the same). The BN *moving* statistics are then averaged over the ranks
-  after every step (one more small all-reduce), which is what TF's MirroredStrategy does with them
-  (sync-on-read variables, MEAN aggregation): the moving-average update is linear, so the average of the
-  per-rank updates equals the update with the mean of the per-rank batch statistics, and every rank
-  keeps bitwise identical weights.
+* Data parallel: under an initialised process group, ONE all-reduce per step (SUM, RCCL over xGMI)
+  carries the flat bucket [transfer gradient | predictor gradient | BN moving statistics]. Summing the
+  gradients equals one step on the concatenated global batch except that each rank normalises with its
+  own BatchNorm batch statistics (TF without SyncBatchNorm does the same). The BN *moving* statistics,
+  which each rank's forward updated from its own batch, come back divided by the world size and are
+  written straight into the canonical weights (``rst_*trainer_set_moving_statistics``, no re-pack):
+  TF MirroredStrategy's MEAN aggregation of the moving-average assignments. The update is linear, so
+  the mean of the per-rank updates equals the update with the mean of the per-rank batch statistics,
+  and every rank keeps bitwise identical weights.
 """
 from __future__ import annotations
 
@@ -33,8 +34,9 @@ import torch
 
 from . import _lib
 from .plan import Plan, init_weights, network_plan
-from .styleLoss import StyleLossModelVGG, make_style_loss_function
+from .styleLoss import DEPTH_LOSS_UNAVAILABLE, StyleLossModelVGG, make_style_loss_function
 from .styleTransfer import StyleTransferModel
+from .styleTransferInferenceModel import StyleTransferInference, make_style_transfer_inference_model
 
 log = logging.getLogger(__name__)
 
@@ -106,7 +108,12 @@ class StyleTransferTrainingModel:
                  loss_model: Optional[StyleLossModelVGG] = None, weights: Optional[Sequence[np.ndarray]] = None,
                  seed: int = 2, max_batch: int = 4, optimizer: Optional[RMSprop] = None, process_group=None,
                  device=None, name: str = "StyleTransferTrainingModel", style_predictor=None,
-                 precision: str = "fp32_winograd"):
+                 precision: str = "fp32_winograd", with_depth_loss: bool = False):
+        """``loss_model``: a StyleLossModelVGG (trainable), or a construct-only loss model such as
+        StyleLossModelMobileNet, with which the model is built (weights, inference ``__call__``) but
+        ``train_step`` raises — what the reference's inference and export scripts need
+        (predict_video_using_checkpoint.py:43-58, save_using_checkpoint.py:39-53). ``with_depth_loss``: the
+        loss asked for the MiDaS depth term (unavailable): construction works, ``train_step`` raises."""
         if precision not in ("fp32", "fp32_winograd", "winograd_bf16x6"):
             raise ValueError("transfer-network training precision must be 'fp32', 'fp32_winograd' or "
                              f"'winograd_bf16x6', got {precision!r}")
@@ -124,10 +131,20 @@ class StyleTransferTrainingModel:
                                                           device=self.device)
         if tuple(self.loss_model.input_shape) != self.output_shape:
             raise ValueError(f"loss model input {self.loss_model.input_shape} != output shape {self.output_shape}")
+        self.with_depth_loss = bool(with_depth_loss)
         self._shapes = [tuple(s) for s in self.plan.weight_shapes()]
         self._sizes = [int(np.prod(s)) for s in self._shapes]
         w = weights if weights is not None else init_weights(self.plan, seed)
         flat = self._flatten(w)
+        self.style_predictor = style_predictor      # StylePredictionTrainer or None
+        self.style_losses: Dict[str, torch.Tensor] = {}
+        self._version, self._inference = 0, None
+        self._handle = None
+        if not isinstance(self.loss_model, StyleLossModelVGG):
+            # construct-only: weights on the host, no trainer (train_step raises)
+            self._host_weights = flat.copy()
+            self.num_weights = flat.size
+            return
         lib = _lib.load()
         H, W, C = self.input_shape
         shape = _lib.RstShape(H, W, C, self.output_shape[0], self.output_shape[1], self.plan.bottleneck_res_y,
@@ -146,7 +163,6 @@ class StyleTransferTrainingModel:
         self.num_weights = int(lib.rst_trainer_num_weights(h))
         if self.num_weights != flat.size or lib.rst_trainer_num_style_params(h) != self.num_style_parameters:
             raise RuntimeError("librst trainer plan disagrees with the host plan")
-        self.style_predictor = style_predictor      # StylePredictionTrainer or None
         n_pred = 0
         if style_predictor is not None:
             if style_predictor.num_top_parameters != self.num_style_parameters:
@@ -155,8 +171,16 @@ class StyleTransferTrainingModel:
             if style_predictor.max_batch < self.max_batch:
                 raise ValueError("style predictor max_batch is smaller than the training batch")
             n_pred = style_predictor.num_weights
-        # one flat gradient bucket: [transfer weights | predictor weights] (a single all-reduce per step)
-        self._bucket = torch.zeros(self.num_weights + n_pred, dtype=torch.float32, device=self.device)
+        # one flat bucket, one all-reduce per step: [transfer gradient | predictor gradient | transfer BN moving
+        # statistics | predictor BN moving statistics]
+        self._n_stat = int(lib.rst_trainer_num_moving_statistics(h))
+        self._n_pstat = int(_lib.load().rst_predictor_trainer_num_moving_statistics(style_predictor._handle)) \
+            if style_predictor is not None else 0
+        nb = self.num_weights + n_pred
+        self._bucket = torch.zeros(nb + self._n_stat + self._n_pstat, dtype=torch.float32, device=self.device)
+        self._grad_bucket = self._bucket[:nb]
+        self._stat = self._bucket[nb:nb + self._n_stat]
+        self._pstat = self._bucket[nb + self._n_stat:]
         # BN moving statistics (contract blocks: layer weights kernel, bias, gamma, beta, moving_mean,
         # moving_variance — styleTransfer.py:190-203) for the cross-rank average after each step
         named = []
@@ -165,8 +189,7 @@ class StyleTransferTrainingModel:
             named += list(zip(attrs, layer.weight_shapes))
         self._bn_index = torch.from_numpy(moving_statistics_index(named)).to(self.device)
         self._grad = self._bucket[:self.num_weights]
-        self._pgrad = self._bucket[self.num_weights:] if n_pred else None
-        self.style_losses: Dict[str, torch.Tensor] = {}
+        self._pgrad = self._bucket[self.num_weights:nb] if n_pred else None
 
     # ------------------------------------------------------------------ lifecycle
     def _flatten(self, weights: Sequence[np.ndarray]) -> np.ndarray:
@@ -190,15 +213,60 @@ class StyleTransferTrainingModel:
             pass
 
     # ------------------------------------------------------------------ Keras-like API
+    @property
+    def trainable_on_device(self) -> bool:
+        return self._handle is not None
+
+    def _require_trainer(self):
+        if self.with_depth_loss:
+            raise NotImplementedError(DEPTH_LOSS_UNAVAILABLE)
+        if self._handle is None:
+            raise NotImplementedError(f"{type(self.loss_model).__name__} is construct-only: training needs "
+                                      "StyleLossModelVGG (train_network.py:85)")
+
     def get_weights(self) -> List[np.ndarray]:
+        if self._handle is None:
+            return self._unflatten(self._host_weights)
         t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
         _lib.check(_lib.load().rst_trainer_copy_weights(self._handle, _lib.dev_ptr(t), t.numel(), _lib.stream_ptr()))
         return self._unflatten(t.cpu().numpy())
 
     def set_weights(self, weights: Sequence[np.ndarray]):
+        self._version += 1
+        if self._handle is None:
+            self._host_weights = self._flatten(weights)
+            return
         t = torch.from_numpy(self._flatten(weights)).to(self.device)
         _lib.check(_lib.load().rst_trainer_set_weights(self._handle, _lib.dev_ptr(t), t.numel(), _lib.stream_ptr()))
         torch.cuda.current_stream(self.device).synchronize()
+
+    def inference_model(self):
+        """The Keras model this training model wraps (styleTransferTrainingModel.py:19: inference_model.input ->
+        output), in inference mode with the current weights: predictor -> transfer, or the transfer alone."""
+        if self._inference is None or self._inference[0] != self._version:
+            transfer = self.transfer_model()
+            model = StyleTransferInference(transfer, self.style_predictor.inference_model(), 1, self.name) \
+                if self.style_predictor is not None else transfer
+            self._inference = (self._version, model)
+        return self._inference[1]
+
+    def __call__(self, inputs: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``training(element)`` (save_using_checkpoint.py:63, predict_video_using_checkpoint.py:71): the forward
+        with BatchNormalization in inference mode (Keras' default training=False)."""
+        return self.inference_model()(inputs, out=out)
+
+    def predict(self, inputs, batch_size=None, verbose=0) -> np.ndarray:
+        return self(inputs).cpu().numpy()
+
+    trainable = True
+
+    def compile(self, run_eagerly=False, optimizer=None, **kwargs):
+        """Keras Model.compile (train_network.py:103-106): takes the optimizer (an RMSprop of this module)."""
+        if optimizer is not None:
+            if not isinstance(optimizer, RMSprop):
+                raise TypeError("optimizer must be styleTransferTrainingModel.RMSprop (the reference's only optimizer, "
+                                "train_network.py:102)")
+            self.optimizer = optimizer
 
     def optimizer_slots(self) -> List[np.ndarray]:
         """RMSprop ``rms`` slots in weight order."""
@@ -248,6 +316,7 @@ class StyleTransferTrainingModel:
                           gt_style: torch.Tensor, grad: Optional[torch.Tensor] = None,
                           grad_style_params: Optional[torch.Tensor] = None):
         """Training-mode forward + loss + backward -> (prediction, losses (B,4), grad, grad_style_params)."""
+        self._require_trainer()
         B, content, sp, gt_content, gt_style = self._check(content, style_params, gt_content, gt_style)
         dev = content.device
         pred = torch.empty((B,) + self.output_shape, dtype=torch.float32, device=dev)
@@ -262,33 +331,60 @@ class StyleTransferTrainingModel:
         return pred, losses, grad, grad_style_params
 
     def apply_gradients(self, grad: torch.Tensor):
+        self._require_trainer()
+        self._version += 1
         o = self.optimizer
         _lib.check(_lib.load().rst_trainer_apply_gradients(self._handle, _lib.dev_ptr(grad), o.learning_rate, o.rho,
                                                            o.epsilon, _lib.stream_ptr()))
 
-    def sync_moving_statistics(self) -> bool:
-        """Average the BatchNorm moving statistics (transfer net and, if trained jointly, the predictor) over the
-        ranks; no-op without a multi-rank process group. The statistics are not read by any training-mode kernel,
-        so writing them back changes nothing else (set_weights re-packs identical conv images)."""
+    def _world(self) -> int:
         dist = torch.distributed
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.process_group) == 1:
-            return False
+        if not (dist.is_available() and dist.is_initialized()):
+            return 1
+        return dist.get_world_size(self.process_group)
+
+    def _get_moving_statistics(self):
+        """BN moving statistics (transfer net, then the jointly trained predictor) -> the bucket's tail."""
         lib = _lib.load()
-        pr = self.style_predictor
-        w = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
-        _lib.check(lib.rst_trainer_copy_weights(self._handle, _lib.dev_ptr(w), w.numel(), _lib.stream_ptr()))
-        parts = [w[self._bn_index]]
-        if pr is not None:
-            pw = pr.weights_tensor()
-            parts.append(pw[pr.moving_statistics_index])
-        stats = torch.cat(parts)
-        average_over_ranks(stats, self.process_group)
-        n0 = self._bn_index.numel()
-        w[self._bn_index] = stats[:n0]
-        _lib.check(lib.rst_trainer_set_weights(self._handle, _lib.dev_ptr(w), w.numel(), _lib.stream_ptr()))
-        if pr is not None:
-            pw[pr.moving_statistics_index] = stats[n0:]
-            pr.set_weights_tensor(pw)
+        if self._n_stat:
+            _lib.check(lib.rst_trainer_get_moving_statistics(self._handle, _lib.dev_ptr(self._stat), self._n_stat,
+                                                             _lib.stream_ptr()))
+        if self._n_pstat:
+            _lib.check(lib.rst_predictor_trainer_get_moving_statistics(
+                self.style_predictor._handle, _lib.dev_ptr(self._pstat), self._n_pstat, _lib.stream_ptr()))
+
+    def _set_moving_statistics(self, divisor: float):
+        lib = _lib.load()
+        if self._n_stat:
+            _lib.check(lib.rst_trainer_set_moving_statistics(self._handle, _lib.dev_ptr(self._stat), self._n_stat,
+                                                             float(divisor), _lib.stream_ptr()))
+        if self._n_pstat:
+            _lib.check(lib.rst_predictor_trainer_set_moving_statistics(
+                self.style_predictor._handle, _lib.dev_ptr(self._pstat), self._n_pstat, float(divisor),
+                _lib.stream_ptr()))
+
+    def exchange(self) -> bool:
+        """The data-parallel step exchange: ONE all-reduce (SUM) of [gradients | BN moving statistics], then the
+        moving statistics divided by the world size go straight back into the weights (no re-pack). No-op
+        without a multi-rank process group."""
+        world = self._world()
+        if world == 1:
+            return False
+        self._get_moving_statistics()
+        _all_reduce_sum(self._bucket, self.process_group)
+        self._set_moving_statistics(world)
+        return True
+
+    def sync_moving_statistics(self) -> bool:
+        """Average only the BatchNorm moving statistics over the ranks (a separate small all-reduce; train_step
+        folds this into the gradient all-reduce instead). No-op without a multi-rank process group."""
+        world = self._world()
+        if world == 1:
+            return False
+        self._get_moving_statistics()
+        tail = self._bucket[self._grad_bucket.numel():]
+        _all_reduce_sum(tail, self.process_group)
+        self._set_moving_statistics(world)
         return True
 
     def compute_loss(self, x=None, y=None, y_pred=None, sample_weight=None):
@@ -305,6 +401,7 @@ class StyleTransferTrainingModel:
     def train_step(self, x: Dict[str, torch.Tensor], y: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         """One Keras fit step. With a style predictor: x = {'content', 'style' (B,1,H,W,3)}; without:
         x = {'content', 'style_params'}. y = {'content', 'style'}."""
+        self._require_trainer()
         pr = self.style_predictor
         if pr is not None:
             style = x['style']
@@ -318,12 +415,11 @@ class StyleTransferTrainingModel:
         pred, losses, grad, gsp = self.compute_gradients(x['content'], sp, y['content'], y['style'])
         if pr is not None:
             pr.backward(gsp, grad=self._pgrad)
-        allreduce_gradients(self._bucket, self.process_group)
+        self.exchange()                       # one collective: gradients + BN moving statistics
         self.apply_gradients(grad)
         if pr is not None:
             o = self.optimizer
             pr.apply_gradients(self._pgrad, o.learning_rate, o.rho, o.epsilon)
-        self.sync_moving_statistics()
         self.style_losses = {n: losses[:, i] for i, n in enumerate(LOSS_NAMES)}
         self.last_prediction = pred
         self.last_style_params = sp
@@ -344,11 +440,17 @@ class StyleTransferModels:
 
     def __init__(self, training: StyleTransferTrainingModel, loss_model):
         self.training = training
-        self.loss_model = loss_model
+        self.style_loss = loss_model
+
+        def end_to_end_loss(inputs):
+            """loss_model((x, y_true)) (styleTransferTrainingModel.py:59,64): the losses of the inference output."""
+            x, y_true = inputs
+            return loss_model.compute(training(x), y_true)
+
+        self.loss_model = end_to_end_loss
         self.refresh()
 
     def refresh(self):
-        from .styleTransferInferenceModel import StyleTransferInference
         tr = self.training
         self.transfer = tr.transfer_model()
         if tr.style_predictor is not None:
@@ -369,7 +471,9 @@ def make_style_transfer_training_model(style_predictor_factory_func: Optional[Ca
     ``style_transfer_factory_func() -> (StyleTransferModel, P)`` supplies the architecture and
     initial weights; ``style_predictor_factory_func(P) -> StylePredictionModel`` (or None: feed
     ``style_params`` directly) the predictor trained jointly with it (stylePrediction.py:25-75);
-    ``style_loss_func_factory_func() -> (compute_loss, StyleLossModelVGG)`` the loss model."""
+    ``style_loss_func_factory_func() -> (compute_loss, StyleLoss)`` the loss (make_style_loss_function). A
+    construct-only loss (StyleLossModelMobileNet, or the MiDaS depth term) builds a model whose train_step
+    raises — enough for the inference / export scripts, which never train."""
     from .stylePrediction import StylePredictionTrainer
     transfer, P = style_transfer_factory_func()
     predictor = None
@@ -378,14 +482,16 @@ def make_style_transfer_training_model(style_predictor_factory_func: Optional[Ca
         predictor = StylePredictionTrainer(pm.input_shape, pm.feature_extractor, pm.num_top_parameters,
                                            pm.num_style_parameters, weights=pm.get_weights(), max_batch=max_batch,
                                            device=transfer.device)
-    _, loss_model = style_loss_func_factory_func()
+    compute_loss, loss = style_loss_func_factory_func()
+    feature_model = getattr(loss, 'feature_model', loss)
     training = StyleTransferTrainingModel(transfer.input_shape, transfer.output_shape, transfer.plan.bottleneck_res_y,
-                                          transfer.plan.bottleneck_num_filters, loss_model=loss_model,
+                                          transfer.plan.bottleneck_num_filters, loss_model=feature_model,
                                           weights=transfer.get_weights(), max_batch=max_batch, optimizer=optimizer,
                                           process_group=process_group, device=transfer.device, name=name,
-                                          style_predictor=predictor)
-    return StyleTransferModels(training, loss_model)
+                                          style_predictor=predictor,
+                                          with_depth_loss=getattr(compute_loss, 'with_depth_loss', False))
+    return StyleTransferModels(training, loss)
 
 
 __all__ = ['allreduce_gradients', 'RMSprop', 'StyleTransferTrainingModel', 'StyleTransferModels', 'make_style_transfer_training_model',
-           'make_style_loss_function']
+           'make_style_loss_function', 'make_style_transfer_inference_model']

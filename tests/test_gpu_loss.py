@@ -67,8 +67,12 @@ def test_style_loss_matches_oracle(precision, rtol, ftol):
         got = model.feature(name, B).cpu().numpy()
         rel = np.abs(got - feats[name]).max() / np.abs(feats[name]).max()
         assert rel < ftol, (name, rel)
+    # with_depth_loss=True (the reference default) constructs; computing the depth term raises
+    depth_loss, _ = make_style_loss_function(model, (H, W, 3), 1)
+    assert depth_loss.with_depth_loss
     with pytest.raises(NotImplementedError):
-        make_style_loss_function(model, (H, W, 3), 1)
+        depth_loss(torch.zeros(B, H, W, 3, device='cuda'), {'content': torch.zeros(B, H, W, 3, device='cuda'),
+                                                           'style': torch.zeros(B, 1, H, W, 3, device='cuda')})
     with pytest.raises(ValueError):
         compute_loss(torch.zeros(B, H, W, 3, device='cuda'), {'content': torch.zeros(B, H, W, 3, device='cuda'),
                                                               'style': torch.zeros(B, 2, H, W, 3, device='cuda')})

@@ -350,35 +350,53 @@ def test_training_model_reference_geometry_with_dummy_predictor():
     assert tuple(out.shape) == (2,) + oe
 
 
-def test_full_size_bf16_training_step_properties():
+@pytest.mark.parametrize("transfer,joint", [("fp32_winograd", False), ("winograd_bf16x6", True)],
+                         ids=["fp32_winograd", "bench_line"])
+def test_full_size_bf16_training_step_properties(transfer, joint):
     """BASELINE config 4 at its real size (train_network.py:61: B=4, 480x960 frames, rst-960-120-128-17;
-    the VGG16 convs in bf16 as bench.py's training headline): the float64 oracle cannot run this size, so
+    the VGG16 convs in bf16 as bench.py's training headline). ``bench_line`` is exactly bench.py's config-4
+    line: transfer convs on winograd_bf16x6, bf16 VGG16 and the MobileNetV3Small style predictor trained
+    jointly (x = {'content', 'style'}, train_network.py:86-138). The float64 oracle cannot run this size, so
     the test checks size-independent properties — every loss / gradient / weight finite, two trainers from
     the same weights and inputs bitwise identical after three steps (no atomics, fixed reduction order),
     and the batch loss decreasing over three RMSprop steps on one batch."""
     _need_gpu()
     from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.stylePrediction import StylePredictionTrainer
+    from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
+    from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
     sc = ShapeConfig.from_spec("rst-960-120-128-17")
     cfg = dict(input_shape=sc.input_shape['content'], output_shape=sc.output_shape,
                bottleneck_res_y=sc.bottleneck_res_y, bottleneck_num_filters=sc.bottleneck_num_filters)
     B = 4
     plan, w, vgg, content, sp, gtc, gts = _case(cfg, B)
     c, s, gc, gs = _cuda(content, sp, gtc, gts)
+    sins = tuple(sc.input_shape['style'][1:])
+    style = torch.from_numpy(np.random.default_rng(11).random((B, 1) + sins, dtype=np.float32)).cuda()
     runs = []
     for _ in range(2):
-        tr = _trainer(cfg, w, vgg, B, precision="bf16", transfer="fp32_winograd")
+        pr = StylePredictionTrainer(sins, sc.style_feature_extractor_type, plan.num_style_params,
+                                    max_batch=B) if joint else None
+        lm = StyleLossModelVGG(cfg['output_shape'], weights=vgg, max_batch=B, precision="bf16")
+        tr = StyleTransferTrainingModel(cfg['input_shape'], cfg['output_shape'], cfg['bottleneck_res_y'],
+                                        cfg['bottleneck_num_filters'], loss_model=lm, weights=w, max_batch=B,
+                                        precision=transfer, style_predictor=pr)
+        x = {'content': c, 'style': style} if joint else {'content': c, 'style_params': s}
         losses = []
         for _step in range(3):
-            m = tr.train_step({'content': c, 'style_params': s}, {'content': gc, 'style': gs})
+            m = tr.train_step(x, {'content': gc, 'style': gs})
             losses.append(float(m['loss']))
             assert all(np.isfinite(float(v)) for v in m.values())
-            assert bool(torch.isfinite(tr._grad).all())
+            assert bool(torch.isfinite(tr._bucket).all())
         torch.cuda.synchronize()
         flat = np.concatenate([a.reshape(-1) for a in tr.get_weights()])
         assert np.all(np.isfinite(flat))
-        runs.append((losses, flat, tr.last_prediction.cpu().numpy()))
-        del tr
+        pflat = np.concatenate([a.reshape(-1) for a in pr.get_weights()]) if joint else np.zeros(0)
+        assert np.all(np.isfinite(pflat))
+        runs.append((losses, flat, pflat, tr.last_prediction.cpu().numpy()))
+        del tr, pr, lm
         torch.cuda.empty_cache()
-    (l0, w0, p0), (l1, w1, p1) = runs
+    (l0, w0, q0, p0), (l1, w1, q1, p1) = runs
     assert l0 == l1 and np.array_equal(w0, w1) and np.array_equal(p0, p1), "training is not bitwise deterministic"
+    assert np.array_equal(q0, q1), "predictor training is not bitwise deterministic"
     assert l0[2] < l0[1] < l0[0], l0
