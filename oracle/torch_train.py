@@ -218,15 +218,16 @@ def style_losses(pred, content, style, vgg, content_factor=1e4, style_factor=1e-
     return torch.stack([feature + style_l + tv, feature, style_l, tv], dim=1)
 
 
-def _nchw(a):
-    return torch.from_numpy(np.ascontiguousarray(a, np.float64)).permute(0, 3, 1, 2)
+def _nchw(a, dtype=torch.float64):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dtype).permute(0, 3, 1, 2)
 
 
 def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarray], content, style_params,
                   gt_content, gt_style, input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters,
                   factors=(1e4, 1e-3, 1e-1), ms: Optional[Sequence[np.ndarray]] = None,
                   lr=1e-3, rho=0.9, eps=1e-7, pool_route: Optional[Dict[int, np.ndarray]] = None,
-                  vgg_bf16: bool = False, relu_route: Optional[Dict[int, np.ndarray]] = None) -> Dict[str, object]:
+                  vgg_bf16: bool = False, relu_route: Optional[Dict[int, np.ndarray]] = None,
+                  dtype=torch.float64) -> Dict[str, object]:
     """One Keras train_step: forward (BN training mode), loss, gradients, RMSprop.
 
     Inputs are NHWC numpy; returns numpy: prediction (B,H,W,3), losses (B,4), grads (Keras order;
@@ -235,21 +236,23 @@ def training_step(weights: Sequence[np.ndarray], vgg_weights: Sequence[np.ndarra
     ``pool_route``: {VGG conv index before a pool: NHWC activations of the prediction} to align
     the max-pool backward's choice among near-equal maxima with an implementation under test;
     ``relu_route``: {VGG conv index: NHWC post-ReLU activations of the prediction} aligning the ReLU
-    backward masks the same way (pre-activations within rounding distance of 0)."""
+    backward masks the same way (pre-activations within rounding distance of 0).
+    ``dtype``: torch.float64 (the checker) or torch.float32 (bench.py's CPU baseline of the step: the same
+    graph in the reference's own fp32 arithmetic)."""
     blocks, P = transfer_structure(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters)
-    w = [torch.tensor(np.asarray(a, np.float64), requires_grad=True) for a in weights]
-    vgg = [torch.tensor(np.asarray(a, np.float64)) for a in vgg_weights]
-    sp = torch.tensor(np.asarray(style_params, np.float64).reshape(len(content), P), requires_grad=True)
+    w = [torch.tensor(np.asarray(a, np.float64), dtype=dtype, requires_grad=True) for a in weights]
+    vgg = [torch.tensor(np.asarray(a, np.float64), dtype=dtype) for a in vgg_weights]
+    sp = torch.tensor(np.asarray(style_params, np.float64).reshape(len(content), P), dtype=dtype, requires_grad=True)
     gts = np.asarray(gt_style)
     if gts.ndim == 5:
         gts = gts[:, 0]
     taps = []
-    pred, bn_stats = transfer_forward_train(_nchw(content), sp, w, blocks, taps=taps)
+    pred, bn_stats = transfer_forward_train(_nchw(content, dtype), sp, w, blocks, taps=taps)
     vtaps = []
-    route = None if pool_route is None else {k: _nchw(v) for k, v in pool_route.items()}
-    rroute = None if relu_route is None else {k: _nchw(v) for k, v in relu_route.items()}
-    losses = style_losses(pred, _nchw(gt_content), _nchw(gts), vgg, *factors, taps=vtaps, route=route, bf16=vgg_bf16,
-                          relu_route=rroute)
+    route = None if pool_route is None else {k: _nchw(v, dtype) for k, v in pool_route.items()}
+    rroute = None if relu_route is None else {k: _nchw(v, dtype) for k, v in relu_route.items()}
+    losses = style_losses(pred, _nchw(gt_content, dtype), _nchw(gts, dtype), vgg, *factors, taps=vtaps, route=route,
+                          bf16=vgg_bf16, relu_route=rroute)
     losses[:, 0].sum().backward()
     # Keras trainable set: conv kernels/biases, BN gamma/beta (moving statistics are not trained)
     grads, new_w, new_ms = [], [], []
