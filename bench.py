@@ -224,6 +224,32 @@ def bench_split(args, ctx, cfg, ins, outs, plan, weights, P, inputs, precision):
     }
 
 
+def bench_two_styles(args, ctx, cfg, ins, outs, plan, weights, precision):
+    """num_styles = 2 (README dual-style use; styleTransfer.py:36-44,288-303): the same B=1 hipGraph frame loop
+    with a per-pixel style-weight map (the AvgPool2 mip chain and the per-pixel blend of the two CIN affines in
+    the consumer prologues). Reported beside the headline."""
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    B = args.batch
+    plan2 = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 2)
+    model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 2,
+                                           weights=weights, max_batch=B, device=ctx.device, precision=precision)
+    rng = np.random.default_rng(5000 + ctx.rank)
+    inputs = {'content': torch.from_numpy(rng.random((B,) + ins, dtype=np.float32)).to(ctx.device),
+              'style_params': torch.from_numpy(synthetic_style_params(B, 2, P, plan2, seed=7)).to(ctx.device),
+              'style_weights': torch.from_numpy(rng.random((B,) + outs[:2] + (1,), dtype=np.float32)).to(ctx.device)}
+    out = torch.empty((B,) + outs, dtype=torch.float32, device=ctx.device)
+    g = capture_graph(lambda: model(inputs, out=out))
+    for _ in range(args.warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    el = ctx.timed(g.replay, args.steps)
+    kinds = sorted({KERNEL_NAMES.get(model.layer_kernel_id(i), "?") for i in range(len(plan2.layers))})
+    return {"workload": f"{SPEC} with num_styles=2: per-pixel blend of two styles' CIN parameters (style_weights "
+                        f"(B,480,960,1), AvgPool2 mips), B={B}, hipGraph replay", "value": round(ctx.world * B * args.steps / el, 3),
+            "unit": "frames/s", "ms_per_step": round(el * 1e3 / args.steps, 4), "precision_mode": precision,
+            "kernels": kinds}
+
+
 def train_executed_work(plan, H, W, vgg_precision: str, transfer_precision: str) -> dict:
     """Per-sample FLOPs the training step issues, split by the pipe they issue on (bf16 / f32 MFMA), for the
     mixed roofline: ideal time = bf16 FLOPs / bf16 peak + f32 FLOPs / f32 peak. Transfer net: forward (the
@@ -475,6 +501,7 @@ def parse_args(argv=None):
                          "(bf16 is not fp32-level)")
     ap.add_argument("--no-bf16x3", action="store_true", help="skip the other precision-mode measurements")
     ap.add_argument("--no-predictor", action="store_true", help="skip the style-predictor measurement")
+    ap.add_argument("--no-two-styles", action="store_true", help="skip the num_styles=2 frame loop")
     ap.add_argument("--no-ingest", action="store_true", help="skip the G-buffer ingest measurement")
     ap.add_argument("--pcie-steps", type=int, default=50, help="host-resident frame loop (PCIe-inclusive); 0 to skip")
     ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
@@ -690,6 +717,9 @@ def run(args, ctx):
                      if p != args.precision]:
             split_models[prec], split[prec] = bench_split(args, ctx, cfg, ins, outs, plan, weights, P, inputs, prec)
 
+    two_styles = None if args.no_two_styles else bench_two_styles(args, ctx, cfg, ins, outs, plan, weights,
+                                                                   args.precision)
+
     # ---------------- style predictor / inference model -----------------------
     predictor = None if args.no_predictor else bench_predictor(args, ctx, cfg, model, inputs, P)
     ingest = None if args.no_ingest else bench_ingest(args, ctx, cfg)
@@ -798,6 +828,7 @@ def run(args, ctx):
             "stream_graph": stream,
             "layers": layer_table,
             "split_bf16_modes": split,
+            "two_styles": two_styles,
             "training": train,
             "style_predictor": predictor,
             "gbuffer_ingest": ingest,

@@ -86,6 +86,8 @@ struct WinoArgs {
     float4* part;           // [B][128][tiles_y*tiles_x] or null
     int batch, H, W, cin, tiles_y, tiles_x, pro_mode;
     int linear;             // 0: out = ReLU(conv + bias) (the residual convs); 1: conv + bias (input gradient)
+    const float2* pro_ab1;  // two styles (wino_x6 only): [B][cin] the second style's affine, or null
+    const float* pro_w;     // with pro_ab1: [B][H][W] per-pixel weight of the second style (style_blend)
 };
 bool wino_supported(int kh, int stride, int cin, int cout);
 

@@ -381,11 +381,14 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         const float* bias = wp + kcount;
         wp += kcount + s.cout;
         std::vector<float> bias_n, packed;
-        // the Winograd kernel has no two-style blend prologue: those layers keep the direct kernel
-        const bool wino_mode = precision == RST_PRECISION_FP32_WINOGRAD || precision == RST_PRECISION_WINOGRAD_BF16X6;
-        const int lp = (wino_mode && shape->num_styles == 2) ? RST_PRECISION_FP32 : precision;
-        // the narrow-conv kernel has no two-style blend prologue either
-        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, shape->num_styles == 1)) != RST_OK) { delete h; return st; }
+        // two styles: a layer whose input is a conditional-instance-normalised output blends the two styles' CIN
+        // affines per pixel in its prologue. The split-bf16 residual kernel (wino_x6) has that blend; the f32
+        // Winograd kernel and the narrow-conv kernel do not (those layers keep the direct kernel); the final
+        // 9x9 layer (last_x6) takes a blended input materialised by a pre-pass
+        const bool blend_in = shape->num_styles == 2 && li > 0 && specs[li - 1].norm == N_CIN;
+        const bool last9 = s.keras_kind == 1 && s.k == 9;
+        const int lp = (blend_in && precision == RST_PRECISION_FP32_WINOGRAD) ? RST_PRECISION_FP32 : precision;
+        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, !blend_in || last9)) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
         if (s.norm == N_BN) {
@@ -589,7 +592,11 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.tiles_x = e.tiles_x;
         a.pro_mode = e.pro;
         a.linear = e.s.conv_relu ? 0 : 1;
-        if (blend) return fail(RST_ERR_UNSUPPORTED, "Winograd conv has no two-style blend prologue");
+        if (blend) {
+            if (e.kind != K_WINOX6) return fail(RST_ERR_UNSUPPORTED, "f32 Winograd conv has no two-style blend prologue");
+            a.pro_ab1 = src->d_ab1;
+            a.pro_w = mip_ptr(h, src->out_mip, sw);
+        }
         if (ext_ev) wino_x6_set_timing_events(ev[0], ev[1]);
         HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
     } else {

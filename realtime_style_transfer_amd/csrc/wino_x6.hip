@@ -80,6 +80,14 @@ __device__ __forceinline__ float pro_apply(int mode, float x, float2 ab, float r
     return y;
 }
 
+// two styles (styleTransfer.py:36-44): the per-pixel blend of the two CIN affines, as conv_mfma.hip's prologue
+__device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, float2 ab1, float w, float r) {
+    float y = style_blend(w, fmaf(ab.x, x, ab.y), fmaf(ab1.x, x, ab1.y));
+    if (mode == PRO_AFF_RELU) y = fmaxf(y, 0.f);
+    else if (mode == PRO_AFF_RES) y = r + y;
+    return y;
+}
+
 }  // namespace
 
 // Experiment knobs (tools/wino_x6_bench only; never set in the library build): X6_SKIP bit0 = no U reloads
@@ -133,16 +141,21 @@ constexpr int YSTR = 132;                           // epilogue image row stride
 constexpr size_t YIMG_BYTES = (size_t)2 * 128 * YSTR * 4;       // epilogue: two halves' partial Y [pixel][channel]
 constexpr size_t YEPI_BYTES = YIMG_BYTES + 2 * 8 * 32 * 16;     // + statistics reduction [2][8 waves][32] float4
 constexpr size_t YLDS_BYTES = XLDS_BYTES > YEPI_BYTES ? XLDS_BYTES : YEPI_BYTES;
+constexpr size_t YLDS_BLEND_BYTES = YLDS_BYTES + XMAX_CIN * sizeof(float2);   // + the second style's affine
 static_assert(8 % YRING == 0, "ring must divide the points per wave");
 
-template <int PRO>
+// BLEND: two styles — the prologue blends the two CIN affines per pixel (pro_ab1, pro_w)
+template <int PRO, bool BLEND = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_x6_kernel(WinoArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* const patch = smem;                                            // [2][180][24] f32
     unsigned char* const vbytes = reinterpret_cast<unsigned char*>(smem + 2 * XPATCH_FL);   // [2][3][16][32][32 B]
     float2* const pab = reinterpret_cast<float2*>(vbytes + 2 * XV_BYTES);
+    float2* const pab1 = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(smem) + YLDS_BYTES);
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // wave-uniform by construction: the U loads' buffer offsets (from h) are then scalar operands; with a per-lane
+    // wave index hipcc wrapped each of the 24 U loads per chunk in a readfirstlane waterfall loop
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 31, lh = lane >> 5;
     const int g = wave & 3, h = wave >> 2;   // output channel group, transform-point half
     XTL(0);
@@ -160,7 +173,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     if constexpr (pro != PRO_NONE) {
         for (int c = tid; c < Cin; c += YT) pab[c] = a.pro_ab[(size_t)b * Cin + c];
+        if constexpr (BLEND)
+            for (int c = tid; c < Cin; c += YT) pab1[c] = a.pro_ab1[(size_t)b * Cin + c];
     }
+    static_assert(!BLEND || PRO != PRO_NONE, "the blend is a prologue");
 
     // ---- staging descriptors (item k = float4 tid + 512k of a chunk's 720-float4 patch), as above --------
     int sg_goff[YST], sg_lf[YST], sg_moff[YST];
@@ -180,8 +196,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const __amdgpu_buffer_rsrc_t msrd = __builtin_amdgcn_make_buffer_rsrc(
         a.mat, 0, a.mat != nullptr ? (int)((size_t)a.batch * H * W * Cin * 4) : 0, 0x00020000);
     f32x4 xr[YST], rr[YST];
+    float wr[YST];   // BLEND: the second style's weight at each staged pixel (loaded once: it has no channels)
 #pragma unroll
-    for (int k = 0; k < YST; ++k) rr[k] = xr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < YST; ++k) {
+        rr[k] = xr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        wr[k] = 0.f;
+        if constexpr (BLEND) wr[k] = a.pro_w[(sg_goff[k] - 4 * (tid & 3)) / Cin];
+    }
     auto gload = [&](int k, int chunk) __attribute__((always_inline)) {
         const int gi = sg_goff[k] + chunk * XCK;
         xr[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
@@ -192,10 +213,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         f32x4 v = xr[k];
         if constexpr (pro != PRO_NONE) {
             const f32x4 r = rr[k];
-            v.x = pro_apply(pro, v.x, float2{p01.x, p01.y}, r.x);
-            v.y = pro_apply(pro, v.y, float2{p01.z, p01.w}, r.y);
-            v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
-            v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
+            if constexpr (BLEND) {
+                const f32x4 q01 = *reinterpret_cast<const f32x4*>(pab1 + chunk * XCK + 4 * (tid & 3));
+                const f32x4 q23 = *reinterpret_cast<const f32x4*>(pab1 + chunk * XCK + 4 * (tid & 3) + 2);
+                const float w = wr[k];
+                v.x = pro_apply_blend(pro, v.x, float2{p01.x, p01.y}, float2{q01.x, q01.y}, w, r.x);
+                v.y = pro_apply_blend(pro, v.y, float2{p01.z, p01.w}, float2{q01.z, q01.w}, w, r.y);
+                v.z = pro_apply_blend(pro, v.z, float2{p23.x, p23.y}, float2{q23.x, q23.y}, w, r.z);
+                v.w = pro_apply_blend(pro, v.w, float2{p23.z, p23.w}, float2{q23.z, q23.w}, w, r.w);
+            } else {
+                v.x = pro_apply(pro, v.x, float2{p01.x, p01.y}, r.x);
+                v.y = pro_apply(pro, v.y, float2{p01.z, p01.w}, r.y);
+                v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
+                v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
+            }
             if (a.mat != nullptr)
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd,
                                                        sg_moff[k] + chunk * XCK * 4, 0, 0);
@@ -611,6 +642,11 @@ hipError_t wino_x6_prepare() {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)YLDS_BYTES);
         if (e != hipSuccess) return e;
     }
+    for (const void* k : {(const void*)wino_x6_kernel<PRO_AFF_RELU, true>, (const void*)wino_x6_kernel<PRO_AFF, true>,
+                          (const void*)wino_x6_kernel<PRO_AFF_RES, true>}) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)YLDS_BLEND_BYTES);
+        if (e != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 
@@ -630,6 +666,16 @@ hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
         a.tiles_x != (a.W + XTW - 1) / XTW || (size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7F000000)
         return hipErrorInvalidValue;   // 32-bit staging offsets; the out-of-range store offset must stay out of range
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
+    if (a.pro_ab1 != nullptr) {   // two styles
+        if (a.pro_w == nullptr) return hipErrorInvalidValue;
+        switch (a.pro_mode) {
+            case PRO_AFF_RELU: hipExtLaunchKernelGGL((wino_x6_kernel<PRO_AFF_RELU, true>), dim3(grid), dim3(YT), YLDS_BLEND_BYTES, st, e0, e1, 0, a); break;
+            case PRO_AFF: hipExtLaunchKernelGGL((wino_x6_kernel<PRO_AFF, true>), dim3(grid), dim3(YT), YLDS_BLEND_BYTES, st, e0, e1, 0, a); break;
+            case PRO_AFF_RES: hipExtLaunchKernelGGL((wino_x6_kernel<PRO_AFF_RES, true>), dim3(grid), dim3(YT), YLDS_BLEND_BYTES, st, e0, e1, 0, a); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (a.pro_mode) {
         case PRO_NONE: hipExtLaunchKernelGGL(wino_x6_kernel<PRO_NONE>, dim3(grid), dim3(YT), YLDS_BYTES, st, e0, e1, 0, a); break;
         case PRO_AFF_RELU: hipExtLaunchKernelGGL(wino_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(YT), YLDS_BYTES, st, e0, e1, 0, a); break;

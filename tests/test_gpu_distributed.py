@@ -106,7 +106,7 @@ def test_bench_two_ranks_on_one_gpu():
     _need_gpu()
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-                        "--steps", "5", "--warmup", "2", "--stream-batch", "0", "--no-bf16x3", "--no-predictor",
+                        "--steps", "5", "--warmup", "2", "--stream-batch", "0", "--no-bf16x3", "--no-predictor", "--no-two-styles",
                         "--no-ingest", "--train-batch", "2", "--train-steps", "2", "--train-modes", "bf16",
                         "--pcie-steps", "0", "--no-cpu-baseline"],
                        capture_output=True, text=True, env=env, timeout=600)

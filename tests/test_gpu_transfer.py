@@ -203,6 +203,68 @@ def test_two_style_blending_matches_golden():
         model({'content': inputs['content'], 'style_params': inputs['style_params']})   # weights missing
 
 
+@pytest.mark.parametrize("precision", ["winograd_bf16x6", "fp32"])
+def test_two_styles_on_fast_kernels_match_oracle(precision):
+    """num_styles=2 (styleTransfer.py:36-44,288-303) with the production residual width (128 filters): the
+    headline precision runs the residual convs on the split-bf16 Winograd kernel with its per-pixel blend
+    prologue (wino_x6 BLEND), the start conv on wino9_x6 and the last layer on last_x6 (blended input
+    materialised); checked against the float64 oracle and, at the 0/1 weight limits, against the single-style
+    model with each style."""
+    _need_gpu()
+    from oracle import numpy_ref as R
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    ins, outs, br, bf = (32, 64, 17), (32, 64, 3), 8, 128
+    plan = network_plan(ins, outs, br, bf, 2)
+    w = init_weights(plan, seed=2)
+    rng = np.random.default_rng(21)
+    x = rng.random((2,) + ins).astype(np.float32)
+    sp = synthetic_style_params(2, 2, plan.num_style_params, plan, seed=4)
+    sw = rng.random((2,) + outs[:2] + (1,)).astype(np.float32)
+    m, P = create_style_transfer_model(ins, outs, br, bf, 2, weights=w, max_batch=2, precision=precision)
+    inputs = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda(),
+              'style_weights': torch.from_numpy(sw).cuda()}
+    y = m(inputs).cpu().numpy()
+    ref = R.transfer_forward(x, sp, w, ins, outs, br, bf, style_weights=sw)
+    err = np.abs(y - ref).max()
+    assert err < 2e-5, f"max abs err {err}"
+    single, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision=precision)
+    for val, s in ((0.0, 0), (1.0, 1)):
+        inputs['style_weights'] = torch.full_like(inputs['style_weights'], val)
+        y2 = m(inputs).cpu().numpy()
+        y1 = single({'content': inputs['content'], 'style_params': inputs['style_params'][:, s:s + 1].contiguous()})
+        assert np.abs(y2 - y1.cpu().numpy()).max() < 1e-5
+
+
+def test_two_styles_full_size_properties():
+    """rst-960-120-128-17 with two styles at full size (480x960): finite, in (0, 1), deterministic, and
+    between-the-styles behaviour at the 0/1 weight limits (the float64 oracle is too slow at this size)."""
+    _need_gpu()
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    cfg = ShapeConfig.from_spec("rst-960-120-128-17", num_styles=2)
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 2)
+    w = init_weights(plan, seed=2)
+    m, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 2, weights=w,
+                                       max_batch=1)
+    single, _ = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1, weights=w,
+                                            max_batch=1)
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.random((1,) + ins, dtype=np.float32)).cuda()
+    sp = torch.from_numpy(synthetic_style_params(1, 2, P, plan, seed=6)).cuda()
+    sw = torch.from_numpy(rng.random((1,) + outs[:2] + (1,), dtype=np.float32)).cuda()
+    y = m({'content': x, 'style_params': sp, 'style_weights': sw})
+    y2 = m({'content': x, 'style_params': sp, 'style_weights': sw})
+    assert torch.equal(y, y2)
+    assert bool(torch.isfinite(y).all()) and float(y.min()) > 0.0 and float(y.max()) < 1.0
+    for val, s in ((0.0, 0), (1.0, 1)):
+        yl = m({'content': x, 'style_params': sp, 'style_weights': torch.full_like(sw, val)})
+        ys = single({'content': x, 'style_params': sp[:, s:s + 1].contiguous()})
+        assert float((yl - ys).abs().max()) < 1e-5
+
+
 @pytest.mark.parametrize("precision,tol", [("bf16x3", 2e-4), ("bf16x6", 2e-5), ("bf16", 2e-4)])
 def test_split_bf16_precision_modes(precision, tol):
     """RST_PRECISION_BF16X3 / BF16X6 / BF16: residual convs on the bf16 MFMA pipe, vs the float64 oracle
