@@ -125,7 +125,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
     int w9_it = 0;
     (void)w9_it;
     const int H = a.H, W = a.W, Cin = CINT > 0 ? CINT : a.cin;
-    constexpr int ROW = PW * (CINT > 0 ? CINT : 17), TOTAL = PH * ROW, NIT = (TOTAL + NTHR - 1) / NTHR;
+    const int ROW = PW * Cin;   // <= 408 <= NTHR (cin <= 17, wino9_supported)
     static_assert(CINT == 17 || CINT == 0, "");
 
     // ---- U pieces: lane (li, lh) reads U[ab][4p + q][piece][co = li][8lh .. 8lh+7] ------------------
@@ -168,24 +168,29 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
         y0 = ty * TH;
         x0 = tx * TW;
     };
-    constexpr int NH = (NIT + 1) / 2;   // patch elements per thread per half
+    // Staging: a patch row (24 pixels x Cin channels = PW*Cin <= 408 floats) is contiguous in NHWC, so thread
+    // j < PW*Cin owns element j of every row (pixel j / Cin, channel j % Cin) and walks the 24 rows: its LDS
+    // destination and column part of the source offset are per-thread constants, the row part is scalar
+    // (one multiply-add per element instead of the two divisions and 64-bit address math of a flat index)
+    constexpr int NPART = 3, NH = PH / NPART;   // staged in three parts of 8 rows
+    const int sj = tid < ROW ? tid : 0, spx = sj / Cin, sc = sj - spx * Cin;
+    const int sloff = pix_off(0, spx) + sc;   // LDS offset of the thread's element in row 0
+    const bool sact = tid < ROW;
+    const __amdgpu_buffer_rsrc_t insrd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.in), 0, (int)((size_t)a.batch * H * W * Cin * 4), 0x00020000);
     float pf[NH];
-    // (the staging index math is recomputed at every use from an opaque copy of tid: hoisted out of the
-    // tile loop it would pin ~3 registers per staged element)
     auto load_half = [&](int t, auto HALF) __attribute__((always_inline)) {   // clamped addresses
         constexpr int hf = decltype(HALF)::value;
         int y0, x0;
         size_t img;
         tile_coords(t, y0, x0, img);
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
+        const int gx = min(max(x0 - 4 + spx, 0), W - 1);
+        const int voff = sact ? (gx * Cin + sc) * 4 : 0x7FFFFFF0;   // idle threads read out of range (-> 0)
         sfor<0, NH>([&](auto K) __attribute__((always_inline)) {
-            constexpr int k = decltype(K)::value;
-            const int i = min(tid + (hf * NH + k) * NTHR, PH * PW * Cin - 1);
-            const int r = i / (PW * Cin), rem = i - r * (PW * Cin);
-            const int px = rem / Cin, c = rem - px * Cin;
-            const int gy = min(max(y0 - 4 + r, 0), H - 1), gx = min(max(x0 - 4 + px, 0), W - 1);
-            pf[k] = a.in[(img + (size_t)gy * W + gx) * Cin + c];
+            constexpr int r = hf * NH + decltype(K)::value;
+            const int gy = min(max(y0 - 4 + r, 0), H - 1);
+            const int soff = __builtin_amdgcn_readfirstlane((int)((img + (size_t)gy * W) * Cin * 4));
+            pf[decltype(K)::value] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(insrd, voff, soff, 0));
         });
     };
     auto store_half = [&](int t, float* pbuf, auto HALF) __attribute__((always_inline)) {   // zero outside
@@ -193,21 +198,17 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
         int y0, x0;
         size_t img;
         tile_coords(t, y0, x0, img);
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const int total = PH * PW * Cin;
-        sfor<0, NH>([&](auto K) __attribute__((always_inline)) {
-            constexpr int k = decltype(K)::value;
-            const int i = tid + (hf * NH + k) * NTHR;
-            if (hf * NH + k < NIT && ((hf * NH + k + 1) * NTHR <= TOTAL || i < total)) {
-                const int r = i / (PW * Cin), rem = i - r * (PW * Cin);
-                const int px = rem / Cin, c = rem - px * Cin;
-                const int gy = y0 - 4 + r, gx = x0 - 4 + px;
-                const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
-                pbuf[pix_off(r, px) + c] = inside ? pf[k] : 0.f;
-            }
-        });
-        if constexpr (hf == 1)   // channels cin..19 (the previous M exchange overwrote them)
+        const int gx = x0 - 4 + spx;
+        const bool inx = gx >= 0 && gx < W;
+        if (sact) {
+            sfor<0, NH>([&](auto K) __attribute__((always_inline)) {
+                constexpr int r = hf * NH + decltype(K)::value;
+                const int gy = y0 - 4 + r;
+                const bool inside = inx && gy >= 0 && gy < H;
+                pbuf[r * RP + sloff] = inside ? pf[decltype(K)::value] : 0.f;
+            });
+        }
+        if constexpr (hf == NPART - 1)   // channels cin..19 (the previous M exchange overwrote them)
             for (int i = tid; i < NPX * (PS - Cin); i += NTHR) {
                 const int px = i / (PS - Cin);
                 pbuf[pix_off(px / PW, px % PW) + Cin + i % (PS - Cin)] = 0.f;
@@ -240,10 +241,10 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
 
     int t = blockIdx.x;   // work unit
     if (t < n_units) {
-        load_half(t, std::integral_constant<int, 0>{});
-        store_half(t, patch_buf(0), std::integral_constant<int, 0>{});
-        load_half(t, std::integral_constant<int, 1>{});
-        store_half(t, patch_buf(0), std::integral_constant<int, 1>{});
+        sfor<0, NPART>([&](auto PART) __attribute__((always_inline)) {
+            load_half(t, PART);
+            store_half(t, patch_buf(0), PART);
+        });
     }
     for (int it = 0; t < n_units; t += gridDim.x, ++it) {
         w9_it = it;
@@ -285,12 +286,13 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
             sfor<0, 9>([&](auto AB) __attribute__((always_inline)) {
                 constexpr int ab = decltype(AB)::value, cur = ab & 1, sa = ab / 3, sb = ab % 3;
                 load_u(std::integral_constant<int, cur ^ 1>{}, ab + 1);   // ab + 1 == 9: the channel-16 step's U
-                // the next tile's patch: loads at sub-kernels 1 and 4, LDS stores at 3 and 6
-                if constexpr (ab == 1 || ab == 4) {
-                    if (tn < n_units) load_half(tn, std::integral_constant<int, ab == 4>{});
+                // the next tile's patch in three parts: loads at sub-kernels 1, 3, 5, LDS stores two later (3, 5, 7;
+                // each store before the next part's loads reuse its registers)
+                if constexpr (ab == 3 || ab == 5 || ab == 7) {
+                    if (tn < n_units) store_half(tn, pnext, std::integral_constant<int, (ab - 3) / 2>{});
                 }
-                if constexpr (ab == 3 || ab == 6) {
-                    if (tn < n_units) store_half(tn, pnext, std::integral_constant<int, ab == 6>{});
+                if constexpr (ab == 1 || ab == 3 || ab == 5) {
+                    if (tn < n_units) load_half(tn, std::integral_constant<int, (ab - 1) / 2>{});
                 }
                 sfor<0, 2>([&](auto Hh) __attribute__((always_inline)) {
                     constexpr int h = decltype(Hh)::value;
@@ -531,6 +533,8 @@ hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st) {
     if (a.cin > 17 || a.cin <= 0 || a.tiles_y != (a.H + TH - 1) / TH || a.tiles_x != (a.W + TW - 1) / TW ||
         a.part != nullptr || a.bn_ab == nullptr)
         return hipErrorInvalidValue;   // inference only: training keeps wino9_launch (batch-statistics BN)
+    if ((size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7FFFFFF0)
+        return hipErrorInvalidValue;   // 32-bit staging offsets; the idle threads' offset must stay out of range
     // persistent: one workgroup per CU (LDS and registers allow one), each looping over tiles
     const int n_tiles = a.batch * a.tiles_y * a.tiles_x;
     static int n_cu = 0;   // queried once (not per launch: graph capture replays the recorded arguments)
