@@ -129,9 +129,15 @@ __host__ __device__ constexpr int t_pos(int s) {
 }
 }  // namespace lite
 
-template <int MODE, int CIN, int NC, int CKC, int PRO, int X6>
+// PROF: the prologue mode (kernels.h ProMode) | LITE_BLEND (two styles: the per-pixel blend of the two CIN
+// affines, styleTransfer.py:36-44, as conv_mfma.hip's prologue)
+constexpr int LITE_BLEND = 8;
+
+template <int MODE, int CIN, int NC, int CKC, int PROF, int X6>
 __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles) {
     using namespace lite;
+    constexpr int PRO = PROF & 7;
+    constexpr bool BLEND = (PROF & LITE_BLEND) != 0;
     using C = Cfg<MODE, CIN, NC, CKC, X6>;
     using M = Mfma<C::MS>;
     typedef typename M::acc_t acc_t;
@@ -180,6 +186,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // under load exceeds one tile's MFMAs); multi-chunk layers use set 0 only
     constexpr int NSET = NCH == 1 ? 2 : 1;
     f32x4 hreg[NSET][NMAIN + 1], rreg[NSET][NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01[NSET], pa23[NSET];
+    f32x4 pb01[NSET], pb23[NSET];   // BLEND: the second style's affine of the thread's channel quad
+    float bw[NSET][NMAIN + 1];      // BLEND: the second style's weight at each staged pixel
     auto load_step = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {
         constexpr int st = decltype(SET)::value;
         const int co = ch * CKC;
@@ -195,11 +203,17 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             hreg[st][k] = *reinterpret_cast<const f32x4*>(a.in + gi);
             if constexpr (PRO == PRO_AFF_RES) rreg[st][k] = *reinterpret_cast<const f32x4*>(a.res + gi);
 #endif
+            if constexpr (BLEND) bw[st][k] = a.pro_w[(rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)];
         });
         if constexpr (PRO != PRO_NONE) {
             const f32x4* pa = reinterpret_cast<const f32x4*>(a.pro_ab + (size_t)T.b * CIN + co + 4 * q);
             pa01[st] = pa[0];
             pa23[st] = pa[1];
+            if constexpr (BLEND) {
+                const f32x4* pb = reinterpret_cast<const f32x4*>(a.pro_ab1 + (size_t)T.b * CIN + co + 4 * q);
+                pb01[st] = pb[0];
+                pb23[st] = pb[1];
+            }
         }
         if constexpr (NCH > 1) {
             sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
@@ -209,12 +223,20 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             });
         }
     };
-    auto xform = [&](f32x4 v, f32x4 r, const f32x4& p01, const f32x4& p23) __attribute__((always_inline)) {
+    auto xform = [&](f32x4 v, f32x4 r, const f32x4& p01, const f32x4& p23, float w, const f32x4& q01,
+                     const f32x4& q23) __attribute__((always_inline)) {
         if constexpr (PRO != PRO_NONE) {
-            v.x = fmaf(p01.x, v.x, p01.y);
-            v.y = fmaf(p01.z, v.y, p01.w);
-            v.z = fmaf(p23.x, v.z, p23.y);
-            v.w = fmaf(p23.z, v.w, p23.w);
+            if constexpr (BLEND) {
+                v.x = style_blend(w, fmaf(p01.x, v.x, p01.y), fmaf(q01.x, v.x, q01.y));
+                v.y = style_blend(w, fmaf(p01.z, v.y, p01.w), fmaf(q01.z, v.y, q01.w));
+                v.z = style_blend(w, fmaf(p23.x, v.z, p23.y), fmaf(q23.x, v.z, q23.y));
+                v.w = style_blend(w, fmaf(p23.z, v.w, p23.w), fmaf(q23.z, v.w, q23.w));
+            } else {
+                v.x = fmaf(p01.x, v.x, p01.y);
+                v.y = fmaf(p01.z, v.y, p01.w);
+                v.z = fmaf(p23.x, v.z, p23.y);
+                v.w = fmaf(p23.z, v.w, p23.w);
+            }
             if constexpr (PRO == PRO_AFF_RELU) {
                 v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
             } else if constexpr (PRO == PRO_AFF_RES) {
@@ -249,13 +271,15 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             constexpr int k = decltype(K)::value;
             const int hy = rsub + RPP * k;
             if (HR % RPP == 0 || k < NMAIN - 1 || hy < HR) {
-                const f32x4 v = okm && row_ok(hy) ? xform(hreg[st][k], rreg[st][k], pa01[st], pa23[st])
+                const f32x4 v = okm && row_ok(hy) ? xform(hreg[st][k], rreg[st][k], pa01[st], pa23[st], bw[st][k],
+                                                          pb01[st], pb23[st])
                                                   : f32x4{0.f, 0.f, 0.f, 0.f};
                 put(hy, col, lcm, v);
             }
         });
         if (tid < NEXTRA) {
-            const f32x4 v = oke && row_ok(ehy) ? xform(hreg[st][NMAIN], rreg[st][NMAIN], pa01[st], pa23[st])
+            const f32x4 v = oke && row_ok(ehy) ? xform(hreg[st][NMAIN], rreg[st][NMAIN], pa01[st], pa23[st],
+                                                       bw[st][NMAIN], pb01[st], pb23[st])
                                                : f32x4{0.f, 0.f, 0.f, 0.f};
             put(ehy, HCM, lce, v);
         }
@@ -729,6 +753,15 @@ static hipError_t lite_launch_cfg(const ConvArgs& a, hipStream_t st) {
         a.tiles_x != (a.Wo + C::TW - 1) / C::TW || (size_t)a.batch * a.H * a.W * CIN >= ((size_t)1 << 31))
         return hipErrorInvalidValue;   // 32-bit staging offsets
     const int n_tiles = a.batch * a.tiles_y * a.tiles_x;
+    if (a.pro_w != nullptr) {   // two styles
+        if (a.pro_ab1 == nullptr) return hipErrorInvalidValue;
+        switch (a.pro_mode) {
+            case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6>(a, n_tiles, st); break;
+            case PRO_AFF_RES: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6>(a, n_tiles, st); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (a.pro_mode) {
         case PRO_NONE: lite_launch_pro<MODE, CIN, NC, CKC, PRO_NONE, X6>(a, n_tiles, st); break;
         case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>(a, n_tiles, st); break;
@@ -743,7 +776,9 @@ static hipError_t lite_prepare_cfg() {
     using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
     for (const void* k : {(const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_NONE, X6>,
                           (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>,
-                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>}) {
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6>}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES);
         if (e != hipSuccess) return e;
     }
@@ -751,6 +786,8 @@ static hipError_t lite_prepare_cfg() {
     lite_slots<MODE, CIN, NC, CKC, PRO_NONE, X6>();
     lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>();
     lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6>();
     return hipSuccess;
 }
 

@@ -382,13 +382,12 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         wp += kcount + s.cout;
         std::vector<float> bias_n, packed;
         // two styles: a layer whose input is a conditional-instance-normalised output blends the two styles' CIN
-        // affines per pixel in its prologue. The split-bf16 residual kernel (wino_x6) has that blend; the f32
-        // Winograd kernel and the narrow-conv kernel do not (those layers keep the direct kernel); the final
-        // 9x9 layer (last_x6) takes a blended input materialised by a pre-pass
+        // affines per pixel in its prologue. The split-bf16 residual kernel (wino_x6), the narrow-conv kernel
+        // (conv_lite) and the direct kernel have that blend; the f32 Winograd kernel does not (its layers keep the
+        // direct kernel); the final 9x9 layer (last_x6) takes a blended input materialised by a pre-pass
         const bool blend_in = shape->num_styles == 2 && li > 0 && specs[li - 1].norm == N_CIN;
-        const bool last9 = s.keras_kind == 1 && s.k == 9;
         const int lp = (blend_in && precision == RST_PRECISION_FP32_WINOGRAD) ? RST_PRECISION_FP32 : precision;
-        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, !blend_in || last9)) != RST_OK) { delete h; return st; }
+        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, true)) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
         if (s.norm == N_BN) {
@@ -632,8 +631,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.epi_mode = e.s.norm == N_BN ? EPI_RELU_BN : (e.s.conv_relu ? EPI_RELU_STATS : EPI_STATS);
         a.shuffle = e.kind == K_CONVT2 ? 1 : 0;
         if (e.kind == K_LITE) {
-            if (blend) return fail(RST_ERR_UNSUPPORTED, "narrow conv kernel has no two-style blend prologue");
-            HIP_TRY(conv_lite_launch(e.lite, a, st));
+            HIP_TRY(conv_lite_launch(e.lite, a, st));   // two styles: its blend prologue (pro_ab1, pro_w)
         } else {
             HIP_TRY(conv_launch(e.tile, a, st));
         }
