@@ -107,9 +107,12 @@ __device__ __forceinline__ float wave_sum(float x) {
 }
 }  // namespace lastx6
 
-template <int PRO>
+// PROF: PRO_NONE / PRO_AFF_RELU, | 8 for two styles (the per-pixel blend of the two CIN affines)
+template <int PROF>
 __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
     using namespace lastx6;
+    constexpr int PRO = PROF & 7;
+    constexpr bool BLEND = (PROF & 8) != 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     unsigned char* const ring = reinterpret_cast<unsigned char*>(smem);        // [RING][3][2][XW][16 B]
     float* const pbuf = reinterpret_cast<float*>(ring + RING_B);               // [4 waves][28][PCOL] P^T
@@ -144,14 +147,20 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
     // it = tid + 256 k -> (row, x', channel quad q = tid & 3); CIN-apply + ReLU of expand_1 fused; each
     // value split into three bf16 pieces and written to the ring in the MFMA operand layout ----------------
     const int q = tid & 3;
-    f32x4 pa01 = {1.f, 0.f, 1.f, 0.f}, pa23 = {1.f, 0.f, 1.f, 0.f};
+    f32x4 pa01 = {1.f, 0.f, 1.f, 0.f}, pa23 = {1.f, 0.f, 1.f, 0.f}, pb01 = pa01, pb23 = pa23;
     if constexpr (PRO != PRO_NONE) {
         const f32x4* pa = reinterpret_cast<const f32x4*>(a.pro_ab + (size_t)b * CIN + 4 * q);
         pa01 = pa[0];
         pa23 = pa[1];
+        if constexpr (BLEND) {
+            const f32x4* pb = reinterpret_cast<const f32x4*>(a.pro_ab1 + (size_t)b * CIN + 4 * q);
+            pb01 = pb[0];
+            pb23 = pb[1];
+        }
     }
     f32x4 pre[PF], pre2[PF];
-    auto load_rows = [&](int r0, f32x4 (&pre)[PF]) __attribute__((always_inline)) {
+    float prw[PF], prw2[PF];   // BLEND: the second style's weight at each staged pixel
+    auto load_rows = [&](int r0, f32x4 (&pre)[PF], float (&prw)[PF]) __attribute__((always_inline)) {
         sfor<0, PF>([&](auto Kk) __attribute__((always_inline)) {
             constexpr int k = decltype(Kk)::value;
             const int it = tid + 256 * k, r = it / ROW_F4, xp = (it % ROW_F4) >> 2;
@@ -161,15 +170,22 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
 #else
             pre[k] = *reinterpret_cast<const f32x4*>(a.in + (((size_t)b * H + iy) * W + ix) * CIN + 4 * q);
 #endif
+            if constexpr (BLEND) prw[k] = a.pro_w[((size_t)b * H + iy) * W + ix];
         });
     };
-    auto store_rows = [&](int r0, const f32x4 (&pre)[PF]) __attribute__((always_inline)) {
+    auto store_rows = [&](int r0, const f32x4 (&pre)[PF], const float (&prw)[PF]) __attribute__((always_inline)) {
         sfor<0, PF>([&](auto Kk) __attribute__((always_inline)) {
             constexpr int k = decltype(Kk)::value;
             const int it = tid + 256 * k, r = it / ROW_F4, xp = (it % ROW_F4) >> 2;
             const int iy = y0 - PAD + r0 + r, ix = x0 - PAD + xp;
             f32x4 t = pre[k];
-            if constexpr (PRO != PRO_NONE) {
+            if constexpr (BLEND) {   // styleTransfer.py:36-44 (conv_mfma.hip's blend prologue)
+                const float w = prw[k];
+                t.x = fmaxf(style_blend(w, fmaf(pa01.x, t.x, pa01.y), fmaf(pb01.x, t.x, pb01.y)), 0.f);
+                t.y = fmaxf(style_blend(w, fmaf(pa01.z, t.y, pa01.w), fmaf(pb01.z, t.y, pb01.w)), 0.f);
+                t.z = fmaxf(style_blend(w, fmaf(pa23.x, t.z, pa23.y), fmaf(pb23.x, t.z, pb23.y)), 0.f);
+                t.w = fmaxf(style_blend(w, fmaf(pa23.z, t.w, pa23.w), fmaf(pb23.z, t.w, pb23.w)), 0.f);
+            } else if constexpr (PRO != PRO_NONE) {
                 t.x = fmaxf(fmaf(pa01.x, t.x, pa01.y), 0.f);
                 t.y = fmaxf(fmaf(pa01.z, t.y, pa01.w), 0.f);
                 t.z = fmaxf(fmaf(pa23.x, t.z, pa23.y), 0.f);
@@ -186,12 +202,12 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
             *reinterpret_cast<uint2*>(dst + 4 * XW * 16) = make_uint2(p2[0], p2[1]);
         });
     };
-    load_rows(0, pre);
-    load_rows(4, pre2);
-    store_rows(0, pre);
-    load_rows(8, pre);
-    store_rows(4, pre2);
-    store_rows(8, pre);
+    load_rows(0, pre, prw);
+    load_rows(4, pre2, prw2);
+    store_rows(0, pre, prw);
+    load_rows(8, pre, prw);
+    store_rows(4, pre2, prw2);
+    store_rows(8, pre, prw);
     lds_barrier();
     LSTL(1);
 
@@ -329,21 +345,21 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
         }
     };
     // rows of step j (j >= 1) are 4 j + 8 .. 4 j + 11; they live in register buffer pre (j odd) / pre2 (j even)
-    if (NS > 1) load_rows(RING, pre);
-    if (NS > 2) load_rows(RING + 4, pre2);
+    if (NS > 1) load_rows(RING, pre, prw);
+    if (NS > 2) load_rows(RING + 4, pre2, prw2);
     for (int k = 0; k < NS; k += 2) {
         step(k);
         if (k + 1 < NS) {
-            store_rows(4 * k + RING, pre);                       // step k+1's rows into rows 4k .. 4k+3's slots
+            store_rows(4 * k + RING, pre, prw);                       // step k+1's rows into rows 4k .. 4k+3's slots
             lds_barrier();
-            if (k + 3 < NS) load_rows(4 * k + 8 + RING, pre);    // step k+3
+            if (k + 3 < NS) load_rows(4 * k + 8 + RING, pre, prw);    // step k+3
             step(k + 1);
             if (k + 2 < NS) {
                 LSST(k + 1, 6);
-                store_rows(4 * k + 4 + RING, pre2);              // step k+2
+                store_rows(4 * k + 4 + RING, pre2, prw2);              // step k+2
                 lds_barrier();
                 LSST(k + 1, 7);
-                if (k + 4 < NS) load_rows(4 * k + 12 + RING, pre2);   // step k+4
+                if (k + 4 < NS) load_rows(4 * k + 12 + RING, pre2, prw2);   // step k+4
             }
         }
     }
@@ -416,7 +432,8 @@ std::vector<float> last_x6_pack_weights(const float* kern, int cin) {
 }
 
 hipError_t last_x6_prepare() {
-    for (const void* k : {(const void*)last_x6_kernel<PRO_NONE>, (const void*)last_x6_kernel<PRO_AFF_RELU>}) {
+    for (const void* k : {(const void*)last_x6_kernel<PRO_NONE>, (const void*)last_x6_kernel<PRO_AFF_RELU>,
+                          (const void*)last_x6_kernel<PRO_AFF_RELU | 8>}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)lastx6::LDS_BYTES);
         if (e != hipSuccess) return e;
@@ -429,7 +446,10 @@ hipError_t last_x6_launch(const LastArgs& a, hipStream_t st) {
         a.part == nullptr)
         return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * ((a.H + lastx6::RB - 1) / lastx6::RB) * a.tiles_x);
-    if (a.pro_ab != nullptr)
+    if (a.pro_ab1 != nullptr) {   // two styles
+        if (a.pro_ab == nullptr || a.pro_w == nullptr) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(last_x6_kernel<PRO_AFF_RELU | 8>, dim3(grid), dim3(256), lastx6::LDS_BYTES, st, a);
+    } else if (a.pro_ab != nullptr)
         hipLaunchKernelGGL(last_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(256), lastx6::LDS_BYTES, st, a);
     else
         hipLaunchKernelGGL(last_x6_kernel<PRO_NONE>, dim3(grid), dim3(256), lastx6::LDS_BYTES, st, a);

@@ -197,6 +197,8 @@ struct LastArgs {
     float* out;             // [B][H][W][3] raw conv output
     float4* part;           // [B][3][tiles_y * tiles_x] {sum, M2, n}
     int batch, H, W, cin, tiles_y, tiles_x;
+    const float2* pro_ab1;  // two styles: [B][16] the second style's affine, or null
+    const float* pro_w;     // with pro_ab1: [B][H][W] per-pixel weight of the second style (style_blend)
 };
 std::vector<float> last_x6_pack_weights(const float* kern, int cin);
 int last_x6_tiles_y(int H);

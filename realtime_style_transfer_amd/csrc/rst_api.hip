@@ -383,8 +383,8 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         std::vector<float> bias_n, packed;
         // two styles: a layer whose input is a conditional-instance-normalised output blends the two styles' CIN
         // affines per pixel in its prologue. The split-bf16 residual kernel (wino_x6), the narrow-conv kernel
-        // (conv_lite) and the direct kernel have that blend; the f32 Winograd kernel does not (its layers keep the
-        // direct kernel); the final 9x9 layer (last_x6) takes a blended input materialised by a pre-pass
+        // (conv_lite), the final 9x9 kernel (last_x6) and the direct kernel have that blend; the f32 Winograd kernel
+        // does not (its layers keep the direct kernel)
         const bool blend_in = shape->num_styles == 2 && li > 0 && specs[li - 1].norm == N_CIN;
         const int lp = (blend_in && precision == RST_PRECISION_FP32_WINOGRAD) ? RST_PRECISION_FP32 : precision;
         if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, true)) != RST_OK) { delete h; return st; }
@@ -516,11 +516,9 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         LastArgs a{};
         a.in = in;
         a.pro_ab = pro_ab;
-        if (blend) {   // no blend prologue: materialise the blended input first (as for the VALU kernel)
-            HIP_TRY(affine_act_blend_launch(in, pro_ab, src->d_ab1, mip_ptr(h, src->out_mip, sw), nullptr, h->d_xlast,
-                                            B, (long)e.s.H * e.s.W, e.s.cin, 1, st));
-            a.in = h->d_xlast;
-            a.pro_ab = nullptr;
+        if (blend) {   // two styles: its blend prologue
+            a.pro_ab1 = src->d_ab1;
+            a.pro_w = mip_ptr(h, src->out_mip, sw);
         }
         if (e.pro != PRO_AFF_RELU && e.pro != PRO_NONE)
             return fail(RST_ERR_UNSUPPORTED, "last layer prologue must be CIN+ReLU");

@@ -7,6 +7,9 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 rm -f gpurun_out/x6b.log gpurun_out/w9b.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_transfer.py -x -v --timeout 200 --timeout-method thread -k "two_style" \
+    > gpurun_out/pytest_s2.log 2>&1 || { tail -30 gpurun_out/pytest_s2.log; exit 1; }
+tail -2 gpurun_out/pytest_s2.log
 for b in wino_x6_bench wino_x6_bench_v2; do
     for args in "1 128 1 0 0 0 0 1" "1 128 1" "1 128 3" "1 128 2"; do
         echo "== $b $args" >> gpurun_out/x6b.log
