@@ -227,6 +227,9 @@ struct FinalizeArgs {
     float eps;
 };
 hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st);
+// The network output: the last layer's CIN finalize (3 channels, num_styles = 1) fused with its affine + sigmoid
+// over the (B, hw, 3) raw output; also stores a.ab
+hipError_t fin_sigmoid3_launch(const FinalizeArgs& a, const float* x, float* y, long hw, hipStream_t st);
 
 // y = act(a*x + b [+ res]) element-wise, act: 0 none, 1 relu, 2 sigmoid.  x,res,y [B][HW][C]
 hipError_t affine_act_launch(const float* x, const float2* ab, const float* res, float* y, int batch, long hw, int C,

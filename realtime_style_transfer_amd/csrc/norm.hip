@@ -76,10 +76,12 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
 // Summation order is fixed (accumulator j = k mod 4, then a fixed-order block sum): deterministic.
 constexpr int FIN_UNROLL = 8;
 
+// One channel's finalize by NT threads (tid < NT): the merged statistics -> the affine (a, b) the consumer
+// applies, written by thread 0 (also returned in aa / bb on thread 0). Shared by finalize_kernel and the fused
+// output kernel below, so both produce the same bits.
 template <int NT, int U = FIN_UNROLL>
-__global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
-    __shared__ double scratch[3][NT / 64];
-    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+__device__ __forceinline__ void finalize_channel(const FinalizeArgs& a, int c, int b, int tid, double (*scratch)[NT / 64],
+                                                 float& aa_out, float& bb_out, bool store = true) {
     const int b0 = a.merge_images ? 0 : b, nb = a.merge_images ? a.batch : 1;
     float scale = 1.f, bias = 0.f, scale1 = 0.f, bias1 = 0.f;
     if (tid == 0) {   // issued before the partial loads: independent of them
@@ -138,7 +140,10 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
         const double var = N > 0.0 ? m2 / N : 0.0;
         const float rstd = (float)(1.0 / sqrt(var + (double)a.eps));
         const float aa = scale * rstd;
-        a.ab[b * a.C + c] = make_float2(aa, bias - (float)mean * aa);
+        aa_out = aa;
+        bb_out = bias - (float)mean * aa;
+        if (!store) return;
+        a.ab[b * a.C + c] = make_float2(aa, bb_out);
         if (a.ab1 != nullptr) {   // second style (styleTransfer.py:36-44 blends the affine per pixel)
             const float a1 = scale1 * rstd;
             a.ab1[b * a.C + c] = make_float2(a1, bias1 - (float)mean * a1);
@@ -150,6 +155,59 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
             a.moving_var[c] = (float)(a.momentum * a.moving_var[c] + (1.0 - a.momentum) * unbiased);
         }
     }
+}
+
+template <int NT, int U = FIN_UNROLL>
+__global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
+    __shared__ double scratch[3][NT / 64];
+    float aa, bb;
+    finalize_channel<NT, U>(a, blockIdx.x, blockIdx.y, threadIdx.x, scratch, aa, bb);
+}
+
+// The network output (styleTransfer.py:269-276, 329): sigmoid(CIN(x)) of the last layer's 3 channels, with that
+// CIN's finalize fused in front (num_styles = 1): workgroup (g, b) first merges image b's statistics of the three
+// channels (waves 0..2, one channel each, the finalize_kernel<64> arithmetic: bitwise the same affine), then
+// applies the affine + sigmoid to its slice of the image as float4s (hw * 3 is a multiple of 4 here). Workgroup
+// (0, b) also stores the affine (rst_copy_activation reads it). Saves the separate finalize launch.
+__global__ __launch_bounds__(256) void fin_sigmoid3_kernel(FinalizeArgs a, const float* __restrict__ x,
+                                                           float* __restrict__ y, int n4_img) {
+    __shared__ double scratch[3][3][1];
+    __shared__ float aff[6];
+    const int b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave < 3) {
+        float aa = 0.f, bb = 0.f;   // only workgroup (0, b) stores the affine
+        finalize_channel<64>(a, wave, b, lane, scratch[wave], aa, bb, blockIdx.x == 0);
+        if (lane == 0) {
+            aff[2 * wave] = aa;
+            aff[2 * wave + 1] = bb;
+        }
+    }
+    __syncthreads();
+    const float a0 = aff[0], b0 = aff[1], a1 = aff[2], b1 = aff[3], a2 = aff[4], b2 = aff[5];
+    const float4* __restrict__ xi = reinterpret_cast<const float4*>(x) + (size_t)b * n4_img;
+    float4* __restrict__ yo = reinterpret_cast<float4*>(y) + (size_t)b * n4_img;
+    auto sig = [](float v) __attribute__((always_inline)) { return 1.f / (1.f + __expf(-v)); };
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n4_img; i += gridDim.x * 256) {
+        const float4 v = xi[i];
+        // element 4i + k has channel (4i + k) % 3: the float4 starts at channel (i % 3) ... (4i % 3 = i % 3)
+        const int c0 = i % 3;
+        const float aA = c0 == 0 ? a0 : (c0 == 1 ? a1 : a2), bA = c0 == 0 ? b0 : (c0 == 1 ? b1 : b2);
+        const float aB = c0 == 0 ? a1 : (c0 == 1 ? a2 : a0), bB = c0 == 0 ? b1 : (c0 == 1 ? b2 : b0);
+        const float aC = c0 == 0 ? a2 : (c0 == 1 ? a0 : a1), bC = c0 == 0 ? b2 : (c0 == 1 ? b0 : b1);
+        yo[i] = make_float4(sig(fmaf(aA, v.x, bA)), sig(fmaf(aB, v.y, bB)), sig(fmaf(aC, v.z, bC)), sig(fmaf(aA, v.w, bA)));
+    }
+}
+
+hipError_t fin_sigmoid3_launch(const FinalizeArgs& a, const float* x, float* y, long hw, hipStream_t st) {
+    if (a.C != 3 || a.ntot != 3 || a.merge_images || a.ab1 != nullptr || (hw * 3) % 4 != 0 ||
+        (long)a.n_part * a.phases > FIN_UNROLL * 64 || hw * 3 / 4 >= (1L << 31))
+        return hipErrorInvalidValue;
+    const int n4 = (int)(hw * 3 / 4);
+    int g = (n4 + 256 * 8 - 1) / (256 * 8);   // ~8 float4 per thread
+    if (g > 256) g = 256;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(fin_sigmoid3_kernel, dim3(g, a.batch), dim3(256), 0, st, a, x, y, n4);
+    return hipGetLastError();
 }
 
 hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st) {

@@ -498,6 +498,13 @@ static const float* mip_ptr(const rst_handle* h, int level, const float* style_w
     return level == 0 ? style_weights : h->d_mip[level];
 }
 
+// num_styles = 1 with last_x6: the last CIN's finalize runs fused into the output kernel (fin_sigmoid3_launch)
+static bool output_finalize_fused(const rst_handle* h) {
+    const LayerExec& last = h->layers.back();
+    return h->shape.num_styles == 1 && last.kind == K_LASTX6 && last.s.cout == 3 && last.n_part <= 512 &&
+           ((long)last.s.Ho * last.s.Wo * 3) % 4 == 0;
+}
+
 static int launch_layer(rst_handle* h, size_t li, const float* content, const float* style, const float* sw, int B,
                         hipStream_t st) {
     LayerExec& e = h->layers[li];
@@ -635,7 +642,9 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         }
     }
     if (ev && !ext_ev) HIP_TRY(hipEventRecord(ev[1], st));
-    if (e.s.norm == N_CIN) {
+    // the last layer's finalize (one style) is fused into the output kernel (fin_sigmoid3_launch, rst_forward)
+    const bool fused_out_fin = li + 1 == h->layers.size() && output_finalize_fused(h);
+    if (e.s.norm == N_CIN && !fused_out_fin) {
         FinalizeArgs f{};
         f.part = e.d_part;
         f.style = style;
@@ -682,11 +691,26 @@ int rst_forward(rst_handle* h, const float* content, const float* style_params, 
         if (r != RST_OK) return r;
     }
     const LayerExec& last = h->layers.back();
-    if (h->shape.num_styles == 2)
+    if (h->shape.num_styles == 2) {
         HIP_TRY(affine_act_blend_launch(last.d_out, last.d_ab, last.d_ab1, mip_ptr(h, last.out_mip, style_weights),
                                         nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
-    else
+    } else if (output_finalize_fused(h)) {   // the last CIN's finalize fused with the output sigmoid
+        FinalizeArgs f{};
+        f.part = last.d_part;
+        f.style = style_params;
+        f.ab = last.d_ab;
+        f.batch = batch;
+        f.C = last.s.cout;
+        f.ntot = last.ntot;
+        f.n_part = last.n_part;
+        f.phases = 1;
+        f.style_stride = h->shape.num_styles * h->P;
+        f.style_offset = last.s.style_offset;
+        f.eps = 1e-5f;
+        HIP_TRY(fin_sigmoid3_launch(f, last.d_out, out, (long)last.s.Ho * last.s.Wo, st));
+    } else {
         HIP_TRY(affine_act_launch(last.d_out, last.d_ab, nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
+    }
     h->last_style_weights = style_weights;
     if (h->prof_on && h->prof_step < h->prof_max_steps) h->prof_step++;
     return RST_OK;
