@@ -95,9 +95,6 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 #ifndef X6_SKIP
 #define X6_SKIP 0
 #endif
-#ifndef X6_PRIO
-#define X6_PRIO 0   // experiment knob: 1 = waves 4-7 at s_setprio 1 in the main loop, 2 = waves 0-3
-#endif
 #ifdef X6_PROF
 // timeline per (workgroup, wave < 8) on the constant 100 MHz clock: start, pipeline filled, chunk loop done, end
 __device__ unsigned long long x6_tl[X6_PROF][8][4];
@@ -366,11 +363,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     lds_barrier();
 
     XTL(1);
-#if X6_PRIO == 1
-    if (h == 1) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half (MI355X_MICROARCH.md, two waves/SIMD item 4)
-#elif X6_PRIO == 2
-    if (h == 0) __builtin_amdgcn_s_setprio(1);
-#endif
     const int varow = li * XVROW + 16 * (lh ^ ((li >> 3) & 1)) + 8 * h * 32 * XVROW;
     unsigned qa0 = 0, qa1 = 0, qb0 = 0, qb1 = 0;
     f32x4 sp01 = f32x4{0.f, 0.f, 0.f, 0.f}, sp23 = sp01, sv = sp01;
