@@ -271,6 +271,12 @@ def train_executed_work(plan, H, W, vgg_precision: str, transfer_precision: str)
         return layer_flops(l)
     t_f32, t_bf16 = 0.0, 0.0
     for i, l in enumerate(plan.layers):
+        if x6 and i == 0 and l.k == 9:   # start conv forward on wino9_x6 (16x16 blocks, K = 9 x 16 + 16 per point)
+            Ho, Wo = l.out_hw
+            tiles = (-(-Ho // 16) * 8) * (-(-Wo // 16) * 8)
+            t_bf16 += 6 * 2.0 * tiles * 16 * (9 * 16 + 16) * l.cout
+            t_f32 += layer_flops(l)   # weight gradient (direct GEMM, f32)
+            continue
         work = conv_exec(i, l) + layer_flops(l) + (conv_exec(i, l) if i > 0 else 0.0)   # fwd + wgrad + dgrad
         if x6 and l.block.startswith('residual'):
             t_bf16 += 6 * work
@@ -339,9 +345,9 @@ def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"
                                    "fp32_winograd": "residual 3x3 convs (forward + input gradient) and the 9x9 start "
                                                     "conv (forward) as Winograd F(2x2,3x3) on f32 MFMA, the other "
                                                     "transfer convs exact f32",
-                                   "winograd_bf16x6": "residual 3x3 convs (forward, input gradient, weight gradient) on "
-                                                      "exact 3-piece split-bf16 MFMA products (fp32-level), the 9x9 start "
-                                                      "conv (forward) as Winograd F(2x2,3x3) on f32 MFMA, the other "
+                                   "winograd_bf16x6": "residual 3x3 convs (forward, input gradient, weight gradient) and "
+                                                      "the 9x9 start conv's forward (nine 3x3 Winograd sub-kernels) on "
+                                                      "exact 3-piece split-bf16 MFMA products (fp32-level), the other "
                                                       "transfer convs exact f32"}[tr.precision],
             "tflop_per_sample": round(per_sample / 1e12, 4),
             "algorithmic_tflops_per_gpu": round(tfs, 2),

@@ -68,7 +68,7 @@ constexpr int PCOL = XW + 4;                // transposed P buffer [28 columns n
 constexpr int P_B = 4 * 28 * PCOL * 4;      // 44800
 constexpr int ROW_F4 = XW * CIN / 4;        // 384 float4 per staged input row
 constexpr int PF = 4 * ROW_F4 / 256;        // 6 prefetch float4 per thread (4 rows)
-constexpr size_t LDS_BYTES = (size_t)RING_B + P_B + 2 * 16 * 4 * 4;
+constexpr size_t LDS_BYTES = (size_t)RING_B + P_B + 2 * 16 * 4 * 4 + 2 * CIN * 8;   // + prologue affine table
 static_assert((4 * ROW_F4) % 256 == 0, "staging map");
 
 template <int I, int N, typename F>
@@ -148,16 +148,33 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
     // value split into three bf16 pieces and written to the ring in the MFMA operand layout ----------------
     const int q = tid & 3;
     f32x4 pa01 = {1.f, 0.f, 1.f, 0.f}, pa23 = {1.f, 0.f, 1.f, 0.f}, pb01 = pa01, pb23 = pa23;
+    // the prologue affine (given, or formed from the producer's f64 accumulators), after the first rows' loads
+    // are issued so its latency overlaps theirs
+    auto load_affine = [&]() __attribute__((always_inline)) {
     if constexpr (PRO != PRO_NONE) {
-        const f32x4* pa = reinterpret_cast<const f32x4*>(a.pro_ab + (size_t)b * CIN + 4 * q);
+        const float2* ab = a.pro_ab + (size_t)b * CIN;
+        const float2* ab1 = BLEND ? a.pro_ab1 + (size_t)b * CIN : nullptr;
+        if (a.pro_stat.acc != nullptr) {   // formed from the producer's f64 accumulators (no finalize ran)
+            float2* const ltab = reinterpret_cast<float2*>(red + 128);   // [2][16]
+            const CinSrc& ps = a.pro_stat;
+            const bool store = rb == 0 && sx == 0;   // one workgroup per image keeps the host-visible copy
+            cin_affine_table<256>(ps, b, 1, ltab, BLEND ? ltab + CIN : nullptr,
+                                  store && ps.ab_out ? ps.ab_out + (size_t)b * CIN : nullptr,
+                                  store && ps.ab1_out ? ps.ab1_out + (size_t)b * CIN : nullptr);
+            lds_barrier();
+            ab = ltab;
+            ab1 = ltab + CIN;
+        }
+        const f32x4* pa = reinterpret_cast<const f32x4*>(ab + 4 * q);
         pa01 = pa[0];
         pa23 = pa[1];
         if constexpr (BLEND) {
-            const f32x4* pb = reinterpret_cast<const f32x4*>(a.pro_ab1 + (size_t)b * CIN + 4 * q);
+            const f32x4* pb = reinterpret_cast<const f32x4*>(ab1 + 4 * q);
             pb01 = pb[0];
             pb23 = pb[1];
         }
     }
+    };
     f32x4 pre[PF], pre2[PF];
     float prw[PF], prw2[PF];   // BLEND: the second style's weight at each staged pixel
     auto load_rows = [&](int r0, f32x4 (&pre)[PF], float (&prw)[PF]) __attribute__((always_inline)) {
@@ -204,6 +221,7 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
     };
     load_rows(0, pre, prw);
     load_rows(4, pre2, prw2);
+    load_affine();
     store_rows(0, pre, prw);
     load_rows(8, pre, prw);
     store_rows(4, pre2, prw2);
@@ -217,6 +235,10 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
     float* const pw = pbuf + wave * (28 * PCOL);
     const int n = lane & 31;
     const int n_tiles4 = (H + 3) / 4;
+    // the output CIN's statistics into f64 accumulators (a.stat): lanes tid < 3 sum this workgroup's tiles
+    // ({S, M2 + S^2/n}, finalize_kernel's merge quantity) and add them once at the end
+    const bool to_acc = a.stat.acc != nullptr;
+    double accS = 0.0, accQ = 0.0;
     auto step = [&](int k) __attribute__((always_inline)) {
         LSST(k, 0);
         f32x16 acc[NT];
@@ -340,8 +362,14 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
                 const float d = nw > 0.f ? rs[w * 16 + 4 * tid] / nw - mean : 0.f;
                 M2 += rs[w * 16 + 4 * tid + 1] + nw * d * d;
             }
-            const int n_part = a.tiles_y * a.tiles_x;
-            a.part[((size_t)b * 3 + tid) * n_part + ty4 * a.tiles_x + sx] = make_float4(S, M2, N, 0.f);
+            if (to_acc) {
+                const double dS = (double)S;
+                accS += dS;
+                if (N > 0.f) accQ += (double)M2 + dS * dS / (double)N;
+            } else {
+                const int n_part = a.tiles_y * a.tiles_x;
+                a.part[((size_t)b * 3 + tid) * n_part + ty4 * a.tiles_x + sx] = make_float4(S, M2, N, 0.f);
+            }
         }
     };
     // rows of step j (j >= 1) are 4 j + 8 .. 4 j + 11; they live in register buffer pre (j odd) / pre2 (j even)
@@ -363,6 +391,7 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
             }
         }
     }
+    if (to_acc && tid < 3) cin_acc_add(a.stat, a.batch, 3, b, tid, (int)blockIdx.x % a.stat.nslot, accS, accQ);
     LSTL(3);
 }
 
@@ -443,13 +472,19 @@ hipError_t last_x6_prepare() {
 
 hipError_t last_x6_launch(const LastArgs& a, hipStream_t st) {
     if (a.cin != lastx6::CIN || a.tiles_y != last_x6_tiles_y(a.H) || a.tiles_x != last_x6_tiles_x(a.W) ||
-        a.part == nullptr)
+        (a.part == nullptr) == (a.stat.acc == nullptr))
+        return hipErrorInvalidValue;   // statistics: partials or accumulators
+    if (a.stat.acc != nullptr && (a.stat.nslot < 1 || a.stat.nslot > CIN_ACC_MAX_SLOTS)) return hipErrorInvalidValue;
+    const bool src_acc = a.pro_stat.acc != nullptr;
+    if (src_acc && (a.pro_stat.nslot < 1 || a.pro_stat.nslot > CIN_ACC_MAX_SLOTS || a.pro_stat.C != lastx6::CIN ||
+                    a.pro_stat.batch != a.batch || a.pro_stat.style == nullptr))
         return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * ((a.H + lastx6::RB - 1) / lastx6::RB) * a.tiles_x);
-    if (a.pro_ab1 != nullptr) {   // two styles
-        if (a.pro_ab == nullptr || a.pro_w == nullptr) return hipErrorInvalidValue;
+    if (a.pro_w != nullptr) {   // two styles
+        if (src_acc ? a.pro_stat.style1_offset < 0 : (a.pro_ab == nullptr || a.pro_ab1 == nullptr))
+            return hipErrorInvalidValue;
         hipLaunchKernelGGL(last_x6_kernel<PRO_AFF_RELU | 8>, dim3(grid), dim3(256), lastx6::LDS_BYTES, st, a);
-    } else if (a.pro_ab != nullptr)
+    } else if (a.pro_ab != nullptr || src_acc)
         hipLaunchKernelGGL(last_x6_kernel<PRO_AFF_RELU>, dim3(grid), dim3(256), lastx6::LDS_BYTES, st, a);
     else
         hipLaunchKernelGGL(last_x6_kernel<PRO_NONE>, dim3(grid), dim3(256), lastx6::LDS_BYTES, st, a);

@@ -148,6 +148,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     float* const halo = smem;                  // [HALO]   one Cin chunk of the tile's input halo
     float* const wts = smem + C::HALO;         // [WCH]    one Cin chunk of the weights
     float* const red = wts + C::WCH;           // [8][NC]  statistics scratch
+    float2* const tab = reinterpret_cast<float2*>(red + 8 * NC);   // prologue affine [batch][CIN] (+ second style)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int H = a.H, W = a.W;
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     f32x4 hreg[NSET][NMAIN + 1], rreg[NSET][NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01[NSET], pa23[NSET];
     f32x4 pb01[NSET], pb23[NSET];   // BLEND: the second style's affine of the thread's channel quad
     float bw[NSET][NMAIN + 1];      // BLEND: the second style's weight at each staged pixel
-    auto load_step = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {
+    auto load_in = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {
         constexpr int st = decltype(SET)::value;
         const int co = ch * CKC;
         const int ixm = min(max(T.ix0 + col, 0), W - 1), ixe = min(max(T.ix0 + HCM, 0), W - 1);
@@ -205,16 +206,6 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
 #endif
             if constexpr (BLEND) bw[st][k] = a.pro_w[(rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)];
         });
-        if constexpr (PRO != PRO_NONE) {
-            const f32x4* pa = reinterpret_cast<const f32x4*>(a.pro_ab + (size_t)T.b * CIN + co + 4 * q);
-            pa01[st] = pa[0];
-            pa23[st] = pa[1];
-            if constexpr (BLEND) {
-                const f32x4* pb = reinterpret_cast<const f32x4*>(a.pro_ab1 + (size_t)T.b * CIN + co + 4 * q);
-                pb01[st] = pb[0];
-                pb23[st] = pb[1];
-            }
-        }
         if constexpr (NCH > 1) {
             sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
                 constexpr int k = decltype(K)::value;
@@ -222,6 +213,24 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 wreg[k] = reinterpret_cast<const f32x4*>(a.wpk)[(size_t)ch * C::WITEMS + it];
             });
         }
+    };
+    auto load_aff = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {   // from the LDS table
+        constexpr int st = decltype(SET)::value;
+        if constexpr (PRO != PRO_NONE) {
+            const int co = ch * CKC;
+            const f32x4* pa = reinterpret_cast<const f32x4*>(tab + T.b * CIN + co + 4 * q);
+            pa01[st] = pa[0];
+            pa23[st] = pa[1];
+            if constexpr (BLEND) {
+                const f32x4* pb = reinterpret_cast<const f32x4*>(tab + (a.batch + T.b) * CIN + co + 4 * q);
+                pb01[st] = pb[0];
+                pb23[st] = pb[1];
+            }
+        }
+    };
+    auto load_step = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {
+        load_in(T, ch, SET);
+        load_aff(T, ch, SET);
     };
     auto xform = [&](f32x4 v, f32x4 r, const f32x4& p01, const f32x4& p23, float w, const f32x4& q01,
                      const f32x4& q23) __attribute__((always_inline)) {
@@ -424,6 +433,15 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     const int n = M::col(lane);
     const float bias = a.bias[n];
     const float2 bn = MODE == 0 ? a.bn_ab[n] : float2{1.f, 0.f};
+    // CIN statistics into f64 accumulators (a.stat): this workgroup's tiles summed per image in the lanes
+    // tid < NC ({S, M2 + S^2/n} per tile, finalize_kernel's merge quantity), added at an image change / the end
+    const bool to_acc = a.stat.acc != nullptr;
+    double accS = 0.0, accQ = 0.0;
+    int acc_b = -1;
+    auto acc_flush = [&]() __attribute__((always_inline)) {
+        if (acc_b >= 0) cin_acc_add(a.stat, a.batch, NC, acc_b, tid, (int)blockIdx.x % a.stat.nslot, accS, accQ);
+        accS = accQ = 0.0;
+    };
     auto epilogue = [&](const Tile& T) __attribute__((always_inline)) {
         if constexpr (MODE == 0) {   // bias + ReLU -> BatchNorm (inference affine) -> ReLU, NHWC store
             const acc_t y = (acc[0] + acc[1]) + acc[2];
@@ -474,7 +492,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         }
                     }
             }
-            if (a.part != nullptr && (LITE_SKIP & 32) == 0) {
+            if ((a.part != nullptr || to_acc) && (LITE_SKIP & 32) == 0) {
                 // lanes n, n + MS, ... hold column n: reduce over them, then over the 4 waves (fixed order)
 #pragma unroll
                 for (int o = MS; o < 64; o <<= 1) {
@@ -505,8 +523,18 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 lds_barrier();
                 if (tid < NC) {   // lane tid < NC holds column tid
                     const float M2 = (red[tid] + red[NC + tid]) + (red[2 * NC + tid] + red[3 * NC + tid]);
-                    const int n_part = a.tiles_y * a.tiles_x;
-                    a.part[((size_t)T.b * NC + tid) * n_part + T.ty * a.tiles_x + T.tx] = make_float4(S, M2, N, 0.f);
+                    if (to_acc) {
+                        if (T.b != acc_b) {
+                            acc_flush();
+                            acc_b = T.b;
+                        }
+                        const double dS = (double)S;
+                        accS += dS;
+                        if (N > 0.f) accQ += (double)M2 + dS * dS / (double)N;
+                    } else {
+                        const int n_part = a.tiles_y * a.tiles_x;
+                        a.part[((size_t)T.b * NC + tid) * n_part + T.ty * a.tiles_x + T.tx] = make_float4(S, M2, N, 0.f);
+                    }
                 }
             }
         }
@@ -518,6 +546,24 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         for (int it = tid; it < C::WITEMS; it += 256)
             reinterpret_cast<f32x4*>(wts)[it] = reinterpret_cast<const f32x4*>(a.wpk)[it];
     }
+    // the prologue affine of every image into the LDS table: given, or formed from the producer's f64
+    // accumulators (no finalize ran); runs after the first tiles' input loads are issued
+    auto fill_table = [&]() __attribute__((always_inline)) {
+    if constexpr (PRO != PRO_NONE) {
+        const CinSrc& ps = a.pro_stat;
+        if (ps.acc != nullptr) {
+            const bool store = blockIdx.x == 0;   // the host-visible copy (rst_copy_activation)
+            cin_affine_table<256>(ps, 0, a.batch, tab, BLEND ? tab + a.batch * CIN : nullptr,
+                                  store ? ps.ab_out : nullptr, store ? ps.ab1_out : nullptr);
+        } else {
+            for (int i = tid; i < a.batch * CIN; i += 256) {
+                tab[i] = a.pro_ab[i];
+                if constexpr (BLEND) tab[a.batch * CIN + i] = a.pro_ab1[i];
+            }
+        }
+        lds_barrier();
+    }
+    };
     const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, NSET - 1>;
@@ -525,11 +571,14 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     if constexpr (NCH == 1) {
         // tile k's input sits in register set k & 1, loaded two tiles ahead
         Tile T0 = tile_of(0), T1 = T0;
-        load_step(T0, 0, S0{});
+        load_in(T0, 0, S0{});
         if (my_tiles > 1) {
             T1 = tile_of(1);
-            load_step(T1, 0, S1{});
+            load_in(T1, 0, S1{});
         }
+        fill_table();
+        load_aff(T0, 0, S0{});
+        if (my_tiles > 1) load_aff(T1, 0, S1{});
         for (int k = 0; k < my_tiles; k += 2) {
             LTL(k, 0);
             if (k > 0) lds_barrier();
@@ -565,7 +614,9 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     } else {
         const int n_steps = my_tiles * NCH;
         Tile cur = tile_of(0);
-        load_step(cur, 0, S0{});
+        load_in(cur, 0, S0{});
+        fill_table();
+        load_aff(cur, 0, S0{});
         for (int s = 0; s < n_steps; ++s) {
             const int ch = s % NCH;
             LTL(s, 0);
@@ -589,6 +640,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             cur = nxt;
         }
     }
+    if (to_acc && tid < NC) acc_flush();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -723,6 +775,13 @@ static int lite_cu_count() {
     return n_cu;
 }
 
+// LDS past the kernel's fixed image: the prologue affine table [batch][CIN] (two styles: both)
+static size_t lite_tab_bytes(int pro, int cin, int batch) {
+    const int p = pro & 7;
+    return p == PRO_NONE ? 0 : (size_t)batch * cin * sizeof(float2) * ((pro & LITE_BLEND) ? 2 : 1);
+}
+constexpr int LITE_MAX_TAB_BATCH = LITE_MAX_BATCH;
+
 template <int MODE, int CIN, int NC, int CKC, int PRO, int X6>
 static int lite_slots() {
     static int slots = 0;
@@ -730,7 +789,8 @@ static int lite_slots() {
         using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6>, 256,
-                                                         C::LDS_BYTES) != hipSuccess || per_cu <= 0)
+                                                         C::LDS_BYTES + lite_tab_bytes(PRO, CIN, 1)) != hipSuccess ||
+            per_cu <= 0)
             per_cu = 1;
         slots = ((lite_cu_count() * per_cu) / 8) * 8;
         if (slots <= 0) slots = 8;
@@ -742,8 +802,8 @@ template <int MODE, int CIN, int NC, int CKC, int PRO, int X6>
 static void lite_launch_pro(const ConvArgs& a, int n_tiles, hipStream_t st) {
     using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
     const int grid = std::min(n_tiles, lite_slots<MODE, CIN, NC, CKC, PRO, X6>());
-    hipLaunchKernelGGL((conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6>), dim3(grid), dim3(256), C::LDS_BYTES, st, a,
-                       n_tiles);
+    hipLaunchKernelGGL((conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6>), dim3(grid), dim3(256),
+                       C::LDS_BYTES + lite_tab_bytes(PRO, CIN, a.batch), st, a, n_tiles);
 }
 
 template <int MODE, int CIN, int NC, int CKC, int X6>
@@ -752,9 +812,17 @@ static hipError_t lite_launch_cfg(const ConvArgs& a, hipStream_t st) {
     if (a.cin != CIN || a.cout != NC || a.tiles_y != (a.Ho + C::TH - 1) / C::TH ||
         a.tiles_x != (a.Wo + C::TW - 1) / C::TW || (size_t)a.batch * a.H * a.W * CIN >= ((size_t)1 << 31))
         return hipErrorInvalidValue;   // 32-bit staging offsets
+    if (a.batch > LITE_MAX_TAB_BATCH && a.pro_mode != PRO_NONE) return hipErrorInvalidValue;   // LDS affine table
+    if (a.stat.acc != nullptr && (MODE != 1 || a.stat.nslot < 1 || a.stat.nslot > CIN_ACC_MAX_SLOTS))
+        return hipErrorInvalidValue;
+    const bool src_acc = a.pro_stat.acc != nullptr;
+    if (src_acc && (a.pro_stat.nslot < 1 || a.pro_stat.nslot > CIN_ACC_MAX_SLOTS || a.pro_stat.C != CIN ||
+                    a.pro_stat.batch != a.batch || a.pro_stat.style == nullptr || a.pro_mode == PRO_NONE))
+        return hipErrorInvalidValue;
     const int n_tiles = a.batch * a.tiles_y * a.tiles_x;
     if (a.pro_w != nullptr) {   // two styles
-        if (a.pro_ab1 == nullptr) return hipErrorInvalidValue;
+        if (src_acc ? a.pro_stat.style1_offset < 0 : (a.pro_ab1 == nullptr || a.pro_ab == nullptr))
+            return hipErrorInvalidValue;
         switch (a.pro_mode) {
             case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6>(a, n_tiles, st); break;
             case PRO_AFF_RES: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6>(a, n_tiles, st); break;
@@ -779,7 +847,9 @@ static hipError_t lite_prepare_cfg() {
                           (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>,
                           (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6>,
                           (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6>}) {
-        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES);
+        const size_t bytes = std::min<size_t>(C::LDS_BYTES + lite_tab_bytes(PRO_AFF_RELU | LITE_BLEND, CIN, LITE_MAX_TAB_BATCH),
+                                              160 * 1024);
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return e;
     }
     // occupancy queries outside any graph capture

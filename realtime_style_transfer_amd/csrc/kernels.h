@@ -34,6 +34,100 @@ __device__ __forceinline__ int xcd_tile_order(int bid, int n) {
     return x * base + min(x, rem) + k;
 }
 
+// ---- CIN statistics through f64 accumulators (inference) ----------------------------------------------
+// The producer of a conditional-instance-normalised layer adds, per workgroup and channel, its
+// {sum, sum of squares} as f64 into one of nslot accumulator copies (no-return f64 atomics, executed at
+// the memory side; the copies bound the adders per address); the consumer's workgroups merge the copies and
+// form the affine themselves (cin_affine: the finalize_kernel arithmetic), so no finalize kernel runs
+// between the two. Per workgroup the sum of squares is M2 + S^2/n of its two-pass tile statistics — the
+// quantity finalize_kernel merges — so the affine equals the finalize path's up to f64 summation order.
+constexpr int CIN_ACC_MAX_SLOTS = 64;
+struct CinAcc {              // producer side (null acc: the per-tile partials path)
+    double* acc;             // [nslot][B][2][C]: sums, then sums of squares; zeroed before the producer runs
+    int nslot;
+};
+struct CinSrc {              // consumer side: the producer's accumulators and its CIN parameters
+    const double* acc;       // [nslot][B][2][C] (null: the prologue reads pro_ab as before)
+    int nslot, C, batch;
+    double n;                // values per (image, channel): the producer's Ho * Wo
+    const float* style;      // style parameters: image b's scale at style[b*style_stride + style_offset + c],
+    int style_stride;        // its bias C further; the second style (two styles) style1_offset further
+    int style_offset;
+    int style1_offset;
+    float eps;
+    float2* ab_out;          // stored by workgroup 0 (rst_copy_activation and the host read them); may be null
+    float2* ab1_out;
+};
+
+__device__ __forceinline__ void cin_acc_add(const CinAcc& a, int batch, int C, int b, int c, int slot, double S,
+                                            double Q) {
+    double* const p = a.acc + ((size_t)(slot * batch + b) * 2) * C + c;
+    unsafeAtomicAdd(p, S);
+    unsafeAtomicAdd(p + C, Q);
+}
+
+// Every thread of an NT-thread workgroup calls this: the affine of images b0 .. b0 + nb - 1, channels [0, C)
+// (finalize_kernel's arithmetic on the merged sums) into tab[j * C + c] for image b0 + j (and the second
+// style's into tab1[j * C + c] when tab1 is given; LDS or global), also into out / out1 when given (the
+// host-visible copies, same indexing). L lanes per (image, channel) (a power of two, L * nb * C <= NT where
+// possible) each read K / L of the K = nslot (rounded up to a power of two) accumulator copies, all loads
+// issued together with the style-parameter loads, and reduce by xor shuffles: about one memory latency per
+// pass instead of nslot dependent loads.
+template <int NT>
+__device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb, float2* tab, float2* tab1,
+                                                 float2* out, float2* out1) {
+    constexpr int RMAX = 8;   // copies per lane
+    int K = 1;
+    while (K < s.nslot) K <<= 1;
+    const int items = nb * s.C;
+    int L = K / RMAX > 1 ? K / RMAX : 1;                   // at most RMAX copies per lane
+    while (L < K && 2 * L * items <= NT) L <<= 1;         // more lanes while one pass still covers every item
+    const int R = K / L, n = items * L;
+    for (int base = 0; base < n; base += NT) {
+        const int i = base + (int)threadIdx.x, it = i / L, l = i & (L - 1);
+        const int j = it / s.C, c = it - j * s.C, b = b0 + j;
+        const bool head = i < n && l == 0;
+        const float* const sp = s.style + (size_t)b * s.style_stride + s.style_offset;
+        float g0 = 0.f, be0 = 0.f, g1 = 0.f, be1 = 0.f;
+        if (head) {   // independent of the accumulators: in flight with them
+            g0 = sp[c];
+            be0 = sp[s.C + c];
+            if (tab1 != nullptr) {
+                g1 = sp[s.style1_offset + c];
+                be1 = sp[s.style1_offset + s.C + c];
+            }
+        }
+        double S = 0.0, Q = 0.0;
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+            const int k = l + L * r;
+            if (r < R && i < n && k < s.nslot) {
+                const double* const p = s.acc + ((size_t)(k * s.batch + b) * 2) * s.C + c;
+                S += p[0];
+                Q += p[s.C];
+            }
+        }
+        for (int o = 1; o < L; o <<= 1) {
+            S += __shfl_xor(S, o);
+            Q += __shfl_xor(Q, o);
+        }
+        if (head) {
+            const double N = s.n, mean = S / N, var = fmax(Q - S * mean, 0.0) / N;
+            const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
+            const float aa = g0 * rstd;
+            const float2 v = make_float2(aa, be0 - (float)mean * aa);
+            tab[it] = v;
+            if (out != nullptr) out[it] = v;
+            if (tab1 != nullptr) {
+                const float a1 = g1 * rstd;
+                const float2 v1 = make_float2(a1, be1 - (float)mean * a1);
+                tab1[it] = v1;
+                if (out1 != nullptr) out1[it] = v1;
+            }
+        }
+    }
+}
+
 // Arguments of the implicit-GEMM MFMA conv kernel (conv_mfma.hip).
 struct ConvArgs {
     const float* in;        // NHWC [B][H][W][cin] raw producer output
@@ -54,6 +148,8 @@ struct ConvArgs {
     int pad_t, pad_l;
     int tiles_y, tiles_x, n_blocks, nchunks;
     int pro_mode, epi_mode, shuffle;
+    CinAcc stat;            // conv_lite inference: CIN statistics into f64 accumulators instead of part
+    CinSrc pro_stat;        // conv_lite inference: the prologue affine formed from the producer's accumulators
 };
 
 // A compiled tile configuration of conv_mfma_kernel.
@@ -88,6 +184,8 @@ struct WinoArgs {
     int linear;             // 0: out = ReLU(conv + bias) (the residual convs); 1: conv + bias (input gradient)
     const float2* pro_ab1;  // two styles (wino_x6 only): [B][cin] the second style's affine, or null
     const float* pro_w;     // with pro_ab1: [B][H][W] per-pixel weight of the second style (style_blend)
+    CinAcc stat;            // wino_x6 inference: CIN statistics into f64 accumulators instead of part
+    CinSrc pro_stat;        // wino_x6 inference: the prologue affine formed from the producer's accumulators
 };
 bool wino_supported(int kh, int stride, int cin, int cout);
 
@@ -100,8 +198,12 @@ struct Wino9Args {
     const float2* bn_ab;    // [32] BatchNorm affine (folded moving statistics); inference only
     float* out;             // NHWC [B][H][W][32]
     float4* part;           // training: out = ReLU(conv + bias) and per-tile {sum, M2, n} at
-                            // [B][32][tiles_y*tiles_x] for the batch-statistics BatchNorm; null: inference
+                            // [B][32][n_part] for the batch-statistics BatchNorm; null: inference.
+                            // n_part = tiles_y*tiles_x (wino9.hip), 2*tiles_y*tiles_x (wino9_x6.hip:
+                            // one entry per 16 x 8 M block)
     int batch, H, W, cin, tiles_y, tiles_x;
+    double* zero;           // wino9_x6 inference: zero [zero_n2] double2 first (the frame's CIN accumulators,
+    long zero_n2;           // kernels.h CinAcc, written by later layers only) or null
 };
 bool wino9_supported(int kh, int stride, int cin, int cout);
 
@@ -128,6 +230,9 @@ hipError_t wino9_launch(const Wino9Args& a, hipStream_t st);
 // U = wino9_x6_pack_weights (bf16 pieces [10][16][3][32][16]).
 std::vector<float> wino9_x6_pack_weights(const float* kern, int cin);
 hipError_t wino9_x6_prepare();
+// device form of wino9_x6_pack_weights (bitwise the host image; training re-packs after every step)
+hipError_t wino9_x6_transform_launch(const float* kern, int cin, float* U, hipStream_t st);
+size_t wino9_x6_weight_floats();
 int wino9_x6_tiles_y(int H);   // 16 x 16-pixel workgroup blocks
 int wino9_x6_tiles_x(int W);
 hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st);
@@ -184,6 +289,7 @@ struct LiteTile {
     int x6;                 // 1: split-bf16 x6 operands on the bf16 MFMA pipe (fp32-level products)
 };
 bool conv_lite_select(int keras_kind, int k, int stride, int cin, int cout, bool x6, LiteTile* t);
+constexpr int LITE_MAX_BATCH = 16;   // the prologue affine table [batch][cin] lives in LDS
 std::vector<float> conv_lite_pack_weights(const LiteTile& t, const float* kern);
 hipError_t conv_lite_launch(const LiteTile& t, const ConvArgs& a, hipStream_t st);
 hipError_t conv_lite_prepare(const LiteTile& t);
@@ -199,6 +305,8 @@ struct LastArgs {
     int batch, H, W, cin, tiles_y, tiles_x;
     const float2* pro_ab1;  // two styles: [B][16] the second style's affine, or null
     const float* pro_w;     // with pro_ab1: [B][H][W] per-pixel weight of the second style (style_blend)
+    CinAcc stat;            // inference: the output CIN's statistics into f64 accumulators instead of part
+    CinSrc pro_stat;        // inference: the prologue affine formed from the producer's accumulators
 };
 std::vector<float> last_x6_pack_weights(const float* kern, int cin);
 int last_x6_tiles_y(int H);
@@ -227,9 +335,9 @@ struct FinalizeArgs {
     float eps;
 };
 hipError_t finalize_launch(const FinalizeArgs& a, hipStream_t st);
-// The network output: the last layer's CIN finalize (3 channels, num_styles = 1) fused with its affine + sigmoid
-// over the (B, hw, 3) raw output; also stores a.ab
-hipError_t fin_sigmoid3_launch(const FinalizeArgs& a, const float* x, float* y, long hw, hipStream_t st);
+// The network output: the last layer's CIN affine (3 channels, num_styles = 1; from its f64 accumulators) fused
+// with the affine + sigmoid over the (B, hw, 3) raw output; also stores s.ab_out
+hipError_t fin_sigmoid3_launch(const CinSrc& s, const float* x, float* y, long hw, int batch, hipStream_t st);
 
 // y = act(a*x + b [+ res]) element-wise, act: 0 none, 1 relu, 2 sigmoid.  x,res,y [B][HW][C]
 hipError_t affine_act_launch(const float* x, const float2* ab, const float* res, float* y, int batch, long hw, int C,

@@ -81,7 +81,7 @@ constexpr int FIN_UNROLL = 8;
 // output kernel below, so both produce the same bits.
 template <int NT, int U = FIN_UNROLL>
 __device__ __forceinline__ void finalize_channel(const FinalizeArgs& a, int c, int b, int tid, double (*scratch)[NT / 64],
-                                                 float& aa_out, float& bb_out, bool store = true) {
+                                                 float& aa_out, float& bb_out) {
     const int b0 = a.merge_images ? 0 : b, nb = a.merge_images ? a.batch : 1;
     float scale = 1.f, bias = 0.f, scale1 = 0.f, bias1 = 0.f;
     if (tid == 0) {   // issued before the partial loads: independent of them
@@ -142,7 +142,6 @@ __device__ __forceinline__ void finalize_channel(const FinalizeArgs& a, int c, i
         const float aa = scale * rstd;
         aa_out = aa;
         bb_out = bias - (float)mean * aa;
-        if (!store) return;
         a.ab[b * a.C + c] = make_float2(aa, bb_out);
         if (a.ab1 != nullptr) {   // second style (styleTransfer.py:36-44 blends the affine per pixel)
             const float a1 = scale1 * rstd;
@@ -165,25 +164,18 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
 }
 
 // The network output (styleTransfer.py:269-276, 329): sigmoid(CIN(x)) of the last layer's 3 channels, with that
-// CIN's finalize fused in front (num_styles = 1): workgroup (g, b) first merges image b's statistics of the three
-// channels (waves 0..2, one channel each, the finalize_kernel<64> arithmetic: bitwise the same affine), then
-// applies the affine + sigmoid to its slice of the image as float4s (hw * 3 is a multiple of 4 here). Workgroup
-// (0, b) also stores the affine (rst_copy_activation reads it). Saves the separate finalize launch.
-__global__ __launch_bounds__(256) void fin_sigmoid3_kernel(FinalizeArgs a, const float* __restrict__ x,
+// CIN's finalize fused in front (num_styles = 1): the last layer added its statistics into f64 accumulators
+// (kernels.h CinAcc), so every workgroup (g, b) forms image b's three affines itself (cin_affine_table), then applies
+// affine + sigmoid to its slice of the image as float4s (hw * 3 is a multiple of 4 here). Workgroup (0, b) also
+// stores the affine (rst_copy_activation reads it). No finalize kernel and no separate activation pass.
+__global__ __launch_bounds__(256) void fin_sigmoid3_kernel(CinSrc s, const float* __restrict__ x,
                                                            float* __restrict__ y, int n4_img) {
-    __shared__ double scratch[3][3][1];
-    __shared__ float aff[6];
-    const int b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (wave < 3) {
-        float aa = 0.f, bb = 0.f;   // only workgroup (0, b) stores the affine
-        finalize_channel<64>(a, wave, b, lane, scratch[wave], aa, bb, blockIdx.x == 0);
-        if (lane == 0) {
-            aff[2 * wave] = aa;
-            aff[2 * wave + 1] = bb;
-        }
-    }
+    __shared__ float2 aff[3];
+    const int b = blockIdx.y;
+    cin_affine_table<256>(s, b, 1, aff, nullptr, blockIdx.x == 0 && s.ab_out != nullptr ? s.ab_out + b * 3 : nullptr,
+                          nullptr);
     __syncthreads();
-    const float a0 = aff[0], b0 = aff[1], a1 = aff[2], b1 = aff[3], a2 = aff[4], b2 = aff[5];
+    const float a0 = aff[0].x, b0 = aff[0].y, a1 = aff[1].x, b1 = aff[1].y, a2 = aff[2].x, b2 = aff[2].y;
     const float4* __restrict__ xi = reinterpret_cast<const float4*>(x) + (size_t)b * n4_img;
     float4* __restrict__ yo = reinterpret_cast<float4*>(y) + (size_t)b * n4_img;
     auto sig = [](float v) __attribute__((always_inline)) { return 1.f / (1.f + __expf(-v)); };
@@ -198,15 +190,15 @@ __global__ __launch_bounds__(256) void fin_sigmoid3_kernel(FinalizeArgs a, const
     }
 }
 
-hipError_t fin_sigmoid3_launch(const FinalizeArgs& a, const float* x, float* y, long hw, hipStream_t st) {
-    if (a.C != 3 || a.ntot != 3 || a.merge_images || a.ab1 != nullptr || (hw * 3) % 4 != 0 ||
-        (long)a.n_part * a.phases > FIN_UNROLL * 64 || hw * 3 / 4 >= (1L << 31))
+hipError_t fin_sigmoid3_launch(const CinSrc& s, const float* x, float* y, long hw, int batch, hipStream_t st) {
+    if (s.acc == nullptr || s.C != 3 || s.batch != batch || s.nslot < 1 || s.nslot > CIN_ACC_MAX_SLOTS ||
+        s.style == nullptr || (hw * 3) % 4 != 0 || hw * 3 / 4 >= (1L << 31))
         return hipErrorInvalidValue;
     const int n4 = (int)(hw * 3 / 4);
     int g = (n4 + 256 * 8 - 1) / (256 * 8);   // ~8 float4 per thread
     if (g > 256) g = 256;
     if (g < 1) g = 1;
-    hipLaunchKernelGGL(fin_sigmoid3_kernel, dim3(g, a.batch), dim3(256), 0, st, a, x, y, n4);
+    hipLaunchKernelGGL(fin_sigmoid3_kernel, dim3(g, batch), dim3(256), 0, st, s, x, y, n4);
     return hipGetLastError();
 }
 

@@ -387,7 +387,10 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         // does not (its layers keep the direct kernel)
         const bool blend_in = shape->num_styles == 2 && li > 0 && specs[li - 1].norm == N_CIN;
         const int lp = (blend_in && precision == RST_PRECISION_FP32_WINOGRAD) ? RST_PRECISION_FP32 : precision;
-        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, true)) != RST_OK) { delete h; return st; }
+        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, shape->max_batch <= LITE_MAX_BATCH)) != RST_OK) {
+            delete h;
+            return st;
+        }
         if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
         if (s.norm == N_BN) {
@@ -434,6 +437,32 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
             }
         }
         if (e.s.res_block >= 1 && e.s.res_conv == 0) block_input = e.d_mat;
+    }
+    // CIN statistics through f64 accumulators (kernels.h CinAcc / CinSrc) where the producer adds them and
+    // the consumer forms its affine from them: no finalize kernel between the two. The copies keep the
+    // adders per address near 16-28: a residual conv has 225 workgroups at B = 1 (8 copies), the persistent
+    // transposed convs up to a few per CU (32), the last layer ~900 (64).
+    {
+        size_t n_acc = 0;
+        auto takes_acc = [](int kind) { return kind == K_WINOX6 || kind == K_LITE || kind == K_LASTX6; };
+        const LayerExec& last = h->layers.back();
+        const bool fused_out = shape->num_styles == 1 && last.kind == K_LASTX6 && last.s.cout == 3 &&
+                               last.s.norm == N_CIN && ((long)last.s.Ho * last.s.Wo * 3) % 4 == 0;
+        for (size_t li = 0; li < h->layers.size(); ++li) {
+            LayerExec& e = h->layers[li];
+            if (e.s.norm != N_CIN || !takes_acc(e.kind)) continue;
+            const bool consumer_ok = li + 1 < h->layers.size()
+                                         ? h->layers[li + 1].pro_src == (int)li && takes_acc(h->layers[li + 1].kind)
+                                         : fused_out;
+            if (!consumer_ok) continue;
+            e.nslot = e.kind == K_WINOX6 ? 8 : (e.kind == K_LITE ? 32 : 64);
+            e.acc_off = (long)n_acc;                   // per image: the layer's block scales with the batch
+            n_acc += (size_t)e.nslot * 2 * e.s.cout;
+        }
+        if (n_acc > 0) {
+            h->acc_per_image = n_acc;
+            if ((st = h->alloc(&h->d_acc_all, n_acc * B * sizeof(double))) != RST_OK) { delete h; return st; }
+        }
     }
     // two styles: the style-weight mip chain (AvgPool2 keyed by width, num_expand_blocks + 1 levels)
     if (shape->num_styles == 2) {
@@ -498,11 +527,31 @@ static const float* mip_ptr(const rst_handle* h, int level, const float* style_w
     return level == 0 ? style_weights : h->d_mip[level];
 }
 
-// num_styles = 1 with last_x6: the last CIN's finalize runs fused into the output kernel (fin_sigmoid3_launch)
-static bool output_finalize_fused(const rst_handle* h) {
-    const LayerExec& last = h->layers.back();
-    return h->shape.num_styles == 1 && last.kind == K_LASTX6 && last.s.cout == 3 && last.n_part <= 512 &&
-           ((long)last.s.Ho * last.s.Wo * 3) % 4 == 0;
+// num_styles = 1 with last_x6: the last CIN's statistics go to f64 accumulators and the output kernel forms the
+// affine itself (fin_sigmoid3_launch): no finalize, no separate activation pass
+static bool output_finalize_fused(const rst_handle* h) { return h->layers.back().acc_off >= 0; }
+
+// layer e's accumulators for a forward of B images (null: e uses partials + finalize)
+static double* acc_ptr(const rst_handle* h, const LayerExec& e, int B) {
+    return e.acc_off >= 0 ? h->d_acc_all + (size_t)e.acc_off * B : nullptr;
+}
+
+// the consumer-side view of a producer's CIN accumulators (the FinalizeArgs fields of its finalize)
+static CinSrc cin_src(const rst_handle* h, const LayerExec& p, const float* style, int B) {
+    CinSrc c{};
+    c.acc = acc_ptr(h, p, B);
+    c.nslot = p.nslot;
+    c.C = p.s.cout;
+    c.batch = B;
+    c.n = (double)p.s.Ho * p.s.Wo;
+    c.style = style;
+    c.style_stride = h->shape.num_styles * h->P;
+    c.style_offset = p.s.style_offset;
+    c.style1_offset = h->shape.num_styles == 2 ? h->P : -1;
+    c.eps = 1e-5f;
+    c.ab_out = p.d_ab;
+    c.ab1_out = p.d_ab1;
+    return c;
 }
 
 static int launch_layer(rst_handle* h, size_t li, const float* content, const float* style, const float* sw, int B,
@@ -539,6 +588,15 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.cin = e.s.cin;
         a.tiles_y = e.tiles_y;
         a.tiles_x = e.tiles_x;
+        if (e.acc_off >= 0) {   // the output CIN's statistics -> f64 accumulators (fin_sigmoid3 reads them)
+            a.part = nullptr;
+            a.stat.acc = acc_ptr(h, e, B);
+            a.stat.nslot = e.nslot;
+        }
+        if (src != nullptr && src->acc_off >= 0 && pro_ab != nullptr) {
+            a.pro_stat = cin_src(h, *src, style, B);
+            a.pro_ab = a.pro_ab1 = nullptr;
+        }
         HIP_TRY(last_x6_launch(a, st));
     } else if (e.kind == K_SMALL) {
         SmallConvArgs a{};
@@ -577,6 +635,10 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.cin = e.s.cin;
         a.tiles_y = e.tiles_y;
         a.tiles_x = e.tiles_x;
+        if (e.kind == K_WINO9X6 && li == 0 && h->d_acc_all != nullptr) {   // it zeroes the frame's accumulators
+            a.zero = h->d_acc_all;
+            a.zero_n2 = (long)(h->acc_per_image * B / 2);
+        }
         HIP_TRY(e.kind == K_WINO9X6 ? wino9_x6_launch(a, st) : wino9_launch(a, st));
     } else if (e.kind == K_WINO || e.kind == K_WINOX6) {
         WinoArgs a{};
@@ -600,6 +662,15 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             if (e.kind != K_WINOX6) return fail(RST_ERR_UNSUPPORTED, "f32 Winograd conv has no two-style blend prologue");
             a.pro_ab1 = src->d_ab1;
             a.pro_w = mip_ptr(h, src->out_mip, sw);
+        }
+        if (e.acc_off >= 0) {   // this layer's statistics -> f64 accumulators (its consumer forms the affine)
+            a.part = nullptr;
+            a.stat.acc = acc_ptr(h, e, B);
+            a.stat.nslot = e.nslot;
+        }
+        if (src != nullptr && src->acc_off >= 0 && pro_ab != nullptr) {   // the affine from the producer's
+            a.pro_stat = cin_src(h, *src, style, B);                            // accumulators (no finalize ran)
+            a.pro_ab = a.pro_ab1 = nullptr;
         }
         if (ext_ev) wino_x6_set_timing_events(ev[0], ev[1]);
         HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
@@ -636,6 +707,15 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.epi_mode = e.s.norm == N_BN ? EPI_RELU_BN : (e.s.conv_relu ? EPI_RELU_STATS : EPI_STATS);
         a.shuffle = e.kind == K_CONVT2 ? 1 : 0;
         if (e.kind == K_LITE) {
+            if (e.acc_off >= 0) {   // this layer's statistics -> f64 accumulators (its consumer forms the affine)
+                a.part = nullptr;
+                a.stat.acc = acc_ptr(h, e, B);
+                a.stat.nslot = e.nslot;
+            }
+            if (src != nullptr && src->acc_off >= 0 && pro_ab != nullptr) {
+                a.pro_stat = cin_src(h, *src, style, B);
+                a.pro_ab = a.pro_ab1 = nullptr;
+            }
             HIP_TRY(conv_lite_launch(e.lite, a, st));   // two styles: its blend prologue (pro_ab1, pro_w)
         } else {
             HIP_TRY(conv_launch(e.tile, a, st));
@@ -644,7 +724,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
     if (ev && !ext_ev) HIP_TRY(hipEventRecord(ev[1], st));
     // the last layer's finalize (one style) is fused into the output kernel (fin_sigmoid3_launch, rst_forward)
     const bool fused_out_fin = li + 1 == h->layers.size() && output_finalize_fused(h);
-    if (e.s.norm == N_CIN && !fused_out_fin) {
+    if (e.s.norm == N_CIN && !fused_out_fin && e.acc_off < 0) {
         FinalizeArgs f{};
         f.part = e.d_part;
         f.style = style;
@@ -683,6 +763,9 @@ int rst_forward(rst_handle* h, const float* content, const float* style_params, 
     if (style_weights == nullptr && h->shape.num_styles == 2)
         return fail(RST_ERR_INVALID, "rst_forward: num_styles == 2 needs style_weights (B, out_h, out_w, 1)");
     hipStream_t st = static_cast<hipStream_t>(stream);
+    // the CIN accumulators start at zero: cleared by the first layer's kernel when that is wino9_x6
+    if (h->d_acc_all != nullptr && h->layers[0].kind != K_WINO9X6)
+        HIP_TRY(hipMemsetAsync(h->d_acc_all, 0, h->acc_per_image * batch * sizeof(double), st));
     for (size_t k = 1; k < h->d_mip.size(); ++k)
         HIP_TRY(avgpool2_1ch_launch(mip_ptr(h, (int)k - 1, style_weights), h->d_mip[k], batch, h->mip_h[k - 1],
                                     h->mip_w[k - 1], st));
@@ -694,20 +777,9 @@ int rst_forward(rst_handle* h, const float* content, const float* style_params, 
     if (h->shape.num_styles == 2) {
         HIP_TRY(affine_act_blend_launch(last.d_out, last.d_ab, last.d_ab1, mip_ptr(h, last.out_mip, style_weights),
                                         nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
-    } else if (output_finalize_fused(h)) {   // the last CIN's finalize fused with the output sigmoid
-        FinalizeArgs f{};
-        f.part = last.d_part;
-        f.style = style_params;
-        f.ab = last.d_ab;
-        f.batch = batch;
-        f.C = last.s.cout;
-        f.ntot = last.ntot;
-        f.n_part = last.n_part;
-        f.phases = 1;
-        f.style_stride = h->shape.num_styles * h->P;
-        f.style_offset = last.s.style_offset;
-        f.eps = 1e-5f;
-        HIP_TRY(fin_sigmoid3_launch(f, last.d_out, out, (long)last.s.Ho * last.s.Wo, st));
+    } else if (output_finalize_fused(h)) {   // the last CIN's affine (from its accumulators) + the output sigmoid
+        HIP_TRY(fin_sigmoid3_launch(cin_src(h, last, style_params, batch), last.d_out, out,
+                                    (long)last.s.Ho * last.s.Wo, batch, st));
     } else {
         HIP_TRY(affine_act_launch(last.d_out, last.d_ab, nullptr, out, batch, (long)last.s.Ho * last.s.Wo, 3, 2, st));
     }

@@ -192,6 +192,7 @@ int repack(rst_trainer* t, hipStream_t st) {
     for (TLayer& T : t->L) {
         int r = RST_OK;
         if (T.e.kind == K_WINO9) RST_HIP_TRY(wino9_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
+        else if (T.e.kind == K_WINO9X6) RST_HIP_TRY(wino9_x6_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
         else if (T.e.kind == K_WINOX6) r = add_job(t->d_wc + T.woff, T.e.s.cin, T.e.d_w);
         else if (T.wino_fwd) RST_HIP_TRY(wino_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
         else RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_w, T.e.d_w, T.n_w, st));
@@ -236,7 +237,7 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.tiles_y = e.tiles_y;
             a.tiles_x = e.tiles_x;
             RST_HIP_TRY(small_conv_launch(a, st));
-        } else if (e.kind == K_WINO9) {
+        } else if (e.kind == K_WINO9 || e.kind == K_WINO9X6) {
             Wino9Args a{};
             a.in = content;
             a.U = e.d_w;
@@ -249,7 +250,7 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.cin = e.s.cin;
             a.tiles_y = e.tiles_y;
             a.tiles_x = e.tiles_x;
-            RST_HIP_TRY(wino9_launch(a, st));
+            RST_HIP_TRY(e.kind == K_WINO9X6 ? wino9_x6_launch(a, st) : wino9_launch(a, st));
         } else if (e.kind == K_WINO || e.kind == K_WINOX6) {
             WinoArgs a{};
             a.in = Pv->e.d_out;
@@ -588,15 +589,15 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
         std::vector<float> packed, bias_n;
         // residual convs on Winograd when asked (their prologue always materialises the input for wgrad)
         // and the 9x9 start conv on the composite Winograd kernel (training mode: raw ReLU output + tile stats)
-        // WINOGRAD_BF16X6: residual convs (forward, input gradient, weight gradient) on the split-bf16 x6
-        // kernels; the start conv keeps the f32 composite Winograd (its x6 kernel is inference-only)
+        // WINOGRAD_BF16X6: residual convs (forward, input gradient, weight gradient) and the start conv's
+        // forward on the split-bf16 x6 kernels (wino9_x6.hip in its training mode)
         const bool wmode = precision == RST_PRECISION_FP32_WINOGRAD || precision == RST_PRECISION_WINOGRAD_BF16X6;
-        const int lp = !wmode || (s.res_block < 0 && li != 0) ? RST_PRECISION_FP32
-                       : (li == 0 ? RST_PRECISION_FP32_WINOGRAD : precision);
+        const int lp = !wmode || (s.res_block < 0 && li != 0) ? RST_PRECISION_FP32 : precision;
         if ((st = prepare_layer(T.e, s, kidx.data(), bidx.data(), packed, bias_n, lp)) != RST_OK)
             return fail_delete(t, st);
-        T.wino_fwd = T.e.kind == K_WINO || T.e.kind == K_WINOX6 || T.e.kind == K_WINO9;
+        T.wino_fwd = T.e.kind == K_WINO || T.e.kind == K_WINOX6 || T.e.kind == K_WINO9 || T.e.kind == K_WINO9X6;
         if (T.e.kind == K_WINO9) T.e.n_part = T.e.tiles_y * T.e.tiles_x;   // batch statistics per tile
+        if (T.e.kind == K_WINO9X6) T.e.n_part = 2 * T.e.tiles_y * T.e.tiles_x;   // per 16 x 8 M block
         std::vector<int> mw = T.wino_fwd ? std::vector<int>() : to_map(packed), mb = to_map(bias_n);
         T.n_w = packed.size();
         T.n_b = mb.size();
@@ -683,6 +684,7 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
     for (auto& T : t->L) {
         if (T.e.kind != K_SMALL) {
             hipError_t pe = T.e.kind == K_WINO9    ? hipSuccess
+                            : T.e.kind == K_WINO9X6 ? wino9_x6_prepare()
                             : T.e.kind == K_WINOX6 ? wino_x6_prepare()
                             : T.wino_fwd           ? wino_prepare()
                                                    : conv_prepare(T.e.tile);

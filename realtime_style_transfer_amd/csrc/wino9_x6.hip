@@ -17,7 +17,8 @@
 // kept in registers by the lanes that feed it. The loop over the nine sub-kernels has no barrier.
 // Each U element (B operand, L2) is loaded by one wave and serves 64 tiles.
 // Epilogue, per M block: M -> LDS [xi][tile][co], output transform per (tile, channel), bias -> ReLU ->
-// BN (folded moving statistics) -> ReLU. Inference only (training keeps wino9.hip's f32 kernel).
+// BN (folded moving statistics) -> ReLU. Training (Wino9Args.part set): the raw ReLU output and a two-pass
+// {sum, M2, n} per (channel, 16 x 8 M block) for the batch-statistics BatchNorm (finalize_kernel).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstring>
@@ -59,7 +60,7 @@ constexpr int V16_FL = NXI * 64 * V16S;        // [xi][tile][12] f32
 // into the other one; the epilogue's M exchange uses the current patch + v16 (contiguous either way).
 constexpr int LDS_FL = 2 * PATCH_FL + V16_FL;
 constexpr int LDS_BYTES = LDS_FL * 4;          // 140 KB
-static_assert(MEX_FL <= PATCH_FL + V16_FL, "M exchange fits in one patch + v16");
+static_assert(MEX_FL + 3 * 256 <= PATCH_FL + V16_FL, "M exchange + statistics scratch fit in one patch + v16");
 constexpr int UBLK = NT * VROW;                // bytes per (ab, xi, piece) U block: 32 co x 16 bf16
 constexpr int NTHR = 512;
 
@@ -111,7 +112,7 @@ __device__ unsigned long long w9_tl[W9_PROF][8][9][4];   // [workgroup][wave][ti
 #define W9TL(k)
 #endif
 
-template <int CINT>
+template <int CINT, bool TRAIN>
 // Work units: units 0 .. n_full-1 are whole tiles; the n_tiles - n_full tiles of the last, partial round
 // are split into two units each (one 32-tile M block, i.e. 8 output rows), so that round occupies twice
 // as many CUs for about half as long (1800 tiles on 256 CUs: 7 full rounds + 8 tiles -> 16 half units).
@@ -120,6 +121,9 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar U offsets, no waterfall)
+    if (a.zero != nullptr)   // the frame's CIN accumulators (no separate memset launch; no layer before this one)
+        for (long i = (long)blockIdx.x * NTHR + tid; i < a.zero_n2; i += (long)gridDim.x * NTHR)
+            reinterpret_cast<double2*>(a.zero)[i] = make_double2(0.0, 0.0);
     const int li = lane & 31, lh = lane >> 5;
     const int p = wave & 3, qh = wave >> 2;   // point row p, points q = 2qh, 2qh + 1
     int w9_it = 0;
@@ -237,7 +241,9 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
     };
     const int co = tid & 31, g = tid >> 5;   // epilogue thread: output channel co, tiles 2g, 2g + 1 of a block
     const float bias = a.bias[co];
-    const float2 bn = a.bn_ab[co];
+    constexpr bool train = TRAIN;            // training: raw ReLU output + per-(tile, M block) statistics
+    const float2 bn = train ? make_float2(1.f, 0.f) : a.bn_ab[co];
+    const int n_tile_img = a.tiles_y * a.tiles_x, n_part = 2 * n_tile_img;
 
     int t = blockIdx.x;   // work unit
     if (t < n_units) {
@@ -394,6 +400,8 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
                     ms[((4 * p + 2 * qh + q) * 32 + row) * MS + li] = acc[q][h][j];
                 }
             lds_barrier();
+            float vals[8];
+            float vs = 0.f, vn = 0.f;
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const int tl = 2 * g + k, tile = 32 * h + tl;
@@ -413,10 +421,53 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int oy = y0 + 2 * wy + (q >> 1), ox = x0 + 2 * wx + (q & 1);
-                    if (oy < H && ox < W) {
-                        const float v = fmaxf(yy[q] + bias, 0.f);                 // Conv2D(..., activation='relu')
-                        a.out[(img + (size_t)oy * W + ox) * NT + co] = fmaxf(fmaf(bn.x, v, bn.y), 0.f);   // BN -> ReLU
+                    const bool inside = oy < H && ox < W;
+                    const float v = fmaxf(yy[q] + bias, 0.f);                     // Conv2D(..., activation='relu')
+                    vals[4 * k + q] = inside ? v : 0.f;
+                    vs += vals[4 * k + q];
+                    vn += inside ? 1.f : 0.f;
+                    if (inside)   // inference: BN (folded moving statistics) -> ReLU; training: the raw ReLU output
+                        a.out[(img + (size_t)oy * W + ox) * NT + co] = train ? v : fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                }
+            }
+            if constexpr (train) {
+                // two-pass {sum, M2, n} of channel co over this M block (32 tiles = 8 output rows x 16 columns):
+                // lanes co / co + 32 of a wave hold groups 2w, 2w + 1; the eight waves meet in LDS just past
+                // the M exchange image (disjoint from it, inside the same dead patch + v16 span)
+                float* const red = ms + MEX_FL;   // [3][8 waves][32]
+                vs += __shfl_xor(vs, 32);
+                vn += __shfl_xor(vn, 32);
+                if (lh == 0) {
+                    red[wave * 32 + co] = vs;
+                    red[256 + wave * 32 + co] = vn;
+                }
+                lds_barrier();
+                float S = 0.f, N = 0.f;
+#pragma unroll
+                for (int w = 0; w < 8; ++w) {
+                    S += red[w * 32 + co];
+                    N += red[256 + w * 32 + co];
+                }
+                const float mean = N > 0.f ? S / N : 0.f;
+                float m2 = 0.f;
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int tl = 2 * g + k, tile = 32 * h + tl;
+                        const int oy = y0 + 2 * (tile >> 3) + (q >> 1), ox = x0 + 2 * (tile & 7) + (q & 1);
+                        const float d = vals[4 * k + q] - mean;
+                        if (oy < H && ox < W) m2 = fmaf(d, d, m2);
                     }
+                m2 += __shfl_xor(m2, 32);
+                if (lh == 0) red[512 + wave * 32 + co] = m2;
+                lds_barrier();
+                if (tid < 32) {
+                    float M2 = 0.f;
+#pragma unroll
+                    for (int w = 0; w < 8; ++w) M2 += red[512 + w * 32 + co];
+                    const int tt = unit_tile(t), bi = tt / n_tile_img, tli = tt - bi * n_tile_img;
+                    a.part[((size_t)bi * NT + co) * n_part + 2 * tli + h] = make_float4(S, M2, N, 0.f);
                 }
             }
         });
@@ -518,8 +569,62 @@ std::vector<float> wino9_x6_pack_weights(const float* kern, int cin) {
     return out;
 }
 
+// Device form of wino9_x6_pack_weights (training re-packs after every optimizer step): one thread per
+// (block, co, K index) writes its 16 points x 3 pieces, zeros included (no reliance on a cleared buffer);
+// f64 with the host's operation order and no contraction, the host's RNE bit formula: bitwise the host image.
+__global__ __launch_bounds__(256) void wino9_x6_transform_kernel(const float* __restrict__ kern, int cin,
+                                                                 unsigned short* __restrict__ U) {
+#pragma clang fp contract(off)
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= 10 * NT * 16) return;
+    const int k = idx & 15, co = (idx >> 4) % NT, blk = idx / (16 * NT);
+    const int ab = blk < 9 ? blk : k, ci = blk < 9 ? k : 16;
+    const bool valid = ci < cin && ab < 9;
+    const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+    const int sa = ab / 3, sb = ab % 3;
+    double gg[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            gg[i][j] = valid ? (double)kern[(((size_t)(3 * sa + i) * 9 + (3 * sb + j)) * cin + ci) * NT + co] : 0.0;
+    auto rne = [](float x) -> unsigned short {
+        const unsigned u = __float_as_uint(x);
+        return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    };
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double u = 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) u = u + G[p][i] * gg[i][j] * G[q][j];
+            const float uf = (float)u;
+            unsigned short pc[3];
+            pc[0] = rne(uf);
+            const float r = uf - __uint_as_float((unsigned)pc[0] << 16);
+            pc[1] = rne(r);
+            pc[2] = rne(r - __uint_as_float((unsigned)pc[1] << 16));
+#pragma unroll
+            for (int pi = 0; pi < 3; ++pi)
+                U[((((size_t)blk * NXI + p * 4 + q) * 3 + pi) * NT + co) * 16 + k] = valid ? pc[pi] : (unsigned short)0;
+        }
+}
+
+hipError_t wino9_x6_transform_launch(const float* kern, int cin, float* U, hipStream_t st) {
+    if (cin > 17 || cin <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wino9_x6_transform_kernel, dim3((10 * NT * 16 + 255) / 256), dim3(256), 0, st, kern, cin,
+                       reinterpret_cast<unsigned short*>(U));
+    return hipGetLastError();
+}
+
+size_t wino9_x6_weight_floats() { return (size_t)10 * NXI * 3 * NT * 16 / 2; }
+
 hipError_t wino9_x6_prepare() {
-    for (const void* k : {(const void*)wino9_x6_kernel<17>, (const void*)wino9_x6_kernel<0>}) {
+    for (const void* k : {(const void*)wino9_x6_kernel<17, false>, (const void*)wino9_x6_kernel<0, false>,
+                          (const void*)wino9_x6_kernel<17, true>, (const void*)wino9_x6_kernel<0, true>}) {
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         if (e != hipSuccess) return e;
     }
@@ -531,8 +636,8 @@ int wino9_x6_tiles_x(int W) { return (W + TW - 1) / TW; }
 
 hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st) {
     if (a.cin > 17 || a.cin <= 0 || a.tiles_y != (a.H + TH - 1) / TH || a.tiles_x != (a.W + TW - 1) / TW ||
-        a.part != nullptr || a.bn_ab == nullptr)
-        return hipErrorInvalidValue;   // inference only: training keeps wino9_launch (batch-statistics BN)
+        (a.part == nullptr && a.bn_ab == nullptr))
+        return hipErrorInvalidValue;   // inference: folded BN affine; training: statistics partials
     if ((size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7FFFFFF0)
         return hipErrorInvalidValue;   // 32-bit staging offsets; the idle threads' offset must stay out of range
     // persistent: one workgroup per CU (LDS and registers allow one), each looping over tiles
@@ -548,10 +653,16 @@ hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st) {
     const int tail = n_tiles % (int)grid;
     const int n_full = (tail > 0 && 2 * tail <= (int)grid) ? n_tiles - tail : n_tiles;
     const int n_units = n_full + 2 * (n_tiles - n_full);
-    if (a.cin == 17)
-        hipLaunchKernelGGL(wino9_x6_kernel<17>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_units, n_full);
-    else
-        hipLaunchKernelGGL(wino9_x6_kernel<0>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_units, n_full);
+    if (a.part != nullptr) {   // training
+        if (a.cin == 17)
+            hipLaunchKernelGGL((wino9_x6_kernel<17, true>), dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_units, n_full);
+        else
+            hipLaunchKernelGGL((wino9_x6_kernel<0, true>), dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_units, n_full);
+    } else if (a.cin == 17) {
+        hipLaunchKernelGGL((wino9_x6_kernel<17, false>), dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_units, n_full);
+    } else {
+        hipLaunchKernelGGL((wino9_x6_kernel<0, false>), dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_units, n_full);
+    }
     return hipGetLastError();
 }
 

@@ -139,7 +139,8 @@ constexpr int YST = (XPF4 + YT - 1) / YT;           // 2 staging float4 per thre
 constexpr int YRING = X6W_RING;                     // U register ring (points in flight), divides 8
 constexpr int YSTR = 132;                           // epilogue image row stride (floats): lh halves 32 banks apart
 constexpr size_t YIMG_BYTES = (size_t)2 * 128 * YSTR * 4;       // epilogue: two halves' partial Y [pixel][channel]
-constexpr size_t YEPI_BYTES = YIMG_BYTES + 2 * 8 * 32 * 16;     // + statistics reduction [2][8 waves][32] float4
+constexpr size_t YRED_BYTES = (size_t)2 * 8 * 32 * 16;          // statistics reduction [2][8 waves][32] float4
+constexpr size_t YEPI_BYTES = YIMG_BYTES + YRED_BYTES + 2 * XN * 8;   // + [2][128] f64 (accumulator adds)
 constexpr size_t YLDS_BYTES = XLDS_BYTES > YEPI_BYTES ? XLDS_BYTES : YEPI_BYTES;
 constexpr size_t YLDS_BLEND_BYTES = YLDS_BYTES + XMAX_CIN * sizeof(float2);   // + the second style's affine
 static_assert(8 % YRING == 0, "ring must divide the points per wave");
@@ -171,11 +172,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* res_src = pro == PRO_AFF_RES ? a.res : a.in;
     const int nchunks = Cin / XCK;
 
-    if constexpr (pro != PRO_NONE) {
-        for (int c = tid; c < Cin; c += YT) pab[c] = a.pro_ab[(size_t)b * Cin + c];
-        if constexpr (BLEND)
-            for (int c = tid; c < Cin; c += YT) pab1[c] = a.pro_ab1[(size_t)b * Cin + c];
-    }
+    // the prologue affine into LDS (pab / pab1): given, or formed from the producer's f64 accumulators; runs
+    // after the first patch and U loads are issued (below), so its latency overlaps theirs
+    auto load_affine = [&]() __attribute__((always_inline)) {
+        if constexpr (pro != PRO_NONE) {
+            if (a.pro_stat.acc != nullptr) {
+                const bool store = tx == 0 && ty == 0;   // one workgroup per image keeps the host-visible copy
+                const CinSrc& ps = a.pro_stat;
+                cin_affine_table<YT>(ps, b, 1, pab, BLEND ? pab1 : nullptr,
+                                     store && ps.ab_out ? ps.ab_out + (size_t)b * Cin : nullptr,
+                                     store && ps.ab1_out ? ps.ab1_out + (size_t)b * Cin : nullptr);
+            } else {
+                for (int c = tid; c < Cin; c += YT) pab[c] = a.pro_ab[(size_t)b * Cin + c];
+                if constexpr (BLEND)
+                    for (int c = tid; c < Cin; c += YT) pab1[c] = a.pro_ab1[(size_t)b * Cin + c];
+            }
+        }
+    };
     static_assert(!BLEND || PRO != PRO_NONE, "the blend is a prologue");
 
     // ---- staging descriptors (item k = float4 tid + 512k of a chunk's 720-float4 patch), as above --------
@@ -345,13 +358,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
 
     // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..R-1) in flight ----
-    if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging
     sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 0); });
     sfor<0, YRING>([&](auto X) __attribute__((always_inline)) {
         sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
             load_u1(0, decltype(X)::value, decltype(X)::value, decltype(Pc)::value);
         });
     });
+    load_affine();
+    if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging
     stage_all(0, patch);
     if (nchunks > 1) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 1); });
     lds_barrier();
@@ -474,8 +488,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         yv[i] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         s4 += yv[i];
     }
-    if (a.part != nullptr) {
+    if (a.part != nullptr || a.stat.acc != nullptr) {
         f32x4* const red = reinterpret_cast<f32x4*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES);   // [2][8][32]
+        double* const dred = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES + YRED_BYTES);
         const float cnt = (float)(min(XTH, H - y0) * min(XTW, W - x0));
         auto xsum = [&](f32x4 v) __attribute__((always_inline)) {
             v.x += __shfl_xor(v.x, 32);
@@ -505,12 +520,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             f32x4 M = red[256 + cq];
 #pragma unroll
             for (int w = 1; w < 8; ++w) M += red[256 + w * 32 + cq];
-            const int n_part = a.tiles_y * a.tiles_x;
-            float4* const dst = a.part + ((size_t)b * XN + 4 * cq) * n_part + ty * a.tiles_x + tx;
-            dst[0] = make_float4(S.x, M.x, cnt, 0.f);
-            dst[n_part] = make_float4(S.y, M.y, cnt, 0.f);
-            dst[2 * n_part] = make_float4(S.z, M.z, cnt, 0.f);
-            dst[3 * n_part] = make_float4(S.w, M.w, cnt, 0.f);
+            if (a.stat.acc != nullptr) {   // {S, M2 + S^2 / n} as f64 (finalize_kernel's merge quantity)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double dS = (double)S[k];
+                    dred[4 * cq + k] = dS;
+                    dred[XN + 4 * cq + k] = (double)M[k] + dS * dS / (double)cnt;
+                }
+            } else {
+                const int n_part = a.tiles_y * a.tiles_x;
+                float4* const dst = a.part + ((size_t)b * XN + 4 * cq) * n_part + ty * a.tiles_x + tx;
+                dst[0] = make_float4(S.x, M.x, cnt, 0.f);
+                dst[n_part] = make_float4(S.y, M.y, cnt, 0.f);
+                dst[2 * n_part] = make_float4(S.z, M.z, cnt, 0.f);
+                dst[3 * n_part] = make_float4(S.w, M.w, cnt, 0.f);
+            }
+        }
+        if (a.stat.acc != nullptr) {   // channel-contiguous adds: 512 B per wave instruction
+            lds_barrier();
+            if (tid < XN) cin_acc_add(a.stat, a.batch, XN, b, tid, (int)blockIdx.x % a.stat.nslot, dred[tid], dred[XN + tid]);
         }
     }
     XTL(3);
@@ -665,9 +693,16 @@ hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
     if (a.cin % XCK != 0 || a.cin > XMAX_CIN || a.tiles_y != (a.H + XTH - 1) / XTH ||
         a.tiles_x != (a.W + XTW - 1) / XTW || (size_t)a.batch * a.H * a.W * a.cin * 4 >= (size_t)0x7F000000)
         return hipErrorInvalidValue;   // 32-bit staging offsets; the out-of-range store offset must stay out of range
+    if (a.stat.acc != nullptr && (a.stat.nslot < 1 || a.stat.nslot > CIN_ACC_MAX_SLOTS))
+        return hipErrorInvalidValue;
+    const bool src_acc = a.pro_stat.acc != nullptr;
+    if (src_acc && (a.pro_stat.nslot < 1 || a.pro_stat.nslot > CIN_ACC_MAX_SLOTS || a.pro_stat.C != a.cin ||
+                    a.pro_stat.batch != a.batch || a.pro_stat.style == nullptr || a.pro_mode == PRO_NONE))
+        return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
-    if (a.pro_ab1 != nullptr) {   // two styles
-        if (a.pro_w == nullptr) return hipErrorInvalidValue;
+    if (a.pro_w != nullptr) {   // two styles: the affines from pro_ab/pro_ab1, or both formed from pro_stat
+        if (src_acc ? a.pro_stat.style1_offset < 0 : (a.pro_ab1 == nullptr || a.pro_ab == nullptr))
+            return hipErrorInvalidValue;
         switch (a.pro_mode) {
             case PRO_AFF_RELU: hipExtLaunchKernelGGL((wino_x6_kernel<PRO_AFF_RELU, true>), dim3(grid), dim3(YT), YLDS_BLEND_BYTES, st, e0, e1, 0, a); break;
             case PRO_AFF: hipExtLaunchKernelGGL((wino_x6_kernel<PRO_AFF, true>), dim3(grid), dim3(YT), YLDS_BLEND_BYTES, st, e0, e1, 0, a); break;

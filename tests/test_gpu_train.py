@@ -101,8 +101,9 @@ def _pool_route(tr, B):
 # Winograd transfer convs, measured)
 # transfer: arithmetic of the transfer network's convs — "fp32" (exact-f32 MFMA), "fp32_winograd"
 # (residual-block convs, forward + input gradient, as Winograd F(2x2,3x3): ~1e-6 relative per conv) or
-# "winograd_bf16x6" (those residual convs and their weight gradient on exact 3-piece split-bf16 MFMA
-# products: dropped terms <= 2^-25 per product, the same 2e-3 bound)
+# "winograd_bf16x6" (those residual convs and their weight gradient, and the 9x9 start conv's forward
+# (wino9_x6 in its training mode: raw ReLU output + per-block statistics), on exact 3-piece split-bf16
+# MFMA products: dropped terms <= 2^-25 per product, the same 2e-3 bound)
 @pytest.mark.parametrize("name,precision,gtol,transfer", [
     ("A", "fp32", 2e-3, "fp32"), ("B", "fp32", 2e-3, "fp32"), ("A", "bf16x6", 2e-3, "fp32"),
     ("A", "bf16x3", 1e-3, "fp32"), ("A", "bf16", 0.05, "fp32"),

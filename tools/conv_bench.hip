@@ -108,16 +108,14 @@ static int run_vgg(int B) {
             });                                                                                            \
             names.push_back(NAME);                                                                         \
         }
-        VV(32, 64, 8, 16, 4, 1, 1, 0, "131 NT64 8x16 WM4 TPS1 (prod)")
-        VV(32, 128, 8, 16, 2, 2, 3, 1, "132 NT128 8x16 TPS3 PF (prod)")
-        VV(32, 64, 8, 16, 2, 2, 3, 1, "133 NT64 8x16 TPS3 PF (prod)")
-        VV(32, 64, 8, 16, 4, 1, 1, 1, "NT64 8x16 WM4 TPS1 PF")
-        VV(32, 64, 8, 16, 4, 1, 3, 0, "NT64 8x16 WM4 TPS3")
-        VV(32, 64, 8, 16, 4, 1, 3, 1, "NT64 8x16 WM4 TPS3 PF")
-        VV(32, 64, 8, 16, 2, 2, 3, 0, "NT64 8x16 TPS3")
-        VV(32, 128, 8, 16, 2, 2, 3, 0, "NT128 8x16 TPS3")
-        VV(32, 128, 4, 16, 2, 2, 3, 1, "NT128 4x16 TPS3 PF")
-        VV(32, 64, 8, 16, 2, 2, 9, 1, "NT64 8x16 TPS9 PF")
+        VV(32, 64, 8, 16, 4, 1, 3, 0, "134 NT64 8x16 WM4 TPS3 (prod)")
+        VV(32, 128, 8, 16, 2, 2, 3, 1, "132 NT128 8x16 TPS3 PF (prod 512)")
+        VV(32, 128, 8, 16, 2, 2, 3, 0, "NT128 8x16 WM2 TPS3")
+        VV(32, 64, 16, 16, 4, 1, 3, 0, "NT64 16x16 WM4 TPS3")
+        VV(32, 128, 16, 16, 2, 2, 3, 0, "NT128 16x16 WM2 TPS3")
+        VV(64, 64, 8, 16, 4, 1, 3, 0, "CK64 NT64 8x16 WM4 TPS3")
+        VV(64, 128, 8, 16, 2, 2, 3, 0, "CK64 NT128 8x16 WM2 TPS3")
+        VV(32, 64, 8, 16, 4, 1, 9, 0, "NT64 8x16 WM4 TPS9")
 #undef VV
         const int nv = (int)launches.size();
         std::vector<std::vector<float>> t(nv);
