@@ -414,8 +414,8 @@ static ConvTile bf3_tile_of() {
     X(111, 3, 3, 1, 32, 128, 4, 16, 2, 2, 1, 3, 0)       \
     X(112, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 3, 0)        \
     X(113, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3, 0)        \
-    X(132, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 1)       \
-    X(134, 3, 3, 1, 32, 64, 8, 16, 4, 1, 3, 1, 0)
+    X(134, 3, 3, 1, 32, 64, 8, 16, 4, 1, 3, 1, 0)        \
+    X(135, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 0)
 
 bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long long pixels, ConvTile* out) {
     if (kh != 3 || stride != 1 || cin % 32 != 0 || ntot % 64 != 0 || planes < 1 || planes > 3) return false;
@@ -428,10 +428,15 @@ bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long lon
     // Register prefetch of the next Cin chunk's halo (PF) only pays on the 512-channel layers with a
     // 128-wide tile while that still fills the chip (block4_conv2 188 -> 174 us); elsewhere its
     // registers cost more occupancy than it hides (bf16x3 residual: 43.8 -> 57.6 us).
+    // Round 3 (tools/conv_bench 4 vgg, profiles/r03/conv_bench_vgg_tiles*.log): the 128-wide tile without the halo
+    // register prefetch (config 135, 2 x 2 waves) beats 134 wherever it still gives >= ~900 workgroups
+    // (b2c2 239 -> 227 us, b3c2 189 -> 182, b4c2 187 -> 170) and 132 everywhere; 134 keeps block 1 (Cout 64)
+    // and block 5 (225 workgroups at 128 wide: 58 vs 66 us). Prefetching the weights two stages ahead (two
+    // register sets) cost a wave per SIMD of occupancy and was 25-70 % slower on every layer.
     int want;
     if (planes == 2) want = 102;
     else if (planes == 3) want = 113;
-    else if (ntot % 128 == 0 && cin >= 512 && (pixels / 128) * (ntot / 128) >= 1024) want = 132;
+    else if (ntot % 128 == 0 && (pixels / 128) * (ntot / 128) >= 896) want = 135;
     else want = 134;
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF)                  \
     if (ID == want) {                                                           \

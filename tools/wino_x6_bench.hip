@@ -49,6 +49,9 @@ int main(int argc, char** argv) {
     const int fin = argc > 7 ? atoi(argv[7]) : 0;
     // nomat = 1: no materialised block output (the frame's conv1 layers: a.mat == nullptr)
     const int nomat = argc > 8 ? atoi(argv[8]) : 0;
+    // accm (x6 only): 1 = CIN statistics into f64 accumulators and the prologue affine formed from them (the
+    // round-3 frame), 2 = producer side only (accumulators out, pro_ab in), 3 = consumer side only
+    const int accm = argc > 9 ? atoi(argv[9]) : 0;
     auto hin = host_rand((size_t)B * H * W * C, zm ? -2.f : -1.f, zm ? 2.f : 3.f, 1);
     auto hres = host_rand((size_t)B * H * W * C, -1, 1, 5);
     // residual init U(0, 0.05); zero-mean in chain mode (a gain near 1 per layer keeps the chained values finite)
@@ -116,11 +119,37 @@ int main(int argc, char** argv) {
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         printf("finalize alone: %.2f us/launch\n", ms * 1e3 / 200);
     }
+    double* acc = nullptr;
+    float* sty = nullptr;
+    if (accm) {
+        CK(hipMalloc(&acc, (size_t)8 * B * 2 * 128 * sizeof(double)));
+        std::vector<double> ha((size_t)8 * B * 2 * 128);
+        for (size_t i = 0; i < ha.size(); ++i) ha[i] = ((i / 128) % 2) ? 2.0e4 : 1.0e2;   // S ~ 1e2, Q ~ 2e4
+        CK(hipMemcpy(acc, ha.data(), ha.size() * 8, hipMemcpyHostToDevice));
+        sty = dev(host_rand((size_t)B * 2 * C, 0.5f, 1.f, 9));
+    }
     const int iters = 200;
     const char* names[2] = {"wino   ", "wino_x6"};
     for (int v = 0; v < 2; ++v) {
         WinoArgs x = a;
         x.U = v ? U6 : U32; x.out = outs[v]; x.mat = nomat ? nullptr : mats[v]; x.part = parts[v];
+        if (v && (accm == 1 || accm == 2)) {
+            x.part = nullptr;
+            x.stat.acc = acc;
+            x.stat.nslot = 8;
+        }
+        if (v && (accm == 1 || accm == 3) && pro != PRO_NONE) {
+            x.pro_stat.acc = acc;
+            x.pro_stat.nslot = 8;
+            x.pro_stat.C = C;
+            x.pro_stat.batch = B;
+            x.pro_stat.n = (double)H * W;
+            x.pro_stat.style = sty;
+            x.pro_stat.style_stride = 2 * C;
+            x.pro_stat.style_offset = 0;
+            x.pro_stat.style1_offset = -1;
+            x.pro_stat.eps = 1e-5f;
+        }
         auto launch = [&]() { return v ? wino_x6_launch(x, 0) : wino_launch(x, 0); };
         for (int i = 0; i < 20; ++i) CK(launch());
         CK(hipDeviceSynchronize());
@@ -146,8 +175,8 @@ int main(int argc, char** argv) {
 #ifdef X6_PROF
         if (v) rst::x6_timeline_print(B * a.tiles_y * a.tiles_x, 8);
 #endif
-        if (v) printf("%s B=%d Cin=%d pro=%d%s: %.2f us/launch, bf16 pipe %.3f (6 terms), direct-equivalent %.1f TF/s\n",
-                      names[v], B, C, pro, cold ? " cold" : (chain == 1 ? " chain" : (chain == 2 ? " zero-mean weights" : "")), us, 6 * exec / (us * 1e-6) / 2.5e15, direct / (us * 1e-6) / 1e12);
+        if (v) printf("%s B=%d Cin=%d pro=%d%s%s: %.2f us/launch, bf16 pipe %.3f (6 terms), direct-equivalent %.1f TF/s\n",
+                      names[v], B, C, pro, accm == 1 ? " acc" : (accm == 2 ? " acc-out" : (accm == 3 ? " acc-in" : "")), cold ? " cold" : (chain == 1 ? " chain" : (chain == 2 ? " zero-mean weights" : "")), us, 6 * exec / (us * 1e-6) / 2.5e15, direct / (us * 1e-6) / 1e12);
         else printf("%s B=%d Cin=%d pro=%d%s: %.2f us/launch, f32 pipe %.3f, direct-equivalent %.1f TF/s\n", names[v], B,
                     C, pro, cold ? " cold" : (chain == 1 ? " chain" : (chain == 2 ? " zero-mean weights" : "")), us, exec / (us * 1e-6) / 157.3e12, direct / (us * 1e-6) / 1e12);
     }
