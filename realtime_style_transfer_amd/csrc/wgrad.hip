@@ -388,19 +388,25 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs a) {
 // partial [1408][32] slab; wgrad_reduce_kernel sums the slabs in a fixed order.
 namespace w9 {
 constexpr int TH = 8, TW = 16, NPX = TH * TW;          // output pixels per tile
-constexpr int PR = TH + 8, PC = TW + 8, PRS = 25;      // patch rows / cols / row stride (floats)
-constexpr int PL = PR * PRS;                           // plane stride (400 floats)
+// Strides chosen by an exhaustive search over the bank mapping of the B-operand reads (lane = column (tap, ci),
+// lane half = pixel row + 4): row stride 24 and plane stride 401 (= 17 mod 64) put the 64 lanes of a
+// ds_read_b32 in at most 2 passes (1.18 on average over the 44 column tiles) instead of 5 (4.8) with 25 / 400
+// (SQ: lds_conflict 0.88 of the LDS cycles at 25 / 400)
+constexpr int PR = TH + 8, PC = TW + 8, PRS = 24;      // patch rows / cols / row stride (floats)
+constexpr int PL = 401;                                // plane stride (floats), >= PR * PRS
 constexpr int CMAX = 17, NCOL = 81 * CMAX, NCOLP = 1408, NT = NCOLP / 32, NTW = NT / 4;   // 44 tiles, 11 per wave
 constexpr int DZS = NPX + 4;                           // dZ^T row stride (floats)
 constexpr int ZERO = CMAX * PL;                        // a zero word after the planes (padding columns)
-constexpr int LDS_FL = CMAX * PL + 8 + 32 * DZS;
+constexpr int DZOFF = (CMAX * PL + 8 + 3) / 4 * 4;     // dZ^T offset (16-B aligned)
+constexpr int LDS_FL = DZOFF + 32 * DZS;
+static_assert(PL >= PR * PRS && PRS >= PC, "patch planes");
 }  // namespace w9
 
 __global__ __launch_bounds__(256, 2) void wgrad9_kernel(WgradArgs a) {
     using namespace w9;
     __shared__ __attribute__((aligned(16))) float lds[LDS_FL];
     float* const patch = lds;                    // [ci][PR][PRS] + zero word
-    float* const dzt = lds + CMAX * PL + 8;      // [co][DZS]
+    float* const dzt = lds + DZOFF;              // [co][DZS]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
     constexpr int C = CMAX;   // wgrad9_applies: cin == 17 (the slab rows are (tap, ci) with stride 17)
@@ -493,13 +499,16 @@ static bool wgrad9_applies(const WgradArgs& a) {
 // of one tile row. Each workgroup writes one [256][16] slab; wgrad_reduce_kernel sums them in a fixed order.
 namespace wt9 {
 constexpr int TH = 8, TW = 16, NPX = TH * TW;         // pixels per tile
-constexpr int PR = TH + 8, PC = TW + 8, PRS = 25;     // dZ patch rows / cols / row stride (floats)
-constexpr int PL = PR * PRS;                          // plane stride (400 floats)
+// strides from the same bank search as w9 (lane = column (tap, co), lane group = pixel row + 2): row stride
+// 24 and plane stride 395 give at most 2 passes per ds_read_b32 (1.5 average) instead of 3 (2.9) with 25 / 400
+constexpr int PR = TH + 8, PC = TW + 8, PRS = 24;     // dZ patch rows / cols / row stride (floats)
+constexpr int PL = 395;                               // plane stride (floats), >= PR * PRS
 constexpr int CS = 3, CU = 16, NCOL = 81 * CS, NTW = 4;   // 243 columns: 16 tiles of 16, 4 per wave
 constexpr int RP = 16 * 16, CP = CU;                  // slab rows (padded columns) x slab columns
 constexpr int XS = NPX + 4;                           // X^T row stride (floats)
 constexpr int ZERO = CS * PL;                         // zero words after the planes (padding columns)
-constexpr int XOFF = CS * PL + 8;                     // X^T offset (16-B aligned)
+constexpr int XOFF = (CS * PL + 8 + 3) / 4 * 4;       // X^T offset (16-B aligned)
+static_assert(PL >= PR * PRS && PRS >= PC, "patch planes");
 constexpr int LDS_FL = XOFF + CU * XS;
 }  // namespace wt9
 
