@@ -109,13 +109,7 @@ static int run_vgg(int B) {
             names.push_back(NAME);                                                                         \
         }
         VV(32, 64, 8, 16, 4, 1, 3, 0, "134 NT64 8x16 WM4 TPS3 (prod)")
-        VV(32, 64, 8, 16, 4, 1, 3, 2, "NT64 8x16 WM4 TPS3 WDEEP")
-        VV(32, 64, 8, 16, 4, 1, 3, 3, "NT64 8x16 WM4 TPS3 WDEEP+PF")
-        VV(32, 64, 8, 16, 4, 1, 1, 2, "NT64 8x16 WM4 TPS1 WDEEP")
-        VV(32, 128, 8, 16, 2, 2, 3, 1, "132 NT128 8x16 TPS3 PF (prod 512)")
-        VV(32, 128, 8, 16, 2, 2, 3, 0, "NT128 8x16 WM2 TPS3")
-        VV(32, 128, 8, 16, 2, 2, 3, 2, "NT128 8x16 WM2 TPS3 WDEEP")
-        VV(32, 64, 4, 16, 2, 2, 3, 2, "NT64 4x16 WM2 TPS3 WDEEP")
+        VV(32, 128, 8, 16, 2, 2, 3, 0, "135 NT128 8x16 WM2 TPS3 (prod)")
 #undef VV
         const int nv = (int)launches.size();
         std::vector<std::vector<float>> t(nv);
