@@ -310,7 +310,10 @@ def style_loss_terms(prediction, gt_content, gt_style, vgg_weights,
     fs = vgg16_features(style, vgg_weights, operand_round)
     fp = vgg16_features(prediction, vgg_weights, operand_round)
     feature_loss = np.mean([mean_l2_loss_on_batch(fp[n] - fc[n]) for n in CONTENT_LAYERS], axis=0) * content_factor
-    style_loss = np.mean([mean_l2_loss_on_batch(gram_matrix(fp[n]) - gram_matrix(fs[n])) for n in STYLE_LAYERS],
+    # operand_round (the device's plain-bf16 loss) also rounds the Gram operands: its Gram runs on bf16 features
+    # (gram.hip gram_partial_bf16_kernel, the mixed_bfloat16 einsum)
+    gram = (lambda f: gram_matrix(operand_round(f))) if operand_round is not None else gram_matrix
+    style_loss = np.mean([mean_l2_loss_on_batch(gram(fp[n]) - gram(fs[n])) for n in STYLE_LAYERS],
                          axis=0) * style_factor
     tv = total_variation(prediction) * tv_factor
     return {'loss': feature_loss + style_loss + tv, 'feature_loss': feature_loss, 'style_loss': style_loss,

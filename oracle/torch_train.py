@@ -202,6 +202,24 @@ def _gram(f):
     return torch.bmm(f2, f2.transpose(1, 2)) / (H * W)
 
 
+class _Bf16Gram(torch.autograd.Function):
+    """The device's RST_PRECISION_BF16 Gram (gram.hip gram_partial_bf16_kernel): forward on bf16-rounded
+    features (products exact, float64 sums); backward as the device's Gram backward, dF = (dG + dG^T) F / HW
+    on the unrounded features (the 1x1 conv over the f32 feature map in train_api vgg_backward)."""
+
+    @staticmethod
+    def forward(ctx, f):
+        ctx.save_for_backward(f)
+        return _gram(_bf16(f))
+
+    @staticmethod
+    def backward(ctx, gg):
+        (f,) = ctx.saved_tensors
+        B, C, H, W = f.shape
+        f2 = f.reshape(B, C, H * W)
+        return (torch.bmm(gg + gg.transpose(1, 2), f2) / (H * W)).reshape(B, C, H, W)
+
+
 def _mean_l2(t):
     return (0.5 * t ** 2).reshape(t.shape[0], -1).mean(dim=1)
 
@@ -212,7 +230,8 @@ def style_losses(pred, content, style, vgg, content_factor=1e4, style_factor=1e-
     fp = vgg_features(pred, vgg, taps, route, bf16, relu_route)
     fc, fs = vgg_features(content, vgg, bf16=bf16), vgg_features(style, vgg, bf16=bf16)
     feature = torch.stack([_mean_l2(fp[n] - fc[n]) for n in CONTENT_LAYERS]).mean(0) * content_factor
-    style_l = torch.stack([_mean_l2(_gram(fp[n]) - _gram(fs[n])) for n in STYLE_LAYERS]).mean(0) * style_factor
+    gram = _Bf16Gram.apply if bf16 else _gram   # plain-bf16 loss: Grams on bf16-rounded features too
+    style_l = torch.stack([_mean_l2(gram(fp[n]) - gram(fs[n])) for n in STYLE_LAYERS]).mean(0) * style_factor
     tv = ((pred[:, :, 1:, :] - pred[:, :, :-1, :]).abs().sum(dim=(1, 2, 3)) +
           (pred[:, :, :, 1:] - pred[:, :, :, :-1]).abs().sum(dim=(1, 2, 3))) * tv_factor
     return torch.stack([feature + style_l + tv, feature, style_l, tv], dim=1)

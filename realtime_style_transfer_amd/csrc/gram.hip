@@ -100,6 +100,89 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restri
     }
 }
 
+// The same partial Gram tiles with the features rounded to bf16 (RNE) and v_mfma_f32_32x32x16_bf16 (fp32
+// accumulation): the RST_PRECISION_BF16 loss, whose VGG16 convs already take bf16 operands — the
+// mixed_bfloat16 compute dtype of the Keras einsum (styleLoss.py gram_matrix). Per KP-pixel chunk each
+// thread loads 16 pixels of one channel of both 64-channel slices (a wave's loads are one pixel's 64
+// consecutive channels: coalesced), rounds them and writes them transposed, [channel][pixel] bf16 with a
+// 72-element row (144 B: the ds_read_b128 lane groups of the operand reads and the 8-lane groups of the
+// stores are conflict-free), so an MFMA operand (8 consecutive pixels of one channel) is one ds_read_b128.
+// At 16x the f32 MFMA rate the kernel is bound by the feature reads, not the products.
+namespace gramb {
+constexpr int KP = 64, TILE = 64, RS = KP + 8;   // pixels per chunk, channels per slice, LDS row (bf16)
+}
+__global__ __launch_bounds__(256) void gram_partial_bf16_kernel(const float* __restrict__ feat, float* __restrict__ slab,
+                                                                int hw, int C, int nsplit, int span) {
+    using namespace gramb;
+    typedef short short8 __attribute__((ext_vector_type(8)));
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    __shared__ __attribute__((aligned(16))) unsigned short la[TILE * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short lb[TILE * RS];
+    const int ntile = C / TILE;
+    int bid = blockIdx.x;
+    const int split = bid % nsplit;
+    bid /= nsplit;
+    const int npairs = ntile * (ntile + 1) / 2;
+    int pair = bid % npairs;
+    const int b = bid / npairs;
+    int ti = 0;   // pair -> (ti, tj), ti <= tj, row-major over the upper triangle
+    while (pair >= ntile - ti) {
+        pair -= ntile - ti;
+        ++ti;
+    }
+    const int tj = ti + pair;
+    const int c0 = ti * TILE, d0 = tj * TILE;
+    const int p_begin = split * span;
+    const int p_end = min(hw, p_begin + span);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wi = wave >> 1, wj = wave & 1;
+    const int li = lane & 31, lh = lane >> 5;
+    const float* fb = feat + (size_t)b * hw * C;
+    const int sc = tid & 63, sg = tid >> 6;   // staging: channel sc, pixels 16 sg .. 16 sg + 15 of the chunk
+
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    auto pack = [](float x, float y) __attribute__((always_inline)) {
+        return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
+    };
+    for (int p0 = p_begin; p0 < p_end; p0 += KP) {
+        float va[16], vb[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int p = p0 + 16 * sg + j;
+            const bool ok = p < p_end;
+            va[j] = ok ? fb[(size_t)p * C + c0 + sc] : 0.f;
+            vb[j] = ok ? fb[(size_t)p * C + d0 + sc] : 0.f;
+        }
+        __syncthreads();   // the previous chunk's operand reads are done
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint4 wa = make_uint4(pack(va[8 * h], va[8 * h + 1]), pack(va[8 * h + 2], va[8 * h + 3]),
+                                        pack(va[8 * h + 4], va[8 * h + 5]), pack(va[8 * h + 6], va[8 * h + 7]));
+            const uint4 wb = make_uint4(pack(vb[8 * h], vb[8 * h + 1]), pack(vb[8 * h + 2], vb[8 * h + 3]),
+                                        pack(vb[8 * h + 4], vb[8 * h + 5]), pack(vb[8 * h + 6], vb[8 * h + 7]));
+            *reinterpret_cast<uint4*>(la + sc * RS + 16 * sg + 8 * h) = wa;
+            *reinterpret_cast<uint4*>(lb + sc * RS + 16 * sg + 8 * h) = wb;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < KP / 16; ++s) {   // K step: pixels 16 s + 8 lh .. + 7
+            const short8 av = *reinterpret_cast<const short8*>(la + (wi * 32 + li) * RS + 16 * s + 8 * lh);
+            const short8 bv = *reinterpret_cast<const short8*>(lb + (wj * 32 + li) * RS + 16 * s + 8 * lh);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+        }
+    }
+    float* out = slab + ((size_t)b * nsplit + split) * C * C;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        out[(size_t)(c0 + wi * 32 + row) * C + d0 + wj * 32 + li] = acc[r];
+        if (ti != tj) out[(size_t)(d0 + wj * 32 + li) * C + c0 + wi * 32 + row] = acc[r];
+    }
+}
+
 // Sums the splits in a fixed order: a workgroup owns 64 float4 of G; its four waves sum contiguous
 // quarters of the split range, wave 0 adds the quarters in order and scales.
 __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
@@ -138,7 +221,8 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
     }
 }
 
-hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st) {
+hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st,
+                       bool bf16) {
     if (channels % gram::TILE != 0) return hipErrorInvalidValue;
     const int ns = gram_splits(batch, hw, channels);
     int span = (hw + ns - 1) / ns;
@@ -146,7 +230,10 @@ hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float
     const int ntile = channels / gram::TILE;
     const unsigned grid = (unsigned)(batch * (ntile * (ntile + 1) / 2) * ns);
     float* slab = static_cast<float*>(ws);
-    hipLaunchKernelGGL(gram_partial_kernel, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns, span);
+    if (bf16)
+        hipLaunchKernelGGL(gram_partial_bf16_kernel, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns, span);
+    else
+        hipLaunchKernelGGL(gram_partial_kernel, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns, span);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if ((reinterpret_cast<uintptr_t>(out) & 15) != 0) return hipErrorInvalidValue;

@@ -355,7 +355,9 @@ hipError_t tile_stats_launch(const float* x, float4* part, int batch, long hw, i
 
 // Gram matrices (gram.hip)
 size_t gram_workspace_bytes(int batch, int hw, int channels);
-hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st);
+// bf16: features rounded to bf16, bf16 MFMA (RST_PRECISION_BF16 loss; the mixed_bfloat16 einsum)
+hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st,
+                       bool bf16 = false);
 
 // Loss kernels (loss.hip)
 hipError_t maxpool2_launch(const float* x, float* y, int B, int H, int W, int C, hipStream_t st);

@@ -169,11 +169,13 @@ int rst_loss_forward(rst_loss_handle* h, const float* prediction, const float* g
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int B = batch;
     int r;
+    // plain-bf16 loss: the Gram matrices on bf16-rounded features as well (mixed_bfloat16 compute dtype)
+    const bool gram_bf16 = h->shape.precision == RST_PRECISION_BF16;
     // style image: grams of the four style layers
     if ((r = vgg_run(h, gt_style, B, STYLE_IDX[3], st)) != RST_OK) return r;
     for (int k = 0; k < 4; ++k) {
         const VggConv& c = h->convs[STYLE_IDX[k]];
-        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_style[k], h->d_gram_ws, st));
+        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_style[k], h->d_gram_ws, st, gram_bf16));
     }
     // ground-truth content: block5_conv3 features
     if ((r = vgg_run(h, gt_content, B, CONTENT_IDX, st)) != RST_OK) return r;
@@ -186,7 +188,7 @@ int rst_loss_forward(rst_loss_handle* h, const float* prediction, const float* g
                                    0.5 / (double)f5 * h->shape.content_factor, losses, 4, 1, 0, st));
     for (int k = 0; k < 4; ++k) {
         const VggConv& c = h->convs[STYLE_IDX[k]];
-        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_pred[k], h->d_gram_ws, st));
+        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_pred[k], h->d_gram_ws, st, gram_bf16));
         const long n = (long)c.cout * c.cout;
         RST_HIP_TRY(sqdiff_loss_launch(h->d_gram_pred[k], h->d_gram_style[k], B, n, h->d_partial,
                                        0.5 / (double)n / 4.0 * h->shape.style_factor, losses, 4, 2, k > 0, st));
