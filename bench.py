@@ -293,9 +293,8 @@ def train_executed_work(plan, H, W, vgg_precision: str, transfer_precision: str)
         else:
             vgg_bf16 += terms * f
         if i in pools:
-            if terms == 1:   # plain bf16: the two Gram forwards on bf16 features (bf16 pipe), the backward f32
-                vgg_bf16 += 2 * 2.0 * h * w * c * c
-                gram += 2.0 * h * w * c * c
+            if terms == 1:   # plain bf16: the Gram forwards and the Gram backward (1x1) on the bf16 pipe
+                vgg_bf16 += 3 * 2.0 * h * w * c * c
             else:
                 gram += 3 * 2.0 * h * w * c * c
             h, w = h // 2, w // 2
@@ -343,7 +342,7 @@ def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"
                                 "transfer net and the rest fp32-level (see transfer_precision)",
                       "bf16x3": "VGG16 3x3 convs: 2-piece split bf16 MFMA (16-bit operands, fp32 accumulate); "
                                 "transfer net and the rest fp32-level (see transfer_precision)",
-                      "bf16": "VGG16 3x3 convs and the Gram forwards: bf16 operands, fp32 accumulate "
+                      "bf16": "VGG16 3x3 convs and the Gram forwards/backward: bf16 operands, fp32 accumulate "
                               "(mixed_bfloat16 arithmetic); transfer net and the rest fp32-level (see "
                               "transfer_precision)"}[precision],
             "transfer_precision": {"fp32": "exact f32 MFMA",

@@ -204,8 +204,9 @@ def _gram(f):
 
 class _Bf16Gram(torch.autograd.Function):
     """The device's RST_PRECISION_BF16 Gram (gram.hip gram_partial_bf16_kernel): forward on bf16-rounded
-    features (products exact, float64 sums); backward as the device's Gram backward, dF = (dG + dG^T) F / HW
-    on the unrounded features (the 1x1 conv over the f32 feature map in train_api vgg_backward)."""
+    features (products exact, float64 sums); backward as the device's Gram backward (train_api vgg_backward:
+    a conv_bf3 1x1 conv), dF = W F with W = (dG + dG^T) / HW rounded to bf16 when packed and F rounded to
+    bf16 as the conv stages it."""
 
     @staticmethod
     def forward(ctx, f):
@@ -216,8 +217,9 @@ class _Bf16Gram(torch.autograd.Function):
     def backward(ctx, gg):
         (f,) = ctx.saved_tensors
         B, C, H, W = f.shape
-        f2 = f.reshape(B, C, H * W)
-        return (torch.bmm(gg + gg.transpose(1, 2), f2) / (H * W)).reshape(B, C, H, W)
+        f2 = _bf16(f.reshape(B, C, H * W))
+        w = _bf16((gg + gg.transpose(1, 2)) / (H * W))
+        return torch.bmm(w, f2).reshape(B, C, H, W)
 
 
 def _mean_l2(t):

@@ -21,6 +21,8 @@ std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int c
 // Same for the split-bf16 kernel: [n_block][cin_chunk][tap_group][tap][kstep][hi/lo][lane_half][n][8]
 // bf16, returned as the float-sized buffer that holds those bits (2 bf16 per float).
 std::vector<float> pack_conv_tiles_bf3(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t);
+// source index in Wg of every bf16 element of the one-plane pack_conv_tiles_bf3 image (-1: padding)
+std::vector<int> pack_conv_tiles_bf3_index(int taps, int cin, int ntot, const ConvTile& t);
 
 }  // namespace rst
 

@@ -415,10 +415,13 @@ static ConvTile bf3_tile_of() {
     X(112, 3, 3, 1, 32, 64, 4, 16, 2, 2, 1, 3, 0)        \
     X(113, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3, 0)        \
     X(134, 3, 3, 1, 32, 64, 8, 16, 4, 1, 3, 1, 0)        \
-    X(135, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 0)
+    X(135, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 0)       \
+    X(140, 1, 1, 1, 32, 64, 8, 16, 4, 1, 1, 1, 0)        \
+    X(141, 1, 1, 1, 32, 128, 8, 16, 2, 2, 1, 1, 0)
 
 bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long long pixels, ConvTile* out) {
-    if (kh != 3 || stride != 1 || cin % 32 != 0 || ntot % 64 != 0 || planes < 1 || planes > 3) return false;
+    if ((kh != 3 && kh != 1) || stride != 1 || cin % 32 != 0 || ntot % 64 != 0 || planes < 1 || planes > 3) return false;
+    if (kh == 1 && planes != 1) return false;   // 1x1: the plain-bf16 Gram backward only
     // measured (tools/conv_bench, residual conv of rst-960-120-128-17): bf16x3 NT64 4x16 42.8 us at B=1;
     // bf16x6 NT64 8x16 62.8 us at B=1 / 437 us at B=8 (exact-f32 MFMA kernel: 92.5 / 611 us).
     // Plain bf16 (one plane, one MFMA per product block; tools/conv_bench vgg, VGG16 at 480x960, B=4):
@@ -434,7 +437,8 @@ bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long lon
     // and block 5 (225 workgroups at 128 wide: 58 vs 66 us). Prefetching the weights two stages ahead (two
     // register sets) cost a wave per SIMD of occupancy and was 25-70 % slower on every layer.
     int want;
-    if (planes == 2) want = 102;
+    if (kh == 1) want = ntot % 128 == 0 ? 141 : 140;
+    else if (planes == 2) want = 102;
     else if (planes == 3) want = 113;
     else if (ntot % 128 == 0 && (pixels / 128) * (ntot / 128) >= 896) want = 135;
     else want = 134;

@@ -169,6 +169,29 @@ std::vector<float> pack_conv_tiles_bf3(const std::vector<float>& Wg, int taps, i
     std::memcpy(packed.data(), out.data(), out.size() * 2);
     return packed;
 }
+
+// The bf16-element positions of pack_conv_tiles_bf3's one-plane image: the index of each element's source
+// in Wg ([tap][cin][ntot]), -1 for padding (a gather map for weights re-packed on the device every step)
+std::vector<int> pack_conv_tiles_bf3_index(int taps, int cin, int ntot, const ConvTile& t) {
+    const int ck = t.ck, nt = t.nt, tps = t.tps, ks_n = ck / 16;
+    const int nchunks = (cin + ck - 1) / ck, nblocks = (ntot + nt - 1) / nt, ngroups = taps / tps;
+    std::vector<int> out((size_t)nblocks * nchunks * ngroups * t.wstage, -1);
+    size_t idx = 0;
+    for (int nb = 0; nb < nblocks; ++nb)
+        for (int c = 0; c < nchunks; ++c)
+            for (int g = 0; g < ngroups; ++g)
+                for (int tt = 0; tt < tps; ++tt)
+                    for (int ks = 0; ks < ks_n; ++ks)
+                        for (int h = 0; h < 2; ++h)
+                            for (int n = 0; n < nt; ++n)
+                                for (int j = 0; j < 8; ++j) {
+                                    const int tap = g * tps + tt;
+                                    const int ci = c * ck + ks * 16 + h * 8 + j;
+                                    const int ng = nb * nt + n;
+                                    out[idx++] = (ci < cin && ng < ntot) ? (int)(((size_t)tap * cin + ci) * ntot + ng) : -1;
+                                }
+    return out;
+}
 }  // namespace rst
 
 namespace rst {

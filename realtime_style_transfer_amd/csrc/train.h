@@ -51,6 +51,8 @@ hipError_t scaled_diff_launch(const float* a, const float* b, float scale, float
                               hipStream_t st);
 hipError_t tv_bwd_launch(const float* x, float factor, float* g, int B, int H, int W, int C, hipStream_t st);
 hipError_t tap3_sum_launch(const float* p, float* out, int B, int H, int W, hipStream_t st);
+hipError_t gram_bwd_weights_bf16_launch(const float* gp, const float* gs, const int* map, int n16, int C, float scale,
+                                        unsigned short* packed, int B, hipStream_t st);
 hipError_t gram_bwd_weights_launch(const float* gp, const float* gs, const int* map, int n_packed, int C, float scale,
                                    float* packed, int B, hipStream_t st);
 hipError_t preprocess_bwd_launch(const float* gpre, float* gx, size_t pixels, int accumulate, hipStream_t st);

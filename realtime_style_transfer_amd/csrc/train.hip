@@ -469,6 +469,27 @@ __global__ __launch_bounds__(256) void gram_bwd_weights_kernel(const float* __re
     }
 }
 
+// plain-bf16 loss: the same weights rounded to bf16 (RNE) into conv_bf3's one-plane image (n16 elements/image)
+__global__ __launch_bounds__(256) void gram_bwd_weights_bf16_kernel(const float* __restrict__ gp,
+                                                                    const float* __restrict__ gs,
+                                                                    const int* __restrict__ map, int n16, int CC,
+                                                                    float scale, unsigned short* __restrict__ packed) {
+    const int b = blockIdx.y;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) {
+        const int m = map[i];
+        const float v = m < 0 ? 0.f : scale * (gp[(size_t)b * CC + m] - gs[(size_t)b * CC + m]);
+        const unsigned u = __float_as_uint(v);
+        packed[(size_t)b * n16 + i] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    }
+}
+
+hipError_t gram_bwd_weights_bf16_launch(const float* gp, const float* gs, const int* map, int n16, int C, float scale,
+                                        unsigned short* packed, int B, hipStream_t st) {
+    hipLaunchKernelGGL(gram_bwd_weights_bf16_kernel, dim3((n16 + 255) / 256, B), dim3(256), 0, st, gp, gs, map, n16,
+                       C * C, scale, packed);
+    return hipGetLastError();
+}
+
 hipError_t gram_bwd_weights_launch(const float* gp, const float* gs, const int* map, int n_packed, int C, float scale,
                                    float* packed, int B, hipStream_t st) {
     hipLaunchKernelGGL(gram_bwd_weights_kernel, dim3((n_packed + 255) / 256, B), dim3(256), 0, st, gp, gs, map,

@@ -396,12 +396,20 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
             const int C = cp.cout;
             const long hw = (long)cp.H * cp.W;
             const float scale = (float)(ls.style_factor / (2.0 * C * C * (double)hw));
-            RST_HIP_TRY(gram_bwd_weights_launch(h->d_gram_pred[k], h->d_gram_style[k], gb.d_map, gb.n_packed, C, scale,
-                                                t->d_gram_packed, B, st));
+            const bool gbf16 = gb.tile.bf3 != 0;   // weights as conv_bf3's bf16 image (n_packed bf16 per image)
+            if (gbf16)
+                RST_HIP_TRY(gram_bwd_weights_bf16_launch(h->d_gram_pred[k], h->d_gram_style[k], gb.d_map, gb.n_packed, C,
+                                                         scale, reinterpret_cast<unsigned short*>(t->d_gram_packed), B,
+                                                         st));
+            else
+                RST_HIP_TRY(gram_bwd_weights_launch(h->d_gram_pred[k], h->d_gram_style[k], gb.d_map, gb.n_packed, C,
+                                                    scale, t->d_gram_packed, B, st));
             for (int b = 0; b < B; ++b) {
                 ConvArgs m{};
                 m.in = cp.d_out + (size_t)b * hw * C;
-                m.wpk = t->d_gram_packed + (size_t)b * gb.n_packed;
+                m.wpk = gbf16 ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(t->d_gram_packed) +
+                                                               (size_t)b * gb.n_packed)
+                              : t->d_gram_packed + (size_t)b * gb.n_packed;
                 m.bias = t->d_zero;
                 m.out = gprev + (size_t)b * hw * C;
                 m.batch = 1;
@@ -752,17 +760,26 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
             const VggConv& c = t->loss->convs[STYLE_IDX[k]];
             const int C = c.cout;
             ConvBwd& gb = t->gram[k];
-            if (!conv_select(1, 1, C, C, &gb.tile))
+            // plain-bf16 loss: the Gram backward dF = F W on bf16 operands as well (conv_bf3 1x1, the weights
+            // rounded to bf16 when packed), the gradient of the bf16 Gram forward
+            const bool gbf16 = loss->precision == RST_PRECISION_BF16 &&
+                               conv_bf3_select(1, 1, C, C, 1, (long long)B * c.H * c.W, &gb.tile);
+            if (!gbf16 && !conv_select(1, 1, C, C, &gb.tile))
                 return fail_delete(t, set_error(RST_ERR_UNSUPPORTED, "no 1x1 tile for the Gram backward"));
             gb.tiles_y = (c.H + gb.tile.th - 1) / gb.tile.th;
             gb.tiles_x = (c.W + gb.tile.tw - 1) / gb.tile.tw;
             gb.n_blocks = (C + gb.tile.nt - 1) / gb.tile.nt;
             gb.nchunks = (C + gb.tile.ck - 1) / gb.tile.ck;
-            std::vector<float> idx((size_t)C * C);
-            for (size_t i = 0; i < idx.size(); ++i) idx[i] = (float)(i + 1);
-            std::vector<int> m = to_map(pack_conv_tiles(idx, 1, C, C, gb.tile));
+            std::vector<int> m;
+            if (gbf16) {
+                m = pack_conv_tiles_bf3_index(1, C, C, gb.tile);   // bf16 elements: n_packed / 2 floats per image
+            } else {
+                std::vector<float> idx((size_t)C * C);
+                for (size_t i = 0; i < idx.size(); ++i) idx[i] = (float)(i + 1);
+                m = to_map(pack_conv_tiles(idx, 1, C, C, gb.tile));
+            }
             gb.n_packed = (int)m.size();
-            max_packed = std::max(max_packed, m.size());
+            max_packed = std::max(max_packed, gbf16 ? (m.size() + 1) / 2 : m.size());
             if ((st = t->alloc(&gb.d_map, m.size() * 4, m.data())) != RST_OK) return fail_delete(t, st);
             hipError_t pe = conv_prepare(gb.tile);
             if (pe != hipSuccess) return fail_delete(t, set_error(RST_ERR_HIP, hipGetErrorString(pe)));
