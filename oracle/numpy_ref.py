@@ -278,8 +278,9 @@ def bf16_round(x):
 
 def vgg16_features(images01, vgg_weights: Dict[str, Tuple[np.ndarray, np.ndarray]], operand_round=None):
     """StyleLossModelVGG.call (styleLoss.py:106-109): x*255, RGB->BGR, -mean, VGG16 trunk.
-    ``operand_round`` (e.g. bf16_round) is applied to the input and kernel of every conv with
-    Cin % 32 == 0 — the layers the device runs in a bf16 precision mode — to simulate that mode."""
+    ``operand_round`` (bf16_round) is applied to the input and kernel of every conv — the device's plain-bf16
+    loss runs all thirteen on bf16 operands (block1_conv1 on vgg_conv0_bf16, the preprocessed image rounded),
+    as Keras mixed_bfloat16 does — to simulate that mode."""
     x = np.asarray(images01, np.float64) * 255.0
     x = x[..., ::-1] - VGG_MEAN_BGR                                   # vgg16.preprocess_input ('caffe')
     feats = {}
@@ -289,7 +290,7 @@ def vgg16_features(images01, vgg_weights: Dict[str, Tuple[np.ndarray, np.ndarray
             continue
         name = entry[0]
         w, b = vgg_weights[name]
-        if operand_round is not None and x.shape[-1] % 32 == 0:
+        if operand_round is not None:
             x, w = operand_round(x), operand_round(w)
         x = relu(conv2d_same(x, w, b, 1))
         if name in STYLE_LAYERS or name in CONTENT_LAYERS:

@@ -160,12 +160,34 @@ class _Bf16Conv(torch.autograd.Function):
         return gx, None, None
 
 
+class _Bf16FwdConv(torch.autograd.Function):
+    """block1_conv1 in the device's plain-bf16 loss: forward on the bf16-rounded preprocessed image and
+    kernel (vgg_conv0_bf16); its input gradient (the gradient reaching the prediction) is the f32 path
+    (train_api vgg_backward: 1x1 conv + tap sum on unrounded weights), so the backward is the exact one."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(w)
+        ctx.xshape = x.shape
+        return conv2d_same(_bf16(x), _bf16(w), b, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (w,) = ctx.saved_tensors
+        xd = torch.zeros(ctx.xshape, dtype=gy.dtype, requires_grad=True)
+        with torch.enable_grad():
+            y = conv2d_same(xd, w, None, 1)
+            (gx,) = torch.autograd.grad(y, xd, gy)
+        return gx, None, None
+
+
 def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None,
                  bf16: bool = False, relu_route=None) -> Dict[str, torch.Tensor]:
     """StyleLossModelVGG.call (styleLoss.py:106-109) on NCHW float64 images in [0, 1].
     ``taps``: list receiving every conv output (retain_grad) when the input requires grad.
     ``route``: {conv index: NCHW activations} whose window maxima route the max-pool backward.
-    ``bf16``: every conv but the first (Cin = 3, fp32 on the device) in bf16 arithmetic (_Bf16Conv).
+    ``bf16``: every conv in bf16 arithmetic (_Bf16Conv; the first, whose input gradient stays f32 on the
+    device, _Bf16FwdConv).
     ``relu_route``: {conv index: NCHW post-ReLU activations} whose positive units set the ReLU backward mask."""
     x = images01 * 255.0
     mean = torch.tensor(VGG_MEAN_BGR, dtype=x.dtype).view(1, 3, 1, 1)
@@ -182,6 +204,8 @@ def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None,
         name = entry[0]
         if bf16 and i > 0:
             x = _Bf16Conv.apply(x, vgg[2 * i], vgg[2 * i + 1])
+        elif bf16:
+            x = _Bf16FwdConv.apply(x, vgg[2 * i], vgg[2 * i + 1])
         else:
             x = conv2d_same(x, vgg[2 * i], vgg[2 * i + 1], 1)
         x = _RoutedRelu.apply(x, relu_route[i]) if relu_route is not None and i in relu_route else F.relu(x)

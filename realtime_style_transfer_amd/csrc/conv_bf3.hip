@@ -19,7 +19,9 @@
 // The prologue (CIN affine / ReLU / residual add / two-style blend / materialise) runs in fp32 and
 // the split happens as the value is written to LDS.
 #include <hip/hip_runtime.h>
+#include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "kernels.h"
 
@@ -328,6 +330,45 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
 
     // ---------------- epilogue (as conv_mfma_kernel) ------------------------------------------
     const int epi = a.epi_mode;
+    // VGG16 (no statistics, no shuffle, bias [+ ReLU]) with 64 channels per wave: through a wave-private LDS
+    // image [32 px][64 ch] per M tile, stored as channel quads — four whole 256-B pixel rows per wave
+    // instruction instead of two 128-B pieces (the accumulator column is one channel of 16 pixels). The
+    // last stage's barrier has retired every operand read, so the halo image is free.
+    if constexpr (NW == 2 && C::LDS_BYTES >= (size_t)4 * 32 * 64 * 4) {   // four 8-KB wave images fit
+        if (a.part == nullptr && !a.shuffle && (epi == EPI_RELU_STATS || epi == EPI_NONE) &&
+            a.ntot % NT == 0) {
+            float* const ep = reinterpret_cast<float*>(smem_b) + wave * (32 * 64);
+            const int ngb = nb * NT + wn * 64;
+            const float bs0 = a.bias[ngb + li], bs1 = a.bias[ngb + 32 + li];
+            const bool relu = epi == EPI_RELU_STATS;
+#pragma unroll
+            for (int m = 0; m < MW; ++m) {
+                const int mt = wm * MW + m;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int px = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const float v0 = acc[m][0][r] + bs0, v1 = acc[m][1][r] + bs1;
+                    ep[px * 64 + li] = relu ? fmaxf(v0, 0.f) : v0;
+                    ep[px * 64 + 32 + li] = relu ? fmaxf(v1, 0.f) : v1;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int px = 4 * it + (lane >> 4), c4 = 4 * (lane & 15), p = mt * 32 + px;
+                    const int oy = y0 + p / TW, ox = x0 + p % TW;
+                    const float4 v = *reinterpret_cast<const float4*>(ep + px * 64 + c4);
+                    if (oy < a.Ho && ox < a.Wo)
+                        *reinterpret_cast<float4*>(a.out + (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ngb + c4) = v;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            }
+            return;
+        }
+    }
     const int n_mtiles = a.tiles_y * a.tiles_x * C::MT;
 #pragma unroll
     for (int n = 0; n < NW; ++n) {
@@ -484,6 +525,128 @@ hipError_t conv_bf3_prepare(const ConvTile& t) {
         default:
             return hipErrorInvalidValue;
     }
+}
+
+// ---- VGG16 block1_conv1 on bf16 operands (the plain-bf16 loss) ----------------------------------------------
+// 3 -> 64 channels, 3x3 SAME: K = 27 (tap, channel) pairs padded to 32 = two k-steps of v_mfma_f32_32x32x16_bf16.
+// The conv_bf3 tiles need Cin % 32 == 0, and the f32 CK-4 kernel it replaces idled most of each f32 MFMA on the
+// 4-channel K (200 us per B=4 forward, 2.4 TB/s of its 472 MB output). Workgroup = 8 x 32 output pixels, wave w
+// rows 2w and 2w + 1 (one 32-pixel M tile each) x all 64 channels; the caffe preprocess (255 x - mean, BGR: the
+// flip is in the weights) is applied as the 10 x 34 x 3 input patch is staged, rounded to bf16, into LDS; each
+// lane gathers its A operand (8 consecutive (tap, channel) values of its pixel) from there; the B operand is
+// pre-packed in lane order on the host (4 x 16 B per lane, loaded once). Epilogue: bias + ReLU, f32 NHWC store.
+namespace vgg0 {
+constexpr int TH = 8, TW = 32, PH = TH + 2, PW = TW + 2, PC = 4;   // patch [row][col][4] bf16 (channel 3 unused)
+}
+__global__ __launch_bounds__(256) void vgg_conv0_bf16_kernel(const float* __restrict__ img, const float2* __restrict__ pre,
+                                                             const unsigned short* __restrict__ wpk,
+                                                             const float* __restrict__ bias, float* __restrict__ out,
+                                                             int H, int W, int tiles_x) {
+    using namespace vgg0;
+    __shared__ __attribute__((aligned(16))) unsigned short patch[PH * PW * PC];
+    __shared__ __attribute__((aligned(16))) float epi[4 * 32 * 64];   // per-wave epilogue images
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    const int b = blockIdx.y, tyx = blockIdx.x;
+    const int y0 = (tyx / tiles_x) * TH, x0 = (tyx % tiles_x) * TW;
+    // B operand: wpk[(s * 2 + n) * 64 + lane] = 8 bf16 (k = 16 s + 8 lh + j, co = 32 n + li)
+    short8 bw[2][2];
+#pragma unroll
+    for (int sn = 0; sn < 4; ++sn)
+        bw[sn >> 1][sn & 1] = *reinterpret_cast<const short8*>(wpk + ((size_t)sn * 64 + lane) * 8);
+    for (int i = tid; i < PH * PW * 3; i += 256) {
+        const int c = i % 3, px = i / 3, r = px / PW, q = px % PW;
+        const int gy = y0 - 1 + r, gx = x0 - 1 + q;
+        float v = 0.f;   // SAME zero padding of the preprocessed image
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+            const float2 ab = pre[b * 3 + c];
+            v = fmaf(ab.x, img[(((size_t)b * H + gy) * W + gx) * 3 + c], ab.y);
+        }
+        patch[px * PC + c] = bf16_rne(v);
+    }
+    __syncthreads();
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int py = 2 * wave + m;   // output row within the tile; the lane's pixel is column li
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            unsigned short av[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = 16 * s + 8 * lh + j;
+                const int tap = k / 3, c = k - 3 * (k / 3), ky = tap / 3, kx = tap - 3 * (tap / 3);
+                av[j] = k < 27 ? patch[((py + ky) * PW + li + kx) * PC + c] : (unsigned short)0;
+            }
+            short8 a8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a8[j] = (short)av[j];
+#pragma unroll
+            for (int n = 0; n < 2; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a8, bw[s][n], acc[m][n], 0, 0, 0);
+        }
+    }
+    // epilogue through a wave-private LDS image [32 px][64 ch] per output row: a lane's accumulator column is
+    // one channel of 16 pixels, so direct stores wrote two 128-B pieces per wave instruction (2.8 TB/s on the
+    // 472 MB output); read back as channel quads, a wave instruction stores four whole pixels, 1 KB contiguous.
+    // Row stride 64 floats: the b32 writes and the b128 reads (lane groups of MI355X_MICROARCH.md) are
+    // conflict-free.
+    float* const ep = epi + wave * (32 * 64);
+    const float bs0 = bias[li], bs1 = bias[32 + li];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int oy = y0 + 2 * wave + m;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int px = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            ep[px * 64 + li] = fmaxf(acc[m][0][r] + bs0, 0.f);
+            ep[px * 64 + 32 + li] = fmaxf(acc[m][1][r] + bs1, 0.f);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int px = 4 * it + (lane >> 4), c4 = 4 * (lane & 15), ox = x0 + px;
+            const float4 v = *reinterpret_cast<const float4*>(ep + px * 64 + c4);
+            if (oy < H && ox < W) *reinterpret_cast<float4*>(out + (((size_t)b * H + oy) * W + ox) * 64 + c4) = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
+}
+
+// Keras HWIO [3][3][3][64] (already BGR-flipped by the caller) -> the lane-order bf16 B image (4 x 64 x 8)
+std::vector<unsigned short> vgg_conv0_bf16_pack(const float* wflip) {
+    std::vector<unsigned short> out(4 * 64 * 8, 0);
+    for (int sn = 0; sn < 4; ++sn)
+        for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) {
+                const int s = sn >> 1, n = sn & 1, li = lane & 31, lh = lane >> 5;
+                const int k = 16 * s + 8 * lh + j, co = 32 * n + li;
+                if (k < 27) {
+                    const float v = wflip[(size_t)k * 64 + co];   // k = tap * 3 + c = (ky * 3 + kx) * 3 + c
+                    unsigned u;
+                    std::memcpy(&u, &v, 4);
+                    out[((size_t)sn * 64 + lane) * 8 + j] = (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+                }
+            }
+    return out;
+}
+
+hipError_t vgg_conv0_bf16_launch(const float* img, const float2* pre, const unsigned short* wpk, const float* bias,
+                                 float* out, int batch, int H, int W, hipStream_t st) {
+    using namespace vgg0;
+    const int tiles_y = (H + TH - 1) / TH, tiles_x = (W + TW - 1) / TW;
+    hipLaunchKernelGGL(vgg_conv0_bf16_kernel, dim3((unsigned)(tiles_y * tiles_x), (unsigned)batch), dim3(256), 0, st,
+                       img, pre, wpk, bias, out, H, W, tiles_x);
+    return hipGetLastError();
 }
 
 }  // namespace rst

@@ -167,6 +167,10 @@ hipError_t conv_prepare(const ConvTile& t);
 bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long long pixels, ConvTile* out);
 hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st);
 hipError_t conv_bf3_prepare(const ConvTile& t);
+// VGG16 block1_conv1 (3 -> 64, preprocess fused) on bf16 operands: the plain-bf16 loss (conv_bf3.hip)
+std::vector<unsigned short> vgg_conv0_bf16_pack(const float* wflip);
+hipError_t vgg_conv0_bf16_launch(const float* img, const float2* pre, const unsigned short* wpk, const float* bias,
+                                 float* out, int batch, int H, int W, hipStream_t st);
 
 // Residual-block conv (3x3 s1 SAME, 128 output channels) as fused Winograd F(2x2,3x3) on f32 MFMA
 // (wino.hip). Epilogue: bias + ReLU + store + per-(workgroup, channel) {sum, M2, n}, n_part =

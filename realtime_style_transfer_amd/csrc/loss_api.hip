@@ -12,7 +12,8 @@
 // mean_l2(t) = mean(0.5 t^2) per image (:290-292). The preprocess is folded into the first conv:
 // its input channels are flipped (BGR) in the packed weights and the prologue applies
 // y = 255 x - mean per channel, so SAME zero padding still applies to the preprocessed image.
-// Every conv runs on conv_mfma_kernel (f32 MFMA); Gram matrices on gram.hip; reductions on loss.hip.
+// Every conv runs on conv_mfma_kernel (f32 MFMA) or, in a bf16 precision mode, conv_bf3 (block1_conv1 in the
+// plain-bf16 mode: vgg_conv0_bf16); Gram matrices on gram.hip; reductions on loss.hip.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -31,6 +32,11 @@ int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t s
     const float* in = img;
     for (int i = 0; i <= last; ++i) {
         VggConv& c = h->convs[i];
+        if (c.d_w0bf != nullptr) {   // plain-bf16 loss: block1_conv1 on bf16 operands, preprocess fused
+            RST_HIP_TRY(vgg_conv0_bf16_launch(in, h->d_pre, c.d_w0bf, c.d_b, c.d_out, B, c.H, c.W, st));
+            in = c.d_out;
+            continue;
+        }
         ConvArgs a{};
         a.in = in;
         a.pro_ab = i == 0 ? h->d_pre : nullptr;
@@ -127,6 +133,10 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
         std::vector<float> pk = c.tile.bf3 ? pack_conv_tiles_bf3(Wg, 9, cin, c.cout, c.tile)
                                            : pack_conv_tiles(Wg, 9, cin, c.cout, c.tile);
         if ((st = h->alloc(&c.d_w, pk.size() * 4, pk.data())) != RST_OK) { delete h; return st; }
+        if (i == 0 && shape->precision == RST_PRECISION_BF16) {   // mixed_bfloat16: block1_conv1 in bf16 as well
+            const std::vector<unsigned short> w0 = vgg_conv0_bf16_pack(Wg.data());
+            if ((st = h->alloc(&c.d_w0bf, w0.size() * 2, w0.data())) != RST_OK) { delete h; return st; }
+        }
         if ((st = h->alloc(&c.d_b, (size_t)c.cout * 4, bias)) != RST_OK) { delete h; return st; }
         if ((st = h->alloc(&c.d_out, (size_t)B * H * W * c.cout * 4)) != RST_OK) { delete h; return st; }
         if (c.pool_after)

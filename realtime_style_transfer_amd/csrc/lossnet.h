@@ -18,6 +18,7 @@ struct VggConv {
     float* d_b = nullptr;
     float* d_out = nullptr;  // [B][H][W][cout]
     float* d_pool = nullptr; // [B][H/2][W/2][cout] when pool_after
+    unsigned short* d_w0bf = nullptr;   // block1_conv1, plain-bf16 loss: vgg_conv0_bf16 B image (else null)
 };
 
 const int VGG_CH[13] = {64, 64, 128, 128, 256, 256, 256, 512, 512, 512, 512, 512, 512};
