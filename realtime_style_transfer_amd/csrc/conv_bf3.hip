@@ -362,6 +362,30 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                     if (oy < a.Ho && ox < a.Wo)
                         *reinterpret_cast<float4*>(a.out + (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ngb + c4) = v;
                 }
+                if constexpr (TW == 16 && TH % 2 == 0) {
+                    // fused 2x2 / 2 max pool (VGG16 block ends; maxpool2_kernel's arithmetic): this M tile is two
+                    // whole 16-pixel rows starting at an even row, so its eight windows are in the wave's image
+                    if (a.pool != nullptr) {
+                        const int Hp = a.Ho >> 1, Wp = a.Wo >> 1;
+#pragma unroll
+                        for (int it = 0; it < 2; ++it) {
+                            const int j = 4 * it + (lane >> 4), c4 = 4 * (lane & 15);
+                            const float* e0 = ep + (2 * j) * 64 + c4;
+                            const f32x4 a0 = *reinterpret_cast<const f32x4*>(e0);
+                            const f32x4 a1 = *reinterpret_cast<const f32x4*>(e0 + 64);
+                            const f32x4 a2 = *reinterpret_cast<const f32x4*>(e0 + 16 * 64);
+                            const f32x4 a3 = *reinterpret_cast<const f32x4*>(e0 + 17 * 64);
+                            float4 m;
+                            m.x = fmaxf(fmaxf(a0.x, a1.x), fmaxf(a2.x, a3.x));
+                            m.y = fmaxf(fmaxf(a0.y, a1.y), fmaxf(a2.y, a3.y));
+                            m.z = fmaxf(fmaxf(a0.z, a1.z), fmaxf(a2.z, a3.z));
+                            m.w = fmaxf(fmaxf(a0.w, a1.w), fmaxf(a2.w, a3.w));
+                            const int py = (y0 >> 1) + mt, qx = (x0 >> 1) + j;
+                            if (py < Hp && qx < Wp)
+                                *reinterpret_cast<float4*>(a.pool + (((size_t)b * Hp + py) * Wp + qx) * a.ntot + ngb + c4) = m;
+                        }
+                    }
+                }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -500,6 +524,7 @@ hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st)
     case ID: {                                                                                   \
         using C = Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>;                            \
         if ((a.cin & 3) != 0) return hipErrorInvalidValue;                                       \
+        if (a.pool != nullptr && !conv_bf3_fuses_pool(t, a)) return hipErrorInvalidValue;        \
         if (a.pro_w != nullptr && a.cin > C::MAX_CIN) return hipErrorInvalidValue;               \
         const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x * a.n_blocks);          \
         hipLaunchKernelGGL((conv_bf3_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>), dim3(grid), \
@@ -511,6 +536,25 @@ hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st)
         default:
             return hipErrorInvalidValue;
     }
+}
+
+bool conv_bf3_fuses_pool(const ConvTile& t, const ConvArgs& a) {
+    // the wave-private epilogue (NW == 2 and its LDS images fit) with 16-pixel-wide, even-height tiles
+    bool wave_epi = false;
+    switch (t.id) {
+#define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF)                                                    \
+    case ID: {                                                                                                 \
+        using C = Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>;                                        \
+        wave_epi = C::NW == 2 && C::LDS_BYTES >= (size_t)4 * 32 * 64 * 4 && TW == 16 && TH % 2 == 0 && S == 1; \
+        break;                                                                                                 \
+    }
+        RST_BF3_CONFIGS(X)
+#undef X
+        default:
+            return false;
+    }
+    return wave_epi && a.part == nullptr && !a.shuffle && (a.epi_mode == EPI_RELU_STATS || a.epi_mode == EPI_NONE) &&
+           a.ntot % t.nt == 0 && a.Ho == a.H && a.Wo == a.W;
 }
 
 hipError_t conv_bf3_prepare(const ConvTile& t) {

@@ -150,7 +150,8 @@ struct ConvArgs {
     int pro_mode, epi_mode, shuffle;
     CinAcc stat;            // conv_lite inference: CIN statistics into f64 accumulators instead of part
     CinSrc pro_stat;        // conv_lite inference: the prologue affine formed from the producer's accumulators
-};
+    float* pool;            // conv_bf3 VGG16 epilogue (conv_bf3_fuses_pool): also the 2x2 / 2 max-pooled output
+};                          // [B][Ho/2][Wo/2][ntot] (VALID, as maxpool2_launch), or null
 
 // A compiled tile configuration of conv_mfma_kernel.
 struct ConvTile {
@@ -167,6 +168,9 @@ hipError_t conv_prepare(const ConvTile& t);
 bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long long pixels, ConvTile* out);
 hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st);
 hipError_t conv_bf3_prepare(const ConvTile& t);
+// whether conv_bf3_launch can also write the 2x2 max-pooled output (ConvArgs.pool) for these arguments: the VGG16
+// epilogue (wave-private image of whole pixel rows, 16-pixel-wide tiles, even row/column origins)
+bool conv_bf3_fuses_pool(const ConvTile& t, const ConvArgs& a);
 // VGG16 block1_conv1 (3 -> 64, preprocess fused) on bf16 operands: the plain-bf16 loss (conv_bf3.hip)
 std::vector<unsigned short> vgg_conv0_bf16_pack(const float* wflip);
 hipError_t vgg_conv0_bf16_launch(const float* img, const float2* pre, const unsigned short* wpk, const float* bias,
@@ -190,6 +194,8 @@ struct WinoArgs {
     const float* pro_w;     // with pro_ab1: [B][H][W] per-pixel weight of the second style (style_blend)
     CinAcc stat;            // wino_x6 inference: CIN statistics into f64 accumulators instead of part
     CinSrc pro_stat;        // wino_x6 inference: the prologue affine formed from the producer's accumulators
+    const float* u_next;    // wino_x6: the next layer's weight image, read into each XCD's L2 during the
+    int u_next_bytes;       // epilogue (speed only: its first chunks then hit L2), or null
 };
 bool wino_supported(int kh, int stride, int cin, int cout);
 

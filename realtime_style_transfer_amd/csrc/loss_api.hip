@@ -59,10 +59,15 @@ int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t s
         a.pro_mode = i == 0 ? PRO_AFF : PRO_NONE;
         a.epi_mode = EPI_RELU_STATS;   // part == nullptr: bias + ReLU only
         a.shuffle = 0;
+        // the block-end max pool inside the conv's epilogue where the tile allows it (one pass over the block's
+        // output fewer), else its own launch
+        const bool pool = c.pool_after && i < last;
+        const bool fused = pool && c.tile.bf3 && conv_bf3_fuses_pool(c.tile, a);
+        if (fused) a.pool = c.d_pool;
         RST_HIP_TRY(conv_launch(c.tile, a, st));
         in = c.d_out;
-        if (c.pool_after && i < last) {
-            RST_HIP_TRY(maxpool2_launch(c.d_out, c.d_pool, B, c.H, c.W, c.cout, st));
+        if (pool) {
+            if (!fused) RST_HIP_TRY(maxpool2_launch(c.d_out, c.d_pool, B, c.H, c.W, c.cout, st));
             in = c.d_pool;
         }
     }

@@ -40,6 +40,7 @@ struct LayerExec {
     int tiles_y = 0, tiles_x = 0, n_blocks = 1, nchunks = 1;
     int n_part = 0;
     float* d_w = nullptr;
+    size_t w_bytes = 0;           // bytes of the packed weight image d_w
     float* d_bias = nullptr;
     float2* d_bn = nullptr;
     float* d_out = nullptr;       // raw (CIN) or final (BN) output [max_batch][Ho][Wo][cout]
@@ -94,6 +95,7 @@ struct rst_handle {
     std::vector<hipEvent_t> prof_events;
     int prof_max_steps = 0, prof_step = 0;
     bool prof_on = false;
+    bool no_u_prefetch = false;       // RST_NO_U_PREFETCH=1 at creation: no next-layer U prefetch (A/B runs)
     void prof_free() {
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
         prof_events.clear();

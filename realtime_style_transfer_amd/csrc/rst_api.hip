@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -392,6 +393,10 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     h->shape = *shape;
     h->P = P;
     h->precision = precision;
+    {
+        const char* nup = getenv("RST_NO_U_PREFETCH");
+        h->no_u_prefetch = nup != nullptr && nup[0] == '1';
+    }
     const int B = shape->max_batch;
     const float* wp = weights_host;
     h->layers.resize(specs.size());
@@ -415,6 +420,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
             return st;
         }
         if ((st = h->alloc(&e.d_w, packed.size() * 4, packed.data())) != RST_OK) { delete h; return st; }
+        e.w_bytes = packed.size() * 4;
         if ((st = h->alloc(&e.d_bias, bias_n.size() * 4, bias_n.data())) != RST_OK) { delete h; return st; }
         if (s.norm == N_BN) {
             const float* gamma = wp;
@@ -694,6 +700,11 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         if (src != nullptr && src->acc_off >= 0 && pro_ab != nullptr) {   // the affine from the producer's
             a.pro_stat = cin_src(h, *src, style, B);                            // accumulators (no finalize ran)
             a.pro_ab = a.pro_ab1 = nullptr;
+        }
+        if (e.kind == K_WINOX6 && li + 1 < h->layers.size() && h->layers[li + 1].kind == K_WINOX6 &&
+            h->layers[li + 1].w_bytes < (size_t)0x7FFFFFFF && !h->no_u_prefetch) {
+            a.u_next = h->layers[li + 1].d_w;   // the next residual conv's U into L2 during this one's epilogue
+            a.u_next_bytes = (int)h->layers[li + 1].w_bytes;
         }
         if (ext_ev) wino_x6_set_timing_events(ev[0], ev[1]);
         HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
