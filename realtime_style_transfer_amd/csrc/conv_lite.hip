@@ -565,6 +565,9 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     }
     };
     const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    // the next layer's weights into this XCD's L2, touched as the workgroup starts its last tile(s) so that this
+    // kernel's own stream does not evict them again (speed only)
+    unsigned l2f = 0;
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, NSET - 1>;
     zero_acc();
@@ -581,6 +584,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         if (my_tiles > 1) load_aff(T1, 0, S1{});
         for (int k = 0; k < my_tiles; k += 2) {
             LTL(k, 0);
+            if (k + 2 >= my_tiles) l2f = l2_touch_xcd_slice<256, 2>(a.w_next, a.w_next_bytes);
             if (k > 0) lds_barrier();
             store_step(T0, S0{});
             lds_barrier();
@@ -620,6 +624,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         for (int s = 0; s < n_steps; ++s) {
             const int ch = s % NCH;
             LTL(s, 0);
+            if (s == n_steps - NCH) l2f = l2_touch_xcd_slice<256, 2>(a.w_next, a.w_next_bytes);
             if (s > 0) lds_barrier();        // the previous step's operand reads are done
             store_step(cur, S0{});
             lds_barrier();
@@ -641,6 +646,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         }
     }
     if (to_acc && tid < NC) acc_flush();
+    l2_touch_keep(l2f, a.batch < 0, smem);
 }
 
 // ------------------------------------------------------------------------------------------------

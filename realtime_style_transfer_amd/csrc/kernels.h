@@ -34,6 +34,32 @@ __device__ __forceinline__ int xcd_tile_order(int bid, int n) {
     return x * base + min(x, rem) + k;
 }
 
+// ---- next-layer weights into L2 (inference; speed only) -----------------------------------------------
+// Every workgroup of a launch reads one slice of the next layer's weight image, one dword per 128-B line, all its
+// loads issued at once: the workgroups with the same blockIdx % 8 (one XCD under the round-robin dispatch) cover the
+// whole image, so the next kernel's first weight loads hit its XCD's L2 instead of all missing together. Returns a
+// fold of the loaded words; the caller passes it to l2_touch_keep at its end (keeps the loads, waits for nothing
+// earlier). Measured on the residual convs: cold U cost 6-9 us per launch in the frame.
+template <int NT, int NLD>
+__device__ __forceinline__ unsigned l2_touch_xcd_slice(const void* p, int bytes) {
+    if (p == nullptr || bytes <= 0) return 0u;
+    const int xr = (int)(blockIdx.x & 7), k = (int)(blockIdx.x >> 3);
+    const int nk = ((int)gridDim.x - xr + 7) >> 3;   // workgroups with this XCD residue
+    const int nl = bytes >> 7, per = (nl + nk - 1) / nk;
+    const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+    const int beg = k * per, end = min(beg + per, nl);
+    unsigned f = 0;
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) {
+        const int i = beg + (int)threadIdx.x + j * NT;
+        f ^= __builtin_amdgcn_raw_buffer_load_b32(srd, i < end ? i * 128 : 0x7FFFFFF0, 0, 0);
+    }
+    return f;
+}
+__device__ __forceinline__ void l2_touch_keep(unsigned f, bool never, float* sink) {
+    if (f == 0x9E3779B9u && never) *sink = 0.f;   // never true: only keeps the loads
+}
+
 // ---- CIN statistics through f64 accumulators (inference) ----------------------------------------------
 // The producer of a conditional-instance-normalised layer adds, per workgroup and channel, its
 // {sum, sum of squares} as f64 into one of nslot accumulator copies (no-return f64 atomics, executed at
@@ -151,7 +177,10 @@ struct ConvArgs {
     CinAcc stat;            // conv_lite inference: CIN statistics into f64 accumulators instead of part
     CinSrc pro_stat;        // conv_lite inference: the prologue affine formed from the producer's accumulators
     float* pool;            // conv_bf3 VGG16 epilogue (conv_bf3_fuses_pool): also the 2x2 / 2 max-pooled output
-};                          // [B][Ho/2][Wo/2][ntot] (VALID, as maxpool2_launch), or null
+                            // [B][Ho/2][Wo/2][ntot] (VALID, as maxpool2_launch), or null
+    const void* w_next;     // conv_lite inference: the next layer's weight image into L2 (l2_touch_xcd_slice)
+    int w_next_bytes;
+};
 
 // A compiled tile configuration of conv_mfma_kernel.
 struct ConvTile {
@@ -194,8 +223,8 @@ struct WinoArgs {
     const float* pro_w;     // with pro_ab1: [B][H][W] per-pixel weight of the second style (style_blend)
     CinAcc stat;            // wino_x6 inference: CIN statistics into f64 accumulators instead of part
     CinSrc pro_stat;        // wino_x6 inference: the prologue affine formed from the producer's accumulators
-    const float* u_next;    // wino_x6: the next layer's weight image, read into each XCD's L2 during the
-    int u_next_bytes;       // epilogue (speed only: its first chunks then hit L2), or null
+    const void* u_next;     // wino_x6: the next layer's weight image, read into each XCD's L2 during the
+    int u_next_bytes;       // epilogue (l2_touch_xcd_slice: its first loads then hit L2), or null
 };
 bool wino_supported(int kh, int stride, int cin, int cout);
 
@@ -214,6 +243,8 @@ struct Wino9Args {
     int batch, H, W, cin, tiles_y, tiles_x;
     double* zero;           // wino9_x6 inference: zero [zero_n2] double2 first (the frame's CIN accumulators,
     long zero_n2;           // kernels.h CinAcc, written by later layers only) or null
+    const void* w_next;     // wino9_x6 inference: the next layer's weight image into L2 (l2_touch_xcd_slice)
+    int w_next_bytes;
 };
 bool wino9_supported(int kh, int stride, int cin, int cout);
 

@@ -583,6 +583,15 @@ static CinSrc cin_src(const rst_handle* h, const LayerExec& p, const float* styl
     return c;
 }
 
+// The next layer's packed weights (what l2_touch_xcd_slice reads into L2 during layer li), unless disabled
+static void next_weights(const rst_handle* h, size_t li, const void** p, int* bytes) {
+    if (h->no_u_prefetch || li + 1 >= h->layers.size()) return;
+    const LayerExec& n = h->layers[li + 1];
+    if (n.d_w == nullptr || n.w_bytes >= (size_t)0x7FFFFFFF) return;
+    *p = n.d_w;
+    *bytes = (int)n.w_bytes;
+}
+
 static int launch_layer(rst_handle* h, size_t li, const float* content, const float* style, const float* sw, int B,
                         hipStream_t st) {
     LayerExec& e = h->layers[li];
@@ -668,6 +677,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             a.zero = h->d_acc_all;
             a.zero_n2 = (long)(h->acc_per_image * B / 2);
         }
+        if (e.kind == K_WINO9X6) next_weights(h, li, &a.w_next, &a.w_next_bytes);
         HIP_TRY(e.kind == K_WINO9X6 ? wino9_x6_launch(a, st) : wino9_launch(a, st));
     } else if (e.kind == K_WINO || e.kind == K_WINOX6) {
         WinoArgs a{};
@@ -701,11 +711,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             a.pro_stat = cin_src(h, *src, style, B);                            // accumulators (no finalize ran)
             a.pro_ab = a.pro_ab1 = nullptr;
         }
-        if (e.kind == K_WINOX6 && li + 1 < h->layers.size() && h->layers[li + 1].kind == K_WINOX6 &&
-            h->layers[li + 1].w_bytes < (size_t)0x7FFFFFFF && !h->no_u_prefetch) {
-            a.u_next = h->layers[li + 1].d_w;   // the next residual conv's U into L2 during this one's epilogue
-            a.u_next_bytes = (int)h->layers[li + 1].w_bytes;
-        }
+        if (e.kind == K_WINOX6) next_weights(h, li, &a.u_next, &a.u_next_bytes);   // into L2 during the epilogue
         if (ext_ev) wino_x6_set_timing_events(ev[0], ev[1]);
         HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
     } else {
@@ -750,6 +756,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
                 a.pro_stat = cin_src(h, *src, style, B);
                 a.pro_ab = a.pro_ab1 = nullptr;
             }
+            next_weights(h, li, &a.w_next, &a.w_next_bytes);
             HIP_TRY(conv_lite_launch(e.lite, a, st));   // two styles: its blend prologue (pro_ab1, pro_w)
         } else {
             HIP_TRY(conv_launch(e.tile, a, st));

@@ -245,6 +245,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
     const float2 bn = train ? make_float2(1.f, 0.f) : a.bn_ab[co];
     const int n_tile_img = a.tiles_y * a.tiles_x, n_part = 2 * n_tile_img;
 
+    unsigned l2f = 0;     // the next layer's weights into this XCD's L2, touched during the last unit (speed only)
     int t = blockIdx.x;   // work unit
     if (t < n_units) {
         sfor<0, NPART>([&](auto PART) __attribute__((always_inline)) {
@@ -256,6 +257,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
         w9_it = it;
         W9TL(0);
         const int tn = t + gridDim.x;
+        if (tn >= n_units) l2f = l2_touch_xcd_slice<NTHR, 1>(a.w_next, a.w_next_bytes);   // late: stays in L2
         const int hmask = __builtin_amdgcn_readfirstlane(unit_mask(t));   // M blocks of this unit
         int y0, x0;
         size_t img;
@@ -474,6 +476,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
         lds_barrier();   // M reads done before the next tile's v16 pads / computations
         W9TL(3);
     }
+    l2_touch_keep(l2f, a.batch < 0, smem);
 }
 
 #ifdef W9_PROF

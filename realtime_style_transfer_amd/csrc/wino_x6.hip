@@ -445,25 +445,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 
     XTL(2);
-    // ---- the next layer's U into this XCD's L2 (speed only): the workgroups of XCD blockIdx % 8 each touch one
-    // slice of it, one dword per 128-B line, every load issued at once; the values are folded into a word checked
-    // at the very end, so the epilogue runs while they land
-    unsigned upf = 0;
-    if (a.u_next != nullptr) {
-        const int xr = (int)(blockIdx.x & 7), k = (int)(blockIdx.x >> 3);
-        const int nk = ((int)gridDim.x - xr + 7) >> 3;   // workgroups with this XCD residue
-        const int nl = a.u_next_bytes >> 7, per = (nl + nk - 1) / nk;
-        const __amdgpu_buffer_rsrc_t nsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.u_next), 0,
-                                                                              a.u_next_bytes, 0x00020000);
-        const int beg = k * per, end = min(beg + per, nl);
-        unsigned f[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int i = beg + tid + j * YT;
-            f[j] = __builtin_amdgcn_raw_buffer_load_b32(nsrd, i < end ? i * 128 : 0x7FFFFFF0, 0, 0);
-        }
-        upf = f[0] ^ f[1];
-    }
+    // ---- the next layer's weights into this XCD's L2 (speed only), landing while the epilogue runs
+    const unsigned upf = l2_touch_xcd_slice<YT, 2>(a.u_next, a.u_next_bytes);
     // ---- epilogue: partial output transform per half -> LDS image, then sum + bias + ReLU + store + stats --
     float* const yimg = smem + h * (128 * YSTR);
     {
@@ -561,7 +544,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
     }
     XTL(3);
-    if (upf == 0x9E3779B9u && a.batch < 0) smem[0] = 0.f;   // never true: keeps the prefetch loads
+    l2_touch_keep(upf, a.batch < 0, smem);
 }
 
 bool wino_x6_supported(int kh, int stride, int cin, int cout) {
