@@ -191,6 +191,15 @@ rst_loss_handle* rst_trainer_loss(rst_trainer* t);
 int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const float* style_params,
                                   const float* gt_content, const float* gt_style, int batch, float* prediction,
                                   float* losses, float* grad, float* grad_style_params, void* stream);
+/* Optional, before the step's style-predictor forward (train_network.py:61's model.fit step runs the loss model's
+ * ground truth through VGG16 as part of the same step): start the loss targets of the next
+ * rst_trainer_compute_gradients — the style image's Gram matrices and the content image's block5_conv3 features —
+ * on the trainer's own stream, ordered after the work already in `stream`, so they run beside the predictor
+ * forward. The next compute_gradients must pass the same gt_content, gt_style and batch (else it fails with
+ * RST_ERR_INVALID) and joins them; without this call compute_gradients starts them itself, beside the transfer
+ * network's forward. Bitwise the same results either way. */
+int rst_trainer_compute_targets(rst_trainer* t, const float* gt_content, const float* gt_style, int batch,
+                                void* stream);
 /* RMSprop on the device-resident weights with gradient grad (num_weights), then re-pack them
  * into the kernels' weight images. Keras defaults: lr 1e-3, rho 0.9, epsilon 1e-7. */
 int rst_trainer_apply_gradients(rst_trainer* t, const float* grad, float learning_rate, float rho, float epsilon,

@@ -28,7 +28,8 @@ EXPORTED_SYMBOLS = [
     "rst_profile_begin", "rst_profile_end", "rst_layer_kernel_id",
     "rst_loss_num_weights", "rst_loss_create", "rst_loss_destroy", "rst_loss_forward", "rst_loss_copy_feature",
     "rst_trainer_create", "rst_trainer_create_ex", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
-    "rst_trainer_compute_gradients", "rst_trainer_apply_gradients", "rst_trainer_copy_weights",
+    "rst_trainer_compute_gradients", "rst_trainer_compute_targets", "rst_trainer_apply_gradients",
+    "rst_trainer_copy_weights",
     "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_copy_output_gradient",
     "rst_trainer_debug_vgg_gradient", "rst_trainer_loss", "rst_trainer_num_moving_statistics",
     "rst_trainer_get_moving_statistics", "rst_trainer_set_moving_statistics",
@@ -142,6 +143,8 @@ def load() -> ctypes.CDLL:
     lib.rst_trainer_num_weights.restype = sz
     lib.rst_trainer_compute_gradients.argtypes = [vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp]
     lib.rst_trainer_compute_gradients.restype = i
+    lib.rst_trainer_compute_targets.argtypes = [vp, vp, vp, i, vp]
+    lib.rst_trainer_compute_targets.restype = i
     lib.rst_trainer_apply_gradients.argtypes = [vp, vp, fp, fp, fp, vp]
     lib.rst_trainer_apply_gradients.restype = i
     for name in ("rst_trainer_copy_weights", "rst_trainer_copy_slots", "rst_trainer_set_weights"):

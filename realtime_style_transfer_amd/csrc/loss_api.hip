@@ -74,6 +74,45 @@ int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t s
     return RST_OK;
 }
 
+int loss_targets(rst_loss_handle* h, const float* gt_content, const float* gt_style, int B, hipStream_t st) {
+    // plain-bf16 loss: the Gram matrices on bf16-rounded features as well (mixed_bfloat16 compute dtype)
+    const bool gram_bf16 = h->shape.precision == RST_PRECISION_BF16;
+    int r;
+    // style image: grams of the four style layers
+    if ((r = vgg_run(h, gt_style, B, STYLE_IDX[3], st)) != RST_OK) return r;
+    for (int k = 0; k < 4; ++k) {
+        const VggConv& c = h->convs[STYLE_IDX[k]];
+        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_style[k], h->d_gram_ws, st, gram_bf16));
+    }
+    // ground-truth content: block5_conv3 features
+    if ((r = vgg_run(h, gt_content, B, CONTENT_IDX, st)) != RST_OK) return r;
+    const VggConv& c5 = h->convs[CONTENT_IDX];
+    const size_t f5 = (size_t)c5.H * c5.W * c5.cout;
+    RST_HIP_TRY(hipMemcpyAsync(h->d_content_feat, c5.d_out, (size_t)B * f5 * 4, hipMemcpyDeviceToDevice, st));
+    return RST_OK;
+}
+
+int loss_prediction(rst_loss_handle* h, const float* prediction, int B, float* losses, hipStream_t st) {
+    const bool gram_bf16 = h->shape.precision == RST_PRECISION_BF16;
+    int r;
+    const VggConv& c5 = h->convs[CONTENT_IDX];
+    const size_t f5 = (size_t)c5.H * c5.W * c5.cout;
+    if ((r = vgg_run(h, prediction, B, CONTENT_IDX, st)) != RST_OK) return r;
+    RST_HIP_TRY(sqdiff_loss_launch(c5.d_out, h->d_content_feat, B, (long)f5, h->d_partial,
+                                   0.5 / (double)f5 * h->shape.content_factor, losses, 4, 1, 0, st));
+    for (int k = 0; k < 4; ++k) {
+        const VggConv& c = h->convs[STYLE_IDX[k]];
+        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_pred[k], h->d_gram_ws, st, gram_bf16));
+        const long n = (long)c.cout * c.cout;
+        RST_HIP_TRY(sqdiff_loss_launch(h->d_gram_pred[k], h->d_gram_style[k], B, n, h->d_partial,
+                                       0.5 / (double)n / 4.0 * h->shape.style_factor, losses, 4, 2, k > 0, st));
+    }
+    RST_HIP_TRY(tv_loss_launch(prediction, B, h->shape.h, h->shape.w, 3, h->d_partial, h->shape.tv_factor, losses, 4,
+                               3, st));
+    RST_HIP_TRY(loss_combine_launch(losses, B, st));
+    return RST_OK;
+}
+
 }  // namespace rst
 
 extern "C" {
@@ -182,36 +221,9 @@ int rst_loss_forward(rst_loss_handle* h, const float* prediction, const float* g
     if (batch <= 0 || batch > h->shape.max_batch)
         return set_error(RST_ERR_INVALID, "rst_loss_forward: batch outside [1, max_batch]");
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const int B = batch;
     int r;
-    // plain-bf16 loss: the Gram matrices on bf16-rounded features as well (mixed_bfloat16 compute dtype)
-    const bool gram_bf16 = h->shape.precision == RST_PRECISION_BF16;
-    // style image: grams of the four style layers
-    if ((r = vgg_run(h, gt_style, B, STYLE_IDX[3], st)) != RST_OK) return r;
-    for (int k = 0; k < 4; ++k) {
-        const VggConv& c = h->convs[STYLE_IDX[k]];
-        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_style[k], h->d_gram_ws, st, gram_bf16));
-    }
-    // ground-truth content: block5_conv3 features
-    if ((r = vgg_run(h, gt_content, B, CONTENT_IDX, st)) != RST_OK) return r;
-    const VggConv& c5 = h->convs[CONTENT_IDX];
-    const size_t f5 = (size_t)c5.H * c5.W * c5.cout;
-    RST_HIP_TRY(hipMemcpyAsync(h->d_content_feat, c5.d_out, (size_t)B * f5 * 4, hipMemcpyDeviceToDevice, st));
-    // prediction
-    if ((r = vgg_run(h, prediction, B, CONTENT_IDX, st)) != RST_OK) return r;
-    RST_HIP_TRY(sqdiff_loss_launch(c5.d_out, h->d_content_feat, B, (long)f5, h->d_partial,
-                                   0.5 / (double)f5 * h->shape.content_factor, losses, 4, 1, 0, st));
-    for (int k = 0; k < 4; ++k) {
-        const VggConv& c = h->convs[STYLE_IDX[k]];
-        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_pred[k], h->d_gram_ws, st, gram_bf16));
-        const long n = (long)c.cout * c.cout;
-        RST_HIP_TRY(sqdiff_loss_launch(h->d_gram_pred[k], h->d_gram_style[k], B, n, h->d_partial,
-                                       0.5 / (double)n / 4.0 * h->shape.style_factor, losses, 4, 2, k > 0, st));
-    }
-    RST_HIP_TRY(tv_loss_launch(prediction, B, h->shape.h, h->shape.w, 3, h->d_partial, h->shape.tv_factor, losses, 4,
-                               3, st));
-    RST_HIP_TRY(loss_combine_launch(losses, B, st));
-    return RST_OK;
+    if ((r = loss_targets(h, gt_content, gt_style, batch, st)) != RST_OK) return r;
+    return loss_prediction(h, prediction, batch, losses, st);
 }
 
 int rst_loss_copy_feature(rst_loss_handle* h, int layer, float* dst, size_t count, int batch, void* stream) {

@@ -57,5 +57,10 @@ struct rst_loss_handle {
 namespace rst {
 // Run the VGG16 trunk on B images up to (and including) conv `last`; conv outputs land in convs[i].d_out.
 int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t st);
+// rst_loss_forward in two parts: the ground-truth targets (style-image Grams, content-image block5_conv3
+// features; independent of the prediction) and the prediction's VGG16 pass + the loss terms. Both use the same
+// per-layer VGG16 buffers: the targets must be complete before loss_prediction runs.
+int loss_targets(rst_loss_handle* h, const float* gt_content, const float* gt_style, int B, hipStream_t st);
+int loss_prediction(rst_loss_handle* h, const float* prediction, int B, float* losses, hipStream_t st);
 }  // namespace rst
 

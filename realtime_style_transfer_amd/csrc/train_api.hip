@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -159,7 +160,22 @@ struct rst_trainer {
     float* d_vgg_dbg[13] = {};    // debug: d loss / d (VGG conv i output), when enabled
     int* d_stat_index = nullptr;  // canonical index of every BN moving_mean / moving_variance entry
     size_t n_stat = 0;
+    // the loss targets (style Grams, content features) run on a side stream beside the predictor / transfer
+    // forward: fork after the caller's stream, join before the prediction's VGG16 pass (same VGG16 buffers)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool targets_pending = false;
+    bool serial_targets = false;  // RST_SERIAL_TARGETS=1 at creation: targets on the caller's stream (A/B runs)
+    const float* pend_content = nullptr;
+    const float* pend_style = nullptr;
+    int pend_batch = 0;
     ~rst_trainer() {
+        if (side) {
+            (void)hipStreamSynchronize(side);
+            (void)hipStreamDestroy(side);
+        }
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
         if (loss) rst_loss_destroy(loss);
         for (void* p : allocs) (void)hipFree(p);
     }
@@ -566,6 +582,14 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
             return set_error(RST_ERR_UNSUPPORTED, "rst_trainer_create: odd size at stride-2 layer " + s.name +
                                                       " (its input gradient needs the even-size phase split)");
     rst_trainer* t = new rst_trainer();
+    if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming) != hipSuccess)
+        return fail_delete(t, set_error(RST_ERR_HIP, "rst_trainer_create_ex: stream / event creation failed"));
+    {
+        const char* ser = getenv("RST_SERIAL_TARGETS");
+        t->serial_targets = ser != nullptr && ser[0] == '1';
+    }
     t->shape = *shape;
     t->P = P;
     t->nw = expect;
@@ -819,6 +843,31 @@ int rst_trainer_num_style_params(const rst_trainer* t) { return t ? t->P : -1; }
 rst_loss_handle* rst_trainer_loss(rst_trainer* t) { return t ? t->loss : nullptr; }
 size_t rst_trainer_num_weights(const rst_trainer* t) { return t ? t->nw : 0; }
 
+int rst_trainer_compute_targets(rst_trainer* t, const float* gt_content, const float* gt_style, int batch,
+                                void* stream) {
+    if (!t || !gt_content || !gt_style) return set_error(RST_ERR_INVALID, "rst_trainer_compute_targets: null argument");
+    if (batch <= 0 || batch > t->shape.max_batch)
+        return set_error(RST_ERR_INVALID, "rst_trainer_compute_targets: batch outside [1, max_batch]");
+    if (t->targets_pending) return set_error(RST_ERR_INVALID, "rst_trainer_compute_targets: targets already pending");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipStream_t ts = t->serial_targets ? st : t->side;
+    if (ts != st) {
+        RST_HIP_TRY(hipEventRecord(t->ev_fork, st));
+        RST_HIP_TRY(hipStreamWaitEvent(ts, t->ev_fork, 0));
+    }
+    int r = loss_targets(t->loss, gt_content, gt_style, batch, ts);
+    RST_HIP_TRY(hipEventRecord(t->ev_join, ts));   // recorded even after a failed launch: joins stay balanced
+    if (r != RST_OK) {
+        RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_join, 0));
+        return r;
+    }
+    t->targets_pending = true;
+    t->pend_content = gt_content;
+    t->pend_style = gt_style;
+    t->pend_batch = batch;
+    return RST_OK;
+}
+
 int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const float* style_params,
                                   const float* gt_content, const float* gt_style, int batch, float* prediction,
                                   float* losses, float* grad, float* grad_style_params, void* stream) {
@@ -829,8 +878,16 @@ int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const fl
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int B = batch;
     int r;
+    if (t->targets_pending && (t->pend_content != gt_content || t->pend_style != gt_style || t->pend_batch != B)) {
+        t->targets_pending = false;
+        RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_join, 0));   // the side stream's work is joined either way
+        return set_error(RST_ERR_INVALID, "rst_trainer_compute_gradients: targets started for other inputs");
+    }
+    if (!t->targets_pending && (r = rst_trainer_compute_targets(t, gt_content, gt_style, B, stream)) != RST_OK) return r;
     if ((r = forward(t, content, style_params, B, prediction, st)) != RST_OK) return r;
-    if ((r = rst_loss_forward(t->loss, prediction, gt_content, gt_style, B, losses, stream)) != RST_OK) return r;
+    RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_join, 0));
+    t->targets_pending = false;
+    if ((r = loss_prediction(t->loss, prediction, B, losses, st)) != RST_OK) return r;
     if ((r = vgg_backward(t, prediction, B, t->L.back().d_g, st)) != RST_OK) return r;
     RST_HIP_TRY(hipMemsetAsync(grad, 0, t->nw * 4, st));
     float* gs = grad_style_params ? grad_style_params : t->d_gstyle;

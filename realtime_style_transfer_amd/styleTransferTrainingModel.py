@@ -312,12 +312,35 @@ class StyleTransferTrainingModel:
                 raise ValueError(f"ground truth must be (B,{self.output_shape}), got {tuple(t.shape)}")
         return B, content.contiguous(), sp.contiguous(), gt_content.contiguous(), gt_style.contiguous()
 
+    def compute_targets(self, gt_content: torch.Tensor, gt_style: torch.Tensor):
+        """Start the loss targets of the next ``compute_gradients`` (the style image's Grams and the content image's
+        block5_conv3 features, rst_trainer_compute_targets) on the trainer's side stream, so that they run beside
+        the work queued after this call (the style predictor's forward in ``train_step``). The next
+        ``compute_gradients`` must get these same ground-truth tensors; results are bitwise those without."""
+        self._require_trainer()
+        gs = gt_style[:, 0] if gt_style.dim() == 5 and gt_style.shape[1] == 1 else gt_style
+        B = gt_content.shape[0]
+        for t in (gt_content, gs):
+            if tuple(t.shape) != (B,) + self.output_shape:
+                raise ValueError(f"ground truth must be (B,{self.output_shape}), got {tuple(t.shape)}")
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} exceeds max_batch={self.max_batch}")
+        gc, gs = gt_content.contiguous(), gs.contiguous()
+        _lib.check(_lib.load().rst_trainer_compute_targets(self._handle, _lib.dev_ptr(gc), _lib.dev_ptr(gs), B,
+                                                           _lib.stream_ptr()))
+        self._pending_targets = (gt_content, gt_style, gc, gs)   # keeps the buffers alive until the join
+
     def compute_gradients(self, content: torch.Tensor, style_params: torch.Tensor, gt_content: torch.Tensor,
                           gt_style: torch.Tensor, grad: Optional[torch.Tensor] = None,
                           grad_style_params: Optional[torch.Tensor] = None):
         """Training-mode forward + loss + backward -> (prediction, losses (B,4), grad, grad_style_params)."""
         self._require_trainer()
+        pending = getattr(self, "_pending_targets", None)
+        self._pending_targets = None
+        gt_in = (gt_content, gt_style)
         B, content, sp, gt_content, gt_style = self._check(content, style_params, gt_content, gt_style)
+        if pending is not None and pending[0] is gt_in[0] and pending[1] is gt_in[1]:
+            gt_content, gt_style = pending[2], pending[3]   # the buffers the targets were started on
         dev = content.device
         pred = torch.empty((B,) + self.output_shape, dtype=torch.float32, device=dev)
         losses = torch.empty((B, 4), dtype=torch.float32, device=dev)
@@ -409,6 +432,7 @@ class StyleTransferTrainingModel:
                 if style.shape[1] != 1:
                     raise ValueError("the training model takes one style (num_styles=1, styleTransferTrainingModel.py:46)")
                 style = style[:, 0]
+            self.compute_targets(y['content'], y['style'])            # loss targets beside the predictor forward
             sp = pr.forward(style)                                     # styleTransferInferenceModel.py:23-28
         else:
             sp = x['style_params']

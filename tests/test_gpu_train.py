@@ -216,6 +216,31 @@ def test_training_step_is_deterministic_and_learns(transfer):
     assert last < first, (first, last)
 
 
+def test_loss_targets_beside_the_predictor_are_bitwise_the_same():
+    """rst_trainer_compute_targets (the style Grams and content features started on the trainer's side stream before
+    the step's predictor forward) gives bitwise the losses and gradients of compute_gradients starting them itself;
+    targets started for other ground truth are refused (RST_ERR_INVALID -> ValueError) and the trainer recovers."""
+    _need_gpu()
+    cfg = CONFIGS['A']
+    B = 2
+    plan, w, vgg, content, sp, gtc, gts = _case(cfg, B)
+    tr = _trainer(cfg, w, vgg, B, precision="bf16", transfer="winograd_bf16x6")
+    c, s, gc, gs = _cuda(content, sp, gtc, gts)
+    _, l1, g1, s1 = tr.compute_gradients(c, s, gc, gs)
+    l1, g1, s1 = l1.clone(), g1.clone(), s1.clone()
+    tr.compute_targets(gc, gs)
+    x = torch.randn(1 << 22, device=c.device)   # unrelated work queued on the main stream meanwhile
+    for _ in range(4):
+        x = torch.tanh(x)
+    _, l2, g2, s2 = tr.compute_gradients(c, s, gc, gs)
+    assert torch.equal(l1, l2) and torch.equal(g1, g2) and torch.equal(s1, s2)
+    tr.compute_targets(gc, gs)
+    with pytest.raises(ValueError, match="targets started for other inputs"):
+        tr.compute_gradients(c, s, gc.clone(), gs)                    # other ground truth than the targets'
+    _, l3, g3, _ = tr.compute_gradients(c, s, gc, gs)
+    assert torch.equal(l1, l3) and torch.equal(g1, g3)
+
+
 def test_trainer_rejects_bad_shapes():
     _need_gpu()
     from realtime_style_transfer_amd._lib import RstError
