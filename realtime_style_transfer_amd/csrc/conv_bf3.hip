@@ -267,14 +267,24 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
     }
     __syncthreads();
 
-    for (int s = 0; s < n_stages; ++s) {
+    // PF bit 0: the next Cin chunk's halo prefetched into registers during the chunk's first stage.
+    // PF bit 1: the weights of stage s + 2 loaded during stage s (two register sets, so a stage's load has two
+    // stages of MFMAs to land instead of one); stage s stores stage s + 1's set, loaded during stage s - 1.
+    constexpr bool HPF = (PF & 1) != 0, WP2 = (PF & 2) != 0;
+    Bf3WeightRegs<C::WCOPY> wA, wB;
+    if constexpr (WP2) wA.load(wsrc + (size_t)(n_stages > 1 ? 1 : 0) * C::WSTAGE, tid);
+    auto stage = [&](int s, auto& wcur, auto& wnxt) __attribute__((always_inline)) {
         const int chunk = s / C::NGROUPS;
         const int g = s - chunk * C::NGROUPS;
-        const int s_next = (s + 1 < n_stages) ? s + 1 : s;
         const unsigned short* wts = wts0 + (s & 1) * C::WSTAGE;
-        Bf3WeightRegs<C::WCOPY> wnext;
-        wnext.load(wsrc + (size_t)s_next * C::WSTAGE, tid);
-        if (PF && g == 0 && chunk + 1 < a.nchunks) load_halo(chunk + 1);
+        if constexpr (WP2) {
+            const int s2 = s + 2 < n_stages ? s + 2 : n_stages - 1;
+            wnxt.load(wsrc + (size_t)s2 * C::WSTAGE, tid);
+        } else {
+            const int s_next = (s + 1 < n_stages) ? s + 1 : s;
+            wcur.load(wsrc + (size_t)s_next * C::WSTAGE, tid);
+        }
+        if (HPF && g == 0 && chunk + 1 < a.nchunks) load_halo(chunk + 1);
         {
             constexpr int U = TPS * KS;
             short8 af[2][NP][MW], bf[2][NP][NW];
@@ -319,13 +329,21 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        wnext.store(wts0 + ((s + 1) & 1) * C::WSTAGE, tid);
+        wcur.store(wts0 + ((s + 1) & 1) * C::WSTAGE, tid);
         __syncthreads();
         if (g == C::NGROUPS - 1 && chunk + 1 < a.nchunks) {
-            if (!PF) load_halo(chunk + 1);
+            if (!HPF) load_halo(chunk + 1);
             store_halo(chunk + 1);
             __syncthreads();
         }
+    };
+    if constexpr (WP2) {
+        for (int s = 0; s < n_stages; s += 2) {
+            stage(s, wA, wB);
+            if (s + 1 < n_stages) stage(s + 1, wB, wA);
+        }
+    } else {
+        for (int s = 0; s < n_stages; ++s) stage(s, wA, wA);
     }
 
     // ---------------- epilogue (as conv_mfma_kernel) ------------------------------------------
@@ -481,6 +499,7 @@ static ConvTile bf3_tile_of() {
     X(113, 3, 3, 1, 32, 64, 8, 16, 2, 2, 1, 3, 0)        \
     X(134, 3, 3, 1, 32, 64, 8, 16, 4, 1, 3, 1, 0)        \
     X(135, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 0)       \
+    X(136, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 2)       \
     X(140, 1, 1, 1, 32, 64, 8, 16, 4, 1, 1, 1, 0)        \
     X(141, 1, 1, 1, 32, 128, 8, 16, 2, 2, 1, 1, 0)
 
@@ -500,7 +519,12 @@ bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long lon
     // register prefetch (config 135, 2 x 2 waves) beats 134 wherever it still gives >= ~900 workgroups
     // (b2c2 239 -> 227 us, b3c2 189 -> 182, b4c2 187 -> 170) and 132 everywhere; 134 keeps block 1 (Cout 64)
     // and block 5 (225 workgroups at 128 wide: 58 vs 66 us). Prefetching the weights two stages ahead (two
-    // register sets) cost a wave per SIMD of occupancy and was 25-70 % slower on every layer.
+    // register sets, PF bit 1) costs the 64-wide tile a wave per SIMD of occupancy (25-70 % slower), but the
+    // 128-wide tile is held to two workgroups per CU by its LDS anyway (200 -> 240 VGPRs, no occupancy lost):
+    // config 136 = 135 + two-stage weights, standalone b2c1 134 -> 129 us, b2c2 216 -> 197, b3c2 176 -> 164,
+    // b4c2 167 -> 162 (profiles/r03/conv_bench_vgg_z.log; with the halo prefetch as well, PF 3, 40-60 % slower) —
+    // but the same within noise in the training step (three alternating same-box pairs 25.30 vs 25.12 ms,
+    // profiles/r03/vgg_wp2_ab.log), so 135 stays selected.
     int want;
     if (kh == 1) want = ntot % 128 == 0 ? 141 : 140;
     else if (planes == 2) want = 102;

@@ -110,6 +110,9 @@ static int run_vgg(int B) {
         }
         VV(32, 64, 8, 16, 4, 1, 3, 0, "134 NT64 8x16 WM4 TPS3 (prod)")
         VV(32, 128, 8, 16, 2, 2, 3, 0, "135 NT128 8x16 WM2 TPS3 (prod)")
+        VV(32, 128, 8, 16, 2, 2, 3, 2, "136 = 135 + 2-stage weight prefetch")
+        VV(32, 128, 8, 16, 2, 2, 3, 3, "135 + 2-stage wts + halo PF")
+        VV(32, 64, 8, 16, 4, 1, 3, 2, "134 + 2-stage weight prefetch")
 #undef VV
         const int nv = (int)launches.size();
         std::vector<std::vector<float>> t(nv);
