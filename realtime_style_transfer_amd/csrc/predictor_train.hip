@@ -113,43 +113,65 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return (lane_d(v, 0) + lane_d(v, 16)) + (lane_d(v, 32) + lane_d(v, 48));
 }
 
-// one block (64 threads) per channel: Chan merge over all tiles of all images
-__global__ __launch_bounds__(64) void bn_finalize_kernel(const float4* __restrict__ part, int n_tiles, int B, int HW,
-                                                         int C, int ppw, float* __restrict__ gamma_beta_mm_mv,
-                                                         float eps, float momentum, float2* __restrict__ ab,
-                                                         float2* __restrict__ mr) {
-    const int c = blockIdx.x, t = threadIdx.x, cg = C >> 2, q = c >> 2, l = c & 3;
+// One workgroup (256 threads) per channel quad: Chan merge over all tiles of all images. Every partial float4
+// carries the quad's four channels, so each is read once for all four (the one-channel-per-workgroup form read
+// every 16-B partial four times, one lane per scattered line: 17.6 us per call on the training step's BN layers).
+// Per channel: f64 sums in a fixed order (lane-strided loop, DPP wave sums, the four wave sums added in order).
+__device__ __forceinline__ double block4_sum_d(double v, double* red, int t) {
+    v = wave_sum_d(v);
+    __syncthreads();
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float4* __restrict__ part, int n_tiles, int B, int HW,
+                                                          int C, int ppw, float* __restrict__ gamma_beta_mm_mv,
+                                                          float eps, float momentum, float2* __restrict__ ab,
+                                                          float2* __restrict__ mr) {
+    __shared__ double red[4];
+    const int q = blockIdx.x, t = threadIdx.x, cg = C >> 2;
     const int total = B * n_tiles;
-    double s = 0.0;
-    for (int i = t; i < total; i += 64) {
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = t; i < total; i += 256) {
         const float4 v = part[(size_t)i * cg * 2 + 2 * q];
-        s += (double)(l == 0 ? v.x : l == 1 ? v.y : l == 2 ? v.z : v.w);
+        s[0] += (double)v.x;
+        s[1] += (double)v.y;
+        s[2] += (double)v.z;
+        s[3] += (double)v.w;
     }
-    s = wave_sum_d(s);
     const double N = (double)B * HW;
-    const double mean = s / N;
-    double m2 = 0.0;
-    for (int i = t; i < total; i += 64) {
+    double mean[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) mean[l] = block4_sum_d(s[l], red, t) / N;
+    double m2[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = t; i < total; i += 256) {
         const int tile = i % n_tiles;
         const double n = (double)max(min(ppw, HW - tile * ppw), 0);
         if (n <= 0.0) continue;
         const float4 sv = part[(size_t)i * cg * 2 + 2 * q];
         const float4 mv = part[(size_t)i * cg * 2 + 2 * q + 1];
-        const double ts = (double)(l == 0 ? sv.x : l == 1 ? sv.y : l == 2 ? sv.z : sv.w);
-        const double tm = (double)(l == 0 ? mv.x : l == 1 ? mv.y : l == 2 ? mv.z : mv.w);
-        const double d = ts / n - mean;
-        m2 += tm + n * d * d;
+        const double ts[4] = {(double)sv.x, (double)sv.y, (double)sv.z, (double)sv.w};
+        const double tm[4] = {(double)mv.x, (double)mv.y, (double)mv.z, (double)mv.w};
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const double d = ts[l] / n - mean[l];
+            m2[l] += tm[l] + n * d * d;
+        }
     }
-    m2 = wave_sum_d(m2);
-    if (t == 0) {
-        const double var = m2 / N;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) m2[l] = block4_sum_d(m2[l], red, t);
+    if (t < 4) {
+        const int c = 4 * q + t;
+        const double mn = t == 0 ? mean[0] : t == 1 ? mean[1] : t == 2 ? mean[2] : mean[3];
+        const double mm = t == 0 ? m2[0] : t == 1 ? m2[1] : t == 2 ? m2[2] : m2[3];
+        const double var = mm / N;
         const double rstd = 1.0 / sqrt(var + (double)eps);
         float* gb = gamma_beta_mm_mv;
         const double a = (double)gb[c] * rstd;
-        ab[c] = make_float2((float)a, (float)((double)gb[C + c] - mean * a));
-        mr[c] = make_float2((float)mean, (float)rstd);
-        const double unbiased = N > 1.0 ? m2 / (N - 1.0) : var;
-        gb[2 * C + c] = (float)((double)gb[2 * C + c] * momentum + mean * (1.0 - momentum));
+        ab[c] = make_float2((float)a, (float)((double)gb[C + c] - mn * a));
+        mr[c] = make_float2((float)mn, (float)rstd);
+        const double unbiased = N > 1.0 ? mm / (N - 1.0) : var;
+        gb[2 * C + c] = (float)((double)gb[2 * C + c] * momentum + mn * (1.0 - momentum));
         gb[3 * C + c] = (float)((double)gb[3 * C + c] * momentum + unbiased * (1.0 - momentum));
     }
 }
@@ -710,10 +732,11 @@ hipError_t bn_forward_launch(const float* z, int B, int HW, int C, float* gamma_
                              float* y_part, hipStream_t st) {
     int block, slots, ppw, nt;
     elem_geometry(C, HW, &block, &slots, &ppw, &nt);
+    if (C % 4 != 0) return hipErrorInvalidValue;   // channel quads (bn_stats / bn_finalize)
     bn_stats_kernel<<<dim3(nt, B), block, 0, st>>>(z, HW, C, ppw, slots, part);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    bn_finalize_kernel<<<C, 64, 0, st>>>(part, nt, B, HW, C, ppw, gamma_beta_mm_mv, eps, momentum, ab, mr);
+    bn_finalize_kernel<<<C / 4, 256, 0, st>>>(part, nt, B, HW, C, ppw, gamma_beta_mm_mv, eps, momentum, ab, mr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bn_apply_kernel<<<dim3(nt, B), block, 0, st>>>(z, ab, res, y, HW, C, ppw, slots, act, y_part);
     return hipGetLastError();
