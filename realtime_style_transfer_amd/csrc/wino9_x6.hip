@@ -99,7 +99,8 @@ __device__ __forceinline__ void split8(const float (&v)[8], short8 (&A)[3]) {
 }  // namespace
 
 // Experiment knobs (tools/wino9_x6_bench only; never set in the library build): W9_SKIP bit0 = no U loads
-// in the loop, bit1 = no transform (patch reads), bit2 = no MFMAs, bit3 = no split
+// in the loop, bit1 = no transform (patch reads), bit2 = no MFMAs, bit3 = no split, bit4 = no global loads of the
+// next tile's patch (the LDS stores stay)
 #ifndef W9_SKIP
 #define W9_SKIP 0
 #endif
@@ -194,7 +195,8 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
             constexpr int r = hf * NH + decltype(K)::value;
             const int gy = min(max(y0 - 4 + r, 0), H - 1);
             const int soff = __builtin_amdgcn_readfirstlane((int)((img + (size_t)gy * W) * Cin * 4));
-            pf[decltype(K)::value] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(insrd, voff, soff, 0));
+            if constexpr (W9_SKIP & 16) pf[decltype(K)::value] = (float)(soff + voff);
+            else pf[decltype(K)::value] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(insrd, voff, soff, 0));
         });
     };
     auto store_half = [&](int t, float* pbuf, auto HALF) __attribute__((always_inline)) {   // zero outside
