@@ -97,6 +97,40 @@ def test_full_size_matches_torch_oracle():
     assert mism < 1e-3
 
 
+def test_l2_weight_prefetch_is_numerically_neutral():
+    """The next-layer weight touches (kernels.h l2_touch_xcd_slice; RST_NO_U_PREFETCH=1 turns them off at handle
+    creation) only move lines into L2: the full-size frame is the same with and without them (bitwise up to the
+    arrival order of the f64 CIN accumulator adds, which can flip an f32 rounding of an affine very rarely)."""
+    _need_gpu()
+    import os
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    cfg = ShapeConfig.from_spec("rst-960-120-128-17")
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    ws = init_weights(plan, seed=2)
+    rng = np.random.default_rng(11)
+    x = torch.from_numpy(rng.random((1,) + ins).astype(np.float32)).cuda()
+    sp = torch.from_numpy(np.ascontiguousarray(synthetic_style_params(1, 1, plan.num_style_params, plan, seed=4))).cuda()
+    ys = []
+    for off in ("1", None):
+        old = os.environ.pop("RST_NO_U_PREFETCH", None)
+        if off:
+            os.environ["RST_NO_U_PREFETCH"] = off
+        try:
+            m, _ = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                               weights=ws, max_batch=1)
+        finally:
+            os.environ.pop("RST_NO_U_PREFETCH", None)
+            if old is not None:
+                os.environ["RST_NO_U_PREFETCH"] = old
+        ys.append(m({'content': x, 'style_params': sp}).cpu().numpy())
+        del m
+    assert np.isfinite(ys[0]).all()
+    assert np.abs(ys[0] - ys[1]).max() <= 1e-6, np.abs(ys[0] - ys[1]).max()
+
+
 def test_full_size_repeated_calls_mixed_batch():
     """Full size, one handle: B=2, then B=1 on other content, then B=2 again all match the oracle and
     the repeated call is bitwise equal (no state — CIN partials, affines, workspaces — carries over
