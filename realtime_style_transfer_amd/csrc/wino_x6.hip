@@ -91,7 +91,8 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 }  // namespace
 
 // Experiment knobs (tools/wino_x6_bench only; never set in the library build): X6_SKIP bit0 = no U reloads
-// in the loop, bit1 = no transform of the next chunk, bit2 = no staging / patch loads in the loop.
+// in the loop, bit1 = no transform of the next chunk, bit2 = no staging / patch loads in the loop, bit3 = no
+// barrier at the end of a chunk (results wrong: timing only).
 #ifndef X6_SKIP
 #define X6_SKIP 0
 #endif
@@ -441,7 +442,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 __builtin_amdgcn_sched_barrier(0);
             });
         });
-        lds_barrier();
+        if constexpr (!(X6_SKIP & 8)) lds_barrier();
     }
 
     XTL(2);
