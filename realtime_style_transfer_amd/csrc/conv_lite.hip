@@ -442,6 +442,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         if (acc_b >= 0) cin_acc_add(a.stat, a.batch, NC, acc_b, tid, (int)blockIdx.x % a.stat.nslot, accS, accQ);
         accS = accQ = 0.0;
     };
+    const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
     auto epilogue = [&](const Tile& T) __attribute__((always_inline)) {
         if constexpr (MODE == 0) {   // bias + ReLU -> BatchNorm (inference affine) -> ReLU, NHWC store
             const acc_t y = (acc[0] + acc[1]) + acc[2];
@@ -453,7 +454,13 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 const int ox = T.x0 + M::row(j, lane);
                 float v = fmaxf(y[j] + bias, 0.f);
                 v = fmaxf(fmaf(bn.x, v, bn.y), 0.f);
-                if (full || (oy < a.Ho && ox < a.Wo)) orow[(size_t)ox * NC] = v;
+                if (full || (oy < a.Ho && ox < a.Wo)) {
+                    if (a.wt_stores)   // write-through (sc1): no dirty lines left for the end-of-kernel write-back
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), osrd,
+                                                              (int)((orow + (size_t)ox * NC - a.out) * 4), 0, 16);
+                    else
+                        orow[(size_t)ox * NC] = v;
+                }
             }
         } else {   // bias, pixel-shuffle store, per-tile CIN statistics over the four phases
             acc[0] = acc[0] + acc[4];
@@ -472,7 +479,12 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         const float v = acc[ph][j] + bias;
                         acc[ph][j] = v;
 #if (LITE_SKIP & 8) == 0
-                        orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
+                        if (a.wt_stores)
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                __builtin_bit_cast(unsigned, v), osrd,
+                                (int)((orow + ((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC - a.out) * 4), 0, 16);
+                        else
+                            orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
 #endif
                         s += v;
                     }

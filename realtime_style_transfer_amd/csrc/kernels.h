@@ -180,6 +180,7 @@ struct ConvArgs {
                             // [B][Ho/2][Wo/2][ntot] (VALID, as maxpool2_launch), or null
     const void* w_next;     // conv_lite inference: the next layer's weight image into L2 (l2_touch_xcd_slice)
     int w_next_bytes;
+    int wt_stores;          // nonzero: output stored write-through (sc1), as WinoArgs::wt_stores
 };
 
 // A compiled tile configuration of conv_mfma_kernel.
@@ -225,6 +226,8 @@ struct WinoArgs {
     CinSrc pro_stat;        // wino_x6 inference: the prologue affine formed from the producer's accumulators
     const void* u_next;     // wino_x6: the next layer's weight image, read into each XCD's L2 during the
     int u_next_bytes;       // epilogue (l2_touch_xcd_slice: its first loads then hit L2), or null
+    int wt_stores;          // wino_x6: bit0 output, bit1 materialised input stored write-through (sc1): no dirty
+                            // lines left in L2 for the end-of-kernel write-back
 };
 bool wino_supported(int kh, int stride, int cin, int cout);
 
@@ -245,6 +248,7 @@ struct Wino9Args {
     long zero_n2;           // kernels.h CinAcc, written by later layers only) or null
     const void* w_next;     // wino9_x6 inference: the next layer's weight image into L2 (l2_touch_xcd_slice)
     int w_next_bytes;
+    int wt_stores;          // nonzero: output stored write-through (sc1), as WinoArgs::wt_stores
 };
 bool wino9_supported(int kh, int stride, int cin, int cout);
 

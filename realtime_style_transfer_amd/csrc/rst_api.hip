@@ -396,6 +396,8 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
     {
         const char* nup = getenv("RST_NO_U_PREFETCH");
         h->no_u_prefetch = nup != nullptr && nup[0] == '1';
+        const char* wts = getenv("RST_WT_STORES");
+        h->wt_stores = wts != nullptr ? atoi(wts) : 13;   // default: every output but the materialised input
     }
     const int B = shape->max_batch;
     const float* wp = weights_host;
@@ -592,6 +594,13 @@ static void next_weights(const rst_handle* h, size_t li, const void** p, int* by
     *bytes = (int)n.w_bytes;
 }
 
+// Write-through store bits of layer e (RST_WT_STORES & mask), when its output (and a wino_x6 materialised input of
+// the same or fewer bytes) is addressable by the kernels' 32-bit buffer offsets
+static int wt_bits(const rst_handle* h, const LayerExec& e, int B, int mask) {
+    const size_t bytes = (size_t)B * e.s.Ho * e.s.Wo * (e.s.cout > e.s.cin ? e.s.cout : e.s.cin) * 4;
+    return bytes < (size_t)0x7FFFFFF0 ? (h->wt_stores & mask) : 0;
+}
+
 static int launch_layer(rst_handle* h, size_t li, const float* content, const float* style, const float* sw, int B,
                         hipStream_t st) {
     LayerExec& e = h->layers[li];
@@ -678,6 +687,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             a.zero_n2 = (long)(h->acc_per_image * B / 2);
         }
         if (e.kind == K_WINO9X6) next_weights(h, li, &a.w_next, &a.w_next_bytes);
+        a.wt_stores = wt_bits(h, e, B, 4);
         HIP_TRY(e.kind == K_WINO9X6 ? wino9_x6_launch(a, st) : wino9_launch(a, st));
     } else if (e.kind == K_WINO || e.kind == K_WINOX6) {
         WinoArgs a{};
@@ -712,6 +722,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             a.pro_ab = a.pro_ab1 = nullptr;
         }
         if (e.kind == K_WINOX6) next_weights(h, li, &a.u_next, &a.u_next_bytes);   // into L2 during the epilogue
+        a.wt_stores = wt_bits(h, e, B, 3);
         if (ext_ev) wino_x6_set_timing_events(ev[0], ev[1]);
         HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
     } else {
@@ -757,6 +768,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
                 a.pro_ab = a.pro_ab1 = nullptr;
             }
             next_weights(h, li, &a.w_next, &a.w_next_bytes);
+            a.wt_stores = wt_bits(h, e, B, 8);
             HIP_TRY(conv_lite_launch(e.lite, a, st));   // two styles: its blend prologue (pro_ab1, pro_w)
         } else {
             HIP_TRY(conv_launch(e.tile, a, st));

@@ -392,6 +392,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
         W9TL(2);
 
         // ---- epilogue, one M block at a time: M -> LDS [xi][tile][co], output transform, store -------
+        const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
         sfor<0, 2>([&](auto Hh) __attribute__((always_inline)) {
             constexpr int h = decltype(Hh)::value;
             if (!(hmask & (1 << h))) return;   // uniform over the workgroup (barriers inside)
@@ -430,8 +431,14 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
                     vals[4 * k + q] = inside ? v : 0.f;
                     vs += vals[4 * k + q];
                     vn += inside ? 1.f : 0.f;
-                    if (inside)   // inference: BN (folded moving statistics) -> ReLU; training: the raw ReLU output
-                        a.out[(img + (size_t)oy * W + ox) * NT + co] = train ? v : fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                    if (inside) {   // inference: BN (folded moving statistics) -> ReLU; training: the raw ReLU output
+                        const float o = train ? v : fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                        const size_t oi = (img + (size_t)oy * W + ox) * NT + co;
+                        if (a.wt_stores)   // write-through (sc1): no dirty lines left for the end-of-kernel write-back
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), osrd, (int)(oi * 4), 0, 16);
+                        else
+                            a.out[oi] = o;
+                    }
                 }
             }
             if constexpr (train) {

@@ -241,9 +241,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
                 v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
             }
-            if (a.mat != nullptr)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd,
-                                                       sg_moff[k] + chunk * XCK * 4, 0, 0);
+            if (a.mat != nullptr) {
+                if (a.wt_stores & 2)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd,
+                                                           sg_moff[k] + chunk * XCK * 4, 0, 16);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd,
+                                                           sg_moff[k] + chunk * XCK * 4, 0, 0);
+            }
         }
         return v;
     };
@@ -473,6 +478,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // thread = (pixel column pr, channel quad cq); rows 0..7 of the tile
     const int cq = tid & 31, pr = tid >> 5;
     const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + 4 * cq);
+    const __amdgpu_buffer_rsrc_t osrd =
+        __builtin_amdgcn_make_buffer_rsrc(a.out, 0, (int)((size_t)a.batch * H * W * XN * 4), 0x00020000);
     const bool col_ok = x0 + pr < W;
     f32x4 yv[XTH];
     f32x4 s4 = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -487,7 +494,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             v.w = fmaxf(v.w, 0.f);
         }
         const bool ok = col_ok && y0 + i < H;
-        if (ok) *reinterpret_cast<f32x4*>(a.out + (img + (size_t)(y0 + i) * W + x0 + pr) * XN + 4 * cq) = v;
+        if (ok) {
+            float* const po = a.out + (img + (size_t)(y0 + i) * W + x0 + pr) * XN + 4 * cq;
+            if (a.wt_stores & 1)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), osrd,
+                                                       (int)((po - a.out) * 4), 0, 16);
+            else
+                *reinterpret_cast<f32x4*>(po) = v;
+        }
         yv[i] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         s4 += yv[i];
     }
