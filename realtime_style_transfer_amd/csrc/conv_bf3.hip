@@ -30,6 +30,7 @@ namespace rst {
 namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef short short8 __attribute__((ext_vector_type(8)));
 typedef unsigned short ushort4v __attribute__((ext_vector_type(4)));
 
@@ -359,6 +360,8 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
             const int ngb = nb * NT + wn * 64;
             const float bs0 = a.bias[ngb + li], bs1 = a.bias[ngb + 32 + li];
             const bool relu = epi == EPI_RELU_STATS;
+            const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
+            const __amdgpu_buffer_rsrc_t psrd = __builtin_amdgcn_make_buffer_rsrc(a.pool, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
             for (int m = 0; m < MW; ++m) {
                 const int mt = wm * MW + m;
@@ -377,8 +380,14 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                     const int px = 4 * it + (lane >> 4), c4 = 4 * (lane & 15), p = mt * 32 + px;
                     const int oy = y0 + p / TW, ox = x0 + p % TW;
                     const float4 v = *reinterpret_cast<const float4*>(ep + px * 64 + c4);
-                    if (oy < a.Ho && ox < a.Wo)
-                        *reinterpret_cast<float4*>(a.out + (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ngb + c4) = v;
+                    if (oy < a.Ho && ox < a.Wo) {
+                        float* const po = a.out + (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ngb + c4;
+                        if (a.wt_stores)   // write-through (sc1): no dirty lines left for the end-of-kernel write-back
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), osrd,
+                                                                   (int)((po - a.out) * 4), 0, 16);
+                        else
+                            *reinterpret_cast<float4*>(po) = v;
+                    }
                 }
                 if constexpr (TW == 16 && TH % 2 == 0) {
                     // fused 2x2 / 2 max pool (VGG16 block ends; maxpool2_kernel's arithmetic): this M tile is two
@@ -399,8 +408,14 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                             m.z = fmaxf(fmaxf(a0.z, a1.z), fmaxf(a2.z, a3.z));
                             m.w = fmaxf(fmaxf(a0.w, a1.w), fmaxf(a2.w, a3.w));
                             const int py = (y0 >> 1) + mt, qx = (x0 >> 1) + j;
-                            if (py < Hp && qx < Wp)
-                                *reinterpret_cast<float4*>(a.pool + (((size_t)b * Hp + py) * Wp + qx) * a.ntot + ngb + c4) = m;
+                            if (py < Hp && qx < Wp) {
+                                float* const pp = a.pool + (((size_t)b * Hp + py) * Wp + qx) * a.ntot + ngb + c4;
+                                if (a.wt_stores)
+                                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, m), psrd,
+                                                                           (int)((pp - a.pool) * 4), 0, 16);
+                                else
+                                    *reinterpret_cast<float4*>(pp) = m;
+                            }
                         }
                     }
                 }

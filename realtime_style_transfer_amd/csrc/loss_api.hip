@@ -15,6 +15,7 @@
 // Every conv runs on conv_mfma_kernel (f32 MFMA) or, in a bf16 precision mode, conv_bf3 (block1_conv1 in the
 // plain-bf16 mode: vgg_conv0_bf16); Gram matrices on gram.hip; reductions on loss.hip.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <cmath>
 #include <string>
@@ -64,6 +65,8 @@ int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t s
         const bool pool = c.pool_after && i < last;
         const bool fused = pool && c.tile.bf3 && conv_bf3_fuses_pool(c.tile, a);
         if (fused) a.pool = c.d_pool;
+        // write-through output stores (sc1, the VGG epilogue of conv_bf3) where the offsets fit 32 bits
+        a.wt_stores = h->wt_stores && c.tile.bf3 && (size_t)B * c.H * c.W * c.cout * 4 < (size_t)0x7FFFFFF0 ? 1 : 0;
         RST_HIP_TRY(conv_launch(c.tile, a, st));
         in = c.d_out;
         if (pool) {
@@ -141,6 +144,10 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
         return set_error(RST_ERR_INVALID, "rst_loss_create: expected " + std::to_string(rst_loss_num_weights()) +
                                               " VGG16 weights, got " + std::to_string(num_weights));
     rst_loss_handle* h = new rst_loss_handle();
+    {
+        const char* wt = getenv("RST_LOSS_WT");
+        h->wt_stores = wt != nullptr && wt[0] == '1' ? 1 : 0;
+    }
     h->shape = *shape;
     h->host_w.assign(vgg_weights_host, vgg_weights_host + num_weights);
     const int B = shape->max_batch;

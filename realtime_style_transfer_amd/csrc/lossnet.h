@@ -40,6 +40,7 @@ struct rst_loss_handle {
     void* d_gram_ws = nullptr;
     float* d_partial = nullptr;
     size_t gram_ws_bytes = 0;
+    int wt_stores = 0;                    // RST_LOSS_WT at creation: VGG conv outputs stored write-through (sc1)
     std::vector<float> host_w;            // VGG16 weights as given (Keras order), for the backward packing
     ~rst_loss_handle() {
         for (void* p : allocs) (void)hipFree(p);
