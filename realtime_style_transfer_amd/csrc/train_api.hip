@@ -166,7 +166,8 @@ struct rst_trainer {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool targets_pending = false;
     bool serial_targets = false;  // RST_SERIAL_TARGETS=1 at creation: targets on the caller's stream (A/B runs)
-    int wt_stores = 1;            // RST_TRAIN_WT=0 at creation: Winograd conv outputs stored plainly (default sc1)
+    int wt_stores = 1;            // RST_TRAIN_WT at creation: bit0 Winograd conv outputs, bit1 the residual convs'
+                                  // materialised inputs stored write-through (sc1); default 1
     const float* pend_content = nullptr;
     const float* pend_style = nullptr;
     int pend_batch = 0;
@@ -231,7 +232,9 @@ int repack(rst_trainer* t, hipStream_t st) {
 }
 
 // Write-through output stores (RST_TRAIN_WT=1) where the outputs' byte offsets fit the kernels' 32-bit buffer offsets
-static int train_wt(const rst_trainer* t, size_t elems) { return t->wt_stores && elems * 4 < (size_t)0x7FFFFFF0 ? 1 : 0; }
+static int train_wt(const rst_trainer* t, size_t elems, int mask = 1) {
+    return elems * 4 < (size_t)0x7FFFFFF0 ? (t->wt_stores & mask) : 0;
+}
 
 // ---- forward (training mode) ------------------------------------------------------------------
 int forward(rst_trainer* t, const float* content, const float* style, int B, float* prediction, hipStream_t st) {
@@ -290,7 +293,7 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.tiles_x = e.tiles_x;
             a.pro_mode = e.pro;
             a.linear = e.s.conv_relu ? 0 : 1;
-            a.wt_stores = train_wt(t, (size_t)B * e.s.H * e.s.W * 128);   // the output only
+            a.wt_stores = train_wt(t, (size_t)B * e.s.H * e.s.W * 128, 3);   // bit 1 (RST_TRAIN_WT=3): also mat
             RST_HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
         } else {
             ConvArgs a = conv_geometry(e, B);
@@ -597,7 +600,7 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
         const char* ser = getenv("RST_SERIAL_TARGETS");
         t->serial_targets = ser != nullptr && ser[0] == '1';
         const char* twt = getenv("RST_TRAIN_WT");
-        t->wt_stores = twt != nullptr && twt[0] == '0' ? 0 : 1;   // default on (measured -1.4 % per step)
+        t->wt_stores = twt != nullptr ? atoi(twt) : 1;   // default 1: outputs (measured -1.4 % per step)
     }
     t->shape = *shape;
     t->P = P;
