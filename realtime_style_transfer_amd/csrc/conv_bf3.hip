@@ -427,6 +427,7 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
         }
     }
     const int n_mtiles = a.tiles_y * a.tiles_x * C::MT;
+    const __amdgpu_buffer_rsrc_t gsrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
     for (int n = 0; n < NW; ++n) {
         const int ng = nb * NT + (wn * NW + n) * 32 + li;
@@ -468,7 +469,10 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                         oi = (((size_t)b * (2 * a.Ho) + 2 * oy + py) * (2 * a.Wo) + 2 * ox + px) * a.cout + co;
                     else
                         oi = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ng;
-                    a.out[oi] = v;
+                    if (a.wt_stores)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), gsrd, (int)(oi * 4), 0, 16);
+                    else
+                        a.out[oi] = v;
                     s += v;
                     cnt += 1.f;
                 }

@@ -400,6 +400,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     // ---------------- epilogue ---------------------------------------------------------------
     const int epi = a.epi_mode;
     const int n_mtiles = a.tiles_y * a.tiles_x * C::MT;
+    const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
     for (int n = 0; n < NW; ++n) {
         const int ng = nb * NT + (wn * NW + n) * 32 + li;
@@ -441,7 +442,10 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                         oi = (((size_t)b * (2 * a.Ho) + 2 * oy + py) * (2 * a.Wo) + 2 * ox + px) * a.cout + co;
                     else
                         oi = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ng;
-                    a.out[oi] = v;
+                    if (a.wt_stores)   // write-through (sc1): no dirty lines left for the end-of-kernel write-back
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), osrd, (int)(oi * 4), 0, 16);
+                    else
+                        a.out[oi] = v;
                     s += v;
                     cnt += 1.f;
                 }

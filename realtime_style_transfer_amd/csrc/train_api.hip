@@ -166,8 +166,9 @@ struct rst_trainer {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool targets_pending = false;
     bool serial_targets = false;  // RST_SERIAL_TARGETS=1 at creation: targets on the caller's stream (A/B runs)
-    int wt_stores = 1;            // RST_TRAIN_WT at creation: bit0 Winograd conv outputs, bit1 the residual convs'
-                                  // materialised inputs stored write-through (sc1); default 1
+    int wt_stores = 5;            // RST_TRAIN_WT at creation: bit0 Winograd conv outputs, bit1 the residual convs'
+                                  // materialised inputs, bit2 the other transfer convs' outputs (forward and input
+                                  // gradient), bit3 the VGG16 input gradients, stored write-through (sc1); default 5
     const float* pend_content = nullptr;
     const float* pend_style = nullptr;
     int pend_batch = 0;
@@ -307,6 +308,7 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.part = e.d_part;
             a.pro_mode = e.pro;
             a.epi_mode = e.s.conv_relu ? EPI_RELU_STATS : EPI_STATS;
+            a.wt_stores = train_wt(t, (size_t)B * e.s.Ho * e.s.Wo * e.s.cout, 4);
             RST_HIP_TRY(conv_launch(e.tile, a, st));
         }
         FinalizeArgs f{};
@@ -407,6 +409,7 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
         a.nchunks = vb.nchunks;
         a.pro_mode = PRO_MASK;
         a.epi_mode = EPI_NONE;
+        a.wt_stores = train_wt(t, (size_t)B * c.H * c.W * c.cin, 8);
         RST_HIP_TRY(conv_launch(vb.tile, a, st));
         if (i == 0) break;
         const int p = i - 1;
@@ -536,6 +539,7 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
             a.out = target;
             a.pro_mode = PRO_NONE;
             a.epi_mode = EPI_NONE;
+            a.wt_stores = train_wt(t, (size_t)B * T.dg.s.Ho * T.dg.s.Wo * T.dg.s.cout, 4);
             RST_HIP_TRY(conv_launch(T.dg.tile, a, st));
         }
         if (open_block) {
@@ -600,7 +604,7 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
         const char* ser = getenv("RST_SERIAL_TARGETS");
         t->serial_targets = ser != nullptr && ser[0] == '1';
         const char* twt = getenv("RST_TRAIN_WT");
-        t->wt_stores = twt != nullptr ? atoi(twt) : 1;   // default 1: outputs (measured -1.4 % per step)
+        t->wt_stores = twt != nullptr ? atoi(twt) : 5;   // default: the transfer convs' outputs (-1.4 %, -0.4 % per step)
     }
     t->shape = *shape;
     t->P = P;
