@@ -197,9 +197,14 @@ int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const fl
  * on the trainer's own stream, ordered after the work already in `stream`, so they run beside the predictor
  * forward. The next compute_gradients must pass the same gt_content, gt_style and batch (else it fails with
  * RST_ERR_INVALID) and joins them; without this call compute_gradients starts them itself, beside the transfer
- * network's forward. Bitwise the same results either way. */
+ * network's forward. Bitwise the same results either way. Targets still pending from a step that never reached
+ * compute_gradients are joined into `stream` and replaced; compute_gradients joins them on every path, its own
+ * failures included. */
 int rst_trainer_compute_targets(rst_trainer* t, const float* gt_content, const float* gt_style, int batch,
                                 void* stream);
+/* Drop pending targets (the caller's step failed between compute_targets and compute_gradients): joins the side
+ * stream into `stream`. No-op when none are pending. */
+int rst_trainer_cancel_targets(rst_trainer* t, void* stream);
 /* RMSprop on the device-resident weights with gradient grad (num_weights), then re-pack them
  * into the kernels' weight images. Keras defaults: lr 1e-3, rho 0.9, epsilon 1e-7. */
 int rst_trainer_apply_gradients(rst_trainer* t, const float* grad, float learning_rate, float rho, float epsilon,
@@ -208,6 +213,9 @@ int rst_trainer_apply_gradients(rst_trainer* t, const float* grad, float learnin
 int rst_trainer_copy_weights(rst_trainer* t, float* dst, size_t count, void* stream);
 int rst_trainer_copy_slots(rst_trainer* t, float* dst, size_t count, void* stream);
 int rst_trainer_set_weights(rst_trainer* t, const float* src, size_t count, void* stream);
+/* Restore the RMSprop `rms` slots (a checkpoint's .OPTIMIZER_SLOT values, Checkpoint.restore,
+ * save_using_checkpoint.py:65-66 / train_network.py:112-113). */
+int rst_trainer_set_slots(rst_trainer* t, const float* src, size_t count, void* stream);
 /* Data parallel: the BatchNormalization moving statistics (every BN layer's moving_mean then
  * moving_variance, get_weights() order), which each rank updates from its own batch. get copies them
  * into dst (e.g. the tail of the gradient bucket, so ONE all-reduce carries both); set writes
@@ -277,6 +285,7 @@ int rst_predictor_trainer_apply_gradients(rst_predictor_trainer* t, const float*
 int rst_predictor_trainer_copy_weights(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
 int rst_predictor_trainer_set_weights(rst_predictor_trainer* t, const float* src, size_t count, void* stream);
 int rst_predictor_trainer_copy_slots(rst_predictor_trainer* t, float* dst, size_t count, void* stream);
+int rst_predictor_trainer_set_slots(rst_predictor_trainer* t, const float* src, size_t count, void* stream);
 /* As rst_trainer_*_moving_statistics for the predictor's BatchNormalization layers (MobileNetV3Small). */
 size_t rst_predictor_trainer_num_moving_statistics(const rst_predictor_trainer* t);
 int rst_predictor_trainer_get_moving_statistics(rst_predictor_trainer* t, float* dst, size_t count, void* stream);

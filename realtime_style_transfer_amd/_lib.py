@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = [
     "rst_trainer_create", "rst_trainer_create_ex", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
     "rst_trainer_compute_gradients", "rst_trainer_compute_targets", "rst_trainer_apply_gradients",
     "rst_trainer_copy_weights",
-    "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_copy_output_gradient",
+    "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_set_slots", "rst_trainer_cancel_targets",
+    "rst_trainer_copy_output_gradient",
     "rst_trainer_debug_vgg_gradient", "rst_trainer_loss", "rst_trainer_num_moving_statistics",
     "rst_trainer_get_moving_statistics", "rst_trainer_set_moving_statistics",
     "rst_predictor_num_weights", "rst_predictor_create", "rst_predictor_destroy", "rst_predictor_forward",
@@ -38,7 +39,7 @@ EXPORTED_SYMBOLS = [
     "rst_predictor_trainer_create", "rst_predictor_trainer_destroy", "rst_predictor_trainer_num_weights",
     "rst_predictor_trainer_forward", "rst_predictor_trainer_backward", "rst_predictor_trainer_apply_gradients",
     "rst_predictor_trainer_copy_weights", "rst_predictor_trainer_set_weights", "rst_predictor_trainer_copy_slots",
-    "rst_predictor_trainer_num_moving_statistics", "rst_predictor_trainer_get_moving_statistics",
+    "rst_predictor_trainer_set_slots", "rst_predictor_trainer_num_moving_statistics", "rst_predictor_trainer_get_moving_statistics",
     "rst_predictor_trainer_set_moving_statistics",
     "rst_gbuffer_resized_size", "rst_gbuffer_preprocess", "rst_crc32c_extend",
 ]
@@ -73,6 +74,28 @@ class RstError(RuntimeError):
 _lib = None
 
 
+class _MissingSymbol:
+    def __init__(self, name):
+        self.name = name
+
+    def __call__(self, *args):
+        raise RuntimeError(f"{self.name} is not exported by the library RST_LIB names")
+
+
+class _OlderLib:
+    """An explicitly selected librst (RST_LIB, same-box A/B runs of an older build) may lack newer entry points."""
+
+    def __init__(self, lib):
+        self._lib = lib
+        self._missing = {}
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._lib, name)
+        except AttributeError:
+            return self._missing.setdefault(name, _MissingSymbol(name))
+
+
 def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
@@ -82,6 +105,8 @@ def load() -> ctypes.CDLL:
         raise RuntimeError(f"librst.so not found at {path}: build it with "
                            f"`python -m realtime_style_transfer_amd.build` (there is no CPU fallback)")
     lib = ctypes.CDLL(path)
+    if "RST_LIB" in os.environ:
+        lib = _OlderLib(lib)        # A/B against an older build: entry points it lacks raise when called
     vp, i, sz, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_float
     lib.rst_create.argtypes = [ctypes.POINTER(RstShape), vp, sz, ctypes.POINTER(vp)]
     lib.rst_create.restype = i
@@ -147,7 +172,10 @@ def load() -> ctypes.CDLL:
     lib.rst_trainer_compute_targets.restype = i
     lib.rst_trainer_apply_gradients.argtypes = [vp, vp, fp, fp, fp, vp]
     lib.rst_trainer_apply_gradients.restype = i
-    for name in ("rst_trainer_copy_weights", "rst_trainer_copy_slots", "rst_trainer_set_weights"):
+    lib.rst_trainer_cancel_targets.argtypes = [vp, vp]
+    lib.rst_trainer_cancel_targets.restype = i
+    for name in ("rst_trainer_copy_weights", "rst_trainer_copy_slots", "rst_trainer_set_weights",
+                 "rst_trainer_set_slots"):
         getattr(lib, name).argtypes = [vp, vp, sz, vp]
         getattr(lib, name).restype = i
     lib.rst_trainer_copy_output_gradient.argtypes = [vp, i, vp, sz, i, vp]
@@ -190,7 +218,7 @@ def load() -> ctypes.CDLL:
     lib.rst_predictor_trainer_apply_gradients.argtypes = [vp, vp, fp, fp, fp, vp]
     lib.rst_predictor_trainer_apply_gradients.restype = i
     for name in ("rst_predictor_trainer_copy_weights", "rst_predictor_trainer_set_weights",
-                 "rst_predictor_trainer_copy_slots"):
+                 "rst_predictor_trainer_copy_slots", "rst_predictor_trainer_set_slots"):
         getattr(lib, name).argtypes = [vp, vp, sz, vp]
         getattr(lib, name).restype = i
     lib.rst_gbuffer_resized_size.argtypes = [i, i, i, i, ctypes.POINTER(ctypes.c_int)]

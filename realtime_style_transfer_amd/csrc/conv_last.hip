@@ -148,13 +148,13 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
     // value split into three bf16 pieces and written to the ring in the MFMA operand layout ----------------
     const int q = tid & 3;
     f32x4 pa01 = {1.f, 0.f, 1.f, 0.f}, pa23 = {1.f, 0.f, 1.f, 0.f}, pb01 = pa01, pb23 = pa23;
-    // the prologue affine (given, or formed from the producer's f64 accumulators), after the first rows' loads
+    // the prologue affine (given, or formed from the producer's fixed-point accumulators), after the first rows' loads
     // are issued so its latency overlaps theirs
     auto load_affine = [&]() __attribute__((always_inline)) {
     if constexpr (PRO != PRO_NONE) {
         const float2* ab = a.pro_ab + (size_t)b * CIN;
         const float2* ab1 = BLEND ? a.pro_ab1 + (size_t)b * CIN : nullptr;
-        if (a.pro_stat.acc != nullptr) {   // formed from the producer's f64 accumulators (no finalize ran)
+        if (a.pro_stat.acc != nullptr) {   // formed from the producer's fixed-point accumulators (no finalize ran)
             float2* const ltab = reinterpret_cast<float2*>(red + 128);   // [2][16]
             const CinSrc& ps = a.pro_stat;
             const bool store = rb == 0 && sx == 0;   // one workgroup per image keeps the host-visible copy
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
     float* const pw = pbuf + wave * (28 * PCOL);
     const int n = lane & 31;
     const int n_tiles4 = (H + 3) / 4;
-    // the output CIN's statistics into f64 accumulators (a.stat): lanes tid < 3 sum this workgroup's tiles
+    // the output CIN's statistics into fixed-point accumulators (a.stat): lanes tid < 3 sum this workgroup's tiles
     // ({S, M2 + S^2/n}, finalize_kernel's merge quantity) and add them once at the end
     const bool to_acc = a.stat.acc != nullptr;
     double accS = 0.0, accQ = 0.0;

@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     const int n = M::col(lane);
     const float bias = a.bias[n];
     const float2 bn = MODE == 0 ? a.bn_ab[n] : float2{1.f, 0.f};
-    // CIN statistics into f64 accumulators (a.stat): this workgroup's tiles summed per image in the lanes
+    // CIN statistics into fixed-point accumulators (a.stat): this workgroup's tiles summed per image in the lanes
     // tid < NC ({S, M2 + S^2/n} per tile, finalize_kernel's merge quantity), added at an image change / the end
     const bool to_acc = a.stat.acc != nullptr;
     double accS = 0.0, accQ = 0.0;

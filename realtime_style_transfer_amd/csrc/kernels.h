@@ -60,20 +60,28 @@ __device__ __forceinline__ void l2_touch_keep(unsigned f, bool never, float* sin
     if (f == 0x9E3779B9u && never) *sink = 0.f;   // never true: only keeps the loads
 }
 
-// ---- CIN statistics through f64 accumulators (inference) ----------------------------------------------
+// ---- CIN statistics through fixed-point accumulators (inference) ---------------------------------------
 // The producer of a conditional-instance-normalised layer adds, per workgroup and channel, its
-// {sum, sum of squares} as f64 into one of nslot accumulator copies (no-return f64 atomics, executed at
-// the memory side; the copies bound the adders per address); the consumer's workgroups merge the copies and
-// form the affine themselves (cin_affine: the finalize_kernel arithmetic), so no finalize kernel runs
+// {sum, sum of squares} (f64, formed in a fixed order) into one of nslot accumulator copies (no-return atomics,
+// executed at the memory side; the copies bound the adders per address); the consumer's workgroups merge the
+// copies and form the affine themselves (cin_affine: the finalize_kernel arithmetic), so no finalize kernel runs
 // between the two. Per workgroup the sum of squares is M2 + S^2/n of its two-pass tile statistics — the
-// quantity finalize_kernel merges — so the affine equals the finalize path's up to f64 summation order.
+// quantity finalize_kernel merges.
+// The adds are exact integer adds, so the merged sums do not depend on the order the atomics land in: each f64
+// addend is cut (magnitude truncated at 2^-48, sign applied to every limb) into CIN_LIMBS signed 64-bit limbs of
+// weights 2^-48, 2^-8 and 2^32 (payloads 40, 40 and up to 52 bits; |addend| < 2^84), added limb by limb; the
+// consumer sums the limbs as integers, carries, and converts once. Bitwise-deterministic CIN statistics
+// (SURVEY §7), at least as accurate as the f64 sums (the merge itself is exact; the truncation is below 2^-48
+// absolute per workgroup, i.e. far below the 1e-5 epsilon the variance is used with).
 constexpr int CIN_ACC_MAX_SLOTS = 64;
+constexpr int CIN_LIMBS = 3;
+typedef long long cin_word;
 struct CinAcc {              // producer side (null acc: the per-tile partials path)
-    double* acc;             // [nslot][B][2][C]: sums, then sums of squares; zeroed before the producer runs
+    cin_word* acc;           // [nslot][B][2][CIN_LIMBS][C]: sums, then sums of squares; zeroed before the producer
     int nslot;
 };
 struct CinSrc {              // consumer side: the producer's accumulators and its CIN parameters
-    const double* acc;       // [nslot][B][2][C] (null: the prologue reads pro_ab as before)
+    const cin_word* acc;     // [nslot][B][2][CIN_LIMBS][C] (null: the prologue reads pro_ab as before)
     int nslot, C, batch;
     double n;                // values per (image, channel): the producer's Ho * Wo
     const float* style;      // style parameters: image b's scale at style[b*style_stride + style_offset + c],
@@ -85,11 +93,64 @@ struct CinSrc {              // consumer side: the producer's accumulators and i
     float2* ab1_out;
 };
 
+// v -> limbs (l0, l1, l2) with v ~= l2 * 2^32 + l1 * 2^-8 + l0 * 2^-48 (every step exact on |v|: the remainders
+// are v's own low bits; bits below 2^-48 dropped)
+__device__ __forceinline__ void cin_fixed_split(double v, cin_word& l0, cin_word& l1, cin_word& l2) {
+    const double a = fabs(v);
+    const double h = floor(a * 0x1p-32);
+    const double r = a - h * 0x1p32;          // [0, 2^32)
+    const double m = floor(r * 0x1p8);
+    const double r2 = r - m * 0x1p-8;         // [0, 2^-8)
+    const cin_word k0 = (cin_word)floor(r2 * 0x1p48), k1 = (cin_word)m, k2 = (cin_word)h;
+    const bool neg = v < 0.0;
+    l0 = neg ? -k0 : k0;
+    l1 = neg ? -k1 : k1;
+    l2 = neg ? -k2 : k2;
+}
+
+// summed limbs -> the value: the magnitude's limbs are carried into canonical form (lower limbs in [0, 2^40)) and
+// converted as a sum of non-negative terms (no cancellation), then the sign is applied; deterministic
+__device__ __forceinline__ double cin_fixed_value(cin_word l0, cin_word l1, cin_word l2) {
+    auto carry = [](cin_word& a0, cin_word& a1, cin_word& a2) __attribute__((always_inline)) {
+        cin_word c = a0 >> 40;
+        a0 -= c << 40;
+        a1 += c;
+        c = a1 >> 40;
+        a1 -= c << 40;
+        a2 += c;
+    };
+    cin_word m0 = l0, m1 = l1, m2 = l2;
+    carry(m0, m1, m2);
+    const bool neg = m2 < 0;                  // the value is l2 * 2^32 + [0, 2^32)
+    if (neg) {
+        m0 = -l0;
+        m1 = -l1;
+        m2 = -l2;
+        carry(m0, m1, m2);
+    }
+    const double v = (double)m2 * 0x1p32 + ((double)m1 * 0x1p-8 + (double)m0 * 0x1p-48);
+    return neg ? -v : v;
+}
+
+__device__ __forceinline__ void cin_word_add(cin_word* p, cin_word v) {
+    if (v != 0) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one value (which = 0: sum, 1: sum of squares) of image b, channel c into copy `slot`
+__device__ __forceinline__ void cin_acc_add_value(const CinAcc& a, int batch, int C, int b, int c, int slot,
+                                                  int which, double v) {
+    cin_word* const p = a.acc + ((size_t)((slot * batch + b) * 2 + which) * CIN_LIMBS) * C + c;
+    cin_word l0, l1, l2;
+    cin_fixed_split(v, l0, l1, l2);
+    cin_word_add(p, l0);
+    cin_word_add(p + C, l1);
+    cin_word_add(p + 2 * C, l2);
+}
+
 __device__ __forceinline__ void cin_acc_add(const CinAcc& a, int batch, int C, int b, int c, int slot, double S,
                                             double Q) {
-    double* const p = a.acc + ((size_t)(slot * batch + b) * 2) * C + c;
-    unsafeAtomicAdd(p, S);
-    unsafeAtomicAdd(p + C, Q);
+    cin_acc_add_value(a, batch, C, b, c, slot, 0, S);
+    cin_acc_add_value(a, batch, C, b, c, slot, 1, Q);
 }
 
 // Every thread of an NT-thread workgroup calls this: the affine of images b0 .. b0 + nb - 1, channels [0, C)
@@ -102,7 +163,7 @@ __device__ __forceinline__ void cin_acc_add(const CinAcc& a, int batch, int C, i
 template <int NT>
 __device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb, float2* tab, float2* tab1,
                                                  float2* out, float2* out1) {
-    constexpr int RMAX = 8;   // copies per lane
+    constexpr int RMAX = 4;   // copies per lane (each 2 x CIN_LIMBS words)
     int K = 1;
     while (K < s.nslot) K <<= 1;
     const int items = nb * s.C;
@@ -123,21 +184,22 @@ __device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb
                 be1 = sp[s.style1_offset + s.C + c];
             }
         }
-        double S = 0.0, Q = 0.0;
+        cin_word w[2 * CIN_LIMBS] = {};
 #pragma unroll
         for (int r = 0; r < RMAX; ++r) {
             const int k = l + L * r;
             if (r < R && i < n && k < s.nslot) {
-                const double* const p = s.acc + ((size_t)(k * s.batch + b) * 2) * s.C + c;
-                S += p[0];
-                Q += p[s.C];
+                const cin_word* const p = s.acc + ((size_t)(k * s.batch + b) * 2 * CIN_LIMBS) * s.C + c;
+#pragma unroll
+                for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += p[q * s.C];
             }
         }
         for (int o = 1; o < L; o <<= 1) {
-            S += __shfl_xor(S, o);
-            Q += __shfl_xor(Q, o);
+#pragma unroll
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += __shfl_xor(w[q], o);
         }
         if (head) {
+            const double S = cin_fixed_value(w[0], w[1], w[2]), Q = cin_fixed_value(w[3], w[4], w[5]);
             const double N = s.n, mean = S / N, var = fmax(Q - S * mean, 0.0) / N;
             const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
             const float aa = g0 * rstd;
@@ -244,7 +306,7 @@ struct Wino9Args {
                             // n_part = tiles_y*tiles_x (wino9.hip), 2*tiles_y*tiles_x (wino9_x6.hip:
                             // one entry per 16 x 8 M block)
     int batch, H, W, cin, tiles_y, tiles_x;
-    double* zero;           // wino9_x6 inference: zero [zero_n2] double2 first (the frame's CIN accumulators,
+    cin_word* zero;         // wino9_x6 inference: zero [zero_n2] 16-B words first (the frame's CIN accumulators,
     long zero_n2;           // kernels.h CinAcc, written by later layers only) or null
     const void* w_next;     // wino9_x6 inference: the next layer's weight image into L2 (l2_touch_xcd_slice)
     int w_next_bytes;

@@ -49,7 +49,7 @@ struct LayerExec {
     float2* d_ab1 = nullptr;      // second style's CIN affine (num_styles == 2)
     int out_mip = -1;             // style-weight mip level at this layer's output width (num_styles == 2)
     float* d_mat = nullptr;       // block input materialised by this layer's prologue (or null)
-    long acc_off = -1;            // CIN statistics as f64 accumulators [nslot][batch][2][cout] (kernels.h
+    long acc_off = -1;            // CIN statistics as fixed-point accumulators [nslot][batch][2][limb][cout] (kernels.h
     int nslot = 0;                // CinAcc) at d_acc_all + acc_off * batch, when producer and consumer both
                                   // take them (else d_part and a finalize kernel)
     // prologue (how this layer reads its input)
@@ -87,8 +87,8 @@ struct rst_handle {
     std::vector<float*> d_mip;
     std::vector<int> mip_h, mip_w;
     float* d_xlast = nullptr;     // blended input of the last (VALU) layer
-    double* d_acc_all = nullptr;  // every layer's accumulators for max_batch (a forward of B images uses the
-    size_t acc_per_image = 0;     // first acc_per_image * B doubles, zeroed at its start)
+    rst::cin_word* d_acc_all = nullptr;  // every layer's accumulators for max_batch (a forward of B images uses the
+    size_t acc_per_image = 0;       // first acc_per_image * B words, zeroed at its start)
     const float* last_style_weights = nullptr;   // for the debug copies of the most recent forward
     std::vector<void*> allocs;
     // optional per-layer timing: 3 events per layer per step (before conv, after conv, after finalize)

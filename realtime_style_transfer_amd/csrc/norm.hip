@@ -164,7 +164,7 @@ __global__ __launch_bounds__(NT) void finalize_kernel(FinalizeArgs a) {
 }
 
 // The network output (styleTransfer.py:269-276, 329): sigmoid(CIN(x)) of the last layer's 3 channels, with that
-// CIN's finalize fused in front (num_styles = 1): the last layer added its statistics into f64 accumulators
+// CIN's finalize fused in front (num_styles = 1): the last layer added its statistics into fixed-point accumulators
 // (kernels.h CinAcc), so every workgroup (g, b) forms image b's three affines itself (cin_affine_table), then applies
 // affine + sigmoid to its slice of the image as float4s (hw * 3 is a multiple of 4 here). Workgroup (0, b) also
 // stores the affine (rst_copy_activation reads it). No finalize kernel and no separate activation pass.

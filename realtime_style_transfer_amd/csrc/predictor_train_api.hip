@@ -398,4 +398,10 @@ int rst_predictor_trainer_copy_slots(rst_predictor_trainer* t, float* dst, size_
     return RST_OK;
 }
 
+int rst_predictor_trainer_set_slots(rst_predictor_trainer* t, const float* src, size_t count, void* stream) {
+    if (!t || !src || count != t->plan.total) return set_error(RST_ERR_INVALID, "rst_predictor_trainer_set_slots");
+    RST_HIP_TRY(hipMemcpyAsync(t->d_ms, src, count * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return RST_OK;
+}
+
 }  // extern "C"

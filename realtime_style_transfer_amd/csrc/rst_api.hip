@@ -469,7 +469,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         }
         if (e.s.res_block >= 1 && e.s.res_conv == 0) block_input = e.d_mat;
     }
-    // CIN statistics through f64 accumulators (kernels.h CinAcc / CinSrc) where the producer adds them and
+    // CIN statistics through fixed-point accumulators (kernels.h CinAcc / CinSrc) where the producer adds them and
     // the consumer forms its affine from them: no finalize kernel between the two. The copies keep the
     // adders per address near 16-28: a residual conv has 225 workgroups at B = 1 (8 copies), the persistent
     // transposed convs up to a few per CU (32), the last layer ~900 (64).
@@ -488,11 +488,11 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
             if (!consumer_ok) continue;
             e.nslot = e.kind == K_WINOX6 ? 8 : (e.kind == K_LITE ? 32 : 64);
             e.acc_off = (long)n_acc;                   // per image: the layer's block scales with the batch
-            n_acc += (size_t)e.nslot * 2 * e.s.cout;
+            n_acc += (size_t)e.nslot * 2 * CIN_LIMBS * e.s.cout;
         }
         if (n_acc > 0) {
             h->acc_per_image = n_acc;
-            if ((st = h->alloc(&h->d_acc_all, n_acc * B * sizeof(double))) != RST_OK) { delete h; return st; }
+            if ((st = h->alloc(&h->d_acc_all, n_acc * B * sizeof(cin_word))) != RST_OK) { delete h; return st; }
         }
     }
     // two styles: the style-weight mip chain (AvgPool2 keyed by width, num_expand_blocks + 1 levels)
@@ -558,12 +558,12 @@ static const float* mip_ptr(const rst_handle* h, int level, const float* style_w
     return level == 0 ? style_weights : h->d_mip[level];
 }
 
-// num_styles = 1 with last_x6: the last CIN's statistics go to f64 accumulators and the output kernel forms the
+// num_styles = 1 with last_x6: the last CIN's statistics go to fixed-point accumulators and the output kernel forms the
 // affine itself (fin_sigmoid3_launch): no finalize, no separate activation pass
 static bool output_finalize_fused(const rst_handle* h) { return h->layers.back().acc_off >= 0; }
 
 // layer e's accumulators for a forward of B images (null: e uses partials + finalize)
-static double* acc_ptr(const rst_handle* h, const LayerExec& e, int B) {
+static cin_word* acc_ptr(const rst_handle* h, const LayerExec& e, int B) {
     return e.acc_off >= 0 ? h->d_acc_all + (size_t)e.acc_off * B : nullptr;
 }
 
@@ -635,7 +635,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.cin = e.s.cin;
         a.tiles_y = e.tiles_y;
         a.tiles_x = e.tiles_x;
-        if (e.acc_off >= 0) {   // the output CIN's statistics -> f64 accumulators (fin_sigmoid3 reads them)
+        if (e.acc_off >= 0) {   // the output CIN's statistics -> fixed-point accumulators (fin_sigmoid3 reads them)
             a.part = nullptr;
             a.stat.acc = acc_ptr(h, e, B);
             a.stat.nslot = e.nslot;
@@ -712,7 +712,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             a.pro_ab1 = src->d_ab1;
             a.pro_w = mip_ptr(h, src->out_mip, sw);
         }
-        if (e.acc_off >= 0) {   // this layer's statistics -> f64 accumulators (its consumer forms the affine)
+        if (e.acc_off >= 0) {   // this layer's statistics -> fixed-point accumulators (its consumer forms the affine)
             a.part = nullptr;
             a.stat.acc = acc_ptr(h, e, B);
             a.stat.nslot = e.nslot;
@@ -758,7 +758,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.epi_mode = e.s.norm == N_BN ? EPI_RELU_BN : (e.s.conv_relu ? EPI_RELU_STATS : EPI_STATS);
         a.shuffle = e.kind == K_CONVT2 ? 1 : 0;
         if (e.kind == K_LITE) {
-            if (e.acc_off >= 0) {   // this layer's statistics -> f64 accumulators (its consumer forms the affine)
+            if (e.acc_off >= 0) {   // this layer's statistics -> fixed-point accumulators (its consumer forms the affine)
                 a.part = nullptr;
                 a.stat.acc = acc_ptr(h, e, B);
                 a.stat.nslot = e.nslot;
@@ -818,7 +818,7 @@ int rst_forward(rst_handle* h, const float* content, const float* style_params, 
     hipStream_t st = static_cast<hipStream_t>(stream);
     // the CIN accumulators start at zero: cleared by the first layer's kernel when that is wino9_x6
     if (h->d_acc_all != nullptr && h->layers[0].kind != K_WINO9X6)
-        HIP_TRY(hipMemsetAsync(h->d_acc_all, 0, h->acc_per_image * batch * sizeof(double), st));
+        HIP_TRY(hipMemsetAsync(h->d_acc_all, 0, h->acc_per_image * batch * sizeof(cin_word), st));
     for (size_t k = 1; k < h->d_mip.size(); ++k)
         HIP_TRY(avgpool2_1ch_launch(mip_ptr(h, (int)k - 1, style_weights), h->d_mip[k], batch, h->mip_h[k - 1],
                                     h->mip_w[k - 1], st));

@@ -864,8 +864,14 @@ int rst_trainer_compute_targets(rst_trainer* t, const float* gt_content, const f
     if (!t || !gt_content || !gt_style) return set_error(RST_ERR_INVALID, "rst_trainer_compute_targets: null argument");
     if (batch <= 0 || batch > t->shape.max_batch)
         return set_error(RST_ERR_INVALID, "rst_trainer_compute_targets: batch outside [1, max_batch]");
-    if (t->targets_pending) return set_error(RST_ERR_INVALID, "rst_trainer_compute_targets: targets already pending");
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (t->targets_pending) {
+        // targets of a step that never reached compute_gradients (its caller failed in between): join the side
+        // stream's work into the caller's stream and start over (the new targets overwrite the same buffers
+        // after that join)
+        t->targets_pending = false;
+        RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_join, 0));
+    }
     hipStream_t ts = t->serial_targets ? st : t->side;
     if (ts != st) {
         RST_HIP_TRY(hipEventRecord(t->ev_fork, st));
@@ -900,9 +906,10 @@ int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const fl
         return set_error(RST_ERR_INVALID, "rst_trainer_compute_gradients: targets started for other inputs");
     }
     if (!t->targets_pending && (r = rst_trainer_compute_targets(t, gt_content, gt_style, B, stream)) != RST_OK) return r;
-    if ((r = forward(t, content, style_params, B, prediction, st)) != RST_OK) return r;
+    r = forward(t, content, style_params, B, prediction, st);
+    t->targets_pending = false;                            // joined on every path, failed forward included
     RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_join, 0));
-    t->targets_pending = false;
+    if (r != RST_OK) return r;
     if ((r = loss_prediction(t->loss, prediction, B, losses, st)) != RST_OK) return r;
     if ((r = vgg_backward(t, prediction, B, t->L.back().d_g, st)) != RST_OK) return r;
     RST_HIP_TRY(hipMemsetAsync(grad, 0, t->nw * 4, st));
@@ -928,6 +935,21 @@ int rst_trainer_copy_weights(rst_trainer* t, float* dst, size_t count, void* str
 int rst_trainer_copy_slots(rst_trainer* t, float* dst, size_t count, void* stream) {
     if (!t || !dst || count != t->nw) return set_error(RST_ERR_INVALID, "rst_trainer_copy_slots: bad argument");
     RST_HIP_TRY(hipMemcpyAsync(dst, t->d_ms, count * 4, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    return RST_OK;
+}
+
+int rst_trainer_set_slots(rst_trainer* t, const float* src, size_t count, void* stream) {
+    if (!t || !src || count != t->nw) return set_error(RST_ERR_INVALID, "rst_trainer_set_slots: bad argument");
+    RST_HIP_TRY(hipMemcpyAsync(t->d_ms, src, count * 4, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    return RST_OK;
+}
+
+int rst_trainer_cancel_targets(rst_trainer* t, void* stream) {
+    if (!t) return set_error(RST_ERR_INVALID, "rst_trainer_cancel_targets: null handle");
+    if (t->targets_pending) {
+        t->targets_pending = false;
+        RST_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), t->ev_join, 0));
+    }
     return RST_OK;
 }
 

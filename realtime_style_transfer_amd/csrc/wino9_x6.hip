@@ -124,7 +124,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar U offsets, no waterfall)
     if (a.zero != nullptr)   // the frame's CIN accumulators (no separate memset launch; no layer before this one)
         for (long i = (long)blockIdx.x * NTHR + tid; i < a.zero_n2; i += (long)gridDim.x * NTHR)
-            reinterpret_cast<double2*>(a.zero)[i] = make_double2(0.0, 0.0);
+            reinterpret_cast<uint4*>(a.zero)[i] = make_uint4(0u, 0u, 0u, 0u);
     const int li = lane & 31, lh = lane >> 5;
     const int p = wave & 3, qh = wave >> 2;   // point row p, points q = 2qh, 2qh + 1
     int w9_it = 0;

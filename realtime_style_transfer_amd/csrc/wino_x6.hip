@@ -173,7 +173,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* res_src = pro == PRO_AFF_RES ? a.res : a.in;
     const int nchunks = Cin / XCK;
 
-    // the prologue affine into LDS (pab / pab1): given, or formed from the producer's f64 accumulators; runs
+    // the prologue affine into LDS (pab / pab1): given, or formed from the producer's fixed-point accumulators; runs
     // after the first patch and U loads are issued (below), so its latency overlaps theirs
     auto load_affine = [&]() __attribute__((always_inline)) {
         if constexpr (pro != PRO_NONE) {
@@ -555,7 +555,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
         if (a.stat.acc != nullptr) {   // channel-contiguous adds: 512 B per wave instruction
             lds_barrier();
-            if (tid < XN) cin_acc_add(a.stat, a.batch, XN, b, tid, (int)blockIdx.x % a.stat.nslot, dred[tid], dred[XN + tid]);
+            if (tid < 2 * XN)   // thread = (value, channel): 3 limb adds each, 512 B per wave instruction
+                cin_acc_add_value(a.stat, a.batch, XN, b, tid % XN, (int)blockIdx.x % a.stat.nslot, tid / XN, dred[tid]);
         }
     }
     XTL(3);

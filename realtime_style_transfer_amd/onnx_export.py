@@ -22,8 +22,12 @@ convs). Everything else restates the reference layers op by op:
   * predictor: Rescaling(2, -1) as Mul/Add, MobileNetV3Small (Conv, depthwise Conv with group = C,
     BatchNormalization, Relu / HardSwish, squeeze-excite with HardSigmoid(1/6, 1/2)), the global
     average pool and the two 1x1 heads (``stylePrediction.py:25-75``).
-Only one style (``num_styles == 1``) is exported: the two-style graph needs the per-pixel
-style-weight mip chain, which tf2onnx would trace from the Keras graph but is not restated here.
+Two styles (``num_styles == 2``) add the ``style_weights`` input (N, Ho, Wo, 1): the full weight map
+``[1 - sum(w), w]`` (``styleTransfer.py:290-303``), its AvgPool2 mip chain keyed by width (``:335-345``,
+``num_expand_blocks + 1`` levels, valid pooling) and, in every CIN, the per-pixel blend of the two styles'
+scale and bias with the mip of the layer's output width (``_apply_style_weights``, ``:36-44``). For more
+than two styles the reference returns the unblended (B, 1, S, F) parameters, which do not broadcast against
+a (B, H, W, F) feature map; that graph is not exported.
 
 Parity: the exported graph is checked by executing it with the repo's own reader and a numpy
 evaluator of these operators (tests/onnx_runner.py) against the float64 oracle; loading it in
@@ -236,8 +240,38 @@ def _style_slice(g: GraphBuilder, sp: str, offset: int, c: int, hint: str) -> st
     return g.op('Reshape', [s, g.const(hint + '_shape', np.array([0, c, 1, 1], np.int64))], hint)
 
 
-def _cin(g: GraphBuilder, x: str, sp: str, offset: int, c: int, hint: str) -> str:
-    """ConditionalInstanceNormalization.call (styleTransfer.py:57-71), one style."""
+def _style_weight_mips(g: GraphBuilder, out_w: int, levels: int) -> Dict[int, str]:
+    """styleTransfer.py:290-303,335-345: NCHW full weights (N, 2, Ho, Wo) and their AvgPool2 mips by width."""
+    w = g.op('Transpose', ['style_weights'], 'sw_nchw', perm=[0, 3, 1, 2])
+    total = g.op('ReduceSum', [w, g.const('sw_axes', np.array([1], np.int64))], 'sw_sum', keepdims=1)
+    w0 = g.op('Sub', [g.const('sw_one', np.array(1.0, np.float32)), total], 'sw_w0')
+    last = g.op('Concat', [w0, w], 'sw_full', axis=1)
+    mips, width = {out_w: last}, out_w
+    for i in range(levels):
+        last = g.op('AveragePool', [last], f'sw_mip{i}', kernel_shape=[2, 2], strides=[2, 2])
+        width //= 2
+        mips[width] = last
+    return mips
+
+
+def _blended_param(g: GraphBuilder, sp: str, offset: int, c: int, mip: str, hint: str) -> str:
+    """_apply_style_weights (styleTransfer.py:36-44) for S == 2: sum_s w_s * params_s -> (N, c, h, w)."""
+    terms = []
+    for si in range(2):
+        p = g.op('Slice', [sp, g.const(hint + f'_st{si}', np.array([si, offset], np.int64)),
+                           g.const(hint + f'_en{si}', np.array([si + 1, offset + c], np.int64)),
+                           g.const(hint + f'_ax{si}', np.array([1, 2], np.int64))], hint + f'_slice{si}')
+        p = g.op('Reshape', [p, g.const(hint + f'_shape{si}', np.array([0, c, 1, 1], np.int64))], hint + f'_p{si}')
+        wgt = g.op('Slice', [mip, g.const(hint + f'_wst{si}', np.array([si], np.int64)),
+                             g.const(hint + f'_wen{si}', np.array([si + 1], np.int64)),
+                             g.const(hint + f'_wax{si}', np.array([1], np.int64))], hint + f'_w{si}')
+        terms.append(g.op('Mul', [wgt, p], hint + f'_wp{si}'))
+    return g.op('Add', terms, hint)
+
+
+def _cin(g: GraphBuilder, x: str, sp: str, offset: int, c: int, hint: str, mip: Optional[str] = None) -> str:
+    """ConditionalInstanceNormalization.call (styleTransfer.py:57-71); with ``mip`` the two styles' parameters
+    are blended per pixel."""
     mean = g.op('ReduceMean', [x], hint + '_mean', axes=[2, 3], keepdims=1)
     d = g.op('Sub', [x, mean], hint + '_d')
     var = g.op('ReduceMean', [g.op('Mul', [d, d], hint + '_d2')], hint + '_var', axes=[2, 3], keepdims=1)
@@ -245,16 +279,21 @@ def _cin(g: GraphBuilder, x: str, sp: str, offset: int, c: int, hint: str) -> st
     inv = g.op('Reciprocal', [g.op('Sqrt', [g.op('Add', [var, eps], hint + '_ve')], hint + '_sd')], hint + '_inv')
     xn = g.op('Add', [g.op('Mul', [x, inv], hint + '_xi'), g.op('Mul', [g.op('Neg', [mean], hint + '_nm'), inv],
                                                                    hint + '_mi')], hint + '_xn')
-    scale = _style_slice(g, sp, offset, c, hint + '_scale')
-    bias = _style_slice(g, sp, offset + c, c, hint + '_bias')
+    if mip is None:
+        scale = _style_slice(g, sp, offset, c, hint + '_scale')
+        bias = _style_slice(g, sp, offset + c, c, hint + '_bias')
+    else:
+        scale = _blended_param(g, sp, offset, c, mip, hint + '_scale')
+        bias = _blended_param(g, sp, offset + c, c, mip, hint + '_bias')
     return g.op('Add', [bias, g.op('Mul', [xn, scale], hint + '_xs')], hint)
 
 
 def transfer_graph(plan: Plan, weights: Sequence[np.ndarray], batch: Optional[int] = None) -> bytes:
-    """ModelProto bytes of create_style_transfer_model (styleTransfer.py:213-332), num_styles == 1."""
-    if plan.num_styles != 1:
-        raise NotImplementedError("ONNX export covers num_styles == 1 (the two-style graph needs the style-weight "
-                                  "mip chain, styleTransfer.py:290-303)")
+    """ModelProto bytes of create_style_transfer_model (styleTransfer.py:213-332), num_styles 1 or 2."""
+    S = plan.num_styles
+    if S not in (1, 2):
+        raise NotImplementedError("ONNX export covers num_styles 1 and 2 (for S > 2 the reference's CIN parameters "
+                                  "stay unblended (B,1,S,F) and do not broadcast, styleTransfer.py:36-44)")
     shapes = plan.weight_shapes()
     if len(weights) != len(shapes) or any(tuple(w.shape) != s for w, s in zip(weights, shapes)):
         raise ValueError("weights do not match the plan's Keras get_weights() shapes")
@@ -263,7 +302,12 @@ def transfer_graph(plan: Plan, weights: Sequence[np.ndarray], batch: Optional[in
     Ho, Wo, _ = plan.output_shape
     P = plan.num_style_params
     g = GraphBuilder('StyleTransferModel')
-    g.inputs += [_value_info('content', [N, H, W, C]), _value_info('style_params', [N, 1, P])]
+    g.inputs += [_value_info('content', [N, H, W, C]), _value_info('style_params', [N, S, P])]
+    mips = None
+    if S == 2:
+        g.inputs.append(_value_info('style_weights', [N, Ho, Wo, S - 1]))
+        n_expand = sum(1 for layer in plan.layers if layer.kind != 'conv' and layer.block != 'expand_last')
+        mips = _style_weight_mips(g, Wo, n_expand + 1)
     x = g.op('Transpose', ['content'], 'to_nchw', perm=[0, 3, 1, 2])
     wi = iter(weights)
     block_in = None
@@ -280,7 +324,8 @@ def transfer_graph(plan: Plan, weights: Sequence[np.ndarray], batch: Optional[in
                 gamma, beta, mm, mv = next(wi), next(wi), next(wi), next(wi)
                 x = g.op('Relu', [_batch_norm(g, x, gamma, beta, mm, mv, BN_EPS, hint + '_bn')], hint + '_bnrelu')
             else:
-                x = _cin(g, x, 'style_params', layer.style_offset, layer.cout, hint + '_cin')
+                x = _cin(g, x, 'style_params', layer.style_offset, layer.cout, hint + '_cin',
+                         mips[layer.out_hw[1]] if mips is not None else None)
                 if layer.post_act == 'relu':
                     x = g.op('Relu', [x], hint + '_post')
                 elif not layer.residual_first:   # second conv of blocks 1..4: skip Add (:184)
@@ -292,7 +337,8 @@ def transfer_graph(plan: Plan, weights: Sequence[np.ndarray], batch: Optional[in
             x = g.op('ConvTranspose', [x, g.const(hint + '_w', w), g.const(hint + '_b', _f32(bias))], hint,
                      kernel_shape=[layer.k, layer.k], strides=[layer.stride, layer.stride], pads=pads,
                      dilations=[1, 1], group=1)
-            x = _cin(g, x, 'style_params', layer.style_offset, layer.cout, hint + '_cin')
+            x = _cin(g, x, 'style_params', layer.style_offset, layer.cout, hint + '_cin',
+                     mips[layer.out_hw[1]] if mips is not None else None)
             x = g.op('Sigmoid' if layer.post_act == 'sigmoid' else 'Relu', [x], hint + '_post')
     assert next(wi, None) is None
     y = g.op('Transpose', [x], 'to_nhwc', perm=[0, 2, 3, 1])

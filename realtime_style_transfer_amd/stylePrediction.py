@@ -102,6 +102,26 @@ def predictor_weight_spec(input_shape, feature_extractor: str, num_top_parameter
     return spec
 
 
+def predictor_layer_tree(spec):
+    """The predictor's weighted Keras layers (stylePrediction.py:25-75) as a checkpoint LayerTree: the feature
+    extractor first — MobileNetV3Small is a functional model used as a layer (:33-36,52), so its layers nest
+    under ``layer_with_weights-0``; DUMMY's ``dummy_conv`` (:31) is a plain layer — then the two 1x1 heads
+    ``StylePredictor`` (:59-63) and ``StyleNormPredictor`` (:66-70)."""
+    from .tf_checkpoint import LayerTree, layer_tree_from_names
+    names = [n for n, _, _ in spec]
+    heads = [n for n in names if n.split('/')[0] in ('StylePredictor', 'StyleNormPredictor')]
+    trunk = [n for n in names if n not in heads]
+    head_layers = layer_tree_from_names(heads).entries
+    if all(n.startswith('dummy_conv/') for n in trunk):
+        return LayerTree(layer_tree_from_names(trunk).entries + head_layers)
+    return LayerTree([layer_tree_from_names(trunk)] + head_layers)
+
+
+def trainable_mask(spec) -> List[bool]:
+    """Which weights are trainable variables (everything but the BatchNormalization moving statistics)."""
+    return [not (n.endswith('/moving_mean') or n.endswith('/moving_variance')) for n, _, _ in spec]
+
+
 def init_predictor_weights(spec, seed: int = 3, perturb: bool = False) -> List[np.ndarray]:
     rng = np.random.default_rng(seed)
     out = []
@@ -209,6 +229,31 @@ class StylePredictionModel:
 
     trainable = False
 
+    # ------------------------------------------------------------------ checkpoints (tracing/checkpoint.py:21-37)
+    def _checkpoint_parts(self, prefix: str = ""):
+        from .tf_checkpoint import _Part
+        return [_Part(prefix, predictor_layer_tree(self.spec), self.get_weights, self.set_weights,
+                      [s for _, s, _ in self.spec])]
+
+    def _checkpoint_tensors(self):
+        from .tf_checkpoint import parts_tensors
+        return parts_tensors(self._checkpoint_parts())
+
+    def _restore_tensors(self, tensors):
+        from .tf_checkpoint import restore_parts
+        return restore_parts(self._checkpoint_parts(), tensors)
+
+    def save_weights(self, filepath) -> None:
+        from .tf_checkpoint import save_weights
+        save_weights(self, filepath)
+
+    def load_weights(self, filepath, model_path: str = ""):
+        """Model.load_weights -> CheckpointLoadStatus; ``model_path`` selects the predictor's subtree of a larger
+        model's checkpoint (``"layer_with_weights-0"`` in the inference / training models)."""
+        from .tf_checkpoint import read_checkpoint, restore_parts
+        pre = model_path.rstrip('/') + '/' if model_path else ''
+        return restore_parts(self._checkpoint_parts(pre), read_checkpoint(filepath))
+
     def __call__(self, style: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
         style = _lib.as_device(style, self.device)
         if style.dim() != 4 or tuple(style.shape[1:]) != self.input_shape:
@@ -291,6 +336,8 @@ class StylePredictionTrainer:
         if self.num_weights != flat.size:
             raise RuntimeError("librst predictor trainer plan disagrees with the host weight list")
         self._style = None
+        self._version = 0          # bumped by every weight change (keys the training model's inference cache)
+        self.iterations = 0
 
     def __del__(self):
         try:
@@ -329,6 +376,8 @@ class StylePredictionTrainer:
 
     def apply_gradients(self, grad: torch.Tensor, learning_rate: float = 1e-3, rho: float = 0.9,
                         epsilon: float = 1e-7):
+        self._version += 1
+        self.iterations += 1
         _lib.check(_lib.load().rst_predictor_trainer_apply_gradients(self._handle, _lib.dev_ptr(grad),
                                                                      float(learning_rate), float(rho), float(epsilon),
                                                                      _lib.stream_ptr()))
@@ -341,6 +390,7 @@ class StylePredictionTrainer:
         return t
 
     def set_weights_tensor(self, t: torch.Tensor):
+        self._version += 1
         _lib.check(_lib.load().rst_predictor_trainer_set_weights(self._handle, _lib.dev_ptr(t.contiguous()), t.numel(),
                                                                  _lib.stream_ptr()))
 
@@ -355,11 +405,32 @@ class StylePredictionTrainer:
     def get_weights(self) -> List[np.ndarray]:
         return self._unflatten(self.weights_tensor().cpu().numpy())
 
+    def set_weights(self, weights: Sequence[np.ndarray]):
+        if len(weights) != len(self._shapes) or any(tuple(np.shape(a)) != s for a, s in zip(weights, self._shapes)):
+            raise ValueError(f"weights do not match the predictor: expected {self._shapes}")
+        flat = np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in weights])
+        self.set_weights_tensor(torch.from_numpy(flat).to(self.device))
+        torch.cuda.current_stream(self.device).synchronize()
+
     def optimizer_slots(self) -> List[np.ndarray]:
         t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
         _lib.check(_lib.load().rst_predictor_trainer_copy_slots(self._handle, _lib.dev_ptr(t), t.numel(),
                                                                 _lib.stream_ptr()))
         return self._unflatten(t.cpu().numpy())
+
+    def set_optimizer_slots(self, slots: Sequence[np.ndarray]):
+        """Restore the RMSprop ``rms`` slots (Keras order; a checkpoint restore)."""
+        flat = np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in slots])
+        if flat.size != self.num_weights:
+            raise ValueError("optimizer slots do not match the predictor")
+        t = torch.from_numpy(flat).to(self.device)
+        _lib.check(_lib.load().rst_predictor_trainer_set_slots(self._handle, _lib.dev_ptr(t), t.numel(),
+                                                               _lib.stream_ptr()))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def _checkpoint_parts(self, prefix: str = ""):
+        from .tf_checkpoint import _Part
+        return [_Part(prefix, predictor_layer_tree(self.spec), self.get_weights, self.set_weights, self._shapes)]
 
     def unflatten(self, grad: torch.Tensor) -> List[np.ndarray]:
         return self._unflatten(grad.detach().cpu().numpy())

@@ -108,33 +108,34 @@ class StyleTransferModel:
     trainable = False
 
     def keras_layer_attributes(self) -> List[List[str]]:
-        """Variables per weighted Keras layer, in model order: each Conv2D/Conv2DTranspose owns
-        (kernel, bias); the BatchNormalization after a contract conv (styleTransfer.py:194-203) is its
-        own layer (gamma, beta, moving_mean, moving_variance); CIN owns none (its affine is an input)."""
-        out = []
-        for layer in self.plan.layers:
-            out.append(["kernel", "bias"])
-            if layer.norm == 'bn':
-                out.append(["gamma", "beta", "moving_mean", "moving_variance"])
-        return out
+        return transfer_layer_attributes(self.plan)
+
+    def _checkpoint_parts(self, prefix: str = ""):
+        from .tf_checkpoint import LayerTree, _Part
+        return [_Part(prefix, LayerTree(self.keras_layer_attributes()), self.get_weights, self.set_weights,
+                      [tuple(w.shape) for w in self._weights])]
+
+    def _checkpoint_tensors(self):
+        from .tf_checkpoint import parts_tensors
+        return parts_tensors(self._checkpoint_parts())
+
+    def _restore_tensors(self, tensors):
+        from .tf_checkpoint import restore_parts
+        return restore_parts(self._checkpoint_parts(), tensors)
 
     def save_weights(self, filepath) -> None:
         """Model.save_weights(filepath) in TF checkpoint format (tracing/checkpoint.py:37)."""
-        from .tf_checkpoint import save_keras_weights
-        save_keras_weights(filepath, self._weights, self.keras_layer_attributes())
+        from .tf_checkpoint import save_weights
+        save_weights(self, filepath)
 
     def load_weights(self, filepath, model_path: str = ""):
         """Model.load_weights(filepath) (predict_using_checkpoint.py:84) from a TF checkpoint prefix or
-        directory; ``model_path`` selects this model's subtree inside a larger model's checkpoint
-        (e.g. ``"layer_with_weights-1"``). Raises if nothing matches (assert_nontrivial_match)."""
-        from .tf_checkpoint import keras_weights, read_checkpoint
-        w = keras_weights(read_checkpoint(filepath), model_path)
-        shapes = [tuple(x.shape) for x in self._weights]
-        if [tuple(x.shape) for x in w] != shapes:
-            raise ValueError(f"checkpoint weights do not match the network plan: expected {shapes}, "
-                             f"got {[tuple(x.shape) for x in w]}")
-        self.set_weights(w)
-        return self
+        directory -> a CheckpointLoadStatus (``assert_nontrivial_match()``, ``assert_consumed()``).
+        ``model_path`` selects this model's subtree inside a larger model's checkpoint (the inference model
+        keeps it under ``"layer_with_weights-1"``)."""
+        from .tf_checkpoint import read_checkpoint, restore_parts
+        pre = model_path.rstrip('/') + '/' if model_path else ''
+        return restore_parts(self._checkpoint_parts(pre), read_checkpoint(filepath))
 
     @property
     def input(self) -> Dict[str, tuple]:
@@ -216,6 +217,18 @@ class StyleTransferModel:
         t = torch.empty((batch, hwc[0], hwc[1], hwc[2]), dtype=torch.float32, device=self.device)
         _lib.check(lib.rst_copy_activation(self._handle, idx, _lib.dev_ptr(t), t.numel(), batch, _lib.stream_ptr()))
         return t
+
+
+def transfer_layer_attributes(plan: Plan) -> List[List[str]]:
+    """Variables per weighted Keras layer of the transfer network, in model order: each Conv2D /
+    Conv2DTranspose owns (kernel, bias); the BatchNormalization after a contract conv (styleTransfer.py:194-203)
+    is its own layer (gamma, beta, moving_mean, moving_variance); CIN owns none (its affine is an input)."""
+    out = []
+    for layer in plan.layers:
+        out.append(["kernel", "bias"])
+        if layer.norm == 'bn':
+            out.append(["gamma", "beta", "moving_mean", "moving_variance"])
+    return out
 
 
 def create_style_transfer_model(input_shape, output_shape, bottleneck_res_y, bottleneck_num_filters, num_styles,

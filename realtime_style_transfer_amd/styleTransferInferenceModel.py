@@ -69,6 +69,33 @@ class StyleTransferInference:
         """Keras Model.predict: the output as a host numpy array (predict_using_checkpoint.py:99)."""
         return self(inputs).cpu().numpy()
 
+    # ------------------------------------------------------------------ checkpoints
+    # The functional model's weighted layers are the two sub-models: the style predictor first
+    # (layer_with_weights-0; its output feeds the stack, :23-26) and the transfer network (layer_with_weights-1,
+    # :37), each keyed by its own layer tree below that prefix (tf_checkpoint.LayerTree).
+    def _checkpoint_parts(self):
+        return self.style_predictor._checkpoint_parts("layer_with_weights-0/") + \
+            self.transfer._checkpoint_parts("layer_with_weights-1/")
+
+    def _checkpoint_tensors(self):
+        from .tf_checkpoint import parts_tensors
+        return parts_tensors(self._checkpoint_parts())
+
+    def _restore_tensors(self, tensors):
+        from .tf_checkpoint import restore_parts
+        return restore_parts(self._checkpoint_parts(), tensors)
+
+    def load_weights(self, filepath):
+        """``inference.load_weights(filepath)`` (predict_using_checkpoint.py:84-85) -> CheckpointLoadStatus
+        (``assert_nontrivial_match()``): a checkpoint of this model, or of the training model (same layers;
+        its optimizer state is left unused)."""
+        from .tf_checkpoint import load_weights
+        return load_weights(self, filepath)
+
+    def save_weights(self, filepath) -> None:
+        from .tf_checkpoint import save_weights
+        save_weights(self, filepath)
+
 
 def make_style_transfer_inference_model(num_styles, style_predictor_factory_func: Callable[[int], object],
                                         style_transfer_factory_func: Callable[[], tuple],

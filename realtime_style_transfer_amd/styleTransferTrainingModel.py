@@ -108,12 +108,14 @@ class StyleTransferTrainingModel:
                  loss_model: Optional[StyleLossModelVGG] = None, weights: Optional[Sequence[np.ndarray]] = None,
                  seed: int = 2, max_batch: int = 4, optimizer: Optional[RMSprop] = None, process_group=None,
                  device=None, name: str = "StyleTransferTrainingModel", style_predictor=None,
-                 precision: str = "fp32_winograd", with_depth_loss: bool = False):
+                 precision: str = "winograd_bf16x6", with_depth_loss: bool = False):
         """``loss_model``: a StyleLossModelVGG (trainable), or a construct-only loss model such as
         StyleLossModelMobileNet, with which the model is built (weights, inference ``__call__``) but
         ``train_step`` raises — what the reference's inference and export scripts need
         (predict_video_using_checkpoint.py:43-58, save_using_checkpoint.py:39-53). ``with_depth_loss``: the
-        loss asked for the MiDaS depth term (unavailable): construction works, ``train_step`` raises."""
+        loss asked for the MiDaS depth term (unavailable): construction works, ``train_step`` raises.
+        ``precision``: the transfer network's arithmetic — "winograd_bf16x6" (default; fp32-level, the benchmarked
+        config-4 line), "fp32_winograd" or "fp32"; the VGG16 loss network's comes from ``loss_model.precision``."""
         if precision not in ("fp32", "fp32_winograd", "winograd_bf16x6"):
             raise ValueError("transfer-network training precision must be 'fp32', 'fp32_winograd' or "
                              f"'winograd_bf16x6', got {precision!r}")
@@ -139,6 +141,7 @@ class StyleTransferTrainingModel:
         self.style_predictor = style_predictor      # StylePredictionTrainer or None
         self.style_losses: Dict[str, torch.Tensor] = {}
         self._version, self._inference = 0, None
+        self.iterations = 0                         # optimizer steps taken (Keras OptimizerV2.iterations)
         self._handle = None
         if not isinstance(self.loss_model, StyleLossModelVGG):
             # construct-only: weights on the host, no trainer (train_step raises)
@@ -240,14 +243,20 @@ class StyleTransferTrainingModel:
         _lib.check(_lib.load().rst_trainer_set_weights(self._handle, _lib.dev_ptr(t), t.numel(), _lib.stream_ptr()))
         torch.cuda.current_stream(self.device).synchronize()
 
+    def _weights_version(self):
+        pr = self.style_predictor
+        return (self._version, getattr(pr, '_version', 0) if pr is not None else 0)
+
     def inference_model(self):
         """The Keras model this training model wraps (styleTransferTrainingModel.py:19: inference_model.input ->
-        output), in inference mode with the current weights: predictor -> transfer, or the transfer alone."""
-        if self._inference is None or self._inference[0] != self._version:
+        output), in inference mode with the current weights: predictor -> transfer, or the transfer alone. Rebuilt
+        whenever the transfer or the predictor weights (BN moving statistics included) changed."""
+        v = self._weights_version()
+        if self._inference is None or self._inference[0] != v:
             transfer = self.transfer_model()
             model = StyleTransferInference(transfer, self.style_predictor.inference_model(), 1, self.name) \
                 if self.style_predictor is not None else transfer
-            self._inference = (self._version, model)
+            self._inference = (v, model)
         return self._inference[1]
 
     def __call__(self, inputs: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -273,6 +282,99 @@ class StyleTransferTrainingModel:
         t = torch.empty(self.num_weights, dtype=torch.float32, device=self.device)
         _lib.check(_lib.load().rst_trainer_copy_slots(self._handle, _lib.dev_ptr(t), t.numel(), _lib.stream_ptr()))
         return self._unflatten(t.cpu().numpy())
+
+    def set_optimizer_slots(self, slots: Sequence[np.ndarray]):
+        """Restore the RMSprop ``rms`` slots (weight order; a checkpoint restore)."""
+        self._require_live()
+        t = torch.from_numpy(self._flatten(slots)).to(self.device)
+        _lib.check(_lib.load().rst_trainer_set_slots(self._handle, _lib.dev_ptr(t), t.numel(), _lib.stream_ptr()))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def _require_live(self):
+        if self._handle is None:
+            raise NotImplementedError(f"{type(self.loss_model).__name__} is construct-only: no optimizer state")
+
+    # ------------------------------------------------------------------ checkpoints
+    # The training model is the functional inference graph (styleTransferTrainingModel.py:19, 44-52), so its
+    # weighted layers are the style predictor (layer_with_weights-0: it runs first, styleTransferInferenceModel.py:
+    # 23-26) and the transfer network (layer_with_weights-1, :37); after compile(optimizer) the RMSprop state
+    # follows: slot ``rms`` of every trainable variable under ``<variable>/.OPTIMIZER_SLOT/optimizer/rms``, and
+    # ``optimizer/{iter, learning_rate, rho, decay, momentum}``. Without a predictor (style_params fed directly)
+    # the model is the transfer network alone, at the root.
+    def _checkpoint_parts(self):
+        from .tf_checkpoint import LayerTree, _Part
+        from .styleTransfer import transfer_layer_attributes
+        tree = LayerTree(transfer_layer_attributes(self.plan))
+        pr = self.style_predictor
+        if pr is None:
+            return [_Part("", tree, self.get_weights, self.set_weights, self._shapes)]
+        return pr._checkpoint_parts("layer_with_weights-0/") + \
+            [_Part("layer_with_weights-1/", tree, self.get_weights, self.set_weights, self._shapes)]
+
+    def _slot_groups(self):
+        """[(part, trainable mask, get slots, set slots)] for the optimizer state."""
+        from .stylePrediction import trainable_mask
+        parts = self._checkpoint_parts()
+        tmask = [not (p.endswith('/moving_mean') or p.endswith('/moving_variance')) for p in parts[-1].tree.paths()]
+        groups = [(parts[-1], tmask, self.optimizer_slots, self.set_optimizer_slots)]
+        if self.style_predictor is not None:
+            pr = self.style_predictor
+            groups.insert(0, (parts[0], trainable_mask(pr.spec), pr.optimizer_slots, pr.set_optimizer_slots))
+        return groups
+
+    def _checkpoint_tensors(self):
+        from .tf_checkpoint import SLOT_MARK, VAR_SUFFIX, parts_tensors
+        out = parts_tensors(self._checkpoint_parts())
+        if self._handle is None:
+            return out
+        for part, mask, get, _ in self._slot_groups():
+            for path, slot, trainable in zip(part.tree.paths(part.prefix), get(), mask):
+                if trainable:
+                    out[f"{path}{SLOT_MARK}optimizer/rms{VAR_SUFFIX}"] = np.asarray(slot, np.float32)
+        o = self.optimizer
+        out["optimizer/iter" + VAR_SUFFIX] = np.array(self.iterations, np.int64)
+        for name, v in (("learning_rate", o.learning_rate), ("rho", o.rho), ("decay", 0.0), ("momentum", 0.0)):
+            out[f"optimizer/{name}{VAR_SUFFIX}"] = np.array(v, np.float32)
+        return out
+
+    def _restore_tensors(self, tensors):
+        from .tf_checkpoint import SLOT_MARK, VAR_SUFFIX, restore_parts
+        used, slot_sets = [], []
+        if self._handle is not None:
+            for part, mask, get, set_ in self._slot_groups():
+                keys = [f"{p}{SLOT_MARK}optimizer/rms{VAR_SUFFIX}" if t else None
+                        for p, t in zip(part.tree.paths(part.prefix), mask)]
+                have = [k in tensors for k in keys if k is not None]
+                if have and all(have):
+                    slot_sets.append((keys, get, set_))
+                    used += [k for k in keys if k is not None]
+            used += [f"optimizer/{n}{VAR_SUFFIX}" for n in ("iter", "learning_rate", "rho", "decay", "momentum")
+                     if f"optimizer/{n}{VAR_SUFFIX}" in tensors]
+        status = restore_parts(self._checkpoint_parts(), tensors, extra_keys=used)   # validates, then sets weights
+        for keys, get, set_ in slot_sets:
+            set_([np.asarray(tensors[k], np.float32).reshape(c.shape) if k is not None else np.zeros_like(c)
+                  for k, c in zip(keys, get())])
+        if self._handle is not None:
+            it = tensors.get("optimizer/iter" + VAR_SUFFIX)
+            if it is not None:
+                self.iterations = int(it)
+                if self.style_predictor is not None:
+                    self.style_predictor.iterations = int(it)
+            for name in ("learning_rate", "rho"):
+                if f"optimizer/{name}{VAR_SUFFIX}" in tensors:
+                    setattr(self.optimizer, name, float(tensors[f"optimizer/{name}{VAR_SUFFIX}"]))
+        return status
+
+    def load_weights(self, filepath):
+        """``training.load_weights(path)`` (predict_video_using_checkpoint.py:74) -> CheckpointLoadStatus: the
+        predictor and transfer weights and, when the checkpoint holds them, the RMSprop state."""
+        from .tf_checkpoint import load_weights
+        return load_weights(self, filepath)
+
+    def save_weights(self, filepath) -> None:
+        """``Model.save_weights`` of the training model (tracing/checkpoint.py:37, TF format): weights + optimizer."""
+        from .tf_checkpoint import save_weights
+        save_weights(self, filepath)
 
     def output_gradient(self, idx: int, batch: int) -> torch.Tensor:
         """Debug: d loss / d (activated output of conv layer idx) of the most recent step."""
@@ -330,6 +432,12 @@ class StyleTransferTrainingModel:
                                                            _lib.stream_ptr()))
         self._pending_targets = (gt_content, gt_style, gc, gs)   # keeps the buffers alive until the join
 
+    def cancel_targets(self):
+        """Drop the loss targets ``compute_targets`` started (the step failed before ``compute_gradients``)."""
+        if self._handle is not None:
+            self._pending_targets = None
+            _lib.check(_lib.load().rst_trainer_cancel_targets(self._handle, _lib.stream_ptr()))
+
     def compute_gradients(self, content: torch.Tensor, style_params: torch.Tensor, gt_content: torch.Tensor,
                           gt_style: torch.Tensor, grad: Optional[torch.Tensor] = None,
                           grad_style_params: Optional[torch.Tensor] = None):
@@ -359,6 +467,7 @@ class StyleTransferTrainingModel:
         o = self.optimizer
         _lib.check(_lib.load().rst_trainer_apply_gradients(self._handle, _lib.dev_ptr(grad), o.learning_rate, o.rho,
                                                            o.epsilon, _lib.stream_ptr()))
+        self.iterations += 1
 
     def _world(self) -> int:
         dist = torch.distributed
@@ -378,6 +487,9 @@ class StyleTransferTrainingModel:
 
     def _set_moving_statistics(self, divisor: float):
         lib = _lib.load()
+        self._version += 1
+        if self.style_predictor is not None:
+            self.style_predictor._version += 1
         if self._n_stat:
             _lib.check(lib.rst_trainer_set_moving_statistics(self._handle, _lib.dev_ptr(self._stat), self._n_stat,
                                                              float(divisor), _lib.stream_ptr()))
@@ -433,7 +545,11 @@ class StyleTransferTrainingModel:
                     raise ValueError("the training model takes one style (num_styles=1, styleTransferTrainingModel.py:46)")
                 style = style[:, 0]
             self.compute_targets(y['content'], y['style'])            # loss targets beside the predictor forward
-            sp = pr.forward(style)                                     # styleTransferInferenceModel.py:23-28
+            try:
+                sp = pr.forward(style)                                 # styleTransferInferenceModel.py:23-28
+            except BaseException:
+                self.cancel_targets()
+                raise
         else:
             sp = x['style_params']
         pred, losses, grad, gsp = self.compute_gradients(x['content'], sp, y['content'], y['style'])
@@ -469,7 +585,10 @@ class StyleTransferModels:
         def end_to_end_loss(inputs):
             """loss_model((x, y_true)) (styleTransferTrainingModel.py:59,64): the losses of the inference output."""
             x, y_true = inputs
-            return loss_model.compute(training(x), y_true)
+            if hasattr(loss_model, 'compute'):
+                return loss_model.compute(training(x), y_true)
+            from .styleLoss import StyleLoss
+            return StyleLoss(loss_model, training.with_depth_loss).compute(training(x), y_true)
 
         self.loss_model = end_to_end_loss
         self.refresh()
@@ -479,17 +598,68 @@ class StyleTransferModels:
         self.transfer = tr.transfer_model()
         if tr.style_predictor is not None:
             self.style_predictor = tr.style_predictor.inference_model()
-            self.inference = StyleTransferInference(self.transfer, self.style_predictor, 1, tr.name)
+            self.inference = _SharedInference(self, self.transfer, self.style_predictor, 1, tr.name)
         else:
             self.style_predictor = None
-            self.inference = lambda inputs: self.transfer(inputs)
+            self.inference = _SharedTransfer(self)
+
+
+class _SharedInference(StyleTransferInference):
+    """``models.inference``: the inference graph of the training model, sharing its variables as the Keras
+    models do (styleTransferTrainingModel.py:52,66). A checkpoint restored through it (``load_weights``,
+    ``Checkpoint(models.inference).restore``, train_network.py:112-113) lands in the trainers, and the
+    inference models are rebuilt from them."""
+
+    def __init__(self, models, *args):
+        super().__init__(*args)
+        self._models = models
+
+    def _restore_tensors(self, tensors):
+        st = self._models.training._restore_tensors(tensors)
+        self._models.refresh()
+        return st
+
+    def _checkpoint_tensors(self):
+        from .tf_checkpoint import parts_tensors
+        return parts_tensors(self._models.training._checkpoint_parts())
+
+
+class _SharedTransfer:
+    """``models.inference`` without a style predictor: the transfer network (style_params are an input)."""
+
+    def __init__(self, models):
+        self._models = models
+
+    def __call__(self, inputs, out=None):
+        return self._models.transfer(inputs, out=out)
+
+    def predict(self, inputs, batch_size=None, verbose=0):
+        return self._models.transfer.predict(inputs)
+
+    def _restore_tensors(self, tensors):
+        st = self._models.training._restore_tensors(tensors)
+        self._models.refresh()
+        return st
+
+    def _checkpoint_tensors(self):
+        from .tf_checkpoint import parts_tensors
+        return parts_tensors(self._models.training._checkpoint_parts())
+
+    def load_weights(self, filepath):
+        from .tf_checkpoint import load_weights
+        return load_weights(self, filepath)
+
+    def save_weights(self, filepath):
+        from .tf_checkpoint import save_weights
+        save_weights(self, filepath)
 
 
 def make_style_transfer_training_model(style_predictor_factory_func: Optional[Callable],
                                        style_transfer_factory_func: Callable,
                                        style_loss_func_factory_func: Callable,
                                        name="StyleTransferTrainingModel", max_batch: int = 4,
-                                       optimizer: Optional[RMSprop] = None, process_group=None):
+                                       optimizer: Optional[RMSprop] = None, process_group=None,
+                                       precision: str = "winograd_bf16x6"):
     """styleTransferTrainingModel.py:39-70 on librst.
 
     ``style_transfer_factory_func() -> (StyleTransferModel, P)`` supplies the architecture and
@@ -497,7 +667,9 @@ def make_style_transfer_training_model(style_predictor_factory_func: Optional[Ca
     ``style_params`` directly) the predictor trained jointly with it (stylePrediction.py:25-75);
     ``style_loss_func_factory_func() -> (compute_loss, StyleLoss)`` the loss (make_style_loss_function). A
     construct-only loss (StyleLossModelMobileNet, or the MiDaS depth term) builds a model whose train_step
-    raises — enough for the inference / export scripts, which never train."""
+    raises — enough for the inference / export scripts, which never train. ``precision``: the transfer network's
+    training arithmetic (default "winograd_bf16x6", the benchmarked config-4 line); the VGG16 loss network's is
+    the loss model's own (``StyleLossModelVGG(..., precision="bf16")`` for BASELINE config 4)."""
     from .stylePrediction import StylePredictionTrainer
     transfer, P = style_transfer_factory_func()
     predictor = None
@@ -512,7 +684,7 @@ def make_style_transfer_training_model(style_predictor_factory_func: Optional[Ca
                                           transfer.plan.bottleneck_num_filters, loss_model=feature_model,
                                           weights=transfer.get_weights(), max_batch=max_batch, optimizer=optimizer,
                                           process_group=process_group, device=transfer.device, name=name,
-                                          style_predictor=predictor,
+                                          style_predictor=predictor, precision=precision,
                                           with_depth_loss=getattr(compute_loss, 'with_depth_loss', False))
     return StyleTransferModels(training, loss)
 

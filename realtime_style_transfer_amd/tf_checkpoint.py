@@ -415,38 +415,345 @@ def keras_weights(tensors: Dict[str, np.ndarray], model_path: str = "") -> List[
     return [np.asarray(v, dtype=np.float32) for _, v in found]
 
 
-def _object_graph(layer_attrs: List[List[str]]) -> bytes:
-    """TrackableObjectGraph for a functional model: root -> layer_with_weights-i -> attr variables."""
-    nodes: List[bytes] = []
-    root_children = []
-    next_id = 1 + len(layer_attrs)
-    var_nodes = []
-    for i, attrs in enumerate(layer_attrs):
-        root_children.append(_pb_bytes(1, _pb_varint(1, 1 + i) + _pb_bytes(2, f"layer_with_weights-{i}".encode())))
-    nodes.append(b''.join(root_children))
-    for i, attrs in enumerate(layer_attrs):
-        ch = []
-        for a in attrs:
-            ch.append(_pb_bytes(1, _pb_varint(1, next_id) + _pb_bytes(2, a.encode())))
-            key = f"layer_with_weights-{i}/{a}/.ATTRIBUTES/VARIABLE_VALUE"
-            var_nodes.append(_pb_bytes(2, _pb_bytes(1, b"VARIABLE_VALUE") + _pb_bytes(2, a.encode()) +
-                                       _pb_bytes(3, key.encode())))
-            next_id += 1
-        nodes.append(b''.join(ch))
-    nodes += var_nodes
+VAR_SUFFIX = "/.ATTRIBUTES/VARIABLE_VALUE"
+SLOT_MARK = "/.OPTIMIZER_SLOT/"
+
+
+def object_graph_from_keys(keys) -> bytes:
+    """A TrackableObjectGraph (trackable_object_graph.proto) for the checkpoint keys of an object-based save.
+
+    Every path component is an ObjectReference (node id, local name) from its parent; a variable node carries
+    one SerializedTensor (name "VARIABLE_VALUE", full_name, checkpoint_key). Slot keys
+    ``<variable path>/.OPTIMIZER_SLOT/<optimizer path>/<slot>/.ATTRIBUTES/VARIABLE_VALUE`` become slot-variable
+    nodes listed by the optimizer node's SlotVariableReferences (original variable node, slot name, slot node).
+    Node ids are assigned breadth first, children in first-appearance order, as TF's saver does."""
+    children: Dict[tuple, List[str]] = {(): []}
+    variables: Dict[tuple, str] = {}
+    slots = []                                     # (variable path, optimizer path, slot name, key)
+
+    def add_path(path: tuple):
+        for i in range(len(path)):
+            parent, name = path[:i], path[i]
+            if path[:i + 1] not in children:
+                children[path[:i + 1]] = []
+                children[parent].append(name)
+
+    for key in keys:
+        if key == OBJECT_GRAPH_KEY or not key.endswith(VAR_SUFFIX):
+            continue
+        body = key[:-len(VAR_SUFFIX)]
+        if SLOT_MARK in body:
+            var, rest = body.split(SLOT_MARK, 1)
+            opt, slot = rest.rsplit('/', 1)
+            add_path(tuple(var.split('/')))
+            add_path(tuple(opt.split('/')))
+            slots.append((tuple(var.split('/')), tuple(opt.split('/')), slot, key))
+        else:
+            path = tuple(body.split('/'))
+            add_path(path)
+            variables[path] = key
+    ids: Dict[tuple, int] = {(): 0}
+    order = [()]
+    for path in order:                              # breadth first
+        for name in children[path]:
+            child = path + (name,)
+            ids[child] = len(order)
+            order.append(child)
+    slot_ids = [len(order) + i for i in range(len(slots))]
+    nodes = []
+    for path in order:
+        msg = b''.join(_pb_bytes(1, _pb_varint(1, ids[path + (n,)]) + _pb_bytes(2, n.encode()))
+                       for n in children[path])
+        if path in variables:
+            msg += _pb_bytes(2, _pb_bytes(1, b"VARIABLE_VALUE") + _pb_bytes(2, "/".join(path).encode()) +
+                             _pb_bytes(3, variables[path].encode()))
+        for (var, opt, slot, _), sid in zip(slots, slot_ids):
+            if opt == path:
+                msg += _pb_bytes(3, _pb_varint(1, ids[var]) + _pb_bytes(2, slot.encode()) + _pb_varint(3, sid))
+        nodes.append(msg)
+    for (var, opt, slot, key) in slots:
+        nodes.append(_pb_bytes(2, _pb_bytes(1, b"VARIABLE_VALUE") + _pb_bytes(2, f"{'/'.join(var)}/{slot}".encode()) +
+                               _pb_bytes(3, key.encode())))
     return b''.join(_pb_bytes(1, n) for n in nodes)
+
+
+def parse_object_graph(buf: bytes) -> List[dict]:
+    """The nodes of a serialized TrackableObjectGraph: [{'children': [(id, name)], 'keys': [checkpoint_key],
+    'slots': [(original id, slot name, slot id)]}] (for tests and inspection)."""
+    out = []
+    for fn, _, node in _pb_fields(buf):
+        if fn != 1:
+            continue
+        d = {'children': [], 'keys': [], 'slots': []}
+        for f2, _, v in _pb_fields(node):
+            if f2 == 1:
+                ref = dict((f3, v3) for f3, _, v3 in _pb_fields(v))
+                d['children'].append((ref.get(1, 0), bytes(ref.get(2, b'')).decode()))
+            elif f2 == 2:
+                st = dict((f3, v3) for f3, _, v3 in _pb_fields(v))
+                d['keys'].append(bytes(st.get(3, b'')).decode())
+            elif f2 == 3:
+                sr = dict((f3, v3) for f3, _, v3 in _pb_fields(v))
+                d['slots'].append((sr.get(1, 0), bytes(sr.get(2, b'')).decode(), sr.get(3, 0)))
+        out.append(d)
+    return out
+
+
+def _write_state_file(prefix) -> None:
+    """TF's ``checkpoint`` state file (CheckpointState text proto) beside ``prefix``."""
+    state = Path(str(prefix)).parent / "checkpoint"
+    name = Path(str(prefix)).name
+    state.write_text(f'model_checkpoint_path: "{name}"\nall_model_checkpoint_paths: "{name}"\n')
 
 
 def save_keras_weights(prefix, weights: List[np.ndarray], layer_attrs: List[List[str]]) -> None:
     """Model.save_weights(prefix) (TF format) of a functional model whose weighted layers own the
     attributes ``layer_attrs[i]`` in get_weights() order."""
-    tensors, it = {}, iter(weights)
-    for i, attrs in enumerate(layer_attrs):
-        for a in attrs:
-            tensors[f"layer_with_weights-{i}/{a}/.ATTRIBUTES/VARIABLE_VALUE"] = np.asarray(next(it), np.float32)
-    if next(it, None) is not None:
-        raise ValueError("more weights than layer attributes")
-    write_checkpoint(prefix, tensors, object_graph=_object_graph(layer_attrs))
-    state = Path(str(prefix)).parent / "checkpoint"
-    name = Path(str(prefix)).name
-    state.write_text(f'model_checkpoint_path: "{name}"\nall_model_checkpoint_paths: "{name}"\n')
+    tensors = LayerTree(layer_attrs).tensors(weights)
+    write_checkpoint(prefix, tensors, object_graph=object_graph_from_keys(tensors))
+    _write_state_file(prefix)
+
+
+# ------------------------------------------------------------------------------------------ Keras layouts
+class LayerTree:
+    """The weighted layers of a Keras functional model, in model order.
+
+    ``Functional._layer_checkpoint_dependencies`` (Keras 2.9, not vendored) names the i-th layer that owns
+    weights ``layer_with_weights-i``, and an object-based checkpoint keys every variable by the first path
+    a breadth-first walk from the root reaches it by: ``layer_with_weights-i/<attr>`` for a layer, and
+    ``layer_with_weights-i/layer_with_weights-j/<attr>`` for a layer of a sub-model used as a layer (the
+    style predictor and the transfer network inside the inference model,
+    styleTransferInferenceModel.py:24,37; MobileNetV3Small inside the predictor, stylePrediction.py:33,52).
+    An entry is either a list of attribute names (a layer, in its get_weights() order) or a nested LayerTree."""
+
+    def __init__(self, entries):
+        self.entries = [e if isinstance(e, LayerTree) else list(e) for e in entries]
+
+    def paths(self, prefix: str = "") -> List[str]:
+        """Variable paths (checkpoint keys without the ``/.ATTRIBUTES/VARIABLE_VALUE`` suffix) in the
+        model's get_weights() order."""
+        out = []
+        for i, e in enumerate(self.entries):
+            p = f"{prefix}layer_with_weights-{i}/"
+            out += e.paths(p) if isinstance(e, LayerTree) else [p + a for a in e]
+        return out
+
+    def __len__(self):
+        return len(self.paths())
+
+    def tensors(self, weights, prefix: str = "") -> Dict[str, np.ndarray]:
+        paths = self.paths(prefix)
+        weights = list(weights)
+        if len(weights) != len(paths):
+            raise ValueError(f"{len(weights)} weights for {len(paths)} layer variables")
+        return {p + VAR_SUFFIX: np.asarray(w, np.float32) for p, w in zip(paths, weights)}
+
+    def weights(self, tensors: Dict[str, np.ndarray], prefix: str = "", shapes=None) -> Optional[List[np.ndarray]]:
+        """The get_weights() list stored under ``prefix``; None when the checkpoint holds none of these
+        variables; ValueError when it holds only some of them or with other shapes (Keras raises on a
+        shape mismatch too)."""
+        keys = [p + VAR_SUFFIX for p in self.paths(prefix)]
+        present = [k in tensors for k in keys]
+        if not any(present):
+            return None
+        if not all(present):
+            missing = [k for k, p in zip(keys, present) if not p]
+            raise ValueError(f"checkpoint holds {sum(present)} of {len(keys)} variables under {prefix!r}; "
+                             f"missing e.g. {missing[:3]}")
+        out = [np.asarray(tensors[k], np.float32) for k in keys]
+        if shapes is not None:
+            got = [tuple(a.shape) for a in out]
+            want = [tuple(s) for s in shapes]
+            if got != want:
+                bad = next(i for i, (g, w) in enumerate(zip(got, want)) if g != w)
+                raise ValueError(f"checkpoint variable {keys[bad]} has shape {got[bad]}, the model expects {want[bad]}")
+        return out
+
+
+def layer_tree_from_names(names: List[str]) -> LayerTree:
+    """Group ``<layer name>/<attr>`` weight names (get_weights() order) into layers."""
+    entries, last = [], None
+    for n in names:
+        layer, attr = n.rsplit('/', 1)
+        if layer != last:
+            entries.append([])
+            last = layer
+        entries[-1].append(attr)
+    return LayerTree(entries)
+
+
+class CheckpointLoadStatus:
+    """What ``Model.load_weights`` / ``Checkpoint.restore`` return (TF's CheckpointLoadStatus): which model
+    variables were restored, which checkpoint values no model variable took, which model variables the
+    checkpoint did not hold."""
+
+    def __init__(self, restored=(), unused=(), missing=()):
+        self.restored, self.unused, self.missing = list(restored), list(unused), list(missing)
+
+    def assert_nontrivial_match(self):
+        """predict_using_checkpoint.py:85: at least one model variable came from the checkpoint."""
+        if not self.restored:
+            raise AssertionError("nothing except the root object matched a checkpointed value")
+        return self
+
+    def assert_existing_objects_matched(self):
+        if self.missing:
+            raise AssertionError(f"{len(self.missing)} model variables not in the checkpoint, e.g. {self.missing[:3]}")
+        return self
+
+    def assert_consumed(self):
+        self.assert_existing_objects_matched()
+        if self.unused:
+            raise AssertionError(f"unresolved checkpoint values, e.g. {self.unused[:3]}")
+        return self
+
+    def expect_partial(self):
+        return self
+
+    def run_restore_ops(self, session=None):
+        """Eager: the restore already ran."""
+
+
+class _Part:
+    """One sub-model's variables inside a checkpoint: its key prefix, layer tree and weight accessors."""
+
+    def __init__(self, prefix: str, tree: LayerTree, get, set_, shapes):
+        self.prefix, self.tree, self.get, self.set, self.shapes = prefix, tree, get, set_, shapes
+
+
+def parts_tensors(parts) -> Dict[str, np.ndarray]:
+    out = {}
+    for p in parts:
+        out.update(p.tree.tensors(p.get(), p.prefix))
+    return out
+
+
+def restore_parts(parts, tensors: Dict[str, np.ndarray], extra_keys=()) -> CheckpointLoadStatus:
+    """Set every part whose variables the checkpoint holds; report the rest. ``extra_keys``: further
+    checkpoint keys the caller consumed (optimizer state)."""
+    restored, missing, used = [], [], set(extra_keys)
+    loaded = []
+    for p in parts:
+        w = p.tree.weights(tensors, p.prefix, p.shapes)       # raises on a partial / mis-shaped match
+        keys = [k + VAR_SUFFIX for k in p.tree.paths(p.prefix)]
+        if w is None:
+            missing += keys
+        else:
+            loaded.append((p, w))
+            restored += keys
+            used.update(keys)
+    for p, w in loaded:
+        p.set(w)
+    unused = [k for k in tensors if k not in used and k != OBJECT_GRAPH_KEY and not k.startswith("save_counter/")]
+    return CheckpointLoadStatus(restored, unused, missing)
+
+
+def save_object(prefix, tensors: Dict[str, np.ndarray], state_file: bool = True) -> str:
+    """Write an object-based checkpoint with its TrackableObjectGraph; returns the prefix."""
+    write_checkpoint(prefix, tensors, object_graph=object_graph_from_keys(tensors))
+    if state_file:
+        _write_state_file(prefix)
+    return str(prefix)
+
+
+def latest_checkpoint(checkpoint_dir) -> Optional[str]:
+    """tf.train.latest_checkpoint (train_network.py:109): the prefix the directory's state file names."""
+    try:
+        return _resolve_prefix(Path(checkpoint_dir)) if Path(checkpoint_dir).is_dir() else None
+    except (FileNotFoundError, ValueError):
+        return None
+
+
+def load_weights(model, filepath) -> CheckpointLoadStatus:
+    """``Model.load_weights(filepath)`` for any mirror model exposing ``_restore_tensors``."""
+    return model._restore_tensors(read_checkpoint(filepath))
+
+
+def save_weights(model, filepath) -> None:
+    """``Model.save_weights(filepath)`` (TF format, tracing/checkpoint.py:37)."""
+    save_object(filepath, model._checkpoint_tensors())
+
+
+class Checkpoint:
+    """``tf.train.Checkpoint(root)`` / ``tf.train.Checkpoint(name=obj, ...)`` over the mirror models
+    (save_using_checkpoint.py:65-66, train_network.py:112-113, tracing/checkpoint.py:21-36). A positional
+    root is checkpointed at the top level (Model.save_weights keys); keyword objects under their names.
+    ``save`` numbers the prefix with ``save_counter`` (saved as ``save_counter``, int64), ``write`` does not."""
+
+    def __init__(self, root=None, **kwargs):
+        self.root = root
+        self.named = dict(kwargs)
+        self.save_counter = 0
+
+    def _objects(self):
+        objs = [("", self.root)] if self.root is not None else []
+        return objs + [(f"{k}/", v) for k, v in self.named.items()]
+
+    def _tensors(self) -> Dict[str, np.ndarray]:
+        out = {}
+        for pre, obj in self._objects():
+            out.update({pre + k: v for k, v in obj._checkpoint_tensors().items()})
+        out["save_counter" + VAR_SUFFIX] = np.array(self.save_counter, np.int64)
+        return out
+
+    def write(self, file_prefix) -> str:
+        return save_object(file_prefix, self._tensors(), state_file=False)
+
+    def save(self, file_prefix) -> str:
+        self.save_counter += 1
+        prefix = f"{file_prefix}-{self.save_counter}"
+        save_object(prefix, self._tensors())
+        return prefix
+
+    def restore(self, save_path) -> CheckpointLoadStatus:
+        if save_path is None:
+            return CheckpointLoadStatus()
+        tensors = read_checkpoint(save_path)
+        restored, missing = [], []
+        claimed = set()
+        for pre, obj in self._objects():
+            sub = {k[len(pre):]: v for k, v in tensors.items() if k.startswith(pre)}
+            st = obj._restore_tensors(sub)
+            restored += [pre + k for k in st.restored]
+            missing += [pre + k for k in st.missing]
+            unused_sub = set(st.unused)
+            claimed.update(pre + k for k in sub if k not in unused_sub)
+        sc = tensors.get("save_counter" + VAR_SUFFIX)
+        if sc is not None:
+            self.save_counter = int(sc)
+            claimed.add("save_counter" + VAR_SUFFIX)
+        unused = [k for k in tensors if k not in claimed and k != OBJECT_GRAPH_KEY]
+        return CheckpointLoadStatus(restored, unused, missing)
+
+    read = restore
+
+
+class CheckpointManager:
+    """``tf.train.CheckpointManager`` as tracing/checkpoint.py:22-34 uses it: numbered saves
+    ``<directory>/<checkpoint_name>-<n>``, the ``checkpoint`` state file, at most ``max_to_keep`` kept."""
+
+    def __init__(self, checkpoint: Checkpoint, directory, max_to_keep: Optional[int] = 5,
+                 checkpoint_name: str = "ckpt", checkpoint_interval=None, step_counter=None):
+        self.checkpoint, self.directory = checkpoint, Path(directory)
+        self.max_to_keep, self.checkpoint_name = max_to_keep, checkpoint_name
+        self.checkpoints: List[str] = []
+        self.directory.mkdir(parents=True, exist_ok=True)
+
+    @property
+    def latest_checkpoint(self) -> Optional[str]:
+        return self.checkpoints[-1] if self.checkpoints else None
+
+    def save(self, checkpoint_number=None, check_interval: bool = True) -> str:
+        n = int(checkpoint_number) if checkpoint_number is not None else self.checkpoint.save_counter + 1
+        prefix = self.directory / f"{self.checkpoint_name}-{n}"
+        self.checkpoint.save_counter = n
+        save_object(prefix, self.checkpoint._tensors(), state_file=False)
+        self.checkpoints = [c for c in self.checkpoints if c != str(prefix)] + [str(prefix)]
+        while self.max_to_keep is not None and len(self.checkpoints) > self.max_to_keep:
+            old = self.checkpoints.pop(0)
+            for f in Path(old).parent.glob(Path(old).name + ".*"):
+                f.unlink()
+        names = [Path(c).name for c in self.checkpoints]
+        (self.directory / "checkpoint").write_text(
+            f'model_checkpoint_path: "{names[-1]}"\n' + ''.join(f'all_model_checkpoint_paths: "{n}"\n' for n in names))
+        return str(prefix)

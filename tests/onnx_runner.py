@@ -4,7 +4,8 @@ Test infrastructure: executes a graph decoded by ``onnx_export.read_model`` so t
 be compared with the float64 oracle. Operator semantics follow the ONNX operator specification (opset
 17): NCHW Conv / ConvTranspose with explicit pads [begin_h, begin_w, end_h, end_w], BatchNormalization
 in inference mode, ReduceMean with the ``axes`` attribute, Slice with tensor inputs, Reshape with 0 =
-copy the input dimension, HardSigmoid max(0, min(1, alpha x + beta)), HardSwish x HardSigmoid(1/6, 1/2).
+copy the input dimension, HardSigmoid max(0, min(1, alpha x + beta)), HardSwish x HardSigmoid(1/6, 1/2),
+ReduceSum with axes as an input, Concat, AveragePool (no pads, floor mode).
 """
 import numpy as np
 
@@ -99,6 +100,20 @@ def run(model, feeds):
             y = a[0].reshape(shape)
         elif op == 'Identity':
             y = a[0]
+        elif op == 'ReduceSum':                       # opset 13+: axes as the second input
+            y = a[0].sum(axis=tuple(int(v) for v in a[1]), keepdims=bool(at.get('keepdims', 1)))
+        elif op == 'Concat':
+            y = np.concatenate(a, axis=at['axis'])
+        elif op == 'AveragePool':                     # no pads, floor mode: Keras AvgPool2D(2) 'valid'
+            kh, kw = at['kernel_shape']
+            sh, sw = at['strides']
+            N, C, H, W = a[0].shape
+            Ho, Wo = (H - kh) // sh + 1, (W - kw) // sw + 1
+            y = np.zeros((N, C, Ho, Wo))
+            for ky in range(kh):
+                for kx in range(kw):
+                    y += a[0][:, :, ky:ky + sh * (Ho - 1) + 1:sh, kx:kx + sw * (Wo - 1) + 1:sw]
+            y /= kh * kw
         else:
             raise NotImplementedError(op)
         env[outs[0]] = y

@@ -142,3 +142,145 @@ def test_string_tensor_checksums_follow_tensorflow(tmp_path):
     (tmp_path / "g.data-00000-of-00001").write_bytes(bytes(bad))
     with pytest.raises(ValueError):
         ck.read_checkpoint(prefix, with_strings=True)
+
+
+# ------------------------------------------------------------------ composite models (verdict r03 item 1)
+class _HostModel:
+    """A host-only stand-in for a mirror model: its weights live in numpy lists behind tf_checkpoint._Part
+    accessors, exactly as the GPU models wire theirs (so the key layout and restore logic run on the CPU)."""
+
+    def __init__(self, groups):
+        self.store = {name: [np.array(w) for w in ws] for name, (_, _, ws) in groups.items()}
+        self.parts = []
+        for name, (prefix, tree, ws) in groups.items():
+            self.parts.append(ck._Part(prefix, tree, (lambda n=name: self.store[n]),
+                                       (lambda w, n=name: self.store.__setitem__(n, [np.array(a) for a in w])),
+                                       [a.shape for a in ws]))
+
+    def _checkpoint_tensors(self):
+        return ck.parts_tensors(self.parts)
+
+    def _restore_tensors(self, tensors):
+        return ck.restore_parts(self.parts, tensors)
+
+
+def _inference_layout(extractor="MOBILE_NET", pseed=4, tseed=3):
+    from realtime_style_transfer_amd.styleTransfer import transfer_layer_attributes
+    from realtime_style_transfer_amd.stylePrediction import (init_predictor_weights, predictor_layer_tree,
+                                                              predictor_weight_spec)
+    plan = network_plan((32, 64, 17), (32, 64, 3), 8, 8)
+    spec = predictor_weight_spec((32, 64, 3), extractor, plan.num_style_params)
+    return {"predictor": ("layer_with_weights-0/", predictor_layer_tree(spec),
+                          init_predictor_weights(spec, seed=pseed, perturb=True)),
+            "transfer": ("layer_with_weights-1/", ck.LayerTree(transfer_layer_attributes(plan)),
+                         init_weights(plan, seed=tseed))}
+
+
+def test_inference_model_key_layout():
+    """styleTransferInferenceModel.py:9-39: predictor = layer_with_weights-0 (MobileNetV3Small nested one level
+    further, stylePrediction.py:33-52), transfer = layer_with_weights-1; Keras get_weights() order within each."""
+    g = _inference_layout()
+    t = _HostModel(g)._checkpoint_tensors()
+    V = ck.VAR_SUFFIX
+    assert t["layer_with_weights-0/layer_with_weights-0/layer_with_weights-0/kernel" + V].shape == (3, 3, 3, 16)
+    assert t["layer_with_weights-0/layer_with_weights-0/layer_with_weights-1/moving_variance" + V].shape == (16,)
+    assert t["layer_with_weights-0/layer_with_weights-0/layer_with_weights-2/depthwise_kernel" + V].shape == (3, 3, 16, 1)
+    assert t["layer_with_weights-0/layer_with_weights-1/kernel" + V].shape == (1, 1, 576, 100)     # StylePredictor
+    P = network_plan((32, 64, 17), (32, 64, 3), 8, 8).num_style_params
+    assert t["layer_with_weights-0/layer_with_weights-2/bias" + V].shape == (P,)                   # StyleNormPredictor
+    assert t["layer_with_weights-1/layer_with_weights-0/kernel" + V].shape == (9, 9, 17, 32)       # start conv
+    assert t["layer_with_weights-1/layer_with_weights-1/moving_mean" + V].shape == (32,)           # its BN
+    n_pred, n_tr = len(g["predictor"][2]), len(g["transfer"][2])
+    assert len(t) == n_pred + n_tr
+    # DUMMY: dummy_conv is a plain layer of the predictor (no nesting)
+    d = _HostModel(_inference_layout("DUMMY"))._checkpoint_tensors()
+    assert d["layer_with_weights-0/layer_with_weights-0/kernel" + V].shape == (9, 9, 3, 1)
+    assert d["layer_with_weights-0/layer_with_weights-2/kernel" + V].shape[:3] == (1, 1, 100)
+
+
+def test_inference_checkpoint_roundtrip_bit_exact(tmp_path):
+    a = _HostModel(_inference_layout(pseed=4, tseed=3))
+    b = _HostModel(_inference_layout(pseed=8, tseed=9))
+    ck.save_weights(a, tmp_path / "weights")
+    st = ck.load_weights(b, tmp_path)                      # directory -> the 'checkpoint' state file
+    st.assert_nontrivial_match().assert_consumed()
+    for name in a.store:
+        assert all(np.array_equal(x, y) and x.dtype == y.dtype for x, y in zip(a.store[name], b.store[name]))
+    # the object graph: root -> the two sub-models -> their layers; every variable key reachable
+    r = ck.read_checkpoint(tmp_path / "weights", with_strings=True)
+    nodes = ck.parse_object_graph(r.pop(ck.OBJECT_GRAPH_KEY).item())
+    assert [n for _, n in nodes[0]['children']] == ["layer_with_weights-0", "layer_with_weights-1"]
+    assert sorted(k for n in nodes for k in n['keys']) == sorted(r)
+
+
+def test_partial_and_mismatched_checkpoints(tmp_path):
+    a = _HostModel(_inference_layout())
+    t = a._checkpoint_tensors()
+    # only the transfer network (e.g. a transfer model saved alone, nested by the caller): predictor untouched
+    only_t = {k: v for k, v in t.items() if k.startswith("layer_with_weights-1/")}
+    b = _HostModel(_inference_layout(pseed=8, tseed=9))
+    before = [w.copy() for w in b.store["predictor"]]
+    st = b._restore_tensors(only_t)
+    st.assert_nontrivial_match()
+    assert st.missing and all(k.startswith("layer_with_weights-0/") for k in st.missing)
+    with pytest.raises(AssertionError):
+        st.assert_consumed()
+    assert all(np.array_equal(x, y) for x, y in zip(before, b.store["predictor"]))
+    assert all(np.array_equal(x, y) for x, y in zip(a.store["transfer"], b.store["transfer"]))
+    # nothing matches -> assert_nontrivial_match raises (predict_using_checkpoint.py:85)
+    with pytest.raises(AssertionError):
+        b._restore_tensors({"other/x" + ck.VAR_SUFFIX: np.zeros(3, np.float32)}).assert_nontrivial_match()
+    # a sub-model with one variable missing, or one of another shape: refused before anything is set
+    broken = dict(t)
+    broken.pop("layer_with_weights-1/layer_with_weights-2/bias" + ck.VAR_SUFFIX)
+    with pytest.raises(ValueError, match="holds"):
+        b._restore_tensors(broken)
+    bad = dict(t)
+    bad["layer_with_weights-1/layer_with_weights-0/kernel" + ck.VAR_SUFFIX] = np.zeros((3, 3, 17, 32), np.float32)
+    with pytest.raises(ValueError, match="shape"):
+        b._restore_tensors(bad)
+
+
+def test_checkpoint_manager_and_save_counter(tmp_path):
+    """tracing/checkpoint.py:21-37: tf.train.Checkpoint(model) + CheckpointManager(max_to_keep) saves; train_network.py:
+    109-113 restores the latest one and reads save_counter."""
+    a = _HostModel(_inference_layout())
+    c = ck.Checkpoint(a)
+    mgr = ck.CheckpointManager(c, tmp_path / "checkpoints", checkpoint_name="ckpt", max_to_keep=2)
+    for epoch in (1, 2, 3):
+        mgr.save(epoch)
+    files = sorted(p.name for p in (tmp_path / "checkpoints").iterdir())
+    assert "ckpt-1.index" not in files and "ckpt-2.index" in files and "ckpt-3.index" in files
+    latest = ck.latest_checkpoint(tmp_path / "checkpoints")
+    assert latest.endswith("ckpt-3") and mgr.latest_checkpoint == latest
+    b = _HostModel(_inference_layout(pseed=8, tseed=9))
+    cb = ck.Checkpoint(b)
+    cb.restore(latest).assert_consumed()
+    assert cb.save_counter == 3
+    assert all(np.array_equal(x, y) for x, y in zip(a.store["transfer"], b.store["transfer"]))
+    # keyword objects nest under their names
+    p = ck.Checkpoint(model=a).save(tmp_path / "kw")
+    assert p.endswith("kw-1")
+    keys = ck.read_checkpoint(p)
+    assert "model/layer_with_weights-1/layer_with_weights-0/kernel" + ck.VAR_SUFFIX in keys
+    assert int(keys["save_counter" + ck.VAR_SUFFIX]) == 1
+
+
+def test_object_graph_slot_variables():
+    """Optimizer slots: <variable>/.OPTIMIZER_SLOT/optimizer/rms keys become slot-variable nodes that the optimizer
+    node references (original variable node, slot name, slot node)."""
+    V = ck.VAR_SUFFIX
+    keys = ["layer_with_weights-0/kernel" + V, "layer_with_weights-0/bias" + V,
+            "layer_with_weights-0/kernel/.OPTIMIZER_SLOT/optimizer/rms" + V, "optimizer/iter" + V]
+    nodes = ck.parse_object_graph(ck.object_graph_from_keys(keys))
+    names = {}
+    def walk(i, path):
+        names[i] = path
+        for c, n in nodes[i]['children']:
+            walk(c, path + (n,))
+    walk(0, ())
+    opt = next(i for i, p in names.items() if p == ("optimizer",))
+    kern = next(i for i, p in names.items() if p == ("layer_with_weights-0", "kernel"))
+    (orig, slot, sid), = nodes[opt]['slots']
+    assert orig == kern and slot == "rms"
+    assert nodes[sid]['keys'] == ["layer_with_weights-0/kernel/.OPTIMIZER_SLOT/optimizer/rms" + V]

@@ -1,7 +1,8 @@
 """The reference's inference / export entry scripts' model-building sequences, restated against the mirror
 modules and run on the device at the scripts' own configuration (ShapeConfig(hdr=True): 480x960x18 G-buffer
 frames, MOBILE_NET style predictor, StyleLossModelMobileNet, the depth term on by default). No checkpoint
-ships with the reference, so the seeded initial weights stand in for load_weights / Checkpoint.restore.
+ships with the reference: the checkpoint tests save one from a seeded model and restore it into a model built
+with other seeds (load_weights / Checkpoint.restore / CheckpointManager, the reference's nested key layout).
 
 * predict_using_checkpoint.py:42-99   one and two styles: build the inference model, setup_model (trainable,
                                       compile), call it on the dummy element, predict -> uint8 export
@@ -111,3 +112,109 @@ def test_save_using_checkpoint_sequence():
     with pytest.raises(NotImplementedError):
         m.training.train_step(element, ground_truth_element)
     assert len(m.transfer.get_weights()) == len(m.training.get_weights())
+
+
+def _inference_models(config, pseed, tseed):
+    return styleTransferTrainingModel.make_style_transfer_inference_model(
+        num_styles=config.num_styles,
+        style_predictor_factory_func=lambda P: stylePrediction.create_style_prediction_model(
+            config.input_shape['style'][1:], config.style_feature_extractor_type, P, seed=pseed),
+        style_transfer_factory_func=lambda: styleTransfer.create_style_transfer_model(
+            config.input_shape['content'], config.output_shape, config.bottleneck_res_y,
+            config.bottleneck_num_filters, config.num_styles, seed=tseed))
+
+
+def test_inference_load_weights_reproduces_outputs(tmp_path):
+    """predict_using_checkpoint.py:84-85: inference.load_weights(path).assert_nontrivial_match() on the full
+    ShapeConfig(hdr=True) model (MobileNetV3Small predictor nested under the functional inference model)."""
+    _need_gpu()
+    config = ShapeConfig(hdr=True, num_styles=1)
+    a, b = _inference_models(config, 3, 2), _inference_models(config, 13, 12)
+    rng = np.random.default_rng(5)
+    element = {'style': torch.from_numpy(rng.random((1, 1) + config.output_shape, dtype=np.float32)).cuda(),
+               'content': torch.from_numpy(rng.random((1,) + config.input_shape['content'], dtype=np.float32)).cuda()}
+    ya = a.inference(element)
+    assert not torch.equal(ya, b.inference(element))
+    a.inference.save_weights(tmp_path / "latest_epoch_weights")
+    st = b.inference.load_weights(tmp_path / "latest_epoch_weights")
+    st.assert_nontrivial_match()
+    st.assert_consumed()
+    assert torch.equal(b.inference(element), ya)
+    # the sub-models alone hold the same weights as the saving model's
+    assert all(np.array_equal(x, y) for x, y in zip(a.transfer.get_weights(), b.transfer.get_weights()))
+    assert all(np.array_equal(x, y) for x, y in zip(a.style_predictor.get_weights(), b.style_predictor.get_weights()))
+
+
+def _training_models(pseed, tseed, oe=(32, 64, 3)):
+    ie = (32, 64, 17)
+    return styleTransferTrainingModel.make_style_transfer_training_model(
+        style_predictor_factory_func=lambda P: stylePrediction.create_style_prediction_model(
+            oe, stylePrediction.StyleFeatureExtractor.MOBILE_NET, P, seed=pseed),
+        style_transfer_factory_func=lambda: styleTransfer.create_style_transfer_model(
+            ie, oe, 8, 8, 1, seed=tseed, max_batch=2),
+        style_loss_func_factory_func=lambda: styleLoss.make_style_loss_function(
+            styleLoss.StyleLossModelVGG(oe, max_batch=2), oe, 1, with_depth_loss=False),
+        max_batch=2)
+
+
+def _batch(seed, oe=(32, 64, 3)):
+    rng = np.random.default_rng(seed)
+    f = lambda *s: torch.from_numpy(rng.random(s, dtype=np.float32)).cuda()
+    return {'content': f(2, 32, 64, 17), 'style': f(2, 1, *oe)}, {'content': f(2, *oe), 'style': f(2, 1, *oe)}
+
+
+def test_training_checkpoint_restore_continues_bitwise(tmp_path):
+    """predict_video_using_checkpoint.py:74 (training.load_weights), save_using_checkpoint.py:65-66 and
+    train_network.py:112-113 (tf.train.Checkpoint(model).restore), tracing/checkpoint.py:21-37 (CheckpointManager
+    saves): a checkpoint taken after a step restores the predictor + transfer weights and the RMSprop state, so the
+    restored model's next step equals the saving model's next step bitwise."""
+    _need_gpu()
+    from realtime_style_transfer_amd import tf_checkpoint as ck
+    a, b = _training_models(3, 2), _training_models(13, 12)
+    x0, y0 = _batch(1)
+    a.training.train_step(x0, y0)
+    a.training.save_weights(tmp_path / "weights" / "latest_epoch_weights")
+    st = b.training.load_weights(tmp_path / "weights" / "latest_epoch_weights")
+    st.assert_nontrivial_match()
+    st.assert_consumed()
+    assert b.training.iterations == a.training.iterations == 1
+    for get in (lambda m: m.training.get_weights(), lambda m: m.training.style_predictor.get_weights(),
+                lambda m: m.training.optimizer_slots(), lambda m: m.training.style_predictor.optimizer_slots()):
+        assert all(np.array_equal(u, v) for u, v in zip(get(a), get(b)))
+    # the inference view shares the training model's variables (styleTransferTrainingModel.py:66)
+    a.refresh()
+    xi = {'content': x0['content'], 'style': x0['style']}
+    assert torch.equal(a.inference(xi), b.inference(xi))
+    x1, y1 = _batch(2)
+    a.training.train_step(x1, y1)
+    b.training.train_step(x1, y1)
+    assert all(np.array_equal(u, v) for u, v in zip(a.training.get_weights(), b.training.get_weights()))
+    assert all(np.array_equal(u, v) for u, v in
+               zip(a.training.style_predictor.get_weights(), b.training.style_predictor.get_weights()))
+    # CheckpointManager + Checkpoint(training).restore; inference.load_weights of a training checkpoint
+    mgr = ck.CheckpointManager(ck.Checkpoint(a.training), tmp_path / "checkpoints", max_to_keep=5)
+    mgr.save(7)
+    c = _training_models(23, 22)
+    chk = ck.Checkpoint(c.training)
+    chk.restore(ck.latest_checkpoint(tmp_path / "checkpoints")).assert_consumed()
+    assert chk.save_counter == 7
+    assert all(np.array_equal(u, v) for u, v in zip(a.training.get_weights(), c.training.get_weights()))
+    d = _training_models(33, 32)
+    d.inference.load_weights(mgr.latest_checkpoint).assert_nontrivial_match()
+    a.refresh()
+    assert torch.equal(a.inference(xi), d.inference(xi))
+    assert all(np.array_equal(u, v) for u, v in zip(a.training.get_weights(), d.training.get_weights()))
+
+
+def test_failed_step_between_targets_and_gradients_recovers():
+    """a step that fails after compute_targets (here the predictor forward raises on a bad style batch)
+    must not wedge the trainer: the next train_step runs and matches a fresh model's step."""
+    _need_gpu()
+    a, b = _training_models(3, 2), _training_models(3, 2)
+    x, y = _batch(1)
+    bad = {'content': x['content'], 'style': torch.zeros((2, 1, 16, 16, 3), device='cuda')}
+    with pytest.raises(ValueError):
+        a.training.train_step(bad, y)
+    a.training.train_step(x, y)
+    b.training.train_step(x, y)
+    assert all(np.array_equal(u, v) for u, v in zip(a.training.get_weights(), b.training.get_weights()))

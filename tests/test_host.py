@@ -99,3 +99,59 @@ def test_create_rejects_bad_arguments_without_device_work():
     shape3 = L.RstShape(32, 64, 17, 32, 64, 8, 8, 3, 1)   # the reference blends only two styles
     rc = lib.rst_create(ctypes.byref(shape3), w.ctypes.data, w.size, ctypes.byref(h))
     assert rc == L.RST_ERR_UNSUPPORTED
+
+
+def _cin_fixed_split(v: float):
+    """Python restatement of kernels.h cin_fixed_split (same IEEE double operations)."""
+    import math
+    a = abs(v)
+    h = math.floor(a * 2.0 ** -32)
+    r = a - h * 2.0 ** 32
+    m = math.floor(r * 2.0 ** 8)
+    r2 = r - m * 2.0 ** -8
+    k = (int(math.floor(r2 * 2.0 ** 48)), int(m), int(h))
+    return tuple(-x for x in k) if v < 0 else k
+
+
+def _cin_fixed_value(l0: int, l1: int, l2: int) -> float:
+    """kernels.h cin_fixed_value."""
+    def carry(a0, a1, a2):
+        c = a0 >> 40
+        a0 -= c << 40
+        a1 += c
+        c = a1 >> 40
+        a1 -= c << 40
+        return a0, a1, a2 + c
+    m0, m1, m2 = carry(l0, l1, l2)
+    neg = m2 < 0
+    if neg:
+        m0, m1, m2 = carry(-l0, -l1, -l2)
+    v = float(m2) * 2.0 ** 32 + (float(m1) * 2.0 ** -8 + float(m0) * 2.0 ** -48)
+    return -v if neg else v
+
+
+def test_cin_fixed_point_accumulation_is_order_independent():
+    """The inference CIN statistics are added as 64-bit integer limbs (kernels.h cin_fixed_split / cin_fixed_value):
+    integer adds commute exactly, so any arrival order of the atomics gives the same bits; the merged value is the
+    exact sum of the addends truncated at 2^-48 (per addend), i.e. at least as accurate as f64 atomics."""
+    from fractions import Fraction
+    rng = np.random.default_rng(0)
+    for scale in (1e-9, 1.0, 3e4, 1e12, 3e18):
+        vals = (rng.standard_normal(300) * scale).tolist() + [0.0, -0.0, scale, -scale]
+        limbs = [_cin_fixed_split(v) for v in vals]
+        for v, (l0, l1, l2) in zip(vals, limbs):
+            assert 0 <= abs(l0) < 2 ** 40 and 0 <= abs(l1) < 2 ** 40 and abs(l2) < 2 ** 52
+            exact = Fraction(l2) * 2 ** 32 + Fraction(l1) / 2 ** 8 + Fraction(l0) / 2 ** 48
+            assert abs(Fraction(v) - exact) < Fraction(1, 2 ** 48)            # truncation only below 2^-48
+        sums = set()
+        for _ in range(5):
+            order = rng.permutation(len(vals))
+            s = [0, 0, 0]
+            for i in order:
+                for q in range(3):
+                    s[q] += limbs[i][q]
+            sums.add(_cin_fixed_value(*s))
+        assert len(sums) == 1                                                  # bitwise independent of order
+        got = sums.pop()
+        exact = sum(Fraction(v) for v in vals)
+        assert abs(Fraction(got) - exact) <= len(vals) * Fraction(1, 2 ** 48) + abs(exact) * Fraction(1, 2 ** 52)

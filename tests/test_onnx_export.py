@@ -50,8 +50,32 @@ def test_transfer_onnx_matches_oracle(tmp_path, ins, outs, br, bf):
     np.testing.assert_allclose(y, ref, rtol=0, atol=1e-9)
 
 
-def test_transfer_onnx_rejects_two_styles(tmp_path):
-    plan = network_plan((32, 64, 17), (32, 64, 3), 8, 8, num_styles=2)
+@pytest.mark.parametrize("ins,outs,br,bf", [((32, 64, 17), (32, 64, 3), 8, 8), ((36, 52, 5), (72, 104, 3), 9, 8)])
+def test_two_style_transfer_onnx_matches_oracle(tmp_path, ins, outs, br, bf):
+    """save_using_checkpoint.py:90-103 on a num_styles=2 model: inputs content, style_params (N,2,P) and
+    style_weights (N,Ho,Wo,1); the weight mips and the per-pixel blend (styleTransfer.py:36-44,288-303,335-345)
+    executed by the numpy evaluator match the float64 oracle."""
+    plan = network_plan(ins, outs, br, bf, num_styles=2)
+    ws = init_weights(plan, seed=4)
+    m = OX.read_model(OX.save_onnx(tmp_path / "two", plan, ws)['transfer'])
+    g = m['graph']
+    assert [n for n, _ in g['inputs']] == ['content', 'style_params', 'style_weights']
+    assert g['inputs'][1][1] == ['N', 2, plan.num_style_params] and g['inputs'][2][1] == ['N', *outs[:2], 1]
+    rng = np.random.default_rng(9)
+    content = rng.random((2,) + tuple(ins)).astype(np.float32)
+    sp = synthetic_style_params(2, 2, plan.num_style_params, plan, seed=6)
+    sw = rng.random((2,) + tuple(outs[:2]) + (1,)).astype(np.float32)
+    y = onnx_runner.run(m, {'content': content, 'style_params': sp, 'style_weights': sw})['output']
+    ref = R.transfer_forward(content, sp, ws, ins, outs, br, bf, style_weights=sw)
+    assert y.shape == ref.shape
+    np.testing.assert_allclose(y, ref, rtol=0, atol=1e-9)
+    # the blend matters: style 1 alone differs
+    ref1 = R.transfer_forward(content, sp[:, :1], ws, ins, outs, br, bf)
+    assert np.abs(ref - ref1).max() > 1e-3
+
+
+def test_transfer_onnx_rejects_three_styles(tmp_path):
+    plan = network_plan((32, 64, 17), (32, 64, 3), 8, 8, num_styles=3)
     with pytest.raises(NotImplementedError):
         OX.transfer_graph(plan, init_weights(plan, seed=4))
 
