@@ -561,7 +561,8 @@ bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long lon
     return false;
 }
 
-hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
+hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a_in, hipStream_t st) {
+    const ConvArgs a = conv_wt_checked(a_in);
     switch (t.id) {
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF)                                      \
     case ID: {                                                                                   \

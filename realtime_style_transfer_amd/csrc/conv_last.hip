@@ -81,11 +81,9 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 // (x, y) -> three packed bf16 pairs, x = x0 + x1 + x2 exactly (round-to-nearest-even at each step)
 __device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned& p1, unsigned& p2) {
-    p0 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
-    const float rx = x - __uint_as_float(p0 << 16), ry = y - __uint_as_float(p0 & 0xFFFF0000u);
-    p1 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){rx, ry}, bf16x2));
-    const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xFFFF0000u);
-    p2 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){sx, sy}, bf16x2));
+    p0 = bf16_piece(x, y);
+    p1 = bf16_piece(x, y);
+    p2 = bf16_last_piece(x, y);
 }
 // Sum over the 64 lanes of a wave, the same value in every lane, fixed order (deterministic): DPP
 // butterflies inside each row of 16 (quad xor 1, xor 2, half-row mirror, row mirror), then the four row

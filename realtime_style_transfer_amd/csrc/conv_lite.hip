@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -54,11 +55,9 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 // (x, y) -> three packed bf16 pairs, x = x0 + x1 + x2 exactly (round-to-nearest-even at each step)
 __device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned& p1, unsigned& p2) {
-    p0 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
-    const float rx = x - __uint_as_float(p0 << 16), ry = y - __uint_as_float(p0 & 0xFFFF0000u);
-    p1 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){rx, ry}, bf16x2));
-    const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xFFFF0000u);
-    p2 = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){sx, sy}, bf16x2));
+    p0 = bf16_piece(x, y);
+    p1 = bf16_piece(x, y);
+    p2 = bf16_last_piece(x, y);
 }
 
 template <int MODE, int CIN, int NC, int CKC, int X6 = 0>
@@ -810,6 +809,8 @@ static int lite_slots() {
                                                          C::LDS_BYTES + lite_tab_bytes(PRO, CIN, 1)) != hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
+        if (const char* e = getenv("RST_LITE_PER_CU"))   // measurement knob: cap the resident workgroups per CU
+            if (atoi(e) > 0 && atoi(e) < per_cu) per_cu = atoi(e);
         slots = ((lite_cu_count() * per_cu) / 8) * 8;
         if (slots <= 0) slots = 8;
     }

@@ -564,8 +564,9 @@ bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
     return false;
 }
 
-hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st) {
-    if (t.bf3) return conv_bf3_launch(t, a, st);
+hipError_t conv_launch(const ConvTile& t, const ConvArgs& a_in, hipStream_t st) {
+    if (t.bf3) return conv_bf3_launch(t, a_in, st);
+    const ConvArgs a = conv_wt_checked(a_in);
     switch (t.id) {
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB) \
     case ID:                                          \

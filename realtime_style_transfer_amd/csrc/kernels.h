@@ -24,6 +24,22 @@ __device__ __forceinline__ void lds_barrier() {
 // uses (conv prologues, the standalone affine kernel, rst_style_param_map).
 __device__ __forceinline__ float style_blend(float w1, float v0, float v1) { return fmaf(w1, v1 - v0, v0); }
 
+// Exact three-piece bf16 split (the split-bf16 x6 kernels): (x, y) -> the packed bf16 pair nearest them (RNE),
+// then (x, y) -= its value. The remainder x - piece is exact in fp32 (x's own low bits); it is formed by
+// v_dot2c_f32_bf16 as x + (-1)·piece + 0·other — one VALU per value instead of a shift or mask plus a subtraction
+// (tools/dot2_split_check: bitwise the shift/subtract split on 2^24 random pairs, ties and zeros included).
+typedef float rst_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 rst_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned bf16_piece(float& x, float& y) {
+    const rst_bf16x2 p = __builtin_convertvector((rst_f32x2){x, y}, rst_bf16x2);
+    x = __builtin_amdgcn_fdot2_f32_bf16(p, (rst_bf16x2){(__bf16)-1.0f, (__bf16)0.0f}, x, false);
+    y = __builtin_amdgcn_fdot2_f32_bf16(p, (rst_bf16x2){(__bf16)0.0f, (__bf16)-1.0f}, y, false);
+    return __builtin_bit_cast(unsigned, p);
+}
+__device__ __forceinline__ unsigned bf16_last_piece(float x, float y) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((rst_f32x2){x, y}, rst_bf16x2));
+}
+
 // XCD-aware block order: the dispatcher deals workgroup ids round-robin over the 8 XCDs (each with
 // its own L2), so consecutive ids (neighbouring tiles, whose halos overlap) land on different L2s.
 // Remap so XCD x processes one contiguous run of the tile order: a bijection on [0, n).
@@ -244,6 +260,17 @@ struct ConvArgs {
     int w_next_bytes;
     int wt_stores;          // nonzero: output stored write-through (sc1), as WinoArgs::wt_stores
 };
+
+// Write-through stores address the output with 32-bit buffer offsets: the byte extent of what the kernel indexes
+// (pixel-shuffled 2Ho x 2Wo x cout for transposed convs, Ho x Wo x ntot otherwise; the fused pool is smaller) must fit,
+// or the launch falls back to plain stores (conv_launch, conv_bf3_launch)
+inline ConvArgs conv_wt_checked(const ConvArgs& a) {
+    const size_t px = a.shuffle ? (size_t)a.batch * (2 * (size_t)a.Ho) * (2 * (size_t)a.Wo) * a.cout
+                                : (size_t)a.batch * a.Ho * a.Wo * a.ntot;
+    ConvArgs b = a;
+    if (px * 4 >= (size_t)0x7FFFFFF0) b.wt_stores = 0;
+    return b;
+}
 
 // A compiled tile configuration of conv_mfma_kernel.
 struct ConvTile {

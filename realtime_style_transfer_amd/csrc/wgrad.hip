@@ -197,12 +197,7 @@ constexpr int PLANE = TR * RSB;               // bytes per piece plane (TR == TC
 typedef short short8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ unsigned piece(float& x, float& y) {   // nearest bf16 pair; (x, y) -= it (exact)
-    const unsigned p = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
-    x = x - __uint_as_float(p << 16);
-    y = y - __uint_as_float(p & 0xFFFF0000u);
-    return p;
-}
+__device__ __forceinline__ unsigned piece(float& x, float& y) { return bf16_piece(x, y); }   // nearest bf16 pair; (x, y) -= it (exact)
 }  // namespace wx6
 
 __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs a) {

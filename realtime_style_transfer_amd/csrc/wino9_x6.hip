@@ -75,12 +75,7 @@ __device__ __forceinline__ void sfor(F&& f) {
 }
 
 // (x, y) -> the bf16 pair nearest them; (x, y) -= its value (exact in fp32)
-__device__ __forceinline__ unsigned piece(float& x, float& y) {
-    const unsigned p = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
-    x = x - __uint_as_float(p << 16);
-    y = y - __uint_as_float(p & 0xFFFF0000u);
-    return p;
-}
+__device__ __forceinline__ unsigned piece(float& x, float& y) { return bf16_piece(x, y); }
 
 // eight fp32 values -> the three short8 bf16 pieces (v = p0 + p1 + p2 exactly)
 __device__ __forceinline__ void split8(const float (&v)[8], short8 (&A)[3]) {

@@ -307,11 +307,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         fx[0][c] = fx[0][c] - fx[1][c];
         fy[0][c] = fy[0][c] - fy[1][c];
     };
-    auto piece = [&](float& x, float& y, unsigned& p) __attribute__((always_inline)) {
-        p = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
-        x = x - __uint_as_float(p << 16);
-        y = y - __uint_as_float(p & 0xFFFF0000u);
-    };
+    auto piece = [&](float& x, float& y, unsigned& p) __attribute__((always_inline)) { p = bf16_piece(x, y); };
     auto last_piece = [&](float x, float y) __attribute__((always_inline)) {
         return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
     };

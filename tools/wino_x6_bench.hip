@@ -119,13 +119,15 @@ int main(int argc, char** argv) {
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         printf("finalize alone: %.2f us/launch\n", ms * 1e3 / 200);
     }
-    double* acc = nullptr;
+    cin_word* acc = nullptr;
     float* sty = nullptr;
-    if (accm) {
-        CK(hipMalloc(&acc, (size_t)8 * B * 2 * 128 * sizeof(double)));
-        std::vector<double> ha((size_t)8 * B * 2 * 128);
-        for (size_t i = 0; i < ha.size(); ++i) ha[i] = ((i / 128) % 2) ? 2.0e4 : 1.0e2;   // S ~ 1e2, Q ~ 2e4
-        CK(hipMemcpy(acc, ha.data(), ha.size() * 8, hipMemcpyHostToDevice));
+    if (accm) {   // [8 slots][B][2][CIN_LIMBS][128] fixed-point limbs (kernels.h): S ~ 1e2, Q ~ 2e4 in the 2^-8 limb
+        const size_t n_acc = (size_t)8 * B * 2 * CIN_LIMBS * 128;
+        CK(hipMalloc(&acc, n_acc * sizeof(cin_word)));
+        std::vector<cin_word> ha(n_acc, 0);
+        for (size_t i = 0; i < ha.size(); ++i)
+            if ((i / 128) % CIN_LIMBS == 1) ha[i] = (cin_word)(((i / (128 * CIN_LIMBS)) % 2 ? 2.0e4 : 1.0e2) * 256.0);
+        CK(hipMemcpy(acc, ha.data(), n_acc * sizeof(cin_word), hipMemcpyHostToDevice));
         sty = dev(host_rand((size_t)B * 2 * C, 0.5f, 1.f, 9));
     }
     const int iters = 200;
