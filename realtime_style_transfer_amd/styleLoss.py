@@ -54,9 +54,15 @@ class StyleLossModelVGG:
     """styleLoss.py:69-109 on librst."""
 
     def __init__(self, input_shape, weights: Optional[Sequence[np.ndarray]] = None, seed: int = 3,
-                 max_batch: int = 4, device=None, precision: str = "fp32"):
+                 max_batch: int = 4, device=None, precision: Optional[str] = None):
         """precision: arithmetic of the VGG16 3x3 convs with Cin % 32 == 0 — "fp32" (f32 MFMA),
-        "bf16x6" (exact 3-piece bf16 split, fp32-level products) or "bf16x3" (2-piece split)."""
+        "bf16x6" (exact 3-piece bf16 split, fp32-level products), "bf16x3" (2-piece split) or "bf16" (bf16
+        operands, fp32 accumulation: Keras mixed_bfloat16). None: from the global policy
+        (``mixed_precision.set_global_policy``, train_network.py:26) — "fp32" by default, "bf16" under
+        'mixed_bfloat16'."""
+        if precision is None:
+            from .mixed_precision import loss_network_precision
+            precision = loss_network_precision()
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"precision must be one of {list(_lib.PRECISIONS)}")
         self.precision = precision

@@ -155,3 +155,24 @@ def test_cin_fixed_point_accumulation_is_order_independent():
         got = sums.pop()
         exact = sum(Fraction(v) for v in vals)
         assert abs(Fraction(got) - exact) <= len(vals) * Fraction(1, 2 ** 48) + abs(exact) * Fraction(1, 2 ** 52)
+
+
+def test_mixed_precision_policy_selects_the_loss_network_arithmetic():
+    """tf.keras.mixed_precision.set_global_policy (train_network.py:26) -> the VGG16 loss network's precision:
+    float32 by default (the reference's run), bf16 under 'mixed_bfloat16' (BASELINE config 4)."""
+    from realtime_style_transfer_amd import mixed_precision as mp
+    try:
+        assert mp.global_policy().name == "float32" and mp.loss_network_precision() == "fp32"
+        mp.set_global_policy("mixed_bfloat16")
+        pol = mp.global_policy()
+        assert (pol.name, pol.compute_dtype, pol.variable_dtype) == ("mixed_bfloat16", "bfloat16", "float32")
+        assert mp.loss_network_precision() == "bf16"
+        mp.set_global_policy(mp.Policy("float32"))
+        assert mp.loss_network_precision() == "fp32"
+        with pytest.raises(NotImplementedError):
+            mp.set_global_policy("mixed_float16")
+        with pytest.raises(ValueError):
+            mp.set_global_policy("float64")
+        assert mp.global_policy().name == "float32"   # a refused policy leaves the global one unchanged
+    finally:
+        mp.set_global_policy("float32")
