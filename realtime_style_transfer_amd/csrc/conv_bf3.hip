@@ -478,8 +478,8 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                 }
             }
             if (a.part != nullptr) {
-                s += __shfl_xor(s, 32);
-                cnt += __shfl_xor(cnt, 32);
+                s = lane_xor_sum<32>(s);
+                cnt = lane_xor_sum<32>(cnt);
                 const float mean = cnt > 0.f ? s / cnt : 0.f;
                 float m2 = 0.f;
 #pragma unroll
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                     const float d = vals[r] - mean;
                     if (ok[r]) m2 = fmaf(d, d, m2);
                 }
-                m2 += __shfl_xor(m2, 32);
+                m2 = lane_xor_sum<32>(m2);
                 if (lh == 0 && nvalid) {
                     const int mtg = (ty * a.tiles_x + tx) * C::MT + mt;
                     a.part[((size_t)b * a.ntot + ng) * n_mtiles + mtg] = make_float4(s, m2, cnt, 0.f);

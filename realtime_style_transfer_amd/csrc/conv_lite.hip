@@ -23,7 +23,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -52,6 +51,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short short8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // (x, y) -> three packed bf16 pairs, x = x0 + x1 + x2 exactly (round-to-nearest-even at each step)
 __device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned& p1, unsigned& p2) {
@@ -72,11 +72,18 @@ struct Cfg {
     static constexpr int HC = MODE == 0 ? 2 * TW + 1 : TW + 1;
     static constexpr int NPIX = HR * HC;
     static constexpr int CS = CKC + 4;                      // floats per halo pixel (odd 16-B slots)
-    // split-bf16 x6 (MODE 1, Cout 32): halo [piece][16-ch step][k half][pixel][8 bf16], weights
-    // [slot][16-ch step][piece][k half][n][8 bf16] — the 32x32x16 bf16 operand layouts, no padding
-    static constexpr int KS2 = CKC / 16;                    // 16-channel K steps per chunk (x6)
-    static constexpr int HALO = X6 ? 3 * KS2 * 2 * NPIX * 4 : NPIX * CS;   // floats per halo buffer
-    static constexpr int WCH = X6 ? 9 * CKC * NC * 3 / 2 : 9 * CKC * NC;   // floats per chunk of weights
+    // split-bf16 x6: the bf16 MFMA of the Cout (32: 32x32x16, K step 16 = two 8-channel lane groups; 16: 16x16x32,
+    // K step 32 = four groups). Halo [piece][K step][group][pixel][8 bf16] (pixels padded to a multiple of 16: the
+    // four groups of a ds_read_b128 lane set then hit disjoint banks), weights [slot][K step][piece][group][n][8 bf16]
+    // — the MFMA operand layouts. Single-chunk layers (Cin <= CKC) hold the split weights in VGPRs (9 slots x 3 pieces
+    // x 4 registers): no weight image in LDS, no B-operand LDS reads.
+    static constexpr int KSTEP = MS == 32 ? 16 : 32;
+    static constexpr int G = KSTEP / 8;                     // 8-channel lane groups per K step
+    static constexpr int KS2 = X6 ? CKC / KSTEP : 1;        // K steps per chunk (x6)
+    static constexpr int NPIXP = (NPIX + 15) / 16 * 16;
+    static constexpr bool WIN_REGS = X6 && NCH == 1;        // x6 weights in registers
+    static constexpr int HALO = X6 ? 3 * KS2 * G * NPIXP * 4 : NPIX * CS;   // floats per halo buffer
+    static constexpr int WCH = WIN_REGS ? 0 : (X6 ? 9 * CKC * NC * 3 / 2 : 9 * CKC * NC);   // floats per chunk of weights in LDS
     static constexpr int HITEMS = HR * HC * QC;             // float4 items per halo chunk
     static constexpr int HREG = (HITEMS + 255) / 256;
     static constexpr int WITEMS = WCH / 4;
@@ -87,7 +94,8 @@ struct Cfg {
     static_assert(CIN % CKC == 0 && CKC % (4 * KS) == 0, "chunking");
     static_assert(MS == 16 || MS == 32, "MFMA shape");
     static_assert(((CS / 4) & 1) == 1, "odd 16-B slots per halo pixel");
-    static_assert(!X6 || (MODE == 1 && NC == 32 && CKC % 16 == 0), "x6: transposed, Cout 32");
+    static_assert(!X6 || CKC % KSTEP == 0, "x6: whole K steps per chunk");
+    static_assert(!WIN_REGS || KS2 == 1, "x6 weights in registers: one K step");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
@@ -184,7 +192,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     const int lcm = halo_off(0, col) + 4 * q, lce = halo_off(0, HCM) + 4 * q;
     // two register sets of staged input (single-chunk layers prefetch two tiles ahead: the HBM latency
     // under load exceeds one tile's MFMAs); multi-chunk layers use set 0 only
-    constexpr int NSET = NCH == 1 ? 2 : 1;
+    // (x6 single-chunk layers hold their weights in VGPRs instead: one set, two workgroups per CU cover the latency)
+    constexpr int NSET = NCH == 1 && !C::WIN_REGS ? 2 : 1;
     f32x4 hreg[NSET][NMAIN + 1], rreg[NSET][NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01[NSET], pa23[NSET];
     f32x4 pb01[NSET], pb23[NSET];   // BLEND: the second style's affine of the thread's channel quad
     float bw[NSET][NMAIN + 1];      // BLEND: the second style's weight at each staged pixel
@@ -253,16 +262,22 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         }
         return v;
     };
-    // x6: channel quad q of the chunk = 16-ch step q >> 2, k half (q >> 1) & 1, bf16 slots 4 (q & 1) .. +3
+    // x6: channel quad q of the chunk = K step q / (KSTEP / 4), lane group (q % (KSTEP / 4)) >> 1, bf16 slots
+    // 4 (q & 1) .. +3 of the group's 8; pixels in halo_off's order (stride-2 columns parity-split)
     unsigned char* const hbytes = reinterpret_cast<unsigned char*>(halo);
-    const int xq = (((q >> 2) * 2 + ((q >> 1) & 1)) * C::NPIX) * 16 + (q & 1) * 8;   // + piece + pixel
-    constexpr int XPIECE = C::KS2 * 2 * C::NPIX * 16;                                 // bytes per piece plane
+    constexpr int QPS = C::KSTEP / 4;                                                  // channel quads per K step
+    const int xq = (((q / QPS) * C::G + ((q % QPS) >> 1)) * C::NPIXP) * 16 + (q & 1) * 8;   // + piece + pixel
+    constexpr int XPIECE = C::KS2 * C::G * C::NPIXP * 16;                             // bytes per piece plane
+    auto hpix = [&](int hy, int hx) __attribute__((always_inline)) {                  // x6 halo pixel index
+        if constexpr (MODE == 0) return hy * HC + (hx & 1) * (TW + 1) + (hx >> 1);
+        else return hy * HC + hx;
+    };
     auto put = [&](int hy, int hx, int lf, f32x4 v) __attribute__((always_inline)) {
         if constexpr (X6) {
             unsigned p0[2], p1[2], p2[2];
             split3(v.x, v.y, p0[0], p1[0], p2[0]);
             split3(v.z, v.w, p0[1], p1[1], p2[1]);
-            unsigned char* dst = hbytes + xq + (hy * HC + hx) * 16;
+            unsigned char* dst = hbytes + xq + hpix(hy, hx) * 16;
             *reinterpret_cast<uint2*>(dst) = make_uint2(p0[0], p0[1]);
             *reinterpret_cast<uint2*>(dst + XPIECE) = make_uint2(p1[0], p1[1]);
             *reinterpret_cast<uint2*>(dst + 2 * XPIECE) = make_uint2(p2[0], p2[1]);
@@ -311,7 +326,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // dependent MFMAs); MODE 1 one r = 4 operand positions x 9 slots, 36 MFMAs into the 4 phase
     // accumulators (phase 0's four slots alternate between two).
     constexpr int NA = MODE == 0 ? 3 : 4, NB = MODE == 0 ? 3 : 9, NSTEP = MODE == 0 ? 3 * R : R;
-    constexpr int NACCS = MODE == 0 ? 3 : 5;
+    // (x6 strided conv with Cout 32: one 32x32x16 accumulator chain, which issues back to back, MI355X_MICROARCH.md)
+    constexpr int NACCS = MODE == 0 ? (X6 && MS == 32 ? 1 : 3) : 5;
     acc_t acc[NACCS];
     auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -360,51 +376,88 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
         });
     };
-    // x6 (MODE 1, Cout 32): per 16-channel step the 4 operand positions x 3 pieces of A are read once;
-    // the slots walk in phase-interleaved order with B (3 pieces) read one slot ahead; 6 terms per slot
+    // x6: per K step, MODE 1 reads the 4 operand positions x 3 pieces of A once and walks the slots in
+    // phase-interleaved order; MODE 0 walks the 9 taps with A read one tap ahead. B (3 pieces) comes from the
+    // weight registers (single-chunk layers) or from LDS one slot ahead; 6 terms per slot.
+    const int kg = lane / MS;   // the lane's 8-channel group of a K step
+    short8 wr6[C::WIN_REGS ? 9 : 1][3];
+    if constexpr (C::WIN_REGS) {   // [slot][piece] B fragments of this lane (n = m, group kg)
+        const u32x4* wp = reinterpret_cast<const u32x4*>(a.wpk);
+        sfor<0, 9>([&](auto S) __attribute__((always_inline)) {
+            constexpr int sl = decltype(S)::value;
+            sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
+                constexpr int pc = decltype(PC)::value;
+                wr6[sl][pc] = __builtin_bit_cast(short8, wp[((sl * 3 + pc) * C::G + kg) * MS + m]);
+            });
+        });
+    }
+    auto mfma6 = [&](acc_t& acc_, const short8 (&A)[3], const short8 (&Bv)[3]) __attribute__((always_inline)) {
+        constexpr int ap[6] = {0, 0, 1, 0, 1, 2}, bp[6] = {0, 1, 0, 2, 1, 0};
+        sfor<0, 6>([&](auto T6) __attribute__((always_inline)) {
+            constexpr int t6 = decltype(T6)::value;
+            if constexpr (MS == 32)
+                acc_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[ap[t6]], Bv[bp[t6]], acc_, 0, 0, 0);
+            else
+                acc_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ap[t6]], Bv[bp[t6]], acc_, 0, 0, 0);
+        });
+    };
     auto compute_x6 = [&]() __attribute__((always_inline)) {
       if constexpr (X6) {   // discarded (not instantiated) for the f32 configurations
         const unsigned char* wbytes = reinterpret_cast<const unsigned char*>(wts);
-        const int kh = lane >> 5;
-        constexpr int order[9] = {0, 4, 6, 8, 1, 5, 7, 2, 3};
-        constexpr int ap[6] = {0, 0, 1, 0, 1, 2}, bp[6] = {0, 1, 0, 2, 1, 0};
+        auto readB = [&](int sl, int ks, short8 (&Bv)[3]) __attribute__((always_inline)) {
+            sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
+                constexpr int pc = decltype(PC)::value;
+                Bv[pc] = *reinterpret_cast<const short8*>(wbytes + ((((sl * C::KS2 + ks) * 3 + pc) * C::G + kg) * MS + m) * 16);
+            });
+        };
+        auto readA = [&](int pix, int ks, short8 (&A)[3]) __attribute__((always_inline)) {
+            sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
+                constexpr int pc = decltype(PC)::value;
+                A[pc] = *reinterpret_cast<const short8*>(hbytes + pc * XPIECE + ((ks * C::G + kg) * C::NPIXP + pix) * 16);
+            });
+        };
         sfor<0, C::KS2>([&](auto KSI) __attribute__((always_inline)) {
             constexpr int ks = decltype(KSI)::value;
-            short8 A[4][3];
-            sfor<0, 4>([&](auto P) __attribute__((always_inline)) {
-                constexpr int pos = decltype(P)::value;
-                const int pix = (wave + (pos >> 1)) * HC + m + (pos & 1);
-                sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
-                    constexpr int pc = decltype(PC)::value;
-                    A[pos][pc] = *reinterpret_cast<const short8*>(hbytes + pc * XPIECE +
-                                                                  ((ks * 2 + kh) * C::NPIX + pix) * 16);
+            if constexpr (MODE == 1) {
+                constexpr int order[9] = {0, 4, 6, 8, 1, 5, 7, 2, 3};
+                short8 A[4][3];
+                sfor<0, 4>([&](auto P) __attribute__((always_inline)) {
+                    constexpr int pos = decltype(P)::value;
+                    readA((wave + (pos >> 1)) * HC + m + (pos & 1), ks, A[pos]);
                 });
-            });
-            auto readB = [&](int sl, short8 (&Bv)[3]) __attribute__((always_inline)) {
-                sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
-                    constexpr int pc = decltype(PC)::value;
-                    Bv[pc] = *reinterpret_cast<const short8*>(wbytes + ((((sl * C::KS2 + ks) * 3 + pc) * 2 + kh) * 32 + m) * 16);
+                short8 B0[3], B1[3];
+                if constexpr (!C::WIN_REGS) readB(order[0], ks, B0);
+                sfor<0, 9>([&](auto J) __attribute__((always_inline)) {
+                    constexpr int j = decltype(J)::value, sl = order[j];
+                    constexpr int ai = (sl == 1 || sl == 3) ? 4 : t_phase(sl), pos = t_pos(sl);
+                    if constexpr (!C::WIN_REGS && j + 1 < 9) {
+                        if constexpr ((j & 1) == 0) readB(order[j + 1], ks, B1);
+                        else readB(order[j + 1], ks, B0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (C::WIN_REGS) mfma6(acc[ai], A[pos], wr6[sl]);
+                    else if constexpr ((j & 1) == 0) mfma6(acc[ai], A[pos], B0);
+                    else mfma6(acc[ai], A[pos], B1);
+                    __builtin_amdgcn_sched_barrier(0);
                 });
-            };
-            short8 B0[3], B1[3];
-            readB(order[0], B0);
-            sfor<0, 9>([&](auto J) __attribute__((always_inline)) {
-                constexpr int j = decltype(J)::value, sl = order[j];
-                constexpr int ai = (sl == 1 || sl == 3) ? 4 : t_phase(sl), pos = t_pos(sl);
-                if constexpr (j + 1 < 9) {
-                    if constexpr ((j & 1) == 0) readB(order[j + 1], B1);
-                    else readB(order[j + 1], B0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                sfor<0, 6>([&](auto T6) __attribute__((always_inline)) {
-                    constexpr int t6 = decltype(T6)::value;
-                    if constexpr ((j & 1) == 0)
-                        acc[ai] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[pos][ap[t6]], B0[bp[t6]], acc[ai], 0, 0, 0);
-                    else
-                        acc[ai] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[pos][ap[t6]], B1[bp[t6]], acc[ai], 0, 0, 0);
+            } else {   // taps t = 3 ky + kx into acc[kx]; A of tap t + 1 read while tap t's MFMAs run
+                static_assert(MODE != 0 || C::WIN_REGS, "x6 strided conv: single-chunk layers");
+                short8 A0[3], A1[3];
+                readA(hpix(2 * wave, 2 * m), ks, A0);
+                sfor<0, 9>([&](auto T) __attribute__((always_inline)) {
+                    constexpr int t = decltype(T)::value, ky = t / 3, kx = t % 3;
+                    if constexpr (t + 1 < 9) {
+                        constexpr int ky1 = (t + 1) / 3, kx1 = (t + 1) % 3;
+                        if constexpr ((t & 1) == 0) readA(hpix(2 * wave + ky1, 2 * m + kx1), ks, A1);
+                        else readA(hpix(2 * wave + ky1, 2 * m + kx1), ks, A0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    constexpr int ai = NACCS == 1 ? 0 : kx;
+                    if constexpr ((t & 1) == 0) mfma6(acc[ai], A0, wr6[t]);
+                    else mfma6(acc[ai], A1, wr6[t]);
+                    __builtin_amdgcn_sched_barrier(0);
                 });
-                __builtin_amdgcn_sched_barrier(0);
-            });
+            }
         });
       }
     };
@@ -444,7 +497,9 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
     auto epilogue = [&](const Tile& T) __attribute__((always_inline)) {
         if constexpr (MODE == 0) {   // bias + ReLU -> BatchNorm (inference affine) -> ReLU, NHWC store
-            const acc_t y = (acc[0] + acc[1]) + acc[2];
+            acc_t y;
+            if constexpr (NACCS == 1) y = acc[0];
+            else y = (acc[0] + acc[1]) + acc[2];
             const int oy = T.y0 + wave;
             const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
             float* const orow = a.out + ((size_t)(T.b * a.Ho + oy) * a.Wo) * NC + n;
@@ -505,11 +560,12 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
             if ((a.part != nullptr || to_acc) && (LITE_SKIP & 32) == 0) {
                 // lanes n, n + MS, ... hold column n: reduce over them, then over the 4 waves (fixed order)
-#pragma unroll
-                for (int o = MS; o < 64; o <<= 1) {
-                    s += __shfl_xor(s, o);
-                    cnt += __shfl_xor(cnt, o);
+                if constexpr (MS == 16) {
+                    s = lane_xor_sum<16>(s);
+                    cnt = lane_xor_sum<16>(cnt);
                 }
+                s = lane_xor_sum<32>(s);
+                cnt = lane_xor_sum<32>(cnt);
                 if (lane < MS) {
                     red[wave * NC + n] = s;
                     red[4 * NC + wave * NC + n] = cnt;
@@ -527,8 +583,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         const float d = acc[ph][j] - mean;
                         if (full || (p < a.Ho && qq < a.Wo)) m2 = fmaf(d, d, m2);
                     }
-#pragma unroll
-                for (int o = MS; o < 64; o <<= 1) m2 += __shfl_xor(m2, o);
+                if constexpr (MS == 16) m2 = lane_xor_sum<16>(m2);
+                m2 = lane_xor_sum<32>(m2);
                 lds_barrier();
                 if (lane < MS) red[wave * NC + n] = m2;
                 lds_barrier();
@@ -553,7 +609,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
 
     // ---- main loop over (tile, chunk) steps: step s+1's global loads are in flight while step s
     // computes and (last chunk) stores its tile ---------------------------------------------------------
-    if constexpr (NCH == 1) {   // one weight image for every tile: staged once
+    if constexpr (NCH == 1 && !C::WIN_REGS) {   // one weight image for every tile: staged once
         for (int it = tid; it < C::WITEMS; it += 256)
             reinterpret_cast<f32x4*>(wts)[it] = reinterpret_cast<const f32x4*>(a.wpk)[it];
     }
@@ -582,7 +638,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, NSET - 1>;
     zero_acc();
-    if constexpr (NCH == 1) {
+    if constexpr (NCH == 1 && NSET == 2) {
         // tile k's input sits in register set k & 1, loaded two tiles ahead
         Tile T0 = tile_of(0), T1 = T0;
         load_in(T0, 0, S0{});
@@ -626,7 +682,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
             T0 = T2;
         }
-    } else {
+    } else {   // multi-chunk layers, and single-chunk layers with one register set (x6: weights in VGPRs)
         const int n_steps = my_tiles * NCH;
         Tile cur = tile_of(0);
         load_in(cur, 0, S0{});
@@ -668,7 +724,10 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     X(2, 0, 16, 32, 16, 0)         \
     X(3, 1, 128, 32, 32, 0)        \
     X(4, 1, 32, 16, 32, 0)         \
-    X(5, 1, 128, 32, 32, 1)
+    X(5, 1, 128, 32, 32, 1)        \
+    X(6, 0, 32, 16, 32, 1)         \
+    X(7, 0, 16, 32, 16, 1)         \
+    X(8, 1, 32, 16, 32, 1)
 
 bool conv_lite_select(int keras_kind, int k, int stride, int cin, int cout, bool x6, LiteTile* t) {
     if (k != 3 || stride != 2) return false;
@@ -709,18 +768,18 @@ static float lite_slot_weight(const LiteTile& t, const float* kern, int s, int c
 }
 
 std::vector<float> conv_lite_pack_weights(const LiteTile& t, const float* kern) {
-    if (t.x6) {   // [chunk][slot][16-ch step][piece][k half][n][8] bf16, each weight split into 3 RNE pieces
-        const int nch = t.cin / t.ckc, ks2 = t.ckc / 16;
-        std::vector<uint16_t> img((size_t)nch * 9 * ks2 * 3 * 2 * t.nc * 8);
+    if (t.x6) {   // [chunk][slot][K step][piece][lane group][n][8] bf16, each weight split into 3 RNE pieces
+        const int kstep = t.nc == 32 ? 16 : 32, ng = kstep / 8, nch = t.cin / t.ckc, ks2 = t.ckc / kstep;
+        std::vector<uint16_t> img((size_t)nch * 9 * ks2 * 3 * ng * t.nc * 8);
         size_t idx = 0;
         for (int ch = 0; ch < nch; ++ch)
             for (int s = 0; s < 9; ++s)
                 for (int k2 = 0; k2 < ks2; ++k2)
                     for (int pc = 0; pc < 3; ++pc)
-                        for (int kh = 0; kh < 2; ++kh)
+                        for (int kg = 0; kg < ng; ++kg)
                             for (int n = 0; n < t.nc; ++n)
                                 for (int e = 0; e < 8; ++e) {
-                                    const float v = lite_slot_weight(t, kern, s, ch * t.ckc + k2 * 16 + kh * 8 + e, n);
+                                    const float v = lite_slot_weight(t, kern, s, ch * t.ckc + k2 * kstep + kg * 8 + e, n);
                                     uint16_t p[3];
                                     p[0] = lite_bf16_rne(v);
                                     const float r = v - lite_bf16_val(p[0]);
@@ -809,8 +868,6 @@ static int lite_slots() {
                                                          C::LDS_BYTES + lite_tab_bytes(PRO, CIN, 1)) != hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
-        if (const char* e = getenv("RST_LITE_PER_CU"))   // measurement knob: cap the resident workgroups per CU
-            if (atoi(e) > 0 && atoi(e) < per_cu) per_cu = atoi(e);
         slots = ((lite_cu_count() * per_cu) / 8) * 8;
         if (slots <= 0) slots = 8;
     }

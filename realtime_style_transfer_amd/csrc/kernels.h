@@ -25,19 +25,36 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ float style_blend(float w1, float v0, float v1) { return fmaf(w1, v1 - v0, v0); }
 
 // Exact three-piece bf16 split (the split-bf16 x6 kernels): (x, y) -> the packed bf16 pair nearest them (RNE),
-// then (x, y) -= its value. The remainder x - piece is exact in fp32 (x's own low bits); it is formed by
-// v_dot2c_f32_bf16 as x + (-1)·piece + 0·other — one VALU per value instead of a shift or mask plus a subtraction
-// (tools/dot2_split_check: bitwise the shift/subtract split on 2^24 random pairs, ties and zeros included).
+// then (x, y) -= its value; the remainder is exact in fp32 (x's own low bits). The subtraction must be an IEEE
+// f32 subtract: v_dot2c_f32_bf16 (x + (-1)·piece in one instruction) was measured NOT to reproduce it —
+// tools/dot2_split_check: 16.5 M of 16.8 M random pairs differ in some piece (round 4) — so the piece is widened
+// with a shift / mask and subtracted.
 typedef float rst_f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 rst_bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned bf16_piece(float& x, float& y) {
-    const rst_bf16x2 p = __builtin_convertvector((rst_f32x2){x, y}, rst_bf16x2);
-    x = __builtin_amdgcn_fdot2_f32_bf16(p, (rst_bf16x2){(__bf16)-1.0f, (__bf16)0.0f}, x, false);
-    y = __builtin_amdgcn_fdot2_f32_bf16(p, (rst_bf16x2){(__bf16)0.0f, (__bf16)-1.0f}, y, false);
-    return __builtin_bit_cast(unsigned, p);
+    const unsigned p = __builtin_bit_cast(unsigned, __builtin_convertvector((rst_f32x2){x, y}, rst_bf16x2));
+    x = x - __uint_as_float(p << 16);
+    y = y - __uint_as_float(p & 0xFFFF0000u);
+    return p;
 }
 __device__ __forceinline__ unsigned bf16_last_piece(float x, float y) {
     return __builtin_bit_cast(unsigned, __builtin_convertvector((rst_f32x2){x, y}, rst_bf16x2));
+}
+
+// x + x[lane ^ O] for O = 16 / 32 on the VALU (v_permlane16/32_swap, gfx950) instead of ds_bpermute (__shfl_xor,
+// an LDS round trip per value): the swap hands each lane the partner's value, the add is commutative, so the result
+// is bitwise __shfl_xor's
+template <int O>
+__device__ __forceinline__ float lane_xor_sum(float x) {
+    static_assert(O == 16 || O == 32, "permlane swaps cover xor 16 / 32");
+    const unsigned u = __float_as_uint(x);
+    if constexpr (O == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    } else {
+        const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
 }
 
 // XCD-aware block order: the dispatcher deals workgroup ids round-robin over the 8 XCDs (each with

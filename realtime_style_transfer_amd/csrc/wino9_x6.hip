@@ -441,8 +441,8 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
                 // lanes co / co + 32 of a wave hold groups 2w, 2w + 1; the eight waves meet in LDS just past
                 // the M exchange image (disjoint from it, inside the same dead patch + v16 span)
                 float* const red = ms + MEX_FL;   // [3][8 waves][32]
-                vs += __shfl_xor(vs, 32);
-                vn += __shfl_xor(vn, 32);
+                vs = lane_xor_sum<32>(vs);
+                vn = lane_xor_sum<32>(vn);
                 if (lh == 0) {
                     red[wave * 32 + co] = vs;
                     red[256 + wave * 32 + co] = vn;
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
                         const float d = vals[4 * k + q] - mean;
                         if (oy < H && ox < W) m2 = fmaf(d, d, m2);
                     }
-                m2 += __shfl_xor(m2, 32);
+                m2 = lane_xor_sum<32>(m2);
                 if (lh == 0) red[512 + wave * 32 + co] = m2;
                 lds_barrier();
                 if (tid < 32) {

@@ -97,8 +97,9 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 #define X6_SKIP 0
 #endif
 #ifdef X6_PROF
-// timeline per (workgroup, wave < 8) on the constant 100 MHz clock: start, pipeline filled, chunk loop done, end
-__device__ unsigned long long x6_tl[X6_PROF][8][4];
+// timeline per (workgroup, wave < 8) on the constant 100 MHz clock: 0 start, 4 first loads + affine issued,
+// 5 chunk 0 staged, 1 pipeline filled, 2 chunk loop done, 6 epilogue image written, 7 outputs stored, 3 end
+__device__ unsigned long long x6_tl[X6_PROF][8][8];
 #define XTL(k) \
     if (blockIdx.x < X6_PROF && lane == 0) x6_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -108,25 +109,26 @@ __device__ unsigned long long x6_tl[X6_PROF][8][4];
 #ifdef X6_PROF
 // timeline summary of the most recent launch (tools/wino_x6_bench)
 void x6_timeline_print(int nwg, int nwave) {
-    std::vector<unsigned long long> tl((size_t)X6_PROF * 32);
+    std::vector<unsigned long long> tl((size_t)X6_PROF * 64);
     if (hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(x6_tl), tl.size() * 8) != hipSuccess) return;
     if (nwg > X6_PROF) nwg = X6_PROF;
     unsigned long long t0 = ~0ull, tend = 0, slast = 0;
-    double fill = 0, loop = 0, epi = 0;
+    // phases in time order: 0 -> 4 -> 5 -> 1 -> 2 -> 6 -> 7 -> 3
+    const int ord[8] = {0, 4, 5, 1, 2, 6, 7, 3};
+    double ph[7] = {0, 0, 0, 0, 0, 0, 0};
     for (int g = 0; g < nwg; ++g)
         for (int w = 0; w < nwave; ++w) {
-            const unsigned long long* q = &tl[((size_t)g * 8 + w) * 4];
+            const unsigned long long* q = &tl[((size_t)g * 8 + w) * 8];
             t0 = q[0] < t0 ? q[0] : t0;
             tend = q[3] > tend ? q[3] : tend;
             slast = q[0] > slast ? q[0] : slast;
-            fill += (double)(q[1] - q[0]);
-            loop += (double)(q[2] - q[1]);
-            epi += (double)(q[3] - q[2]);
+            for (int k = 0; k < 7; ++k) ph[k] += (double)(q[ord[k + 1]] - q[ord[k]]);
         }
-    const double nw = nwg * (double)nwave;
-    printf("  timeline (us): first start -> last end %.2f, last start +%.2f; per wave: fill %.2f, loop %.2f, "
-           "epilogue %.2f\n", (tend - t0) * 0.01, (slast - t0) * 0.01, fill / nw * 0.01, loop / nw * 0.01,
-           epi / nw * 0.01);
+    const double nw = nwg * (double)nwave * 100.0;
+    printf("  timeline (us): first start -> last end %.2f, last start +%.2f; per wave: issue+affine %.2f, stage0 %.2f, "
+           "transform0+stage1 %.2f, loop %.2f, epilogue image %.2f, stores %.2f, statistics %.2f\n",
+           (tend - t0) * 0.01, (slast - t0) * 0.01, ph[0] / nw, ph[1] / nw, ph[2] / nw, ph[3] / nw, ph[4] / nw,
+           ph[5] / nw, ph[6] / nw);
 }
 #endif
 
@@ -221,6 +223,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const int gi = sg_goff[k] + chunk * XCK;
         xr[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
         if constexpr (pro == PRO_AFF_RES) rr[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
+    };
+    // chunk 1's staging loads, issued with chunk 0's at the start (registers that are free before the loop), so the
+    // staging of chunk 1 does not wait for a load issued after chunk 0's staging
+    f32x4 xr1[YST], rr1[YST];
+    auto gload1 = [&](int k) __attribute__((always_inline)) {
+        const int gi = sg_goff[k] + XCK;
+        xr1[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
+        if constexpr (pro == PRO_AFF_RES) rr1[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
     };
     // prologue of the staged value (affine [+ ReLU | + residual]) and the materialised block output
     auto stage_math = [&](int k, int chunk, f32x4 p01, f32x4 p23) __attribute__((always_inline)) {
@@ -361,18 +371,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..R-1) in flight ----
     sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 0); });
+    if (nchunks > 1) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload1(decltype(K)::value); });
     sfor<0, YRING>([&](auto X) __attribute__((always_inline)) {
         sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
             load_u1(0, decltype(X)::value, decltype(X)::value, decltype(Pc)::value);
         });
     });
     load_affine();
+    XTL(4);
     if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging
     stage_all(0, patch);
-    if (nchunks > 1) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 1); });
     lds_barrier();
+    XTL(5);
     transform_all(patch, vbytes);
     if (nchunks > 1) {
+#pragma unroll
+        for (int k = 0; k < YST; ++k) {
+            xr[k] = xr1[k];
+            rr[k] = rr1[k];
+        }
         stage_all(1, patch + XPATCH_FL);
         if (nchunks > 2) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 2); });
     }
@@ -471,6 +488,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
     }
     lds_barrier();
+    XTL(6);
     // thread = (pixel column pr, channel quad cq); rows 0..7 of the tile
     const int cq = tid & 31, pr = tid >> 5;
     const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + 4 * cq);
@@ -501,15 +519,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         yv[i] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         s4 += yv[i];
     }
+    XTL(7);
     if (a.part != nullptr || a.stat.acc != nullptr) {
         f32x4* const red = reinterpret_cast<f32x4*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES);   // [2][8][32]
         double* const dred = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES + YRED_BYTES);
         const float cnt = (float)(min(XTH, H - y0) * min(XTW, W - x0));
         auto xsum = [&](f32x4 v) __attribute__((always_inline)) {
-            v.x += __shfl_xor(v.x, 32);
-            v.y += __shfl_xor(v.y, 32);
-            v.z += __shfl_xor(v.z, 32);
-            v.w += __shfl_xor(v.w, 32);
+            v.x = lane_xor_sum<32>(v.x);
+            v.y = lane_xor_sum<32>(v.y);
+            v.z = lane_xor_sum<32>(v.z);
+            v.w = lane_xor_sum<32>(v.w);
             return v;
         };
         s4 = xsum(s4);

@@ -48,7 +48,14 @@ int main(int argc, char** argv) {
             const size_t nout = (size_t)B * (s.kind == 0 ? Ho * Wo : 4 * Ho * Wo) * s.cout;
             float* in = dev_rand(nin, -1.f, 1.f, 1);
             float* res = dev_rand(nin, -1.f, 1.f, 2);
-            float* w = dev_rand((size_t)9 * s.cin * s.cout, -0.1f, 0.1f, 3);
+            // the packed weight image of a random kernel (the x6 image is 1.5x the f32 one)
+            std::vector<float> hk((size_t)9 * s.cin * s.cout);
+            srand(3);
+            for (auto& v : hk) v = -0.1f + 0.2f * (rand() / (float)RAND_MAX);
+            const std::vector<float> pk = conv_lite_pack_weights(t, hk.data());
+            float* w;
+            CK(hipMalloc(&w, pk.size() * 4));
+            CK(hipMemcpy(w, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
             float* bias = dev_rand(s.cout, -0.1f, 0.1f, 4);
             float* ab = dev_rand((size_t)2 * B * s.cin, 0.5f, 1.f, 5);
             float* out;
