@@ -391,6 +391,7 @@ def write_checkpoint(prefix, tensors: Dict[str, np.ndarray], object_graph: Optio
         data += raw
     entries.sort(key=lambda t: t[0])
     header = _pb_varint(1, 1) + _pb_bytes(3, _pb_varint(1, 1))   # num_shards 1, little-endian, version{producer 1}
+    Path(prefix).parent.mkdir(parents=True, exist_ok=True)   # as TF's saver, which creates the checkpoint directory
     Path(f"{prefix}.data-00000-of-00001").write_bytes(bytes(data))
     _write_table(_index_path(prefix), [(b'', header)] + [(k, e.serialize()) for k, e in entries])
 

@@ -284,3 +284,13 @@ def test_object_graph_slot_variables():
     (orig, slot, sid), = nodes[opt]['slots']
     assert orig == kern and slot == "rms"
     assert nodes[sid]['keys'] == ["layer_with_weights-0/kernel/.OPTIMIZER_SLOT/optimizer/rms" + V]
+
+
+def test_write_checkpoint_creates_the_directory(tmp_path):
+    """Model.save_weights / CheckpointManager create the checkpoint directory (tracing/checkpoint.py:21-37 saves into
+    a directory that need not exist yet)."""
+    import numpy as np
+    from realtime_style_transfer_amd import tf_checkpoint as ck
+    prefix = tmp_path / "not" / "yet" / "there" / "ckpt"
+    ck.write_checkpoint(prefix, {"v/.ATTRIBUTES/VARIABLE_VALUE": np.arange(3, dtype=np.float32)})
+    assert np.array_equal(ck.read_checkpoint(prefix)["v/.ATTRIBUTES/VARIABLE_VALUE"], np.arange(3, dtype=np.float32))

@@ -218,3 +218,23 @@ def test_failed_step_between_targets_and_gradients_recovers():
     a.training.train_step(x, y)
     b.training.train_step(x, y)
     assert all(np.array_equal(u, v) for u, v in zip(a.training.get_weights(), b.training.get_weights()))
+
+
+def test_mixed_bfloat16_policy_builds_the_benchmarked_training_line():
+    """train_network.py:26's global policy switch, set to 'mixed_bfloat16' (BASELINE config 4): the reference-signature
+    construction sequence (make_style_loss_function(StyleLossModelVGG(...)) + make_style_transfer_training_model)
+    then builds the benchmarked line — bf16 VGG16 loss network, winograd_bf16x6 transfer net — and steps it."""
+    _need_gpu()
+    from realtime_style_transfer_amd import mixed_precision
+    mixed_precision.set_global_policy("mixed_bfloat16")
+    try:
+        m = _training_models(3, 2)
+        assert m.style_loss.feature_model.precision == "bf16"
+        assert m.training.loss_model.precision == "bf16"
+        assert m.training.precision == "winograd_bf16x6"
+        x, y = _batch(1)
+        losses = m.training.train_step(x, y)
+        assert all(np.isfinite(float(v.sum())) for v in losses.values())
+    finally:
+        mixed_precision.set_global_policy("float32")
+    assert styleLoss.StyleLossModelVGG((32, 64, 3), max_batch=1).precision == "fp32"

@@ -3,7 +3,7 @@
 # chained so the first failure ends the call (no retries). Outputs go to gpurun_out/<step>_<TAG>.* (TAG env, default "x").
 #
 # Usage: bash tools/gpu_measure.sh STEP...
-#   tests[=K]        pytest -m gpu (optionally -k K)                      -> pytest_<TAG>.log
+#   tests[=K]        pytest -m gpu (optionally -k K; PYTEST_X overrides -x) -> pytest_<TAG>.log
 #   smoke            __graft_entry__.smoke()                              -> smoke_<TAG>.log
 #   bench[=ARGS]     bench.py (default flags, or ARGS with ',' for ' ')   -> bench_<TAG>.log
 #   short            bench.py headline only (no side legs)                -> bench_short_<TAG>.log
@@ -37,7 +37,7 @@ for step in "$@"; do
     case $name in
     tests)
         k=(); [ -n "$arg" ] && k=(-k "$arg")
-        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" \
+        timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_X:--x} -v --timeout 300 --timeout-method thread "${k[@]}" \
             > $O/pytest_$TAG.log 2>&1 || { tail -40 $O/pytest_$TAG.log; exit 1; }
         tail -1 $O/pytest_$TAG.log ;;
     smoke)
