@@ -39,10 +39,14 @@ namespace rst {
 // s_memtime per (workgroup < 64, wave, step < 16, point): 0 step top, 1 after staging + barrier,
 // 2 after the MFMAs, 3 after the epilogue (tools/lite_bench)
 __device__ unsigned long long lite_tl[64][4][16][4];
+__device__ unsigned long long lite_t0[64][4][2];   // kernel start, end of the last step
 #define LTL(st, pt) \
     if (blockIdx.x < 64 && lane == 0 && (st) < 16) lite_tl[blockIdx.x][wave][(st)][(pt)] = __builtin_amdgcn_s_memtime()
+#define LT0(k) \
+    if (blockIdx.x < 64 && lane == 0) lite_t0[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memtime()
 #else
 #define LTL(st, pt)
+#define LT0(k)
 #endif
 
 namespace lite {
@@ -158,6 +162,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     float2* const tab = reinterpret_cast<float2*>(red + 8 * NC);   // prologue affine [batch][CIN] (+ second style)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    LT0(0);
     const int H = a.H, W = a.W;
     auto halo_off = [&](int hy, int hx) __attribute__((always_inline)) {
         if constexpr (MODE == 0) return (hy * HC + (hx & 1) * (TW + 1) + (hx >> 1)) * CS;
@@ -713,6 +718,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         }
     }
     if (to_acc && tid < NC) acc_flush();
+    LT0(1);
     l2_touch_keep(l2f, a.batch < 0, smem);
 }
 
@@ -831,8 +837,24 @@ void lite_timeline_print(int nsteps) {
                     if (q1[0] >= q[3] && q1[0] != 0) { gap += (double)(q1[0] - q[3]); ++ng; }
                 }
             }
-    if (n) printf("    per step (us): staging+barrier %.2f, MFMA %.2f, epilogue %.2f (n=%d)\n", d[0] / n * 0.01,
+    if (n) printf("    per step (100 cycles): staging+barrier %.2f, MFMA %.2f, epilogue %.2f (n=%d)\n", d[0] / n * 0.01,
                   d[1] / n * 0.01, d[2] / n * 0.01, n);
+    std::vector<unsigned long long> t0((size_t)64 * 4 * 2);
+    if (hipMemcpyFromSymbol(t0.data(), HIP_SYMBOL(lite_t0), t0.size() * 8) == hipSuccess) {
+        double fill = 0, span = 0;
+        int nw = 0;
+        for (int g = 0; g < 64; ++g)
+            for (int w = 0; w < 4; ++w) {
+                const unsigned long long s0 = t0[(g * 4 + w) * 2], s1 = t0[(g * 4 + w) * 2 + 1];
+                const unsigned long long f = tl[(((size_t)g * 4 + w) * 16) * 4];
+                if (s0 == 0 || s1 < s0 || f < s0) continue;
+                fill += (double)(f - s0);
+                span += (double)(s1 - s0);
+                ++nw;
+            }
+        if (nw) printf("    per wave (100 cycles): start -> first step %.2f, start -> end %.2f\n", fill / nw * 0.01,
+                       span / nw * 0.01);
+    }
     std::vector<unsigned long long> z(tl.size(), 0);   // clear for the next measured launch
     (void)hipMemcpyToSymbol(HIP_SYMBOL(lite_tl), z.data(), z.size() * 8);
 }

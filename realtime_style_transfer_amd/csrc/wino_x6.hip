@@ -97,9 +97,9 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 #define X6_SKIP 0
 #endif
 #ifdef X6_PROF
-// timeline per (workgroup, wave < 8) on the constant 100 MHz clock: 0 start, 4 first loads + affine issued,
+// timeline per (workgroup, wave < 8) on the constant 100 MHz clock: 0 start, 8 first loads issued, 4 affine formed,
 // 5 chunk 0 staged, 1 pipeline filled, 2 chunk loop done, 6 epilogue image written, 7 outputs stored, 3 end
-__device__ unsigned long long x6_tl[X6_PROF][8][8];
+__device__ unsigned long long x6_tl[X6_PROF][8][9];
 #define XTL(k) \
     if (blockIdx.x < X6_PROF && lane == 0) x6_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -109,26 +109,26 @@ __device__ unsigned long long x6_tl[X6_PROF][8][8];
 #ifdef X6_PROF
 // timeline summary of the most recent launch (tools/wino_x6_bench)
 void x6_timeline_print(int nwg, int nwave) {
-    std::vector<unsigned long long> tl((size_t)X6_PROF * 64);
+    std::vector<unsigned long long> tl((size_t)X6_PROF * 72);
     if (hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(x6_tl), tl.size() * 8) != hipSuccess) return;
     if (nwg > X6_PROF) nwg = X6_PROF;
     unsigned long long t0 = ~0ull, tend = 0, slast = 0;
-    // phases in time order: 0 -> 4 -> 5 -> 1 -> 2 -> 6 -> 7 -> 3
-    const int ord[8] = {0, 4, 5, 1, 2, 6, 7, 3};
-    double ph[7] = {0, 0, 0, 0, 0, 0, 0};
+    // phases in time order: 0 -> 8 -> 4 -> 5 -> 1 -> 2 -> 6 -> 7 -> 3
+    const int ord[9] = {0, 8, 4, 5, 1, 2, 6, 7, 3};
+    double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int g = 0; g < nwg; ++g)
         for (int w = 0; w < nwave; ++w) {
-            const unsigned long long* q = &tl[((size_t)g * 8 + w) * 8];
+            const unsigned long long* q = &tl[((size_t)g * 8 + w) * 9];
             t0 = q[0] < t0 ? q[0] : t0;
             tend = q[3] > tend ? q[3] : tend;
             slast = q[0] > slast ? q[0] : slast;
-            for (int k = 0; k < 7; ++k) ph[k] += (double)(q[ord[k + 1]] - q[ord[k]]);
+            for (int k = 0; k < 8; ++k) ph[k] += (double)(q[ord[k + 1]] - q[ord[k]]);
         }
     const double nw = nwg * (double)nwave * 100.0;
-    printf("  timeline (us): first start -> last end %.2f, last start +%.2f; per wave: issue+affine %.2f, stage0 %.2f, "
-           "transform0+stage1 %.2f, loop %.2f, epilogue image %.2f, stores %.2f, statistics %.2f\n",
+    printf("  timeline (us): first start -> last end %.2f, last start +%.2f; per wave: issue %.2f, affine %.2f, "
+           "stage0 %.2f, transform0+stage1 %.2f, loop %.2f, epilogue image %.2f, stores %.2f, statistics %.2f\n",
            (tend - t0) * 0.01, (slast - t0) * 0.01, ph[0] / nw, ph[1] / nw, ph[2] / nw, ph[3] / nw, ph[4] / nw,
-           ph[5] / nw, ph[6] / nw);
+           ph[5] / nw, ph[6] / nw, ph[7] / nw);
 }
 #endif
 
@@ -377,6 +377,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             load_u1(0, decltype(X)::value, decltype(X)::value, decltype(Pc)::value);
         });
     });
+    XTL(8);
     load_affine();
     XTL(4);
     if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging

@@ -575,8 +575,9 @@ class StyleTransferTrainingModel:
 
 class StyleTransferModels:
     """The object make_style_transfer_training_model returns (styleTransferTrainingModel.py:60-68).
-    ``transfer`` / ``style_predictor`` / ``inference`` are inference models holding the weights of
-    the moment they are built; ``refresh()`` rebuilds them from the trainers."""
+    ``transfer`` / ``style_predictor`` / ``inference`` share the training model's variables, as the Keras models
+    do: every access sees the trainers' current weights (a train step, a restore through any of them, moving
+    statistics), rebuilt lazily from the trainers when their weight versions changed. ``refresh()`` forces it."""
 
     def __init__(self, training: StyleTransferTrainingModel, loss_model):
         self.training = training
@@ -591,28 +592,56 @@ class StyleTransferModels:
             return StyleLoss(loss_model, training.with_depth_loss).compute(training(x), y_true)
 
         self.loss_model = end_to_end_loss
+        self._views = None
+        self._inference = (_SharedInference(self) if training.style_predictor is not None
+                           else _SharedTransfer(self))
         self.refresh()
 
-    def refresh(self):
+    def _current(self):
+        """(transfer, style_predictor) inference models holding the trainers' current weights."""
         tr = self.training
-        self.transfer = tr.transfer_model()
-        if tr.style_predictor is not None:
-            self.style_predictor = tr.style_predictor.inference_model()
-            self.inference = _SharedInference(self, self.transfer, self.style_predictor, 1, tr.name)
-        else:
-            self.style_predictor = None
-            self.inference = _SharedTransfer(self)
+        v = tr._weights_version()
+        if self._views is None or self._views[0] != v:
+            transfer = tr.transfer_model()
+            sp = tr.style_predictor.inference_model() if tr.style_predictor is not None else None
+            self._views = (v, transfer, sp)
+        return self._views[1], self._views[2]
+
+    @property
+    def transfer(self):
+        return self._current()[0]
+
+    @property
+    def style_predictor(self):
+        return self._current()[1]
+
+    @property
+    def inference(self):
+        return self._inference
+
+    def refresh(self):
+        self._views = None
+        self._current()
 
 
 class _SharedInference(StyleTransferInference):
     """``models.inference``: the inference graph of the training model, sharing its variables as the Keras
-    models do (styleTransferTrainingModel.py:52,66). A checkpoint restored through it (``load_weights``,
-    ``Checkpoint(models.inference).restore``, train_network.py:112-113) lands in the trainers, and the
-    inference models are rebuilt from them."""
+    models do (styleTransferTrainingModel.py:52,66): it runs the trainers' current weights, and a checkpoint
+    restored through it (``load_weights``, ``Checkpoint(models.inference).restore``, train_network.py:112-113)
+    lands in the trainers."""
 
-    def __init__(self, models, *args):
-        super().__init__(*args)
+    def __init__(self, models):
         self._models = models
+        self.num_styles = 1
+        self.name = models.training.name
+
+    @property
+    def transfer(self):
+        return self._models.transfer
+
+    @property
+    def style_predictor(self):
+        return self._models.style_predictor
 
     def _restore_tensors(self, tensors):
         st = self._models.training._restore_tensors(tensors)

@@ -1,0 +1,10 @@
+# r04 call: GPU tests (all failures listed); wino_x6 accumulator-mode timelines (0 none, 1 both, 2 producer, 3 consumer);
+# then smoke, A/B against HEAD's library, default bench
+mkdir -p gpurun_out
+O=gpurun_out
+TAG=r3 PYTEST_X=--maxfail=15 bash tools/gpu_measure.sh tests; trc=$?
+{ for m in 0 1 2 3; do timeout -k 10 120 ./tools/wino_x6_bench_prof 1 128 1 0 0 0 0 0 $m || exit 1; done
+  for m in 0 1; do timeout -k 10 120 ./tools/wino_x6_bench 1 128 1 0 0 0 0 0 $m || exit 1; done; } > $O/x6_accm.log 2>&1 || { tail -20 $O/x6_accm.log; exit 1; }
+grep -E "timeline|us/launch" $O/x6_accm.log
+[ $trc -eq 0 ] || exit 1
+TAG=r3 bash tools/gpu_measure.sh smoke ab=RST_LIB=tools/librst_head.so@-@3 bench
