@@ -94,7 +94,7 @@ struct Cfg {
     static constexpr int WREG = (WITEMS + 255) / 256;
     static constexpr int NACC = MS == 16 ? 4 : 16;          // accumulator floats per MFMA tile and lane
     static constexpr int NPH = MODE == 0 ? 1 : 4;           // output phases
-    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 + 8 * NC * 4;
+    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 + 12 * NC * 4;   // + statistics [12][NC]
     static_assert(CIN % CKC == 0 && CKC % (4 * KS) == 0, "chunking");
     static_assert(MS == 16 || MS == 32, "MFMA shape");
     static_assert(((CS / 4) & 1) == 1, "odd 16-B slots per halo pixel");
@@ -158,8 +158,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* const halo = smem;                  // [HALO]   one Cin chunk of the tile's input halo
     float* const wts = smem + C::HALO;         // [WCH]    one Cin chunk of the weights
-    float* const red = wts + C::WCH;           // [8][NC]  statistics scratch
-    float2* const tab = reinterpret_cast<float2*>(red + 8 * NC);   // prologue affine [batch][CIN] (+ second style)
+    float* const red = wts + C::WCH;           // [12][NC] statistics scratch: S, n, M2 per wave
+    float2* const tab = reinterpret_cast<float2*>(red + 12 * NC);   // prologue affine [batch][CIN] (+ second style)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     LT0(0);
@@ -590,11 +590,10 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                     }
                 if constexpr (MS == 16) m2 = lane_xor_sum<16>(m2);
                 m2 = lane_xor_sum<32>(m2);
-                lds_barrier();
-                if (lane < MS) red[wave * NC + n] = m2;
+                if (lane < MS) red[8 * NC + wave * NC + n] = m2;   // its own rows: no barrier before the write
                 lds_barrier();
                 if (tid < NC) {   // lane tid < NC holds column tid
-                    const float M2 = (red[tid] + red[NC + tid]) + (red[2 * NC + tid] + red[3 * NC + tid]);
+                    const float M2 = (red[8 * NC + tid] + red[9 * NC + tid]) + (red[10 * NC + tid] + red[11 * NC + tid]);
                     if (to_acc) {
                         if (T.b != acc_b) {
                             acc_flush();

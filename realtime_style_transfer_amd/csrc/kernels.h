@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstddef>
+#include <type_traits>
 #include <vector>
 
 namespace rst {
@@ -227,7 +228,24 @@ __device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb
                 for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += p[q * s.C];
             }
         }
-        for (int o = 1; o < L; o <<= 1) {
+        // the L lanes of an item are consecutive: within a quad (L <= 4) the partner words move by DPP (VALU) instead
+        // of ds_bpermute round trips; integer adds, so the merged words do not depend on the order
+        auto dpp64 = [](cin_word v, auto CTRL) __attribute__((always_inline)) {
+            constexpr int ctrl = decltype(CTRL)::value;
+            const unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)v, ctrl, 0xF, 0xF, true);
+            const unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)((unsigned long long)v >> 32), ctrl, 0xF,
+                                                            0xF, true);
+            return (cin_word)(((unsigned long long)hi << 32) | lo);
+        };
+        if (L >= 2) {
+#pragma unroll
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += dpp64(w[q], std::integral_constant<int, 0xB1>{});   // xor 1
+        }
+        if (L >= 4) {
+#pragma unroll
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += dpp64(w[q], std::integral_constant<int, 0x4E>{});   // xor 2
+        }
+        for (int o = 4; o < L; o <<= 1) {
 #pragma unroll
             for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += __shfl_xor(w[q], o);
         }

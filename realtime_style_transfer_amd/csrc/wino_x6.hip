@@ -523,7 +523,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     XTL(7);
     if (a.part != nullptr || a.stat.acc != nullptr) {
         f32x4* const red = reinterpret_cast<f32x4*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES);   // [2][8][32]
-        double* const dred = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES + YRED_BYTES);
         const float cnt = (float)(min(XTH, H - y0) * min(XTW, W - x0));
         auto xsum = [&](f32x4 v) __attribute__((always_inline)) {
             v.x = lane_xor_sum<32>(v.x);
@@ -549,30 +548,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         m2 = xsum(m2);
         if (lh == 0) red[256 + wave * 32 + cq] = m2;
         lds_barrier();
-        if (tid < 32) {
+        if (a.stat.acc != nullptr) {
+            // one thread per channel c (128 of them): S and M2 summed over the 8 waves in the order of the partials
+            // path, {S, M2 + S^2 / n} in f64 (finalize_kernel's merge quantity), straight into the fixed-point limbs
+            if (tid < XN) {
+                const float* const rf = reinterpret_cast<const float*>(red);   // [2][8 waves][128 channels]
+                float Sc = rf[tid], Mc = rf[1024 + tid];
+#pragma unroll
+                for (int w = 1; w < 8; ++w) {
+                    Sc += rf[w * 128 + tid];
+                    Mc += rf[1024 + w * 128 + tid];
+                }
+                const double dS = (double)Sc;
+                const int slot = (int)blockIdx.x % a.stat.nslot;
+                cin_acc_add_value(a.stat, a.batch, XN, b, tid, slot, 0, dS);
+                cin_acc_add_value(a.stat, a.batch, XN, b, tid, slot, 1, (double)Mc + dS * dS / (double)cnt);
+            }
+        } else if (tid < 32) {
             f32x4 M = red[256 + cq];
 #pragma unroll
             for (int w = 1; w < 8; ++w) M += red[256 + w * 32 + cq];
-            if (a.stat.acc != nullptr) {   // {S, M2 + S^2 / n} as f64 (finalize_kernel's merge quantity)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const double dS = (double)S[k];
-                    dred[4 * cq + k] = dS;
-                    dred[XN + 4 * cq + k] = (double)M[k] + dS * dS / (double)cnt;
-                }
-            } else {
-                const int n_part = a.tiles_y * a.tiles_x;
-                float4* const dst = a.part + ((size_t)b * XN + 4 * cq) * n_part + ty * a.tiles_x + tx;
-                dst[0] = make_float4(S.x, M.x, cnt, 0.f);
-                dst[n_part] = make_float4(S.y, M.y, cnt, 0.f);
-                dst[2 * n_part] = make_float4(S.z, M.z, cnt, 0.f);
-                dst[3 * n_part] = make_float4(S.w, M.w, cnt, 0.f);
-            }
-        }
-        if (a.stat.acc != nullptr) {   // channel-contiguous adds: 512 B per wave instruction
-            lds_barrier();
-            if (tid < 2 * XN)   // thread = (value, channel): 3 limb adds each, 512 B per wave instruction
-                cin_acc_add_value(a.stat, a.batch, XN, b, tid % XN, (int)blockIdx.x % a.stat.nslot, tid / XN, dred[tid]);
+            const int n_part = a.tiles_y * a.tiles_x;
+            float4* const dst = a.part + ((size_t)b * XN + 4 * cq) * n_part + ty * a.tiles_x + tx;
+            dst[0] = make_float4(S.x, M.x, cnt, 0.f);
+            dst[n_part] = make_float4(S.y, M.y, cnt, 0.f);
+            dst[2 * n_part] = make_float4(S.z, M.z, cnt, 0.f);
+            dst[3 * n_part] = make_float4(S.w, M.w, cnt, 0.f);
         }
     }
     XTL(3);
