@@ -96,6 +96,9 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 #ifndef X6_SKIP
 #define X6_SKIP 0
 #endif
+#ifndef RST_X6_AFFINE_FIRST
+#define RST_X6_AFFINE_FIRST 0   // fill order: prologue affine before (1) or after (0) the first staging / U loads
+#endif
 #ifdef X6_PROF
 // timeline per (workgroup, wave < 8) on the constant 100 MHz clock: 0 start, 8 first loads issued, 4 affine formed,
 // 5 chunk 0 staged, 1 pipeline filled, 2 chunk loop done, 6 epilogue image written, 7 outputs stored, 3 end
@@ -370,6 +373,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
 
     // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..R-1) in flight ----
+#if RST_X6_AFFINE_FIRST
+    // the prologue affine first: its accumulator loads are then not queued behind (vmcnt is in order) the staging
+    // and U loads, which are issued after it and land while it is formed
+    XTL(8);
+    load_affine();
+    XTL(4);
+#endif
     sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 0); });
     if (nchunks > 1) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload1(decltype(K)::value); });
     sfor<0, YRING>([&](auto X) __attribute__((always_inline)) {
@@ -377,9 +387,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             load_u1(0, decltype(X)::value, decltype(X)::value, decltype(Pc)::value);
         });
     });
+#if !RST_X6_AFFINE_FIRST
     XTL(8);
     load_affine();
     XTL(4);
+#endif
     if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging
     stage_all(0, patch);
     lds_barrier();

@@ -4,8 +4,11 @@ mkdir -p gpurun_out
 O=gpurun_out
 TAG=r3 PYTEST_X=--maxfail=15 bash tools/gpu_measure.sh tests; trc=$?
 { for m in 0 1 2 3; do timeout -k 10 120 ./tools/wino_x6_bench_prof 1 128 1 0 0 0 0 0 $m || exit 1; done
-  for m in 0 1; do timeout -k 10 120 ./tools/wino_x6_bench 1 128 1 0 0 0 0 0 $m || exit 1; done; } > $O/x6_accm.log 2>&1 || { tail -20 $O/x6_accm.log; exit 1; }
+  for m in 0 1; do timeout -k 10 120 ./tools/wino_x6_bench 1 128 1 0 0 0 0 0 $m || exit 1; done
+  echo "== affine first"; timeout -k 10 120 ./tools/wino_x6_bench_prof_af 1 128 1 0 0 0 0 0 1 || exit 1; } > $O/x6_accm.log 2>&1 || { tail -20 $O/x6_accm.log; exit 1; }
 grep -E "timeline|us/launch" $O/x6_accm.log
+timeout -k 10 120 ./tools/affine_probe > $O/affine_probe.log 2>&1 || { cat $O/affine_probe.log; exit 1; }
+cat $O/affine_probe.log
 # packed-f32 (SLP-vectorised) transforms vs scalar, standalone, alternating
 { for i in 1 2; do timeout -k 10 120 ./tools/wino9_x6_bench 1 && timeout -k 10 120 ./tools/wino9_x6_bench_slp 1 && \
   timeout -k 10 120 ./tools/wino_x6_bench 1 128 1 0 0 0 0 0 1 && timeout -k 10 120 ./tools/wino_x6_bench_slp 1 128 1 0 0 0 0 0 1 || exit 1; done; } > $O/slp_ab.log 2>&1 || { tail -20 $O/slp_ab.log; exit 1; }
