@@ -197,12 +197,13 @@ __device__ __forceinline__ void cin_acc_add(const CinAcc& a, int batch, int C, i
 template <int NT>
 __device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb, float2* tab, float2* tab1,
                                                  float2* out, float2* out1) {
-    constexpr int RMAX = 4;   // copies per lane (each 2 x CIN_LIMBS words)
+    constexpr int RMAX = 8;   // copies per lane (each 2 x CIN_LIMBS words)
     int K = 1;
     while (K < s.nslot) K <<= 1;
     const int items = nb * s.C;
     int L = K / RMAX > 1 ? K / RMAX : 1;                   // at most RMAX copies per lane
-    while (L < K && 2 * L * items <= NT) L <<= 1;         // more lanes while one pass still covers every item
+    // more lanes while one pass still covers every item, up to a quad (the lanes of an item merge by DPP: VALU only)
+    while (L < K && L < 4 && 2 * L * items <= NT) L <<= 1;
     const int R = K / L, n = items * L;
     for (int base = 0; base < n; base += NT) {
         const int i = base + (int)threadIdx.x, it = i / L, l = i & (L - 1);

@@ -486,7 +486,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
                                          ? h->layers[li + 1].pro_src == (int)li && takes_acc(h->layers[li + 1].kind)
                                          : fused_out;
             if (!consumer_ok) continue;
-            e.nslot = e.kind == K_WINOX6 ? 8 : (e.kind == K_LITE ? 32 : 64);
+            e.nslot = e.kind == K_WINOX6 ? 8 : 32;   // <= 32: consumers merge the copies inside a lane quad
             e.acc_off = (long)n_acc;                   // per image: the layer's block scales with the batch
             n_acc += (size_t)e.nslot * 2 * CIN_LIMBS * e.s.cout;
         }
