@@ -64,6 +64,9 @@ KERNEL_NAMES = {
     303: "conv_lite<3x3 s2 transposed Cin128 Cout32 f32 32x32x2 MFMA>",
     304: "conv_lite<3x3 s2 transposed Cin32 Cout16 f32 16x16x4 MFMA>",
     305: "conv_lite<3x3 s2 transposed Cin128 Cout32 split-bf16 x6 32x32x16 MFMA>",
+    306: "conv_lite<3x3 s2 Cin32 Cout16 split-bf16 x6 16x16x32 MFMA>",
+    307: "conv_lite<3x3 s2 Cin16 Cout32 split-bf16 x6 32x32x16 MFMA>",
+    308: "conv_lite<3x3 s2 transposed Cin32 Cout16 split-bf16 x6 16x16x32 MFMA>",
     203: "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 16x16 N32 split-bf16 x6 MFMA persistent>",
 }
 
@@ -82,7 +85,8 @@ DTYPE_DESC = {
                        "F(2x2,3x3) whose transform-domain products are exact 3-piece split-bf16 MFMA terms (each "
                        "fp32 operand = 3 bf16 pieces holding all 24 significant bits, 6 product terms, dropped "
                        "terms <= 2^-25 of each product, fp32 accumulate); the final 9x9 transposed conv as a GEMM "
-                       "over (kx, co) columns with the same exact split-bf16 products; other layers f32 MFMA",
+                       "over (kx, co) columns and the narrow stride-2 (transposed) convs with the same exact "
+                       "split-bf16 products",
 }
 
 
@@ -108,8 +112,11 @@ def executed_mfma(model, plan, i: int, B: int):
         return 6 * 2.0 * tiles * 16 * (9 * 16 + 16) * l.cout, BF16_MFMA_PEAK_TFLOPS
     if kid == 204:   # per output row and 88-column strip: 3 x' tiles of 32, N = 32 columns (27 used), K = 9 x 16
         return 6 * 2.0 * B * Ho * (-(-Wo // 88)) * 3 * 32 * 32 * 144, BF16_MFMA_PEAK_TFLOPS
-    if kid == 305:   # 9 (phase, tap) slots x Cin x Cout per input pixel, 6 bf16 terms, tiles of 4 x 32
-        tiles = B * (-(-l.in_hw[0] // 4)) * (-(-l.in_hw[1] // 32)) * 4 * 32
+    if kid in (305, 308):   # 9 (phase, tap) slots x Cin x Cout per input pixel, 6 bf16 terms, tiles of 4 x Cout
+        tiles = B * (-(-l.in_hw[0] // 4)) * (-(-l.in_hw[1] // l.cout)) * 4 * l.cout
+        return 6 * 2.0 * tiles * 9 * l.cin * l.cout, BF16_MFMA_PEAK_TFLOPS
+    if kid in (306, 307):   # strided: 9 taps x Cin x Cout per output pixel, 6 bf16 terms, tiles of 4 x Cout
+        tiles = B * (-(-Ho // 4)) * (-(-Wo // l.cout)) * 4 * l.cout
         return 6 * 2.0 * tiles * 9 * l.cin * l.cout, BF16_MFMA_PEAK_TFLOPS
     if 101 <= kid < 200:
         terms = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}.get(model.precision, 6)
