@@ -13,5 +13,8 @@ cat $O/affine_probe.log
 { for i in 1 2; do timeout -k 10 120 ./tools/wino9_x6_bench 1 && timeout -k 10 120 ./tools/wino9_x6_bench_slp 1 && \
   timeout -k 10 120 ./tools/wino_x6_bench 1 128 1 0 0 0 0 0 1 && timeout -k 10 120 ./tools/wino_x6_bench_slp 1 128 1 0 0 0 0 0 1 || exit 1; done; } > $O/slp_ab.log 2>&1 || { tail -20 $O/slp_ab.log; exit 1; }
 grep -E "us/launch" $O/slp_ab.log
+# start-conv wave stagger (W9_STAGGER s_sleep units), alternating
+{ for i in 1 2; do for v in "" _st2 _st4 _st8 _pipe _pipeslp _slp; do echo "== w9$v"; timeout -k 10 120 ./tools/wino9_x6_bench$v 1 || exit 1; done; done; } > $O/w9_stagger.log 2>&1 || { tail -20 $O/w9_stagger.log; exit 1; }
+grep -E "==|us/launch" $O/w9_stagger.log
 [ $trc -eq 0 ] || exit 1
 TAG=r3 bash tools/gpu_measure.sh smoke ab=RST_LIB=tools/librst_head.so@-@3 bench
