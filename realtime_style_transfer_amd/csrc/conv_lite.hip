@@ -29,6 +29,16 @@
 
 #include "kernels.h"
 
+// expand_0 x6 chunk width: 32 (default: 4 chunks, one LDS buffer) or 16 (8 chunks through the double-buffered PIPE
+// loop; measured equal at B = 8 and 3.5 us slower at B = 1, profiles/r04/lite_pipe.log)
+#ifndef RST_LITE_E0_CKC
+#define RST_LITE_E0_CKC 32
+#endif
+// x6 B-operand ring depth (slots of weights read ahead of their MFMAs): 2 = one slot ahead
+#ifndef LITE_BDEPTH
+#define LITE_BDEPTH 2
+#endif
+
 #ifndef LITE_SKIP
 #define LITE_SKIP 0   // tools/lite_bench knobs: 1 no halo loads, 2 no MFMAs, 8 no output stores, 32 no statistics
 #endif
@@ -88,13 +98,16 @@ struct Cfg {
     static constexpr bool WIN_REGS = X6 && NCH == 1;        // x6 weights in registers
     static constexpr int HALO = X6 ? 3 * KS2 * G * NPIXP * 4 : NPIX * CS;   // floats per halo buffer
     static constexpr int WCH = WIN_REGS ? 0 : (X6 ? 9 * CKC * NC * 3 / 2 : 9 * CKC * NC);   // floats per chunk of weights in LDS
+    // x6 multi-chunk layers whose double buffer fits (expand_0 at 16-channel chunks): halo + weight images
+    // double-buffered in LDS, chunk c + 1 staged while chunk c's MFMAs run (its global loads two chunks ahead)
+    static constexpr bool PIPE = X6 && NCH > 1 && (HALO + WCH) * 8 + 16 * NC * 4 <= 128 * 1024;
     static constexpr int HITEMS = HR * HC * QC;             // float4 items per halo chunk
     static constexpr int HREG = (HITEMS + 255) / 256;
     static constexpr int WITEMS = WCH / 4;
     static constexpr int WREG = (WITEMS + 255) / 256;
     static constexpr int NACC = MS == 16 ? 4 : 16;          // accumulator floats per MFMA tile and lane
     static constexpr int NPH = MODE == 0 ? 1 : 4;           // output phases
-    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 + 12 * NC * 4;   // + statistics [12][NC]
+    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 * (PIPE ? 2 : 1) + 16 * NC * 4;   // + statistics [16][NC]
     static_assert(CIN % CKC == 0 && CKC % (4 * KS) == 0, "chunking");
     static_assert(MS == 16 || MS == 32, "MFMA shape");
     static_assert(((CS / 4) & 1) == 1, "odd 16-B slots per halo pixel");
@@ -156,10 +169,16 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     constexpr int QC = C::QC, NCH = C::NCH;
 
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* const halo = smem;                  // [HALO]   one Cin chunk of the tile's input halo
-    float* const wts = smem + C::HALO;         // [WCH]    one Cin chunk of the weights
-    float* const red = wts + C::WCH;           // [12][NC] statistics scratch: S, n, M2 per wave
-    float2* const tab = reinterpret_cast<float2*>(red + 12 * NC);   // prologue affine [batch][CIN] (+ second style)
+    // [HALO] one Cin chunk of the tile's input halo, then [WCH] its weights (PIPE: two such buffers); halo / wts are
+    // where compute reads, halo_w / wts_w where staging writes (the same buffer unless PIPE)
+    float* halo = smem;
+    float* wts = smem + C::HALO;
+    float* halo_w = halo;
+    float* wts_w = wts;
+    // [16][NC] statistics: S, n, M2 per wave (partials path) / [4][NC][2] f64 (accumulator flush)
+    float* const red = smem + (C::HALO + C::WCH) * (C::PIPE ? 2 : 1);
+    static_assert((C::HALO + C::WCH) % 2 == 0, "f64-aligned statistics scratch");
+    float2* const tab = reinterpret_cast<float2*>(red + 16 * NC);   // prologue affine [batch][CIN] (+ second style)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     LT0(0);
@@ -198,10 +217,19 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // two register sets of staged input (single-chunk layers prefetch two tiles ahead: the HBM latency
     // under load exceeds one tile's MFMAs); multi-chunk layers use set 0 only
     // (x6 single-chunk layers hold their weights in VGPRs instead: one set, two workgroups per CU cover the latency)
-    constexpr int NSET = NCH == 1 && !C::WIN_REGS ? 2 : 1;
+    constexpr int NSET = (NCH == 1 && !C::WIN_REGS) || C::PIPE ? 2 : 1;
     f32x4 hreg[NSET][NMAIN + 1], rreg[NSET][NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01[NSET], pa23[NSET];
     f32x4 pb01[NSET], pb23[NSET];   // BLEND: the second style's affine of the thread's channel quad
     float bw[NSET][NMAIN + 1];      // BLEND: the second style's weight at each staged pixel
+    // one chunk's weight image (multi-chunk layers; one register set: PIPE loads it one step ahead, before the halo
+    // loads of the step after, and stores it in the step's last MFMA slots)
+    auto load_w = [&](int ch) __attribute__((always_inline)) {
+        sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
+            constexpr int k = decltype(K)::value;
+            const int it = min(tid + 256 * k, C::WITEMS - 1);
+            wreg[k] = reinterpret_cast<const f32x4*>(a.wpk)[(size_t)ch * C::WITEMS + it];
+        });
+    };
     auto load_in = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {
         constexpr int st = decltype(SET)::value;
         const int co = ch * CKC;
@@ -219,13 +247,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
 #endif
             if constexpr (BLEND) bw[st][k] = a.pro_w[(rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)];
         });
-        if constexpr (NCH > 1) {
-            sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
-                constexpr int k = decltype(K)::value;
-                const int it = min(tid + 256 * k, C::WITEMS - 1);
-                wreg[k] = reinterpret_cast<const f32x4*>(a.wpk)[(size_t)ch * C::WITEMS + it];
-            });
-        }
+        if constexpr (NCH > 1 && !C::PIPE) load_w(ch);
     };
     auto load_aff = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {   // from the LDS table
         constexpr int st = decltype(SET)::value;
@@ -269,7 +291,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     };
     // x6: channel quad q of the chunk = K step q / (KSTEP / 4), lane group (q % (KSTEP / 4)) >> 1, bf16 slots
     // 4 (q & 1) .. +3 of the group's 8; pixels in halo_off's order (stride-2 columns parity-split)
-    unsigned char* const hbytes = reinterpret_cast<unsigned char*>(halo);
+    auto hbytes_r = [&]() __attribute__((always_inline)) { return reinterpret_cast<const unsigned char*>(halo); };
     constexpr int QPS = C::KSTEP / 4;                                                  // channel quads per K step
     const int xq = (((q / QPS) * C::G + ((q % QPS) >> 1)) * C::NPIXP) * 16 + (q & 1) * 8;   // + piece + pixel
     constexpr int XPIECE = C::KS2 * C::G * C::NPIXP * 16;                             // bytes per piece plane
@@ -282,21 +304,23 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             unsigned p0[2], p1[2], p2[2];
             split3(v.x, v.y, p0[0], p1[0], p2[0]);
             split3(v.z, v.w, p0[1], p1[1], p2[1]);
-            unsigned char* dst = hbytes + xq + hpix(hy, hx) * 16;
+            unsigned char* dst = reinterpret_cast<unsigned char*>(halo_w) + xq + hpix(hy, hx) * 16;
             *reinterpret_cast<uint2*>(dst) = make_uint2(p0[0], p0[1]);
             *reinterpret_cast<uint2*>(dst + XPIECE) = make_uint2(p1[0], p1[1]);
             *reinterpret_cast<uint2*>(dst + 2 * XPIECE) = make_uint2(p2[0], p2[1]);
         } else {
-            *reinterpret_cast<f32x4*>(halo + lf + hy * (HC * CS)) = v;
+            *reinterpret_cast<f32x4*>(halo_w + lf + hy * (HC * CS)) = v;
         }
     };
-    auto store_step = [&](const Tile& T, auto SET) __attribute__((always_inline)) {
-        constexpr int st = decltype(SET)::value;
-        const bool okm = T.ix0 + col >= 0 && T.ix0 + col < W;
-        const bool oke = T.ix0 + HCM >= 0 && T.ix0 + HCM < W;
+    // staging of one chunk into the write buffer, as NSTORE items (PIPE interleaves them with the MFMAs): the
+    // NMAIN main-column rows, the last halo column, then the WREG weight float4s
+    constexpr int NSTORE = NMAIN + 1 + (NCH > 1 ? C::WREG : 0);
+    auto store_item = [&](const Tile& T, auto SET, auto IDX) __attribute__((always_inline)) {
+        constexpr int st = decltype(SET)::value, idx = decltype(IDX)::value;
         auto row_ok = [&](int hy) __attribute__((always_inline)) { return T.iy0 + hy >= 0 && T.iy0 + hy < H; };
-        sfor<0, NMAIN>([&](auto K) __attribute__((always_inline)) {
-            constexpr int k = decltype(K)::value;
+        if constexpr (idx < NMAIN) {
+            constexpr int k = idx;
+            const bool okm = T.ix0 + col >= 0 && T.ix0 + col < W;
             const int hy = rsub + RPP * k;
             if (HR % RPP == 0 || k < NMAIN - 1 || hy < HR) {
                 const f32x4 v = okm && row_ok(hy) ? xform(hreg[st][k], rreg[st][k], pa01[st], pa23[st], bw[st][k],
@@ -304,20 +328,22 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                                                   : f32x4{0.f, 0.f, 0.f, 0.f};
                 put(hy, col, lcm, v);
             }
-        });
-        if (tid < NEXTRA) {
-            const f32x4 v = oke && row_ok(ehy) ? xform(hreg[st][NMAIN], rreg[st][NMAIN], pa01[st], pa23[st],
-                                                       bw[st][NMAIN], pb01[st], pb23[st])
-                                               : f32x4{0.f, 0.f, 0.f, 0.f};
-            put(ehy, HCM, lce, v);
+        } else if constexpr (idx == NMAIN) {
+            const bool oke = T.ix0 + HCM >= 0 && T.ix0 + HCM < W;
+            if (tid < NEXTRA) {
+                const f32x4 v = oke && row_ok(ehy) ? xform(hreg[st][NMAIN], rreg[st][NMAIN], pa01[st], pa23[st],
+                                                           bw[st][NMAIN], pb01[st], pb23[st])
+                                                   : f32x4{0.f, 0.f, 0.f, 0.f};
+                put(ehy, HCM, lce, v);
+            }
+        } else if constexpr (NCH > 1) {
+            constexpr int k = idx - NMAIN - 1;
+            const int it = tid + 256 * k;
+            if (C::WITEMS % 256 == 0 || it < C::WITEMS) reinterpret_cast<f32x4*>(wts_w)[it] = wreg[k];
         }
-        if constexpr (NCH > 1) {
-            sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
-                constexpr int k = decltype(K)::value;
-                const int it = tid + 256 * k;
-                if (C::WITEMS % 256 == 0 || it < C::WITEMS) reinterpret_cast<f32x4*>(wts)[it] = wreg[k];
-            });
-        }
+    };
+    auto store_step = [&](const Tile& T, auto SET) __attribute__((always_inline)) {
+        sfor<0, NSTORE>([&](auto I) __attribute__((always_inline)) { store_item(T, SET, I); });
     };
 
     // ---- operands: A = pixel m of this wave's row, quad g + KS r; B = row (slot, r, g), column m ------
@@ -406,9 +432,11 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 acc_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ap[t6]], Bv[bp[t6]], acc_, 0, 0, 0);
         });
     };
-    auto compute_x6 = [&]() __attribute__((always_inline)) {
+    auto no_hook = [](auto) __attribute__((always_inline)) {};
+    auto compute_x6 = [&](auto&& hook) __attribute__((always_inline)) {
       if constexpr (X6) {   // discarded (not instantiated) for the f32 configurations
         const unsigned char* wbytes = reinterpret_cast<const unsigned char*>(wts);
+        const unsigned char* hbytes = hbytes_r();
         auto readB = [&](int sl, int ks, short8 (&Bv)[3]) __attribute__((always_inline)) {
             sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
                 constexpr int pc = decltype(PC)::value;
@@ -430,19 +458,20 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                     constexpr int pos = decltype(P)::value;
                     readA((wave + (pos >> 1)) * HC + m + (pos & 1), ks, A[pos]);
                 });
-                short8 B0[3], B1[3];
-                if constexpr (!C::WIN_REGS) readB(order[0], ks, B0);
+                constexpr int BD = LITE_BDEPTH;
+                short8 Bq[BD][3];
+                if constexpr (!C::WIN_REGS)
+                    sfor<0, BD - 1>([&](auto P) __attribute__((always_inline)) {
+                        readB(order[decltype(P)::value], ks, Bq[decltype(P)::value]);
+                    });
                 sfor<0, 9>([&](auto J) __attribute__((always_inline)) {
                     constexpr int j = decltype(J)::value, sl = order[j];
                     constexpr int ai = (sl == 1 || sl == 3) ? 4 : t_phase(sl), pos = t_pos(sl);
-                    if constexpr (!C::WIN_REGS && j + 1 < 9) {
-                        if constexpr ((j & 1) == 0) readB(order[j + 1], ks, B1);
-                        else readB(order[j + 1], ks, B0);
-                    }
+                    if constexpr (!C::WIN_REGS && j + BD - 1 < 9) readB(order[j + BD - 1], ks, Bq[(j + BD - 1) % BD]);
                     __builtin_amdgcn_sched_barrier(0);
                     if constexpr (C::WIN_REGS) mfma6(acc[ai], A[pos], wr6[sl]);
-                    else if constexpr ((j & 1) == 0) mfma6(acc[ai], A[pos], B0);
-                    else mfma6(acc[ai], A[pos], B1);
+                    else mfma6(acc[ai], A[pos], Bq[j % BD]);
+                    hook(std::integral_constant<int, ks * 9 + j>{});   // PIPE: staging items beside the MFMAs
                     __builtin_amdgcn_sched_barrier(0);
                 });
             } else {   // taps t = 3 ky + kx into acc[kx]; A of tap t + 1 read while tap t's MFMAs run
@@ -468,7 +497,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     };
     auto compute = [&]() __attribute__((always_inline)) {
         if constexpr (X6) {
-            if constexpr ((LITE_SKIP & 2) == 0) compute_x6();
+            if constexpr ((LITE_SKIP & 2) == 0) compute_x6(no_hook);
         } else if constexpr ((LITE_SKIP & 2) == 0) {
             f32x4 A0[NA], B0[NB], A1[NA], B1[NB];
             read_step(std::integral_constant<int, 0>{}, A0, B0);
@@ -490,13 +519,30 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     const int n = M::col(lane);
     const float bias = a.bias[n];
     const float2 bn = MODE == 0 ? a.bn_ab[n] : float2{1.f, 0.f};
-    // CIN statistics into fixed-point accumulators (a.stat): this workgroup's tiles summed per image in the lanes
-    // tid < NC ({S, M2 + S^2/n} per tile, finalize_kernel's merge quantity), added at an image change / the end
+    // CIN statistics into fixed-point accumulators (a.stat): per wave and tile a two-pass {S, M2} over the wave's
+    // pixel row, summed per image as {S, M2 + S^2/n} (finalize_kernel's merge quantity: the sum of squares formed
+    // around the row mean) in the wave's lanes < MS (lane = channel) — no cross-wave exchange per tile. At an
+    // image change / the end (every thread, uniform) the four waves' sums meet in LDS in a fixed order and lanes
+    // tid < NC add them to the accumulators.
     const bool to_acc = a.stat.acc != nullptr;
     double accS = 0.0, accQ = 0.0;
     int acc_b = -1;
+    double* const red_d = reinterpret_cast<double*>(red);   // [4 waves][NC][2] at the flush
     auto acc_flush = [&]() __attribute__((always_inline)) {
-        if (acc_b >= 0) cin_acc_add(a.stat, a.batch, NC, acc_b, tid, (int)blockIdx.x % a.stat.nslot, accS, accQ);
+        if (acc_b >= 0) {
+            if (lane < MS) {
+                red_d[(wave * NC + lane) * 2] = accS;
+                red_d[(wave * NC + lane) * 2 + 1] = accQ;
+            }
+            lds_barrier();   // (the next write of red_d comes after the next step's top barrier)
+            if (tid < NC) {
+                const double S = (red_d[tid * 2] + red_d[(NC + tid) * 2]) +
+                                 (red_d[(2 * NC + tid) * 2] + red_d[(3 * NC + tid) * 2]);
+                const double Q = (red_d[tid * 2 + 1] + red_d[(NC + tid) * 2 + 1]) +
+                                 (red_d[(2 * NC + tid) * 2 + 1] + red_d[(3 * NC + tid) * 2 + 1]);
+                cin_acc_add(a.stat, a.batch, NC, acc_b, tid, (int)blockIdx.x % a.stat.nslot, S, Q);
+            }
+        }
         accS = accQ = 0.0;
     };
     const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
@@ -563,7 +609,35 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         }
                     }
             }
-            if ((a.part != nullptr || to_acc) && (LITE_SKIP & 32) == 0) {
+            if (to_acc && (LITE_SKIP & 32) == 0) {   // per-wave two-pass partials (see acc_flush)
+                if constexpr (MS == 16) {
+                    s = lane_xor_sum<16>(s);
+                    cnt = lane_xor_sum<16>(cnt);
+                }
+                s = lane_xor_sum<32>(s);
+                cnt = lane_xor_sum<32>(cnt);
+                const float mean = cnt > 0.f ? s / cnt : 0.f;
+                float m2 = 0.f;
+#pragma unroll
+                for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+                    for (int j = 0; j < C::NACC; ++j) {
+                        const int qq = T.x0 + M::row(j, lane);
+                        const float d = acc[ph][j] - mean;
+                        if (full || (p < a.Ho && qq < a.Wo)) m2 = fmaf(d, d, m2);
+                    }
+                if constexpr (MS == 16) m2 = lane_xor_sum<16>(m2);
+                m2 = lane_xor_sum<32>(m2);
+                if (T.b != acc_b) {   // uniform over the workgroup
+                    acc_flush();
+                    acc_b = T.b;
+                }
+                if (lane < MS) {
+                    const double dS = (double)s;
+                    accS += dS;
+                    if (cnt > 0.f) accQ += (double)m2 + dS * dS / (double)cnt;
+                }
+            } else if (a.part != nullptr && (LITE_SKIP & 32) == 0) {
                 // lanes n, n + MS, ... hold column n: reduce over them, then over the 4 waves (fixed order)
                 if constexpr (MS == 16) {
                     s = lane_xor_sum<16>(s);
@@ -594,18 +668,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 lds_barrier();
                 if (tid < NC) {   // lane tid < NC holds column tid
                     const float M2 = (red[8 * NC + tid] + red[9 * NC + tid]) + (red[10 * NC + tid] + red[11 * NC + tid]);
-                    if (to_acc) {
-                        if (T.b != acc_b) {
-                            acc_flush();
-                            acc_b = T.b;
-                        }
-                        const double dS = (double)S;
-                        accS += dS;
-                        if (N > 0.f) accQ += (double)M2 + dS * dS / (double)N;
-                    } else {
-                        const int n_part = a.tiles_y * a.tiles_x;
-                        a.part[((size_t)T.b * NC + tid) * n_part + T.ty * a.tiles_x + T.tx] = make_float4(S, M2, N, 0.f);
-                    }
+                    const int n_part = a.tiles_y * a.tiles_x;
+                    a.part[((size_t)T.b * NC + tid) * n_part + T.ty * a.tiles_x + T.tx] = make_float4(S, M2, N, 0.f);
                 }
             }
         }
@@ -638,7 +702,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     const int my_tiles = (n_tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     // the next layer's weights into this XCD's L2, touched as the workgroup starts its last tile(s) so that this
     // kernel's own stream does not evict them again (speed only)
-    unsigned l2f = 0;
+    l2_touch_t l2f = {0u, 0u};
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, NSET - 1>;
     zero_acc();
@@ -686,6 +750,72 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
             T0 = T2;
         }
+    } else if constexpr (C::PIPE) {
+        // global step s = (tile s / NCH, chunk s % NCH) computes from LDS buffer s & 1 while its MFMA slots stage step
+        // s + 1 (register set (s + 1) & 1, loaded two steps earlier) into buffer (s + 1) & 1; one barrier per step,
+        // after which the freed set takes step s + 3's global loads. n_steps is even (NCH even): the loop body
+        // runs a step pair so that buffer and set indices are compile-time.
+        static_assert(NCH % 2 == 0 && NCH >= 4, "PIPE: even chunk count, at least 4");
+        const int n_steps = my_tiles * NCH;
+        float* const buf1 = smem + C::HALO + C::WCH;
+        auto tile_at = [&](int st) __attribute__((always_inline)) { return tile_of(st / NCH); };
+        Tile cur = tile_of(0), nx1 = tile_at(1);
+        load_w(0);
+        load_in(cur, 0, S0{});
+        load_in(nx1, 1, S1{});
+        fill_table();
+        load_aff(cur, 0, S0{});
+        load_aff(nx1, 1, S1{});
+        store_step(cur, S0{});   // halo_w / wts_w = buffer 0
+        lds_barrier();
+        load_w(1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_step(tile_at(2), 2, S0{});   // n_steps >= NCH >= 4
+        auto pipe_step = [&](int s, auto PAR) __attribute__((always_inline)) {
+            constexpr int par = decltype(PAR)::value;   // s & 1
+            using SN = std::integral_constant<int, par ^ 1>;
+            const int ch = s % NCH;
+            LTL(s, 0);
+            if (s == n_steps - NCH) l2f = l2_touch_xcd_slice<256, 2>(a.w_next, a.w_next_bytes);
+            halo = par ? buf1 : smem;
+            wts = halo + C::HALO;
+            halo_w = par ? smem : buf1;
+            wts_w = halo_w + C::HALO;
+            LTL(s, 1);
+            // (the last step stages a repeat of itself into the idle buffer: no branch, so that the compiler's
+            // vmcnt bookkeeping stays exact across the step)
+            if constexpr ((LITE_SKIP & 2) == 0) {
+                // NSTORE items over the 9 KS2 slots: one per slot, the rest after the last
+                compute_x6([&](auto J) __attribute__((always_inline)) {
+                    constexpr int j = decltype(J)::value, nsl = 9 * C::KS2;
+                    if constexpr (j < nsl - 1) {
+                        if constexpr (j < NSTORE) store_item(nx1, SN{}, std::integral_constant<int, j>{});
+                    } else {
+                        sfor<nsl - 1, NSTORE>([&](auto I) __attribute__((always_inline)) { store_item(nx1, SN{}, I); });
+                    }
+                });
+            } else {
+                store_step(nx1, SN{});
+            }
+            LTL(s, 2);
+            if (ch == NCH - 1) {
+                epilogue(cur);
+                zero_acc();
+            }
+            lds_barrier();   // buffer par read, buffer par ^ 1 written
+            // steps past the end re-load the last one (unconditional loads, see above)
+            const int s2 = min(s + 2, n_steps - 1), s3 = min(s + 3, n_steps - 1);
+            load_w(s2 % NCH);
+            __builtin_amdgcn_sched_barrier(0);
+            load_step(tile_at(s3), s3 % NCH, SN{});
+            LTL(s, 3);
+            cur = nx1;
+            nx1 = tile_at(s2);
+        };
+        for (int s = 0; s < n_steps; s += 2) {
+            pipe_step(s, S0{});
+            pipe_step(s + 1, S1{});
+        }
     } else {   // multi-chunk layers, and single-chunk layers with one register set (x6: weights in VGPRs)
         const int n_steps = my_tiles * NCH;
         Tile cur = tile_of(0);
@@ -716,7 +846,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             cur = nxt;
         }
     }
-    if (to_acc && tid < NC) acc_flush();
+    if (to_acc) acc_flush();
     LT0(1);
     l2_touch_keep(l2f, a.batch < 0, smem);
 }
@@ -729,7 +859,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     X(2, 0, 16, 32, 16, 0)         \
     X(3, 1, 128, 32, 32, 0)        \
     X(4, 1, 32, 16, 32, 0)         \
-    X(5, 1, 128, 32, 32, 1)        \
+    X(5, 1, 128, 32, RST_LITE_E0_CKC, 1) \
     X(6, 0, 32, 16, 32, 1)         \
     X(7, 0, 16, 32, 16, 1)         \
     X(8, 1, 32, 16, 32, 1)

@@ -71,27 +71,31 @@ __device__ __forceinline__ int xcd_tile_order(int bid, int n) {
 // ---- next-layer weights into L2 (inference; speed only) -----------------------------------------------
 // Every workgroup of a launch reads one slice of the next layer's weight image, one dword per 128-B line, all its
 // loads issued at once: the workgroups with the same blockIdx % 8 (one XCD under the round-robin dispatch) cover the
-// whole image, so the next kernel's first weight loads hit its XCD's L2 instead of all missing together. Returns a
-// fold of the loaded words; the caller passes it to l2_touch_keep at its end (keeps the loads, waits for nothing
-// earlier). Measured on the residual convs: cold U cost 6-9 us per launch in the frame.
+// whole image, so the next kernel's first weight loads hit its XCD's L2 instead of all missing together. The caller
+// passes the loaded words to l2_touch_keep at its end (keeps the loads). Measured on the residual convs: cold U cost
+// 6-9 us per launch in the frame.
+// The loaded words are returned unfolded: their first use (l2_touch_keep, at the kernel's end) is where the compiler
+// waits for them, so a touch issued inside a branch does not drain the caller's outstanding loads there.
+typedef unsigned l2_touch_t __attribute__((ext_vector_type(2)));
 template <int NT, int NLD>
-__device__ __forceinline__ unsigned l2_touch_xcd_slice(const void* p, int bytes) {
-    if (p == nullptr || bytes <= 0) return 0u;
+__device__ __forceinline__ l2_touch_t l2_touch_xcd_slice(const void* p, int bytes) {
+    static_assert(NLD == 1 || NLD == 2, "one or two lines per thread");
+    l2_touch_t f = {0u, 0u};
+    if (p == nullptr || bytes <= 0) return f;
     const int xr = (int)(blockIdx.x & 7), k = (int)(blockIdx.x >> 3);
     const int nk = ((int)gridDim.x - xr + 7) >> 3;   // workgroups with this XCD residue
     const int nl = bytes >> 7, per = (nl + nk - 1) / nk;
     const __amdgpu_buffer_rsrc_t srd = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
     const int beg = k * per, end = min(beg + per, nl);
-    unsigned f = 0;
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
         const int i = beg + (int)threadIdx.x + j * NT;
-        f ^= __builtin_amdgcn_raw_buffer_load_b32(srd, i < end ? i * 128 : 0x7FFFFFF0, 0, 0);
+        f[j] = __builtin_amdgcn_raw_buffer_load_b32(srd, i < end ? i * 128 : 0x7FFFFFF0, 0, 0);
     }
     return f;
 }
-__device__ __forceinline__ void l2_touch_keep(unsigned f, bool never, float* sink) {
-    if (f == 0x9E3779B9u && never) *sink = 0.f;   // never true: only keeps the loads
+__device__ __forceinline__ void l2_touch_keep(l2_touch_t f, bool never, float* sink) {
+    if ((f.x ^ f.y) == 0x9E3779B9u && never) *sink = 0.f;   // never true: only keeps the loads
 }
 
 // ---- CIN statistics through fixed-point accumulators (inference) ---------------------------------------

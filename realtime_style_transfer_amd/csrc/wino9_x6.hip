@@ -260,7 +260,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
         w9_it = it;
         W9TL(0);
         const int tn = t + gridDim.x;
-        if (tn >= n_units) l2f = l2_touch_xcd_slice<NTHR, 1>(a.w_next, a.w_next_bytes);   // late: stays in L2
+        if (tn >= n_units) l2f = l2_touch_xcd_slice<NTHR, 1>(a.w_next, a.w_next_bytes).x;   // late: stays in L2
         const int hmask = __builtin_amdgcn_readfirstlane(unit_mask(t));   // M blocks of this unit
         int y0, x0;
         size_t img;
@@ -593,7 +593,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
         lds_barrier();   // M reads done before the next tile's v16 pads / computations
         W9TL(3);
     }
-    l2_touch_keep(l2f, a.batch < 0, smem);
+    l2_touch_keep(l2_touch_t{l2f, 0u}, a.batch < 0, smem);
 }
 
 #ifdef W9_PROF

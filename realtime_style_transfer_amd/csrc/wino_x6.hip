@@ -478,7 +478,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     XTL(2);
     // ---- the next layer's weights into this XCD's L2 (speed only), landing while the epilogue runs
-    const unsigned upf = l2_touch_xcd_slice<YT, 2>(a.u_next, a.u_next_bytes);
+    const l2_touch_t upf = l2_touch_xcd_slice<YT, 2>(a.u_next, a.u_next_bytes);
     // ---- epilogue: partial output transform per half -> LDS image, then sum + bias + ReLU + store + stats --
     float* const yimg = smem + h * (128 * YSTR);
     {

@@ -4,6 +4,7 @@
 // Build: bash tools/build_lite_bench.sh   Run: ./tools/lite_bench [iters]
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -57,7 +58,9 @@ int main(int argc, char** argv) {
             CK(hipMalloc(&w, pk.size() * 4));
             CK(hipMemcpy(w, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
             float* bias = dev_rand(s.cout, -0.1f, 0.1f, 4);
-            float* ab = dev_rand((size_t)2 * B * s.cin, 0.5f, 1.f, 5);
+            // prologue affine [B][cin] and the epilogue BatchNorm affine [cout] read from one buffer
+            const size_t nab = (size_t)2 * B * (s.cin > s.cout ? s.cin : s.cout);
+            float* ab = dev_rand(nab, 0.5f, 1.f, 5);
             float* out;
             CK(hipMalloc(&out, nout * 4));
             const int tiles_y = (Ho + t.th - 1) / t.th, tiles_x = (Wo + t.tw - 1) / t.tw;
@@ -71,7 +74,17 @@ int main(int argc, char** argv) {
             a.bias = bias;
             a.bn_ab = reinterpret_cast<const float2*>(ab);
             a.out = out;
-            a.part = s.kind == 1 ? part : nullptr;
+            // transposed convs feed a CIN: their statistics go to fixed-point accumulators as in the frame
+            // (LITE_PART=1: the per-tile partials of the training path instead)
+            cin_word* acc = nullptr;
+            CK(hipMalloc(&acc, (size_t)32 * B * 2 * CIN_LIMBS * s.cout * sizeof(cin_word)));
+            CK(hipMemset(acc, 0, (size_t)32 * B * 2 * CIN_LIMBS * s.cout * sizeof(cin_word)));
+            const bool use_part = getenv("LITE_PART") != nullptr;
+            a.part = s.kind == 1 && use_part ? part : nullptr;
+            if (s.kind == 1 && !use_part) {
+                a.stat.acc = acc;
+                a.stat.nslot = 32;
+            }
             a.batch = B;
             a.H = s.H;
             a.W = s.W;
@@ -92,6 +105,48 @@ int main(int argc, char** argv) {
             float ms;
             CK(hipEventElapsedTime(&ms, e0, e1));
             const double us = ms * 1e3 / iters;
+            {   // sampled CPU check of the output (f64 sums): max |err| / (sum of |terms| + |bias|) over 4096 points
+                std::vector<float> hin(nin), hres(nin), hb(s.cout), hab(nab), hout(nout);
+                CK(hipMemcpy(hin.data(), in, nin * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(hres.data(), res, nin * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(hb.data(), bias, s.cout * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(hab.data(), ab, hab.size() * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(hout.data(), out, nout * 4, hipMemcpyDeviceToHost));
+                const int OH = s.kind == 0 ? Ho : 2 * Ho, OW = s.kind == 0 ? Wo : 2 * Wo;
+                double worst = 0;
+                srand(7);
+                for (int i = 0; i < 4096; ++i) {
+                    const int b = rand() % B, oy = rand() % OH, ox = rand() % OW, n = rand() % s.cout;
+                    double acc = 0, mag = 0;
+                    for (int ky = 0; ky < 3; ++ky)
+                        for (int kx = 0; kx < 3; ++kx) {
+                            int iy, ix;
+                            if (s.kind == 0) { iy = 2 * oy + ky; ix = 2 * ox + kx; }
+                            else {   // out(2p + py) takes in(p - 1 + ty) through ky = py + 2 (1 - ty)
+                                const int py = oy & 1, px = ox & 1;
+                                if ((ky - py) & 1 || (kx - px) & 1) continue;
+                                iy = (oy >> 1) - 1 + (1 - (ky - py) / 2);
+                                ix = (ox >> 1) - 1 + (1 - (kx - px) / 2);
+                            }
+                            if (iy < 0 || iy >= s.H || ix < 0 || ix >= s.W) continue;
+                            for (int ci = 0; ci < s.cin; ++ci) {
+                                const size_t gi = (((size_t)b * s.H + iy) * s.W + ix) * s.cin + ci;
+                                double x = hin[gi];
+                                if (s.pro == PRO_AFF_RES) x = (double)fmaf(hab[2 * (b * s.cin + ci)], hin[gi], hab[2 * (b * s.cin + ci) + 1]) + hres[gi];
+                                if (s.pro == PRO_AFF_RELU) x = fmaxf(fmaf(hab[2 * (b * s.cin + ci)], hin[gi], hab[2 * (b * s.cin + ci) + 1]), 0.f);
+                                const double wv = s.kind == 0 ? hk[((size_t)(ky * 3 + kx) * s.cin + ci) * s.cout + n]
+                                                              : hk[((size_t)(ky * 3 + kx) * s.cout + n) * s.cin + ci];
+                                acc += x * wv;
+                                mag += fabs(x * wv);
+                            }
+                        }
+                    double ref = acc + hb[n];
+                    if (s.kind == 0) { ref = fmax(ref, 0.0); ref = fmax(hab[2 * n] * ref + hab[2 * n + 1], 0.0); }
+                    const double got = hout[(((size_t)b * OH + oy) * OW + ox) * s.cout + n];
+                    worst = fmax(worst, fabs(got - ref) / (mag + fabs(hb[n]) + 1e-30));
+                }
+                printf("B=%d %-11s check: max |err| / sum|terms| = %.2e%s\n", B, s.name, worst, worst > 2e-6 ? "   <-- MISMATCH" : "");
+            }
             const double flops = 2.0 * B * (s.kind == 0 ? (double)Ho * Wo : (double)s.H * s.W) * 9 * s.cin * s.cout;
             const double bytes = 4.0 * (nin * (s.pro == PRO_AFF_RES ? 2 : 1) + nout);
 #ifdef LITE_PROF
@@ -101,7 +156,7 @@ int main(int argc, char** argv) {
                    s.name, us, flops / us * 1e-6, flops / us * 1e-6 / 157.3, bytes / us * 1e-3,
                    bytes / us * 1e-3 / 8000.0, B * tiles_y * tiles_x);
             CK(hipFree(in)); CK(hipFree(res)); CK(hipFree(w)); CK(hipFree(bias)); CK(hipFree(ab));
-            CK(hipFree(out)); CK(hipFree(part));
+            CK(hipFree(out)); CK(hipFree(part)); CK(hipFree(acc));
         }
     return 0;
 }
