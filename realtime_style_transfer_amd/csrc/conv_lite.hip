@@ -100,14 +100,15 @@ struct Cfg {
     static constexpr int WCH = WIN_REGS ? 0 : (X6 ? 9 * CKC * NC * 3 / 2 : 9 * CKC * NC);   // floats per chunk of weights in LDS
     // x6 multi-chunk layers whose double buffer fits (expand_0 at 16-channel chunks): halo + weight images
     // double-buffered in LDS, chunk c + 1 staged while chunk c's MFMAs run (its global loads two chunks ahead)
-    static constexpr bool PIPE = X6 && NCH > 1 && (HALO + WCH) * 8 + 16 * NC * 4 <= 128 * 1024;
+    static constexpr bool PIPE = X6 && NCH > 1 && (HALO + WCH) * 8 + 64 * NC <= 128 * 1024;
     static constexpr int HITEMS = HR * HC * QC;             // float4 items per halo chunk
     static constexpr int HREG = (HITEMS + 255) / 256;
     static constexpr int WITEMS = WCH / 4;
     static constexpr int WREG = (WITEMS + 255) / 256;
     static constexpr int NACC = MS == 16 ? 4 : 16;          // accumulator floats per MFMA tile and lane
     static constexpr int NPH = MODE == 0 ? 1 : 4;           // output phases
-    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 * (PIPE ? 2 : 1) + 16 * NC * 4;   // + statistics [16][NC]
+    static constexpr int RED = MODE == 1 ? 16 * NC : 0;     // statistics scratch (floats): [16][NC]
+    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 * (PIPE ? 2 : 1) + RED * 4;
     static_assert(CIN % CKC == 0 && CKC % (4 * KS) == 0, "chunking");
     static_assert(MS == 16 || MS == 32, "MFMA shape");
     static_assert(((CS / 4) & 1) == 1, "odd 16-B slots per halo pixel");
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // [16][NC] statistics: S, n, M2 per wave (partials path) / [4][NC][2] f64 (accumulator flush)
     float* const red = smem + (C::HALO + C::WCH) * (C::PIPE ? 2 : 1);
     static_assert((C::HALO + C::WCH) % 2 == 0, "f64-aligned statistics scratch");
-    float2* const tab = reinterpret_cast<float2*>(red + 16 * NC);   // prologue affine [batch][CIN] (+ second style)
+    float2* const tab = reinterpret_cast<float2*>(red + C::RED);   // prologue affine [batch][CIN] (+ second style)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     LT0(0);
