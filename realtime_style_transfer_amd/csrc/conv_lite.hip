@@ -34,6 +34,10 @@
 #ifndef RST_LITE_E0_CKC
 #define RST_LITE_E0_CKC 32
 #endif
+// x6 transposed convs: full tiles' output staged through LDS and stored as whole lines (0: per-accumulator stores)
+#ifndef LITE_OSTAGE
+#define LITE_OSTAGE 1
+#endif
 // x6 B-operand ring depth (slots of weights read ahead of their MFMAs): 2 = one slot ahead
 #ifndef LITE_BDEPTH
 #define LITE_BDEPTH 2
@@ -547,6 +551,10 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         accS = accQ = 0.0;
     };
     const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
+    // x6 transposed convs (not PIPE: its other buffer holds the next chunk) stage full tiles' output through LDS
+    constexpr bool OSTAGE = X6 && MODE == 1 && !C::PIPE && LITE_OSTAGE;
+    constexpr int OST_FL = 4 * TW * NC;   // floats per wave
+    static_assert(!OSTAGE || 4 * OST_FL <= C::HALO + C::WCH, "output staging fits the halo + weight images");
     auto epilogue = [&](const Tile& T) __attribute__((always_inline)) {
         if constexpr (MODE == 0) {   // bias + ReLU -> BatchNorm (inference affine) -> ReLU, NHWC store
             acc_t y;
@@ -576,7 +584,43 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             // interior tiles (every pixel inside) store without per-element guards
             const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
             float* const orow = a.out + ((size_t)(T.b * Ho2 + 2 * p) * Wo2) * NC + n;
-            if (full) {
+            if (full && OSTAGE) {
+                // x6: the wave's 2 output rows x 2 TW pixels x NC channels through LDS (the tile's halo / weight
+                // images are dead after the barrier), then stored as whole 128-B lines, 16 B per lane: 4x fewer
+                // store instructions than the per-accumulator dword stores, no half-line writes
+#pragma unroll
+                for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+                    for (int j = 0; j < C::NACC; ++j) {
+                        acc[ph][j] += bias;
+                        s += acc[ph][j];
+                    }
+                cnt = 4.f * C::NACC;
+#if (LITE_SKIP & 8) == 0
+                lds_barrier();   // every wave's MFMA operand reads are done
+                float* const ob = smem + wave * OST_FL;
+#pragma unroll
+                for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+                    for (int j = 0; j < C::NACC; ++j)
+                        ob[((ph >> 1) * 2 * TW + 2 * M::row(j, lane) + (ph & 1)) * NC + n] = acc[ph][j];
+                constexpr int ROWF = 2 * TW * NC;   // floats of one output row segment (contiguous in NHWC)
+#pragma unroll
+                for (int py = 0; py < 2; ++py) {
+                    const size_t obase = ((size_t)(T.b * Ho2 + 2 * p + py) * Wo2 + 2 * T.x0) * NC;
+#pragma unroll
+                    for (int it = 0; it < ROWF / 256; ++it) {
+                        const int e = (it * 64 + lane) * 4;
+                        const f32x4 v = *reinterpret_cast<const f32x4*>(ob + py * ROWF + e);
+                        if (a.wt_stores)
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), osrd,
+                                                                   (int)((obase + e) * 4), 0, 16);
+                        else
+                            *reinterpret_cast<f32x4*>(a.out + obase + e) = v;
+                    }
+                }
+#endif
+            } else if (full) {
 #pragma unroll
                 for (int ph = 0; ph < 4; ++ph)
 #pragma unroll
