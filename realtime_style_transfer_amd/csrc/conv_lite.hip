@@ -38,6 +38,9 @@
 #ifndef LITE_OSTAGE
 #define LITE_OSTAGE 1
 #endif
+#ifndef LITE_OSTAGE0
+#define LITE_OSTAGE0 1   // the same for the x6 strided convs
+#endif
 // x6 B-operand ring depth (slots of weights read ahead of their MFMAs): 2 = one slot ahead
 #ifndef LITE_BDEPTH
 #define LITE_BDEPTH 2
@@ -554,6 +557,9 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // x6 transposed convs (not PIPE: its other buffer holds the next chunk) stage full tiles' output through LDS
     constexpr bool OSTAGE = X6 && MODE == 1 && !C::PIPE && LITE_OSTAGE;
     constexpr int OST_FL = 4 * TW * NC;   // floats per wave
+    // x6 strided convs (contract_0 / _1, weights in VGPRs): the same for their one output row per wave
+    constexpr bool OSTAGE0 = X6 && MODE == 0 && C::WIN_REGS && LITE_OSTAGE0;
+    static_assert(!OSTAGE0 || 4 * TW * NC <= C::HALO, "output staging fits the halo image");
     static_assert(!OSTAGE || 4 * OST_FL <= C::HALO + C::WCH, "output staging fits the halo + weight images");
     auto epilogue = [&](const Tile& T) __attribute__((always_inline)) {
         if constexpr (MODE == 0) {   // bias + ReLU -> BatchNorm (inference affine) -> ReLU, NHWC store
@@ -563,6 +569,29 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             const int oy = T.y0 + wave;
             const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
             float* const orow = a.out + ((size_t)(T.b * a.Ho + oy) * a.Wo) * NC + n;
+            if (OSTAGE0 && full) {   // the wave's TW x NC output row segment through LDS, 16 B per lane
+#pragma unroll
+                for (int j = 0; j < C::NACC; ++j) {
+                    float v = fmaxf(y[j] + bias, 0.f);
+                    y[j] = fmaxf(fmaf(bn.x, v, bn.y), 0.f);
+                }
+                lds_barrier();   // every wave's MFMA operand reads are done
+                float* const ob = smem + wave * (TW * NC);
+#pragma unroll
+                for (int j = 0; j < C::NACC; ++j) ob[M::row(j, lane) * NC + n] = y[j];
+                const size_t obase = ((size_t)(T.b * a.Ho + oy) * a.Wo + T.x0) * NC;
+#pragma unroll
+                for (int it = 0; it < TW * NC / 256; ++it) {
+                    const int e = (it * 64 + lane) * 4;
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(ob + e);
+                    if (a.wt_stores)
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), osrd, (int)((obase + e) * 4),
+                                                               0, 16);
+                    else
+                        *reinterpret_cast<f32x4*>(a.out + obase + e) = v;
+                }
+                return;
+            }
 #pragma unroll
             for (int j = 0; j < C::NACC; ++j) {
                 const int ox = T.x0 + M::row(j, lane);
