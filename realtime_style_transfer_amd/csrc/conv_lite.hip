@@ -41,6 +41,9 @@
 #ifndef LITE_OSTAGE0
 #define LITE_OSTAGE0 1   // the same for the x6 strided convs
 #endif
+#ifndef LITE_REMAP
+#define LITE_REMAP 1   // x6 layers: bank-conflict-free staging thread map (0: quad fastest)
+#endif
 // x6 B-operand ring depth (slots of weights read ahead of their MFMAs): 2 = one slot ahead
 #ifndef LITE_BDEPTH
 #define LITE_BDEPTH 2
@@ -220,7 +223,20 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     constexpr int HCM = HC - 1, TPR = HCM * QC, RPP = 256 / TPR, NMAIN = (HR + RPP - 1) / RPP;
     constexpr int NEXTRA = HR * QC;
     static_assert(256 % TPR == 0 && NEXTRA <= 256, "staging map");
-    const int q = tid % QC, col = (tid / QC) % HCM, rsub = tid / TPR, ehy = min(tid / QC, HR - 1);
+    // x6 layers with 8 channel quads: within each 16-lane group of a ds_write_b64 the lanes vary the quad's half
+    // (q & 1) and 8 columns whose halo pixels are consecutive (MODE 1: consecutive columns; MODE 0: one parity plane,
+    // every other column) at one 8-channel group (q >> 1), whose planes lie NPIXP x 16 B apart (0 mod 32 banks): the
+    // default order (quad fastest) put the four groups' 16-B slots on the same banks, 4-way. The last halo column is
+    // then staged by the threads of columns 0 .. HR - 1 of the first row group (same quad per thread).
+    constexpr bool REMAP = X6 && QC == 8 && HCM % 16 == 0 && TPR % 64 == 0 && HR <= HCM && LITE_REMAP;
+    const int tr = tid % TPR;
+    const int q = REMAP ? ((tr >> 4) & 3) * 2 + (tr & 1) : tid % QC;
+    const int col = !REMAP      ? (tid / QC) % HCM
+                    : MODE == 1 ? ((tr >> 1) & 7) + 8 * (tr >> 6)
+                                : ((tr >> 6) & 1) + 2 * (((tr >> 1) & 7) + 8 * (tr >> 7));
+    const int rsub = tid / TPR;
+    const bool ext = REMAP ? (rsub == 0 && col < HR) : tid < NEXTRA;   // stages the last halo column
+    const int ehy = REMAP ? min(col, HR - 1) : min(tid / QC, HR - 1);
     const int lcm = halo_off(0, col) + 4 * q, lce = halo_off(0, HCM) + 4 * q;
     // two register sets of staged input (single-chunk layers prefetch two tiles ahead: the HBM latency
     // under load exceeds one tile's MFMAs); multi-chunk layers use set 0 only
@@ -338,7 +354,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
         } else if constexpr (idx == NMAIN) {
             const bool oke = T.ix0 + HCM >= 0 && T.ix0 + HCM < W;
-            if (tid < NEXTRA) {
+            if (ext) {
                 const f32x4 v = oke && row_ok(ehy) ? xform(hreg[st][NMAIN], rreg[st][NMAIN], pa01[st], pa23[st],
                                                            bw[st][NMAIN], pb01[st], pb23[st])
                                                    : f32x4{0.f, 0.f, 0.f, 0.f};
