@@ -42,7 +42,10 @@
 #define LITE_OSTAGE0 1   // the same for the x6 strided convs
 #endif
 #ifndef LITE_REMAP
-#define LITE_REMAP 1   // x6 layers: bank-conflict-free staging thread map (0: quad fastest)
+// x6 layers: bank-conflict-free staging thread map (1) or quad fastest (0, default). SQ: LDS bank conflicts of the
+// Cout-16 layers 0.556 -> 0.103 of the LDS cycles, expand_0's 0.258 -> 0.000, with no layer faster (contract_0 B=1
+// +1.5 %, expand_0 B=8 +2 %; profiles/r04/lite_remap.log, sq_frame_r12.json): LDS banking does not bound them
+#define LITE_REMAP 0
 #endif
 // x6 B-operand ring depth (slots of weights read ahead of their MFMAs): 2 = one slot ahead
 #ifndef LITE_BDEPTH
