@@ -36,8 +36,9 @@ def short_name(k: str) -> str:
     if m:
         f = [int(v) for v in m.group(1).split(",")]
         mode, cin, nc = f[:3]
-        if len(f) > 5 and f[5]:
-            return f"conv_lite<3x3 s2 transposed Cin{cin} Cout{nc} split-bf16 x6 32x32x16 MFMA>"
+        if len(f) > 5 and f[5]:   # x6: 16x16x32 bf16 for Cout 16, 32x32x16 for Cout 32; the mode picks the conv kind
+            shape6 = "16x16x32" if nc == 16 else "32x32x16"
+            return f"conv_lite<3x3 s2 {'transposed ' if mode else ''}Cin{cin} Cout{nc} split-bf16 x6 {shape6} MFMA>"
         shape = "16x16x4" if nc == 16 else "32x32x2"
         return f"conv_lite<3x3 s2 {'transposed ' if mode else ''}Cin{cin} Cout{nc} f32 {shape} MFMA>"
     if "last_x6_kernel" in k:
