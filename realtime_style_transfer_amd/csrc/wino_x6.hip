@@ -146,9 +146,10 @@ constexpr int YRING = X6W_RING;                     // U register ring (points i
 constexpr int YSTR = 132;                           // epilogue image row stride (floats): lh halves 32 banks apart
 constexpr size_t YIMG_BYTES = (size_t)2 * 128 * YSTR * 4;       // epilogue: two halves' partial Y [pixel][channel]
 constexpr size_t YRED_BYTES = (size_t)2 * 8 * 32 * 16;          // statistics reduction [2][8 waves][32] float4
-constexpr size_t YEPI_BYTES = YIMG_BYTES + YRED_BYTES + 2 * XN * 8;   // + [2][128] f64 (accumulator adds)
+constexpr size_t YEPI_BYTES = YIMG_BYTES + YRED_BYTES + 8 * XN * 8;   // + [8 waves][128] f64 (accumulator path)
 constexpr size_t YLDS_BYTES = XLDS_BYTES > YEPI_BYTES ? XLDS_BYTES : YEPI_BYTES;
 constexpr size_t YLDS_BLEND_BYTES = YLDS_BYTES + XMAX_CIN * sizeof(float2);   // + the second style's affine
+static_assert(YLDS_BLEND_BYTES <= 160 * 1024, "LDS");
 static_assert(8 % YRING == 0, "ring must divide the points per wave");
 
 // BLEND: two styles — the prologue blends the two CIN affines per pixel (pro_ab1, pro_w)
@@ -533,16 +534,55 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         s4 += yv[i];
     }
     XTL(7);
-    if (a.part != nullptr || a.stat.acc != nullptr) {
-        f32x4* const red = reinterpret_cast<f32x4*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES);   // [2][8][32]
+    auto xsum = [&](f32x4 v) __attribute__((always_inline)) {
+        v.x = lane_xor_sum<32>(v.x);
+        v.y = lane_xor_sum<32>(v.y);
+        v.z = lane_xor_sum<32>(v.z);
+        v.w = lane_xor_sum<32>(v.w);
+        return v;
+    };
+    f32x4* const red = reinterpret_cast<f32x4*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES);   // [2][8][32]
+    if (a.stat.acc != nullptr) {
+        // accumulator path: {S, M2 + S^2 / n} (finalize_kernel's merge quantity, a sum of squares formed around a
+        // local mean) is additive over any partition of the tile, so each wave forms it over its own two pixel
+        // columns (two-pass around the wave's mean, in registers) and the eight waves meet in LDS once, in f64 and
+        // a fixed order: one barrier instead of the tile mean's two
+        s4 = xsum(s4);
+        const int vc = (x0 + 2 * wave < W ? 1 : 0) + (x0 + 2 * wave + 1 < W ? 1 : 0);
+        const float nw = (float)(vc * min(XTH, H - y0));
+        const f32x4 mw = nw > 0.f ? s4 / nw : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 m2 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < XTH; ++i) {
+            const bool ok = col_ok && y0 + i < H;
+            const f32x4 d = yv[i] - mw;
+            if (ok) m2 += d * d;
+        }
+        m2 = xsum(m2);
+        float* const sf = reinterpret_cast<float*>(red);                                                  // [8][128]
+        double* const qd = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(smem) + YIMG_BYTES + YRED_BYTES);
+        if (lh == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const double dS = (double)s4[k];
+                sf[wave * XN + 4 * cq + k] = s4[k];
+                qd[wave * XN + 4 * cq + k] = nw > 0.f ? (double)m2[k] + dS * dS / (double)nw : 0.0;
+            }
+        }
+        lds_barrier();
+        if (tid < XN) {
+            double S = 0.0, Q = 0.0;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                S += (double)sf[w * XN + tid];
+                Q += qd[w * XN + tid];
+            }
+            const int slot = (int)blockIdx.x % a.stat.nslot;
+            cin_acc_add_value(a.stat, a.batch, XN, b, tid, slot, 0, S);
+            cin_acc_add_value(a.stat, a.batch, XN, b, tid, slot, 1, Q);
+        }
+    } else if (a.part != nullptr) {
         const float cnt = (float)(min(XTH, H - y0) * min(XTW, W - x0));
-        auto xsum = [&](f32x4 v) __attribute__((always_inline)) {
-            v.x = lane_xor_sum<32>(v.x);
-            v.y = lane_xor_sum<32>(v.y);
-            v.z = lane_xor_sum<32>(v.z);
-            v.w = lane_xor_sum<32>(v.w);
-            return v;
-        };
         s4 = xsum(s4);
         if (lh == 0) red[wave * 32 + cq] = s4;
         lds_barrier();
@@ -560,23 +600,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         m2 = xsum(m2);
         if (lh == 0) red[256 + wave * 32 + cq] = m2;
         lds_barrier();
-        if (a.stat.acc != nullptr) {
-            // one thread per channel c (128 of them): S and M2 summed over the 8 waves in the order of the partials
-            // path, {S, M2 + S^2 / n} in f64 (finalize_kernel's merge quantity), straight into the fixed-point limbs
-            if (tid < XN) {
-                const float* const rf = reinterpret_cast<const float*>(red);   // [2][8 waves][128 channels]
-                float Sc = rf[tid], Mc = rf[1024 + tid];
-#pragma unroll
-                for (int w = 1; w < 8; ++w) {
-                    Sc += rf[w * 128 + tid];
-                    Mc += rf[1024 + w * 128 + tid];
-                }
-                const double dS = (double)Sc;
-                const int slot = (int)blockIdx.x % a.stat.nslot;
-                cin_acc_add_value(a.stat, a.batch, XN, b, tid, slot, 0, dS);
-                cin_acc_add_value(a.stat, a.batch, XN, b, tid, slot, 1, (double)Mc + dS * dS / (double)cnt);
-            }
-        } else if (tid < 32) {
+        if (tid < 32) {
             f32x4 M = red[256 + cq];
 #pragma unroll
             for (int w = 1; w < 8; ++w) M += red[256 + w * 32 + cq];
