@@ -378,6 +378,8 @@ struct Wino9Args {
     const void* w_next;     // wino9_x6 inference: the next layer's weight image into L2 (l2_touch_xcd_slice)
     int w_next_bytes;
     int wt_stores;          // nonzero: output stored write-through (sc1), as WinoArgs::wt_stores
+    unsigned* queue;        // inference: [2] work-queue counters (zero at the first launch, reset by the last workgroup
+                            // of each launch), or null: the static unit order
 };
 bool wino9_supported(int kh, int stride, int cin, int cout);
 

@@ -89,6 +89,8 @@ struct rst_handle {
     float* d_xlast = nullptr;     // blended input of the last (VALU) layer
     rst::cin_word* d_acc_all = nullptr;  // every layer's accumulators for max_batch (a forward of B images uses the
     size_t acc_per_image = 0;       // first acc_per_image * B words, zeroed at its start)
+    unsigned* d_w9_queue = nullptr;   // the start conv's work-queue counters [2] (wino9_x6, self-resetting)
+    bool w9_queue = true;             // RST_W9_QUEUE=0 at creation: static unit order (A/B runs)
     const float* last_style_weights = nullptr;   // for the debug copies of the most recent forward
     std::vector<void*> allocs;
     // optional per-layer timing: 3 events per layer per step (before conv, after conv, after finalize)

@@ -502,6 +502,10 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
             h->acc_per_image = n_acc;
             if ((st = h->alloc(&h->d_acc_all, n_acc * B * sizeof(cin_word))) != RST_OK) { delete h; return st; }
         }
+        const unsigned qz[2] = {0u, 0u};
+        if ((st = h->alloc(&h->d_w9_queue, sizeof(qz), qz)) != RST_OK) { delete h; return st; }
+        const char* wq = getenv("RST_W9_QUEUE");
+        h->w9_queue = !(wq != nullptr && wq[0] == '0');
     }
     // two styles: the style-weight mip chain (AvgPool2 keyed by width, num_expand_blocks + 1 levels)
     if (shape->num_styles == 2) {
@@ -695,6 +699,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             a.zero_n2 = (long)(h->acc_per_image * B / 2);
         }
         if (e.kind == K_WINO9X6) next_weights(h, li, &a.w_next, &a.w_next_bytes);
+        if (e.kind == K_WINO9X6 && h->w9_queue) a.queue = h->d_w9_queue;
         a.wt_stores = wt_bits(h, e, B, 4);
         HIP_TRY(e.kind == K_WINO9X6 ? wino9_x6_launch(a, st) : wino9_launch(a, st));
     } else if (e.kind == K_WINO || e.kind == K_WINOX6) {

@@ -249,17 +249,25 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
     const int n_tile_img = a.tiles_y * a.tiles_x, n_part = 2 * n_tile_img;
 
     unsigned l2f = 0;     // the next layer's weights into this XCD's L2, touched during the last unit (speed only)
+    // work units: the first two of each workgroup static (blockIdx.x, + gridDim.x), the rest from a queue (a.queue):
+    // the partial last round's half units go to the workgroups that finish their whole units first, not to the
+    // first 16 by index (their spread of finishing times is several microseconds). Thread 0 fetches the unit after
+    // next at the top of each unit and publishes it at the end (the atomic's latency hides behind the unit).
+    __shared__ int w9_next;
+    const bool dyn = a.queue != nullptr;
+    unsigned qv = 0u;
     int t = blockIdx.x;   // work unit
+    int tn = t + (int)gridDim.x;   // the next one (its patch is staged during this one)
     if (t < n_units) {
         sfor<0, NPART>([&](auto PART) __attribute__((always_inline)) {
             load_half(t, PART);
             store_half(t, patch_buf(0), PART);
         });
     }
-    for (int it = 0; t < n_units; t += gridDim.x, ++it) {
+    for (int it = 0; t < n_units; ++it) {
         w9_it = it;
         W9TL(0);
-        const int tn = t + gridDim.x;
+        if (dyn && tid == 0) qv = 2u * gridDim.x + atomicAdd(a.queue, 1u);
         if (tn >= n_units) l2f = l2_touch_xcd_slice<NTHR, 1>(a.w_next, a.w_next_bytes).x;   // late: stays in L2
         const int hmask = __builtin_amdgcn_readfirstlane(unit_mask(t));   // M blocks of this unit
         int y0, x0;
@@ -590,8 +598,17 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
                 }
             }
         });
-        lds_barrier();   // M reads done before the next tile's v16 pads / computations
+        if (dyn && tid == 0) w9_next = (int)min(qv, 0x7FFFFFFFu);
+        lds_barrier();   // M reads done before the next tile's v16 pads / computations; w9_next published
         W9TL(3);
+        t = tn;
+        tn = dyn ? __builtin_amdgcn_readfirstlane(w9_next) : tn + (int)gridDim.x;   // uniform: an SGPR
+    }
+    if (dyn && tid == 0) {   // the last workgroup out (all fetches done) resets the queue for the next launch
+        if (atomicAdd(a.queue + 1, 1u) == gridDim.x - 1) {
+            atomicExch(a.queue, 0u);
+            atomicExch(a.queue + 1, 0u);
+        }
     }
     l2_touch_keep(l2_touch_t{l2f, 0u}, a.batch < 0, smem);
 }

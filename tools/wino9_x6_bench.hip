@@ -48,6 +48,12 @@ int main(int argc, char** argv) {
     a6.tiles_x = wino9_x6_tiles_x(W);
     a32.U = U32; a32.out = o32;
     a6.U = U6; a6.out = o6;
+    if (getenv("W9_QUEUE")) {   // the inference work queue (rst_api passes it), zeroed once, self-resetting
+        unsigned* q;
+        CK(hipMalloc(&q, 8));
+        CK(hipMemset(q, 0, 8));
+        a6.queue = q;
+    }
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int iters = 50;
     for (int v = 0; v < 2; ++v) {
