@@ -97,7 +97,7 @@ struct rst_handle {
     std::vector<hipEvent_t> prof_events;
     int prof_max_steps = 0, prof_step = 0;
     bool prof_on = false;
-    int wt_stores = 13;               // RST_WT_STORES at creation: write-through output stores (1 wino_x6 output, 2 its
+    int wt_stores = 15;               // RST_WT_STORES at creation: write-through output stores (1 wino_x6 output, 2 its
                                       // materialised input, 4 wino9_x6 output, 8 conv_lite output)
     bool no_u_prefetch = false;       // RST_NO_U_PREFETCH=1 at creation: no next-layer U prefetch (A/B runs)
     void prof_free() {

@@ -397,7 +397,9 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         const char* nup = getenv("RST_NO_U_PREFETCH");
         h->no_u_prefetch = nup != nullptr && nup[0] == '1';
         const char* wts = getenv("RST_WT_STORES");
-        h->wt_stores = wts != nullptr ? atoi(wts) : 13;   // default: every output but the materialised input
+        // default: every output and the residual convs' materialised input (round 4: 15 vs round 3's 13 +0.6 % frames,
+        // 7 same-box pairs, profiles/r04/ab_wt_stores.log)
+        h->wt_stores = wts != nullptr ? atoi(wts) : 15;
     }
     const int B = shape->max_batch;
     const float* wp = weights_host;
