@@ -47,6 +47,13 @@
 // +1.5 %, expand_0 B=8 +2 %; profiles/r04/lite_remap.log, sq_frame_r12.json): LDS banking does not bound them
 #define LITE_REMAP 0
 #endif
+// prologue affine formed (accumulator merge) before the first tile's input loads are issued (1) or after (0):
+// small L2-resident accumulator reads queued behind a tile of HBM loads gate the first staging. Standalone with the
+// frame's accumulator prologue expand_0 -1 % (B=1) / -3 % (B=8); in the frame neutral (1625 vs 1622 FPS, four
+// same-box pairs; profiles/r04/lite_tf.log, ab_table_first.log): off
+#ifndef LITE_TABLE_FIRST
+#define LITE_TABLE_FIRST 0
+#endif
 // x6 B-operand ring depth (slots of weights read ahead of their MFMAs): 2 = one slot ahead
 #ifndef LITE_BDEPTH
 #define LITE_BDEPTH 2
@@ -912,8 +919,9 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     } else {   // multi-chunk layers, and single-chunk layers with one register set (x6: weights in VGPRs)
         const int n_steps = my_tiles * NCH;
         Tile cur = tile_of(0);
+        if constexpr (LITE_TABLE_FIRST) fill_table();
         load_in(cur, 0, S0{});
-        fill_table();
+        if constexpr (!LITE_TABLE_FIRST) fill_table();
         load_aff(cur, 0, S0{});
         for (int s = 0; s < n_steps; ++s) {
             const int ch = s % NCH;
