@@ -506,7 +506,7 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
         w.dW = grad + T.woff;
         // WINOGRAD_BF16X6: the residual convs' weight gradient on the split-bf16 x6 kernel (fp32-level
         // products, wgrad.hip); the other layers and modes keep the f32-MFMA kernel
-        w.x6 = T.e.kind == K_WINOX6 ? 1 : 0;
+        w.x6 = T.e.kind == K_WINOX6 || T.e.kind == K_WINO9X6 ? 1 : 0;   // the split-bf16 trainer's convs
         w.nsplit = wgrad_choose_splits(w);
         RST_HIP_TRY(wgrad_launch(w, st));
         if (!T.has_dgrad) continue;

@@ -15,6 +15,7 @@
 // lane half: conflict-free (banks (a/4)%32 per 32-lane half).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernels.h"
@@ -477,6 +478,129 @@ __global__ __launch_bounds__(256, 2) void wgrad9_kernel(WgradArgs a) {
     }
 }
 
+// ---- contract_start weight gradient on split-bf16 x6 (the x6 trainer's start conv) --------------------------
+// As wgrad9_kernel (M = the 32 output channels, N = the 1377 (tap, ci) columns, K = pixels, one [1408][32] slab per
+// workgroup) with the products on v_mfma_f32_32x32x16_bf16: dZ^T and the input patch are split once at staging into
+// three exact bf16 pieces, six product terms per k-step (fp32-level, the wgrad_x6 scheme). K-step = one 16-pixel tile
+// row: lane half lh takes pixels 8lh .. 8lh + 7. The B operand of column (ky, kx, ci) is 8 consecutive patch
+// pixels starting at column kx + 8lh — kx odd is not 4-byte aligned in a bf16 row, so the patch is kept twice, as
+// written (copy 0) and shifted one element left (copy 1): column kx reads copy kx & 1 at the even offset kx & ~1,
+// four ds_read_b32 per piece.
+namespace w9x {
+constexpr int TH = 8, TW = 16, NPX = TH * TW;
+constexpr int PR = TH + 8, PC = TW + 8, PRS = 24;           // patch rows / cols / row stride (bf16 elements)
+constexpr int CMAX = 17, PLANE = PR * PRS;                   // one channel's plane
+constexpr int PIECE = CMAX * PLANE, COPY = 3 * PIECE;        // elements per piece / per copy
+constexpr int DZS = NPX + 8;                                 // dZ^T row stride (elements; 16-B aligned rows)
+constexpr int DZOFF = 2 * COPY;                              // dZ^T [piece][co][DZS] after the two copies
+constexpr int LDS_EL = DZOFF + 3 * 32 * DZS;
+constexpr size_t LDS_BYTES = (size_t)LDS_EL * 2;
+constexpr int NCOL = 81 * CMAX, NCOLP = 1408, NTW = NCOLP / 32 / 4;   // 11 column tiles per wave
+static_assert(LDS_BYTES <= 160 * 1024 && (COPY % 2) == 0 && (PLANE % 2) == 0, "layout");
+}  // namespace w9x
+
+__global__ __launch_bounds__(256, 1) void wgrad9_x6_kernel(WgradArgs a) {
+    using namespace w9x;
+    typedef short short8 __attribute__((ext_vector_type(8)));
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds9x[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    constexpr int C = CMAX;
+    const int tiles_x = (a.Qw + TW - 1) / TW, tiles_y = (a.Qh + TH - 1) / TH;
+    const int ntiles = a.batch * tiles_x * tiles_y;
+    // per-lane column decode: element offset of (copy, piece 0, ci, ky, kx & ~1) for this wave's column tiles
+    int coff[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = (wave + 4 * j) * 32 + li;
+        if (n < NCOL) {
+            const int tap = n / C, ci = n % C, ky = tap / 9, kx = tap % 9;
+            coff[j] = (kx & 1) * COPY + ci * PLANE + ky * PRS + (kx & ~1);
+        } else {
+            coff[j] = -1;
+        }
+    }
+    floatx16 acc[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    auto split = [](float v, unsigned short (&p)[3]) __attribute__((always_inline)) {   // exact: v = p0 + p1 + p2
+        float y = 0.f;
+        const unsigned q0 = bf16_piece(v, y), q1 = bf16_piece(v, y), q2 = bf16_last_piece(v, y);
+        p[0] = (unsigned short)(q0 & 0xFFFFu);
+        p[1] = (unsigned short)(q1 & 0xFFFFu);
+        p[2] = (unsigned short)(q2 & 0xFFFFu);
+    };
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int b = t / (tiles_x * tiles_y), rem = t % (tiles_x * tiles_y);
+        const int y0 = (rem / tiles_x) * TH, x0 = (rem % tiles_x) * TW;
+        __syncthreads();   // previous tile's operands consumed
+        for (int i = tid; i < PR * PC * C; i += 256) {
+            const int c = i % C, px = i / C;
+            const int r = px / PC, q = px % PC;
+            const int gy = y0 - a.pad_t + r, gx = x0 - a.pad_l + q;
+            float v = 0.f;
+            if (gy >= 0 && gy < a.XH && gx >= 0 && gx < a.XW) v = a.X[(((size_t)b * a.XH + gy) * a.XW + gx) * C + c];
+            unsigned short p[3];
+            split(v, p);
+            const int e = c * PLANE + r * PRS + q;
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+                lds9x[pc * PIECE + e] = p[pc];
+                if (q > 0) lds9x[COPY + pc * PIECE + e - 1] = p[pc];
+            }
+        }
+        for (int i = tid; i < NPX * 32; i += 256) {
+            const int co = i & 31, px = i >> 5;
+            const int oy = y0 + px / TW, ox = x0 + px % TW;
+            float v = 0.f;
+            if (oy < a.Qh && ox < a.Qw) v = a.D[(((size_t)b * a.DH + oy) * a.DW + ox) * 32 + co];
+            unsigned short p[3];
+            split(v, p);
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) lds9x[DZOFF + (pc * 32 + co) * DZS + px] = p[pc];
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int ks = 0; ks < TH; ++ks) {   // k-step = tile row ks, pixels 16 ks + 8 lh ..
+            short8 A[3];
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                A[pc] = *reinterpret_cast<const short8*>(lds9x + DZOFF + (pc * 32 + li) * DZS + 16 * ks + 8 * lh);
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                short8 B[3];
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc) {
+                    if (coff[j] >= 0) {
+                        const unsigned* src =
+                            reinterpret_cast<const unsigned*>(lds9x + coff[j] + pc * PIECE + ks * PRS + 8 * lh);
+                        B[pc] = __builtin_bit_cast(short8, u32x4{src[0], src[1], src[2], src[3]});
+                    } else {
+                        B[pc] = short8{0, 0, 0, 0, 0, 0, 0, 0};
+                    }
+                }
+                floatx16& Cc = acc[j];
+                Cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], Cc, 0, 0, 0);
+                Cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], Cc, 0, 0, 0);
+                Cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], Cc, 0, 0, 0);
+                Cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], Cc, 0, 0, 0);
+                Cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], Cc, 0, 0, 0);
+                Cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], Cc, 0, 0, 0);
+            }
+        }
+    }
+    float* slab = a.slab + (size_t)blockIdx.x * NCOLP * 32;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int n = (wave + 4 * j) * 32 + li;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) slab[(size_t)n * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh] = acc[j][r];
+    }
+}
+
 static bool wgrad9_applies(const WgradArgs& a) {
     return !a.transposed && a.kh == 9 && a.kw == 9 && a.stride == 1 && a.C1 == w9::CMAX && a.C2 == 32 &&
            a.pad_t == 4 && a.pad_l == 4 && a.Qh == a.XH && a.Qw == a.XW;
@@ -680,7 +804,19 @@ hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
     wgrad_dims(a, R, Cu, Cs);
     if (wgrad9_applies(a)) {
         if (a.nsplit < 1) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(wgrad9_kernel, dim3((unsigned)a.nsplit), dim3(256), 0, st, a);
+        // RST_WGRAD9_X6=1: the split-bf16 kernel for the x6 trainer. Off by default: parity-green but 6.4 vs 1.8 ms per
+        // step (config-4 step 29.6 vs 25.0 ms, profiles/r04/trainab_wgrad9_x6.log) — its staging (two patch copies x
+        // three pieces in 16-bit LDS stores) and the 4-byte B reads are not yet shaped for the MFMA rate
+        static const bool x6_ok = [] {
+            const char* v = getenv("RST_WGRAD9_X6");
+            if (v == nullptr || v[0] != '1') return false;
+            return hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad9_x6_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)w9x::LDS_BYTES) == hipSuccess;
+        }();
+        if (a.x6 && x6_ok)
+            hipLaunchKernelGGL(wgrad9_x6_kernel, dim3((unsigned)a.nsplit), dim3(256), w9x::LDS_BYTES, st, a);
+        else
+            hipLaunchKernelGGL(wgrad9_kernel, dim3((unsigned)a.nsplit), dim3(256), 0, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         const size_t n4 = (size_t)R * Cu / 4;
