@@ -489,7 +489,9 @@ __global__ __launch_bounds__(256, 2) void wgrad9_kernel(WgradArgs a) {
 namespace w9x {
 constexpr int TH = 8, TW = 16, NPX = TH * TW;
 constexpr int PR = TH + 8, PC = TW + 8, PRS = 24;           // patch rows / cols / row stride (bf16 elements)
-constexpr int CMAX = 17, PLANE = PR * PRS;                   // one channel's plane
+// one channel's plane, padded to an odd number of dwords (193): the 32 columns of a B read are mostly consecutive
+// channels, which an even-dword pitch (192 = 0 mod 64 banks) put on one bank
+constexpr int CMAX = 17, PLANE = PR * PRS + 2;
 constexpr int PIECE = CMAX * PLANE, COPY = 3 * PIECE;        // elements per piece / per copy
 constexpr int DZS = NPX + 8;                                 // dZ^T row stride (elements; 16-B aligned rows)
 constexpr int DZOFF = 2 * COPY;                              // dZ^T [piece][co][DZS] after the two copies
@@ -533,36 +535,63 @@ __global__ __launch_bounds__(256, 1) void wgrad9_x6_kernel(WgradArgs a) {
         p[1] = (unsigned short)(q1 & 0xFFFFu);
         p[2] = (unsigned short)(q2 & 0xFFFFu);
     };
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    // the next tile's global values are loaded into registers while this tile's MFMAs run (one workgroup per CU:
+    // no other workgroup hides the load latency), split and stored after the barrier
+    constexpr int NXL = (PR * PC * C + 255) / 256, NDL = NPX * 32 / 256;
+    float xs[NXL], dz[NDL];
+    auto load_tile = [&](int t) __attribute__((always_inline)) {
         const int b = t / (tiles_x * tiles_y), rem = t % (tiles_x * tiles_y);
         const int y0 = (rem / tiles_x) * TH, x0 = (rem % tiles_x) * TW;
-        __syncthreads();   // previous tile's operands consumed
-        for (int i = tid; i < PR * PC * C; i += 256) {
+#pragma unroll
+        for (int k = 0; k < NXL; ++k) {
+            const int i = tid + 256 * k;
             const int c = i % C, px = i / C;
             const int r = px / PC, q = px % PC;
             const int gy = y0 - a.pad_t + r, gx = x0 - a.pad_l + q;
-            float v = 0.f;
-            if (gy >= 0 && gy < a.XH && gx >= 0 && gx < a.XW) v = a.X[(((size_t)b * a.XH + gy) * a.XW + gx) * C + c];
-            unsigned short p[3];
-            split(v, p);
-            const int e = c * PLANE + r * PRS + q;
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) {
-                lds9x[pc * PIECE + e] = p[pc];
-                if (q > 0) lds9x[COPY + pc * PIECE + e - 1] = p[pc];
-            }
+            xs[k] = (i < PR * PC * C && gy >= 0 && gy < a.XH && gx >= 0 && gx < a.XW)
+                        ? a.X[(((size_t)b * a.XH + gy) * a.XW + gx) * C + c] : 0.f;
         }
-        for (int i = tid; i < NPX * 32; i += 256) {
+#pragma unroll
+        for (int k = 0; k < NDL; ++k) {
+            const int i = tid + 256 * k;
             const int co = i & 31, px = i >> 5;
             const int oy = y0 + px / TW, ox = x0 + px % TW;
-            float v = 0.f;
-            if (oy < a.Qh && ox < a.Qw) v = a.D[(((size_t)b * a.DH + oy) * a.DW + ox) * 32 + co];
-            unsigned short p[3];
-            split(v, p);
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) lds9x[DZOFF + (pc * 32 + co) * DZS + px] = p[pc];
+            dz[k] = (oy < a.Qh && ox < a.Qw) ? a.D[(((size_t)b * a.DH + oy) * a.DW + ox) * 32 + co] : 0.f;
         }
+    };
+    auto store_tile = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < NXL; ++k) {
+            const int i = tid + 256 * k;
+            if (i < PR * PC * C) {
+                const int c = i % C, px = i / C;
+                const int r = px / PC, q = px % PC;
+                unsigned short pcs[3];
+                split(xs[k], pcs);
+                const int e = c * PLANE + r * PRS + q;
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc) {
+                    lds9x[pc * PIECE + e] = pcs[pc];
+                    if (q > 0) lds9x[COPY + pc * PIECE + e - 1] = pcs[pc];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NDL; ++k) {
+            const int i = tid + 256 * k;
+            const int co = i & 31, px = i >> 5;
+            unsigned short pcs[3];
+            split(dz[k], pcs);
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) lds9x[DZOFF + (pc * 32 + co) * DZS + px] = pcs[pc];
+        }
+    };
+    if ((int)blockIdx.x < ntiles) load_tile(blockIdx.x);
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        __syncthreads();   // previous tile's operands consumed
+        store_tile();
         __syncthreads();
+        if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);
 #pragma unroll 1
         for (int ks = 0; ks < TH; ++ks) {   // k-step = tile row ks, pixels 16 ks + 8 lh ..
             short8 A[3];
