@@ -833,12 +833,12 @@ hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
     wgrad_dims(a, R, Cu, Cs);
     if (wgrad9_applies(a)) {
         if (a.nsplit < 1) return hipErrorInvalidValue;
-        // RST_WGRAD9_X6=1: the split-bf16 kernel for the x6 trainer. Off by default: parity-green but 6.4 vs 1.8 ms per
-        // step (config-4 step 29.6 vs 25.0 ms, profiles/r04/trainab_wgrad9_x6.log) — its staging (two patch copies x
-        // three pieces in 16-bit LDS stores) and the 4-byte B reads are not yet shaped for the MFMA rate
+        // the split-bf16 kernel for the x6 trainer (RST_WGRAD9_X6=0: the f32 kernel). Config-4 step 24.97 -> 24.29 ms
+        // same box (profiles/r04/trainab_wgrad9_x6_prefetch.log); the first form, before the odd channel pitch and the
+        // register prefetch, ran 29.6 ms (trainab_wgrad9_x6.log)
         static const bool x6_ok = [] {
             const char* v = getenv("RST_WGRAD9_X6");
-            if (v == nullptr || v[0] != '1') return false;
+            if (v != nullptr && v[0] == '0') return false;
             return hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad9_x6_kernel),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)w9x::LDS_BYTES) == hipSuccess;
         }();
