@@ -127,6 +127,11 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
     const int y0 = rb * RB, x0 = sx * TWO;
     const int H = a.H, W = a.W;
 
+    // the prologue affine's accumulator loads first (CinAffineSplit): merged after the weight and first row loads are
+    // issued, so its wait does not include their latency (vmcnt retires in issue order)
+    const bool split_aff = PRO != PRO_NONE && a.pro_stat.acc != nullptr;   // last_x6_launch: nslot <= 8
+    CinAffineSplit<256, 2> aff;
+    if (split_aff) aff.issue(a.pro_stat, b, BLEND);
     // ---- weights: lane (n = lane & 31, k half) holds B[ky][piece] = 8 bf16 of column n, 108 VGPRs -------
     short8 bw[K][3];
     {
@@ -156,9 +161,8 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
             float2* const ltab = reinterpret_cast<float2*>(red + 128);   // [2][16]
             const CinSrc& ps = a.pro_stat;
             const bool store = rb == 0 && sx == 0;   // one workgroup per image keeps the host-visible copy
-            cin_affine_table<256>(ps, b, 1, ltab, BLEND ? ltab + CIN : nullptr,
-                                  store && ps.ab_out ? ps.ab_out + (size_t)b * CIN : nullptr,
-                                  store && ps.ab1_out ? ps.ab1_out + (size_t)b * CIN : nullptr);
+            aff.finish(ps, ltab, BLEND ? ltab + CIN : nullptr, store && ps.ab_out ? ps.ab_out + (size_t)b * CIN : nullptr,
+                       store && ps.ab1_out ? ps.ab1_out + (size_t)b * CIN : nullptr);
             lds_barrier();
             ab = ltab;
             ab1 = ltab + CIN;
@@ -474,7 +478,8 @@ hipError_t last_x6_launch(const LastArgs& a, hipStream_t st) {
         return hipErrorInvalidValue;   // statistics: partials or accumulators
     if (a.stat.acc != nullptr && (a.stat.nslot < 1 || a.stat.nslot > CIN_ACC_MAX_SLOTS)) return hipErrorInvalidValue;
     const bool src_acc = a.pro_stat.acc != nullptr;
-    if (src_acc && (a.pro_stat.nslot < 1 || a.pro_stat.nslot > CIN_ACC_MAX_SLOTS || a.pro_stat.C != lastx6::CIN ||
+    // (nslot <= 8: the kernel's split affine form, CinAffineSplit<256, 2>, covers the accumulators)
+    if (src_acc && (a.pro_stat.nslot < 1 || a.pro_stat.nslot > 8 || a.pro_stat.C != lastx6::CIN ||
                     a.pro_stat.batch != a.batch || a.pro_stat.style == nullptr))
         return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * ((a.H + lastx6::RB - 1) / lastx6::RB) * a.tiles_x);

@@ -18,8 +18,12 @@
 //     positions (ty, tx) are read once and shared by the phases that use them;
 //   * the CIN statistics {sum, M2, n} of a tile merge its four phases (finalize sees one partial per
 //     tile and channel), two-pass inside the tile, fixed order: deterministic.
-// Multi-chunk layers (expand_0, Cin 128 in 4 chunks of 32) double-buffer the halo + weight image:
-// chunk c+1 is loaded into registers while chunk c's MFMAs run and written to the other buffer after.
+// Multi-chunk layers (expand_0, Cin 128 in 4 chunks of 32): chunk c+1 is loaded into registers while chunk c's
+// MFMAs run and written to the (single) halo + weight image after.
+// (Measured and removed, round 4: a double-buffered 16-channel chunk pipeline for expand_0 — equal at B = 8, 3.5 us
+// slower at B = 1, profiles/r04/lite_pipe.log; a bank-conflict-free staging map — LDS conflicts 0.56 -> 0.10 with no
+// layer faster, lite_remap.log; the prologue affine formed before the first input loads — neutral in the frame,
+// ab_table_first.log; a deeper B-operand ring — neutral.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,34 +33,12 @@
 
 #include "kernels.h"
 
-// expand_0 x6 chunk width: 32 (default: 4 chunks, one LDS buffer) or 16 (8 chunks through the double-buffered PIPE
-// loop; measured equal at B = 8 and 3.5 us slower at B = 1, profiles/r04/lite_pipe.log)
-#ifndef RST_LITE_E0_CKC
-#define RST_LITE_E0_CKC 32
-#endif
 // x6 transposed convs: full tiles' output staged through LDS and stored as whole lines (0: per-accumulator stores)
 #ifndef LITE_OSTAGE
 #define LITE_OSTAGE 1
 #endif
 #ifndef LITE_OSTAGE0
 #define LITE_OSTAGE0 1   // the same for the x6 strided convs
-#endif
-#ifndef LITE_REMAP
-// x6 layers: bank-conflict-free staging thread map (1) or quad fastest (0, default). SQ: LDS bank conflicts of the
-// Cout-16 layers 0.556 -> 0.103 of the LDS cycles, expand_0's 0.258 -> 0.000, with no layer faster (contract_0 B=1
-// +1.5 %, expand_0 B=8 +2 %; profiles/r04/lite_remap.log, sq_frame_r12.json): LDS banking does not bound them
-#define LITE_REMAP 0
-#endif
-// prologue affine formed (accumulator merge) before the first tile's input loads are issued (1) or after (0):
-// small L2-resident accumulator reads queued behind a tile of HBM loads gate the first staging. Standalone with the
-// frame's accumulator prologue expand_0 -1 % (B=1) / -3 % (B=8); in the frame neutral (1625 vs 1622 FPS, four
-// same-box pairs; profiles/r04/lite_tf.log, ab_table_first.log): off
-#ifndef LITE_TABLE_FIRST
-#define LITE_TABLE_FIRST 0
-#endif
-// x6 B-operand ring depth (slots of weights read ahead of their MFMAs): 2 = one slot ahead
-#ifndef LITE_BDEPTH
-#define LITE_BDEPTH 2
 #endif
 
 #ifndef LITE_SKIP
@@ -118,9 +100,6 @@ struct Cfg {
     static constexpr bool WIN_REGS = X6 && NCH == 1;        // x6 weights in registers
     static constexpr int HALO = X6 ? 3 * KS2 * G * NPIXP * 4 : NPIX * CS;   // floats per halo buffer
     static constexpr int WCH = WIN_REGS ? 0 : (X6 ? 9 * CKC * NC * 3 / 2 : 9 * CKC * NC);   // floats per chunk of weights in LDS
-    // x6 multi-chunk layers whose double buffer fits (expand_0 at 16-channel chunks): halo + weight images
-    // double-buffered in LDS, chunk c + 1 staged while chunk c's MFMAs run (its global loads two chunks ahead)
-    static constexpr bool PIPE = X6 && NCH > 1 && (HALO + WCH) * 8 + 64 * NC <= 128 * 1024;
     static constexpr int HITEMS = HR * HC * QC;             // float4 items per halo chunk
     static constexpr int HREG = (HITEMS + 255) / 256;
     static constexpr int WITEMS = WCH / 4;
@@ -128,7 +107,7 @@ struct Cfg {
     static constexpr int NACC = MS == 16 ? 4 : 16;          // accumulator floats per MFMA tile and lane
     static constexpr int NPH = MODE == 0 ? 1 : 4;           // output phases
     static constexpr int RED = MODE == 1 ? 16 * NC : 0;     // statistics scratch (floats): [16][NC]
-    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 * (PIPE ? 2 : 1) + RED * 4;
+    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 + RED * 4;
     static_assert(CIN % CKC == 0 && CKC % (4 * KS) == 0, "chunking");
     static_assert(MS == 16 || MS == 32, "MFMA shape");
     static_assert(((CS / 4) & 1) == 1, "odd 16-B slots per halo pixel");
@@ -190,14 +169,11 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     constexpr int QC = C::QC, NCH = C::NCH;
 
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    // [HALO] one Cin chunk of the tile's input halo, then [WCH] its weights (PIPE: two such buffers); halo / wts are
-    // where compute reads, halo_w / wts_w where staging writes (the same buffer unless PIPE)
-    float* halo = smem;
-    float* wts = smem + C::HALO;
-    float* halo_w = halo;
-    float* wts_w = wts;
+    // [HALO] one Cin chunk of the tile's input halo, then [WCH] its weights
+    float* const halo = smem;
+    float* const wts = smem + C::HALO;
     // [16][NC] statistics: S, n, M2 per wave (partials path) / [4][NC][2] f64 (accumulator flush)
-    float* const red = smem + (C::HALO + C::WCH) * (C::PIPE ? 2 : 1);
+    float* const red = smem + (C::HALO + C::WCH);
     static_assert((C::HALO + C::WCH) % 2 == 0, "f64-aligned statistics scratch");
     float2* const tab = reinterpret_cast<float2*>(red + C::RED);   // prologue affine [batch][CIN] (+ second style)
 
@@ -233,30 +209,20 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     constexpr int HCM = HC - 1, TPR = HCM * QC, RPP = 256 / TPR, NMAIN = (HR + RPP - 1) / RPP;
     constexpr int NEXTRA = HR * QC;
     static_assert(256 % TPR == 0 && NEXTRA <= 256, "staging map");
-    // x6 layers with 8 channel quads: within each 16-lane group of a ds_write_b64 the lanes vary the quad's half
-    // (q & 1) and 8 columns whose halo pixels are consecutive (MODE 1: consecutive columns; MODE 0: one parity plane,
-    // every other column) at one 8-channel group (q >> 1), whose planes lie NPIXP x 16 B apart (0 mod 32 banks): the
-    // default order (quad fastest) put the four groups' 16-B slots on the same banks, 4-way. The last halo column is
-    // then staged by the threads of columns 0 .. HR - 1 of the first row group (same quad per thread).
-    constexpr bool REMAP = X6 && QC == 8 && HCM % 16 == 0 && TPR % 64 == 0 && HR <= HCM && LITE_REMAP;
-    const int tr = tid % TPR;
-    const int q = REMAP ? ((tr >> 4) & 3) * 2 + (tr & 1) : tid % QC;
-    const int col = !REMAP      ? (tid / QC) % HCM
-                    : MODE == 1 ? ((tr >> 1) & 7) + 8 * (tr >> 6)
-                                : ((tr >> 6) & 1) + 2 * (((tr >> 1) & 7) + 8 * (tr >> 7));
+    const int q = tid % QC;
+    const int col = (tid / QC) % HCM;
     const int rsub = tid / TPR;
-    const bool ext = REMAP ? (rsub == 0 && col < HR) : tid < NEXTRA;   // stages the last halo column
-    const int ehy = REMAP ? min(col, HR - 1) : min(tid / QC, HR - 1);
+    const bool ext = tid < NEXTRA;   // stages the last halo column
+    const int ehy = min(tid / QC, HR - 1);
     const int lcm = halo_off(0, col) + 4 * q, lce = halo_off(0, HCM) + 4 * q;
     // two register sets of staged input (single-chunk layers prefetch two tiles ahead: the HBM latency
     // under load exceeds one tile's MFMAs); multi-chunk layers use set 0 only
     // (x6 single-chunk layers hold their weights in VGPRs instead: one set, two workgroups per CU cover the latency)
-    constexpr int NSET = (NCH == 1 && !C::WIN_REGS) || C::PIPE ? 2 : 1;
+    constexpr int NSET = NCH == 1 && !C::WIN_REGS ? 2 : 1;
     f32x4 hreg[NSET][NMAIN + 1], rreg[NSET][NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01[NSET], pa23[NSET];
     f32x4 pb01[NSET], pb23[NSET];   // BLEND: the second style's affine of the thread's channel quad
     float bw[NSET][NMAIN + 1];      // BLEND: the second style's weight at each staged pixel
-    // one chunk's weight image (multi-chunk layers; one register set: PIPE loads it one step ahead, before the halo
-    // loads of the step after, and stores it in the step's last MFMA slots)
+    // one chunk's weight image (multi-chunk layers, one register set)
     auto load_w = [&](int ch) __attribute__((always_inline)) {
         sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
             constexpr int k = decltype(K)::value;
@@ -281,7 +247,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
 #endif
             if constexpr (BLEND) bw[st][k] = a.pro_w[(rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)];
         });
-        if constexpr (NCH > 1 && !C::PIPE) load_w(ch);
+        if constexpr (NCH > 1) load_w(ch);
     };
     auto load_aff = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {   // from the LDS table
         constexpr int st = decltype(SET)::value;
@@ -338,16 +304,16 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             unsigned p0[2], p1[2], p2[2];
             split3(v.x, v.y, p0[0], p1[0], p2[0]);
             split3(v.z, v.w, p0[1], p1[1], p2[1]);
-            unsigned char* dst = reinterpret_cast<unsigned char*>(halo_w) + xq + hpix(hy, hx) * 16;
+            unsigned char* dst = reinterpret_cast<unsigned char*>(halo) + xq + hpix(hy, hx) * 16;
             *reinterpret_cast<uint2*>(dst) = make_uint2(p0[0], p0[1]);
             *reinterpret_cast<uint2*>(dst + XPIECE) = make_uint2(p1[0], p1[1]);
             *reinterpret_cast<uint2*>(dst + 2 * XPIECE) = make_uint2(p2[0], p2[1]);
         } else {
-            *reinterpret_cast<f32x4*>(halo_w + lf + hy * (HC * CS)) = v;
+            *reinterpret_cast<f32x4*>(halo + lf + hy * (HC * CS)) = v;
         }
     };
-    // staging of one chunk into the write buffer, as NSTORE items (PIPE interleaves them with the MFMAs): the
-    // NMAIN main-column rows, the last halo column, then the WREG weight float4s
+    // staging of one chunk into LDS, as NSTORE items: the NMAIN main-column rows, the last halo column, then the WREG
+    // weight float4s
     constexpr int NSTORE = NMAIN + 1 + (NCH > 1 ? C::WREG : 0);
     auto store_item = [&](const Tile& T, auto SET, auto IDX) __attribute__((always_inline)) {
         constexpr int st = decltype(SET)::value, idx = decltype(IDX)::value;
@@ -373,7 +339,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         } else if constexpr (NCH > 1) {
             constexpr int k = idx - NMAIN - 1;
             const int it = tid + 256 * k;
-            if (C::WITEMS % 256 == 0 || it < C::WITEMS) reinterpret_cast<f32x4*>(wts_w)[it] = wreg[k];
+            if (C::WITEMS % 256 == 0 || it < C::WITEMS) reinterpret_cast<f32x4*>(wts)[it] = wreg[k];
         }
     };
     auto store_step = [&](const Tile& T, auto SET) __attribute__((always_inline)) {
@@ -466,8 +432,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 acc_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ap[t6]], Bv[bp[t6]], acc_, 0, 0, 0);
         });
     };
-    auto no_hook = [](auto) __attribute__((always_inline)) {};
-    auto compute_x6 = [&](auto&& hook) __attribute__((always_inline)) {
+    auto compute_x6 = [&]() __attribute__((always_inline)) {
       if constexpr (X6) {   // discarded (not instantiated) for the f32 configurations
         const unsigned char* wbytes = reinterpret_cast<const unsigned char*>(wts);
         const unsigned char* hbytes = hbytes_r();
@@ -492,7 +457,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                     constexpr int pos = decltype(P)::value;
                     readA((wave + (pos >> 1)) * HC + m + (pos & 1), ks, A[pos]);
                 });
-                constexpr int BD = LITE_BDEPTH;
+                constexpr int BD = 2;   // B operand one slot ahead
                 short8 Bq[BD][3];
                 if constexpr (!C::WIN_REGS)
                     sfor<0, BD - 1>([&](auto P) __attribute__((always_inline)) {
@@ -505,7 +470,6 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                     __builtin_amdgcn_sched_barrier(0);
                     if constexpr (C::WIN_REGS) mfma6(acc[ai], A[pos], wr6[sl]);
                     else mfma6(acc[ai], A[pos], Bq[j % BD]);
-                    hook(std::integral_constant<int, ks * 9 + j>{});   // PIPE: staging items beside the MFMAs
                     __builtin_amdgcn_sched_barrier(0);
                 });
             } else {   // taps t = 3 ky + kx into acc[kx]; A of tap t + 1 read while tap t's MFMAs run
@@ -531,7 +495,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     };
     auto compute = [&]() __attribute__((always_inline)) {
         if constexpr (X6) {
-            if constexpr ((LITE_SKIP & 2) == 0) compute_x6(no_hook);
+            if constexpr ((LITE_SKIP & 2) == 0) compute_x6();
         } else if constexpr ((LITE_SKIP & 2) == 0) {
             f32x4 A0[NA], B0[NB], A1[NA], B1[NB];
             read_step(std::integral_constant<int, 0>{}, A0, B0);
@@ -580,8 +544,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         accS = accQ = 0.0;
     };
     const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
-    // x6 transposed convs (not PIPE: its other buffer holds the next chunk) stage full tiles' output through LDS
-    constexpr bool OSTAGE = X6 && MODE == 1 && !C::PIPE && LITE_OSTAGE;
+    // x6 transposed convs stage full tiles' output through LDS
+    constexpr bool OSTAGE = X6 && MODE == 1 && LITE_OSTAGE;
     constexpr int OST_FL = 4 * TW * NC;   // floats per wave
     // x6 strided convs (contract_0 / _1, weights in VGPRs): the same for their one output row per wave
     constexpr bool OSTAGE0 = X6 && MODE == 0 && C::WIN_REGS && LITE_OSTAGE0;
@@ -781,15 +745,27 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         for (int it = tid; it < C::WITEMS; it += 256)
             reinterpret_cast<f32x4*>(wts)[it] = reinterpret_cast<const f32x4*>(a.wpk)[it];
     }
-    // the prologue affine of every image into the LDS table: given, or formed from the producer's f64
-    // accumulators (no finalize ran); runs after the first tiles' input loads are issued
+    // the prologue affine of every image into the LDS table: given, or formed from the producer's fixed-point
+    // accumulators (no finalize ran). One image: the accumulator loads go out first (fill_issue, CinAffineSplit) and
+    // are merged after the first tiles' input loads are issued (fill_table), so their wait excludes those loads'
+    // latency (vmcnt retires in issue order); more images: cin_affine_table after the input loads
+    const bool split_aff = PRO != PRO_NONE && a.pro_stat.acc != nullptr && a.batch == 1 &&
+                           CinAffineSplit<256, 2>::usable(a.pro_stat);
+    CinAffineSplit<256, 2> aff;
+    auto fill_issue = [&]() __attribute__((always_inline)) {
+        if constexpr (PRO != PRO_NONE)
+            if (split_aff) aff.issue(a.pro_stat, 0, BLEND);
+    };
     auto fill_table = [&]() __attribute__((always_inline)) {
     if constexpr (PRO != PRO_NONE) {
         const CinSrc& ps = a.pro_stat;
         if (ps.acc != nullptr) {
             const bool store = blockIdx.x == 0;   // the host-visible copy (rst_copy_activation)
-            cin_affine_table<256>(ps, 0, a.batch, tab, BLEND ? tab + a.batch * CIN : nullptr,
-                                  store ? ps.ab_out : nullptr, store ? ps.ab1_out : nullptr);
+            if (split_aff)
+                aff.finish(ps, tab, BLEND ? tab + CIN : nullptr, store ? ps.ab_out : nullptr, store ? ps.ab1_out : nullptr);
+            else
+                cin_affine_table<256>(ps, 0, a.batch, tab, BLEND ? tab + a.batch * CIN : nullptr,
+                                      store ? ps.ab_out : nullptr, store ? ps.ab1_out : nullptr);
         } else {
             for (int i = tid; i < a.batch * CIN; i += 256) {
                 tab[i] = a.pro_ab[i];
@@ -809,6 +785,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     if constexpr (NCH == 1 && NSET == 2) {
         // tile k's input sits in register set k & 1, loaded two tiles ahead
         Tile T0 = tile_of(0), T1 = T0;
+        fill_issue();
         load_in(T0, 0, S0{});
         if (my_tiles > 1) {
             T1 = tile_of(1);
@@ -850,78 +827,12 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
             T0 = T2;
         }
-    } else if constexpr (C::PIPE) {
-        // global step s = (tile s / NCH, chunk s % NCH) computes from LDS buffer s & 1 while its MFMA slots stage step
-        // s + 1 (register set (s + 1) & 1, loaded two steps earlier) into buffer (s + 1) & 1; one barrier per step,
-        // after which the freed set takes step s + 3's global loads. n_steps is even (NCH even): the loop body
-        // runs a step pair so that buffer and set indices are compile-time.
-        static_assert(NCH % 2 == 0 && NCH >= 4, "PIPE: even chunk count, at least 4");
-        const int n_steps = my_tiles * NCH;
-        float* const buf1 = smem + C::HALO + C::WCH;
-        auto tile_at = [&](int st) __attribute__((always_inline)) { return tile_of(st / NCH); };
-        Tile cur = tile_of(0), nx1 = tile_at(1);
-        load_w(0);
-        load_in(cur, 0, S0{});
-        load_in(nx1, 1, S1{});
-        fill_table();
-        load_aff(cur, 0, S0{});
-        load_aff(nx1, 1, S1{});
-        store_step(cur, S0{});   // halo_w / wts_w = buffer 0
-        lds_barrier();
-        load_w(1);
-        __builtin_amdgcn_sched_barrier(0);
-        load_step(tile_at(2), 2, S0{});   // n_steps >= NCH >= 4
-        auto pipe_step = [&](int s, auto PAR) __attribute__((always_inline)) {
-            constexpr int par = decltype(PAR)::value;   // s & 1
-            using SN = std::integral_constant<int, par ^ 1>;
-            const int ch = s % NCH;
-            LTL(s, 0);
-            if (s == n_steps - NCH) l2f = l2_touch_xcd_slice<256, 2>(a.w_next, a.w_next_bytes);
-            halo = par ? buf1 : smem;
-            wts = halo + C::HALO;
-            halo_w = par ? smem : buf1;
-            wts_w = halo_w + C::HALO;
-            LTL(s, 1);
-            // (the last step stages a repeat of itself into the idle buffer: no branch, so that the compiler's
-            // vmcnt bookkeeping stays exact across the step)
-            if constexpr ((LITE_SKIP & 2) == 0) {
-                // NSTORE items over the 9 KS2 slots: one per slot, the rest after the last
-                compute_x6([&](auto J) __attribute__((always_inline)) {
-                    constexpr int j = decltype(J)::value, nsl = 9 * C::KS2;
-                    if constexpr (j < nsl - 1) {
-                        if constexpr (j < NSTORE) store_item(nx1, SN{}, std::integral_constant<int, j>{});
-                    } else {
-                        sfor<nsl - 1, NSTORE>([&](auto I) __attribute__((always_inline)) { store_item(nx1, SN{}, I); });
-                    }
-                });
-            } else {
-                store_step(nx1, SN{});
-            }
-            LTL(s, 2);
-            if (ch == NCH - 1) {
-                epilogue(cur);
-                zero_acc();
-            }
-            lds_barrier();   // buffer par read, buffer par ^ 1 written
-            // steps past the end re-load the last one (unconditional loads, see above)
-            const int s2 = min(s + 2, n_steps - 1), s3 = min(s + 3, n_steps - 1);
-            load_w(s2 % NCH);
-            __builtin_amdgcn_sched_barrier(0);
-            load_step(tile_at(s3), s3 % NCH, SN{});
-            LTL(s, 3);
-            cur = nx1;
-            nx1 = tile_at(s2);
-        };
-        for (int s = 0; s < n_steps; s += 2) {
-            pipe_step(s, S0{});
-            pipe_step(s + 1, S1{});
-        }
     } else {   // multi-chunk layers, and single-chunk layers with one register set (x6: weights in VGPRs)
         const int n_steps = my_tiles * NCH;
         Tile cur = tile_of(0);
-        if constexpr (LITE_TABLE_FIRST) fill_table();
+        fill_issue();
         load_in(cur, 0, S0{});
-        if constexpr (!LITE_TABLE_FIRST) fill_table();
+        fill_table();
         load_aff(cur, 0, S0{});
         for (int s = 0; s < n_steps; ++s) {
             const int ch = s % NCH;
@@ -960,7 +871,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     X(2, 0, 16, 32, 16, 0)         \
     X(3, 1, 128, 32, 32, 0)        \
     X(4, 1, 32, 16, 32, 0)         \
-    X(5, 1, 128, 32, RST_LITE_E0_CKC, 1) \
+    X(5, 1, 128, 32, 32, 1)        \
     X(6, 0, 32, 16, 32, 1)         \
     X(7, 0, 16, 32, 16, 1)         \
     X(8, 1, 32, 16, 32, 1)

@@ -191,54 +191,50 @@ __device__ __forceinline__ void cin_acc_add(const CinAcc& a, int batch, int C, i
     cin_acc_add_value(a, batch, C, b, c, slot, 1, Q);
 }
 
-// Every thread of an NT-thread workgroup calls this: the affine of images b0 .. b0 + nb - 1, channels [0, C)
-// (finalize_kernel's arithmetic on the merged sums) into tab[j * C + c] for image b0 + j (and the second
-// style's into tab1[j * C + c] when tab1 is given; LDS or global), also into out / out1 when given (the
-// host-visible copies, same indexing). L lanes per (image, channel) (a power of two, L * nb * C <= NT where
-// possible) each read K / L of the K = nslot (rounded up to a power of two) accumulator copies, all loads
-// issued together with the style-parameter loads, and reduce by xor shuffles: about one memory latency per
-// pass instead of nslot dependent loads.
-template <int NT>
-__device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb, float2* tab, float2* tab1,
-                                                 float2* out, float2* out1) {
-    constexpr int RMAX = 8;   // copies per lane (each 2 x CIN_LIMBS words)
-    int K = 1;
-    while (K < s.nslot) K <<= 1;
-    const int items = nb * s.C;
-    int L = K / RMAX > 1 ? K / RMAX : 1;                   // at most RMAX copies per lane
-    // more lanes while one pass still covers every item, up to a quad (the lanes of an item merge by DPP: VALU only)
-    while (L < K && L < 4 && 2 * L * items <= NT) L <<= 1;
-    const int R = K / L, n = items * L;
-    for (int base = 0; base < n; base += NT) {
-        const int i = base + (int)threadIdx.x, it = i / L, l = i & (L - 1);
+// One pass structure of cin_affine_table with R copies per lane (compile time): every lane issues its R x 2 x CIN_LIMBS
+// accumulator loads and its style-parameter loads unconditionally (clamped to a valid address, masked after), so they
+// are all in flight together and the lane waits once. (The round-4 form guarded each load by its copy / item test:
+// hipcc then waited for every load before issuing the next — 6 R serialized L2 round trips after a full drain of the
+// caller's staging loads, 4.2 us of a 31 us residual conv at the frame's 8 copies.)
+template <int NT, int R>
+__device__ __forceinline__ void cin_affine_pass(const CinSrc& s, int b0, int n, int L, float2* tab, float2* tab1,
+                                                float2* out, float2* out1) {
+    auto pass = [&](int base) __attribute__((always_inline)) {
+        const int i = base + (int)threadIdx.x;
+        const bool live = i < n;
+        const int ic = live ? i : n - 1;
+        const int it = ic / L, l = ic & (L - 1);
         const int j = it / s.C, c = it - j * s.C, b = b0 + j;
-        const bool head = i < n && l == 0;
+        const bool head = live && l == 0;
         const float* const sp = s.style + (size_t)b * s.style_stride + s.style_offset;
-        float g0 = 0.f, be0 = 0.f, g1 = 0.f, be1 = 0.f;
-        if (head) {   // independent of the accumulators: in flight with them
-            g0 = sp[c];
-            be0 = sp[s.C + c];
-            if (tab1 != nullptr) {
-                g1 = sp[s.style1_offset + c];
-                be1 = sp[s.style1_offset + s.C + c];
-            }
+        const float g0 = sp[c], be0 = sp[s.C + c];   // independent of the accumulators: in flight with them
+        float g1 = 0.f, be1 = 0.f;
+        if (tab1 != nullptr) {   // uniform
+            g1 = sp[s.style1_offset + c];
+            be1 = sp[s.style1_offset + s.C + c];
+        }
+        cin_word v[R][2 * CIN_LIMBS];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int k = l + L * r;
+            const int kc = k < s.nslot ? k : 0;
+            const cin_word* const p = s.acc + ((size_t)(kc * s.batch + b) * 2 * CIN_LIMBS) * s.C + c;
+#pragma unroll
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) v[r][q] = p[q * s.C];
         }
         cin_word w[2 * CIN_LIMBS] = {};
 #pragma unroll
-        for (int r = 0; r < RMAX; ++r) {
-            const int k = l + L * r;
-            if (r < R && i < n && k < s.nslot) {
-                const cin_word* const p = s.acc + ((size_t)(k * s.batch + b) * 2 * CIN_LIMBS) * s.C + c;
+        for (int r = 0; r < R; ++r) {
+            const cin_word m = l + L * r < s.nslot ? ~(cin_word)0 : (cin_word)0;   // copies past nslot add nothing
 #pragma unroll
-                for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += p[q * s.C];
-            }
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += v[r][q] & m;
         }
         // the L lanes of an item are consecutive: within a quad (L <= 4) the partner words move by DPP (VALU) instead
         // of ds_bpermute round trips; integer adds, so the merged words do not depend on the order
-        auto dpp64 = [](cin_word v, auto CTRL) __attribute__((always_inline)) {
+        auto dpp64 = [](cin_word x, auto CTRL) __attribute__((always_inline)) {
             constexpr int ctrl = decltype(CTRL)::value;
-            const unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)v, ctrl, 0xF, 0xF, true);
-            const unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)((unsigned long long)v >> 32), ctrl, 0xF,
+            const unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)x, ctrl, 0xF, 0xF, true);
+            const unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)((unsigned long long)x >> 32), ctrl, 0xF,
                                                             0xF, true);
             return (cin_word)(((unsigned long long)hi << 32) | lo);
         };
@@ -259,9 +255,127 @@ __device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb
             const double N = s.n, mean = S / N, var = fmax(Q - S * mean, 0.0) / N;
             const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
             const float aa = g0 * rstd;
-            const float2 v = make_float2(aa, be0 - (float)mean * aa);
-            tab[it] = v;
-            if (out != nullptr) out[it] = v;
+            const float2 vv = make_float2(aa, be0 - (float)mean * aa);
+            tab[it] = vv;
+            if (out != nullptr) out[it] = vv;
+            if (tab1 != nullptr) {
+                const float a1 = g1 * rstd;
+                const float2 v1 = make_float2(a1, be1 - (float)mean * a1);
+                tab1[it] = v1;
+                if (out1 != nullptr) out1[it] = v1;
+            }
+        }
+    };
+    // the first pass outside the loop: a loop's back edge makes hipcc wait for the previous iteration's loads at the
+    // loop top (register reuse), which at the first entry drains every load the caller has in flight
+    pass(0);
+    for (int base = NT; base < n; base += NT) pass(base);
+}
+
+// Every thread of an NT-thread workgroup calls this: the affine of images b0 .. b0 + nb - 1, channels [0, C)
+// (finalize_kernel's arithmetic on the merged sums) into tab[j * C + c] for image b0 + j (and the second
+// style's into tab1[j * C + c] when tab1 is given; LDS or global), also into out / out1 when given (the
+// host-visible copies, same indexing). L lanes per (image, channel) (a power of two, L * nb * C <= NT where
+// possible) each read K / L of the K = nslot (rounded up to a power of two) accumulator copies, all loads
+// issued together with the style-parameter loads, and reduce by DPP / xor shuffles: one memory latency per pass.
+template <int NT>
+__device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb, float2* tab, float2* tab1,
+                                                 float2* out, float2* out1) {
+    constexpr int RMAX = 8;   // copies per lane (each 2 x CIN_LIMBS words)
+    int K = 1;
+    while (K < s.nslot) K <<= 1;
+    const int items = nb * s.C;
+    int L = K / RMAX > 1 ? K / RMAX : 1;                   // at most RMAX copies per lane
+    // more lanes while one pass still covers every item, up to a quad (the lanes of an item merge by DPP: VALU only)
+    while (L < K && L < 4 && 2 * L * items <= NT) L <<= 1;
+    const int R = K / L, n = items * L;
+    switch (R) {   // uniform
+        case 1: cin_affine_pass<NT, 1>(s, b0, n, L, tab, tab1, out, out1); break;
+        case 2: cin_affine_pass<NT, 2>(s, b0, n, L, tab, tab1, out, out1); break;
+        case 4: cin_affine_pass<NT, 4>(s, b0, n, L, tab, tab1, out, out1); break;
+        default: cin_affine_pass<NT, RMAX>(s, b0, n, L, tab, tab1, out, out1); break;
+    }
+}
+
+// Split form of cin_affine_table for one image (nb = 1) whose whole table is one pass (C * L <= NT) and whose copies
+// per lane fit RS: issue() sends the accumulator and style-parameter loads, finish() (after the caller has issued its
+// own first loads) merges them and writes the table. vmcnt retires loads in issue order, so the accumulator loads
+// issued first are waited for without waiting for the caller's later (HBM) loads — the two latencies overlap instead
+// of adding. usable() says whether the split form applies (uniform); otherwise call cin_affine_table.
+template <int NT, int RS>
+struct CinAffineSplit {
+    cin_word v[RS][2 * CIN_LIMBS];
+    float g0, be0, g1, be1;
+    int it, l, L;
+    bool head;
+    static __device__ __forceinline__ int lanes(const CinSrc& s, int& K) {
+        K = 1;
+        while (K < s.nslot) K <<= 1;
+        int L = K / 8 > 1 ? K / 8 : 1;
+        while (L < K && L < 4 && 2 * L * s.C <= NT) L <<= 1;
+        return L;
+    }
+    static __device__ __forceinline__ bool usable(const CinSrc& s) {
+        int K;
+        const int L = lanes(s, K);
+        return K / L <= RS && s.C * L <= NT;
+    }
+    __device__ __forceinline__ void issue(const CinSrc& s, int b, bool two_styles) {
+        int K;
+        L = lanes(s, K);
+        const int n = s.C * L;
+        const int i = (int)threadIdx.x, ic = i < n ? i : n - 1;
+        it = ic / L;
+        l = ic & (L - 1);
+        head = i < n && l == 0;
+        const float* const sp = s.style + (size_t)b * s.style_stride + s.style_offset;
+        g0 = sp[it];
+        be0 = sp[s.C + it];
+        g1 = be1 = 0.f;
+        if (two_styles) {
+            g1 = sp[s.style1_offset + it];
+            be1 = sp[s.style1_offset + s.C + it];
+        }
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            const int k = l + L * r;
+            const int kc = k < s.nslot ? k : 0;
+            const cin_word* const p = s.acc + ((size_t)(kc * s.batch + b) * 2 * CIN_LIMBS) * s.C + it;
+#pragma unroll
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) v[r][q] = p[q * s.C];
+        }
+    }
+    __device__ __forceinline__ void finish(const CinSrc& s, float2* tab, float2* tab1, float2* out, float2* out1) {
+        cin_word w[2 * CIN_LIMBS] = {};
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            const cin_word m = l + L * r < s.nslot ? ~(cin_word)0 : (cin_word)0;
+#pragma unroll
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += v[r][q] & m;
+        }
+        auto dpp64 = [](cin_word x, auto CTRL) __attribute__((always_inline)) {
+            constexpr int ctrl = decltype(CTRL)::value;
+            const unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)x, ctrl, 0xF, 0xF, true);
+            const unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)((unsigned long long)x >> 32), ctrl, 0xF,
+                                                            0xF, true);
+            return (cin_word)(((unsigned long long)hi << 32) | lo);
+        };
+        if (L >= 2) {
+#pragma unroll
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += dpp64(w[q], std::integral_constant<int, 0xB1>{});
+        }
+        if (L >= 4) {
+#pragma unroll
+            for (int q = 0; q < 2 * CIN_LIMBS; ++q) w[q] += dpp64(w[q], std::integral_constant<int, 0x4E>{});
+        }
+        if (head) {
+            const double S = cin_fixed_value(w[0], w[1], w[2]), Q = cin_fixed_value(w[3], w[4], w[5]);
+            const double N = s.n, mean = S / N, var = fmax(Q - S * mean, 0.0) / N;
+            const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
+            const float aa = g0 * rstd;
+            const float2 vv = make_float2(aa, be0 - (float)mean * aa);
+            tab[it] = vv;
+            if (out != nullptr) out[it] = vv;
             if (tab1 != nullptr) {
                 const float a1 = g1 * rstd;
                 const float2 v1 = make_float2(a1, be1 - (float)mean * a1);
@@ -270,7 +384,7 @@ __device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb
             }
         }
     }
-}
+};
 
 // Arguments of the implicit-GEMM MFMA conv kernel (conv_mfma.hip).
 struct ConvArgs {

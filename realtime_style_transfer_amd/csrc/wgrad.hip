@@ -494,11 +494,13 @@ constexpr int PR = TH + 8, PC = TW + 8, PRS = 24;           // patch rows / cols
 constexpr int CMAX = 17, PLANE = PR * PRS + 2;
 constexpr int PIECE = CMAX * PLANE, COPY = 3 * PIECE;        // elements per piece / per copy
 constexpr int DZS = NPX + 8;                                 // dZ^T row stride (elements; 16-B aligned rows)
-constexpr int DZOFF = 2 * COPY;                              // dZ^T [piece][co][DZS] after the two copies
+constexpr int DZOFF = (2 * COPY + 7) / 8 * 8;                // dZ^T [piece][co][DZS] after the two copies, 16-B aligned
 constexpr int LDS_EL = DZOFF + 3 * 32 * DZS;
 constexpr size_t LDS_BYTES = (size_t)LDS_EL * 2;
 constexpr int NCOL = 81 * CMAX, NCOLP = 1408, NTW = NCOLP / 32 / 4;   // 11 column tiles per wave
 static_assert(LDS_BYTES <= 160 * 1024 && (COPY % 2) == 0 && (PLANE % 2) == 0, "layout");
+// the A operand (dZ^T, short8 per lane and piece) is read with ds_read_b128: every row 16-B aligned
+static_assert((DZOFF * 2) % 16 == 0 && (DZS * 2) % 16 == 0, "16-B aligned dZ^T rows");
 }  // namespace w9x
 
 __global__ __launch_bounds__(256, 1) void wgrad9_x6_kernel(WgradArgs a) {
@@ -805,7 +807,38 @@ void wgrad_dims(const WgradArgs& a, int& R, int& Cu, int& Cs) {
 
 constexpr int W9_BLOCKS = 512;   // two workgroups per CU, each a persistent walk over the pixel tiles
 
+// the split-bf16 start-conv kernel for the x6 trainer (RST_WGRAD9_X6=0: the f32 kernel). Config-4 step 24.97 -> 24.29 ms
+// same box (profiles/r04/trainab_wgrad9_x6_prefetch.log); the first form, before the odd channel pitch and the
+// register prefetch, ran 29.6 ms (trainab_wgrad9_x6.log)
+static bool wgrad9_x6_enabled() {
+    static const bool ok = [] {
+        const char* v = getenv("RST_WGRAD9_X6");
+        if (v != nullptr && v[0] == '0') return false;
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad9_x6_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)w9x::LDS_BYTES) == hipSuccess;
+    }();
+    return ok;
+}
+
+static int wgrad_cu_count() {
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            n_cu = 256;
+    }
+    return n_cu;
+}
+
 int wgrad_choose_splits(const WgradArgs& a) {
+    if (wgrad9_applies(a) && a.x6 && wgrad9_x6_enabled()) {
+        // one workgroup per CU (104 KB of LDS, launch_bounds(256, 1)): one round of persistent workgroups, never more
+        // than the pixel tiles (each writes a slab the reduce then reads)
+        const int ntiles = a.batch * ((a.Qh + w9x::TH - 1) / w9x::TH) * ((a.Qw + w9x::TW - 1) / w9x::TW);
+        const int n = wgrad_cu_count();
+        return ntiles < n ? (ntiles < 1 ? 1 : ntiles) : n;
+    }
     if (wgrad9_applies(a) || wgradT9_applies(a)) return W9_BLOCKS;
     int R, Cu, Cs;
     wgrad_dims(a, R, Cu, Cs);
@@ -833,16 +866,7 @@ hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
     wgrad_dims(a, R, Cu, Cs);
     if (wgrad9_applies(a)) {
         if (a.nsplit < 1) return hipErrorInvalidValue;
-        // the split-bf16 kernel for the x6 trainer (RST_WGRAD9_X6=0: the f32 kernel). Config-4 step 24.97 -> 24.29 ms
-        // same box (profiles/r04/trainab_wgrad9_x6_prefetch.log); the first form, before the odd channel pitch and the
-        // register prefetch, ran 29.6 ms (trainab_wgrad9_x6.log)
-        static const bool x6_ok = [] {
-            const char* v = getenv("RST_WGRAD9_X6");
-            if (v != nullptr && v[0] == '0') return false;
-            return hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad9_x6_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)w9x::LDS_BYTES) == hipSuccess;
-        }();
-        if (a.x6 && x6_ok)
+        if (a.x6 && wgrad9_x6_enabled())
             hipLaunchKernelGGL(wgrad9_x6_kernel, dim3((unsigned)a.nsplit), dim3(256), w9x::LDS_BYTES, st, a);
         else
             hipLaunchKernelGGL(wgrad9_kernel, dim3((unsigned)a.nsplit), dim3(256), 0, st, a);

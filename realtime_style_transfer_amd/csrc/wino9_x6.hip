@@ -99,12 +99,9 @@ __device__ __forceinline__ void split8(const float (&v)[8], short8 (&A)[3]) {
 #ifndef W9_SKIP
 #define W9_SKIP 0
 #endif
-#ifndef W9_PIPE
-#define W9_PIPE 0      // 1: software-pipelined whole units (the next unit's operand preparation beside the MFMAs)
-#endif
-#ifndef W9_STAGGER
-#define W9_STAGGER 0   // s_sleep argument (64-cycle units) of the qh = 1 waves at each tile start; 0: none
-#endif
+// (Measured and removed, round 4: a software-pipelined unit loop with the next unit's operand preparation beside
+// the MFMAs, and an s_sleep stagger of the qh = 1 waves at each tile start — both slower,
+// profiles/r04/w9_stagger_pipe_slp.log.)
 #ifdef W9_PROF
 // timeline per (workgroup, wave) on the constant 100 MHz clock: start, staged, loop done, end
 __device__ unsigned long long w9_tl[W9_PROF][8][9][4];   // [workgroup][wave][tile iteration][stamp]
@@ -293,11 +290,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[q][h][r] = 0.f;
         lds_barrier();   // patch + pads visible
-#if W9_STAGGER
-        // the two waves of a SIMD (qh = 0 / 1, same point row) run the same VALU-then-MFMA sequence in lockstep; the
-        // qh = 1 wave starts each tile later so its transform VALU runs beside the other's MFMAs
-        if (qh == 1) __builtin_amdgcn_s_sleep(W9_STAGGER);
-#endif
         W9TL(1);
         // The q pair is a compile-time parameter (one code path per wave-uniform value): pair 0 uses the
         // columns 0..2 of B^T d (V0 = T0 - T2, V1 = T1 + T2), pair 1 the columns 1..3 (V2 = T2 - T1,
@@ -375,109 +367,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
                 });
             });
         };
-#if W9_PIPE
-        // Software-pipelined form of main_loop for whole units (both M blocks): the 18 (sub-kernel, block) units run
-        // in order, and the 12 MFMAs of unit u are interleaved one by one with the 12 stages of unit u + 1's operand
-        // preparation (patch reads, B^T d rows, the point pair, the 3-piece split), so a wave's transform VALU issues
-        // beside its own MFMAs instead of in a separate phase (the two waves of a SIMD otherwise alternate whole
-        // VALU and MFMA phases in lockstep). Same arithmetic as main_loop, unit for unit.
-        auto pipe_loop = [&](auto QH) __attribute__((always_inline)) {
-            constexpr int QHC = decltype(QH)::value;
-            f32x4 rd[3][4];
-            float r16[3][2], tv[3][8], t16[3], v0[8], v1[8];
-            unsigned pk[2][3][4];
-            short8 An[2][3];   // the next unit's A operands (point q of the pair, piece)
-            // stage st (0..11) of the preparation of unit (ab, h)
-            auto stage = [&](auto AB, auto Hh, auto ST) __attribute__((always_inline)) {
-                constexpr int ab = decltype(AB)::value, h = decltype(Hh)::value, st = decltype(ST)::value;
-                constexpr int sa = ab / 3, sb = ab % 3;
-                if constexpr (st < 3) {   // patch reads of column cc = st
-                    constexpr int cc = st;
-                    constexpr int off = (8 * h + 3 * sa) * RP + ((3 * sb + QHC + cc) & 1) * PLANE +
-                                        ((3 * sb + QHC + cc) >> 1) * PS;
-                    rd[cc][0] = *reinterpret_cast<const f32x4*>(bx + off);
-                    rd[cc][1] = *reinterpret_cast<const f32x4*>(bx + off + 4);
-                    rd[cc][2] = *reinterpret_cast<const f32x4*>(by + off);
-                    rd[cc][3] = *reinterpret_cast<const f32x4*>(by + off + 4);
-                    r16[cc][0] = bx16[off];
-                    r16[cc][1] = by16[off];
-                } else if constexpr (st < 6) {   // row p of B^T d for column cc
-                    constexpr int cc = st - 3;
-                    const float xv[8] = {rd[cc][0].x, rd[cc][0].y, rd[cc][0].z, rd[cc][0].w,
-                                         rd[cc][1].x, rd[cc][1].y, rd[cc][1].z, rd[cc][1].w};
-                    const float yv[8] = {rd[cc][2].x, rd[cc][2].y, rd[cc][2].z, rd[cc][2].w,
-                                         rd[cc][3].x, rd[cc][3].y, rd[cc][3].z, rd[cc][3].w};
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) tv[cc][k] = fmaf(sx, xv[k], yv[k]);
-                    t16[cc] = fmaf(sx, r16[cc][0], r16[cc][1]);
-                } else if constexpr (st == 6) {   // the point pair; channel 16 -> LDS
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        v0[k] = QHC == 0 ? tv[0][k] - tv[2][k] : tv[1][k] - tv[0][k];
-                        v1[k] = QHC == 0 ? tv[1][k] + tv[2][k] : tv[0][k] - tv[2][k];
-                    }
-                    const float w0 = QHC == 0 ? t16[0] - t16[2] : t16[1] - t16[0];
-                    const float w1 = QHC == 0 ? t16[1] + t16[2] : t16[0] - t16[2];
-                    v16s[((4 * p + 2 * QHC + lh) * 64 + 32 * h + li) * V16S + ab] = lh ? w1 : w0;
-                } else if constexpr (st < 11) {   // the split, two channel pairs per stage
-                    constexpr int q = (st - 7) >> 1, j0 = ((st - 7) & 1) * 2;
-                    float* const v = q ? v1 : v0;
-#pragma unroll
-                    for (int j = j0; j < j0 + 2; ++j) {
-                        float x = v[2 * j], y = v[2 * j + 1];
-                        pk[q][0][j] = piece(x, y);
-                        pk[q][1][j] = piece(x, y);
-                        pk[q][2][j] = piece(x, y);
-                    }
-                } else {   // pack
-#pragma unroll
-                    for (int q = 0; q < 2; ++q)
-#pragma unroll
-                        for (int pc = 0; pc < 3; ++pc)
-                            An[q][pc] = __builtin_bit_cast(short8, (u32x4){pk[q][pc][0], pk[q][pc][1], pk[q][pc][2], pk[q][pc][3]});
-                }
-            };
-            auto prep_all = [&](auto AB, auto Hh) __attribute__((always_inline)) {
-                sfor<0, 12>([&](auto ST) __attribute__((always_inline)) { stage(AB, Hh, ST); });
-            };
-            constexpr int ap[6] = {0, 0, 1, 0, 1, 2}, bp[6] = {0, 1, 0, 2, 1, 0};
-            prep_all(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-            sfor<0, 18>([&](auto U) __attribute__((always_inline)) {
-                constexpr int u = decltype(U)::value, ab = u >> 1, h = u & 1, cur = ab & 1;
-                constexpr int un = u + 1, abn = un >> 1, hn = un & 1;
-                if constexpr (h == 0) {
-                    load_u(std::integral_constant<int, cur ^ 1>{}, ab + 1);   // ab + 1 == 9: the channel-16 step's U
-                    if constexpr (ab == 3 || ab == 5 || ab == 7) {
-                        if (tn < n_units) store_half(tn, pnext, std::integral_constant<int, (ab - 3) / 2>{});
-                    }
-                    if constexpr (ab == 1 || ab == 3 || ab == 5) {
-                        if (tn < n_units) load_half(tn, std::integral_constant<int, (ab - 1) / 2>{});
-                    }
-                }
-                short8 A[2][3];
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-#pragma unroll
-                    for (int pc = 0; pc < 3; ++pc) A[q][pc] = An[q][pc];
-                __builtin_amdgcn_sched_barrier(0);
-                sfor<0, 12>([&](auto T) __attribute__((always_inline)) {
-                    constexpr int t = decltype(T)::value, q = t / 6, k = t % 6;
-                    if constexpr (!(W9_SKIP & 4))
-                        acc[q][h] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[q][ap[k]], ub[cur][q][bp[k]], acc[q][h], 0, 0, 0);
-                    if constexpr (un < 18) stage(std::integral_constant<int, abn>{}, std::integral_constant<int, hn>{}, T);
-                    __builtin_amdgcn_sched_barrier(0);
-                });
-            });
-        };
-#endif
         auto main_loop_q = [&](auto MK) __attribute__((always_inline)) {
-#if W9_PIPE
-            if constexpr (decltype(MK)::value == 3) {
-                if (__builtin_amdgcn_readfirstlane(qh) == 0) pipe_loop(std::integral_constant<int, 0>{});
-                else pipe_loop(std::integral_constant<int, 1>{});
-                return;
-            }
-#endif
             if (__builtin_amdgcn_readfirstlane(qh) == 0) main_loop(std::integral_constant<int, 0>{}, MK);
             else main_loop(std::integral_constant<int, 1>{}, MK);
         };

@@ -96,9 +96,6 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 #ifndef X6_SKIP
 #define X6_SKIP 0
 #endif
-#ifndef RST_X6_AFFINE_FIRST
-#define RST_X6_AFFINE_FIRST 0   // fill order: prologue affine before (1) or after (0) the first staging / U loads
-#endif
 #ifdef X6_PROF
 // timeline per (workgroup, wave < 8) on the constant 100 MHz clock: 0 start, 8 first loads issued, 4 affine formed,
 // 5 chunk 0 staged, 1 pipeline filled, 2 chunk loop done, 6 epilogue image written, 7 outputs stored, 3 end
@@ -179,16 +176,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* res_src = pro == PRO_AFF_RES ? a.res : a.in;
     const int nchunks = Cin / XCK;
 
-    // the prologue affine into LDS (pab / pab1): given, or formed from the producer's fixed-point accumulators; runs
-    // after the first patch and U loads are issued (below), so its latency overlaps theirs
+    // the prologue affine into LDS (pab / pab1): given, or formed from the producer's fixed-point accumulators. The
+    // accumulator loads are issued first (aff.issue, below) and merged after the first patch and U loads are issued
+    // (aff.finish): vmcnt retires in order, so their wait does not include the later loads' HBM latency
+    const bool split_aff = pro != PRO_NONE && a.pro_stat.acc != nullptr;   // wino_x6_launch: nslot <= 8
+    CinAffineSplit<YT, 2> aff;
     auto load_affine = [&]() __attribute__((always_inline)) {
         if constexpr (pro != PRO_NONE) {
             if (a.pro_stat.acc != nullptr) {
                 const bool store = tx == 0 && ty == 0;   // one workgroup per image keeps the host-visible copy
                 const CinSrc& ps = a.pro_stat;
-                cin_affine_table<YT>(ps, b, 1, pab, BLEND ? pab1 : nullptr,
-                                     store && ps.ab_out ? ps.ab_out + (size_t)b * Cin : nullptr,
-                                     store && ps.ab1_out ? ps.ab1_out + (size_t)b * Cin : nullptr);
+                aff.finish(ps, pab, BLEND ? pab1 : nullptr, store && ps.ab_out ? ps.ab_out + (size_t)b * Cin : nullptr,
+                           store && ps.ab1_out ? ps.ab1_out + (size_t)b * Cin : nullptr);
             } else {
                 for (int c = tid; c < Cin; c += YT) pab[c] = a.pro_ab[(size_t)b * Cin + c];
                 if constexpr (BLEND)
@@ -374,13 +373,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
 
     // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..R-1) in flight ----
-#if RST_X6_AFFINE_FIRST
-    // the prologue affine first: its accumulator loads are then not queued behind (vmcnt is in order) the staging
-    // and U loads, which are issued after it and land while it is formed
-    XTL(8);
-    load_affine();
-    XTL(4);
-#endif
+    if (split_aff) aff.issue(a.pro_stat, b, BLEND);
     sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 0); });
     if (nchunks > 1) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload1(decltype(K)::value); });
     sfor<0, YRING>([&](auto X) __attribute__((always_inline)) {
@@ -388,11 +381,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             load_u1(0, decltype(X)::value, decltype(X)::value, decltype(Pc)::value);
         });
     });
-#if !RST_X6_AFFINE_FIRST
     XTL(8);
     load_affine();
     XTL(4);
-#endif
     if constexpr (pro != PRO_NONE) lds_barrier();   // pab visible before the first staging
     stage_all(0, patch);
     lds_barrier();
@@ -768,7 +759,8 @@ hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
     if (a.stat.acc != nullptr && (a.stat.nslot < 1 || a.stat.nslot > CIN_ACC_MAX_SLOTS))
         return hipErrorInvalidValue;
     const bool src_acc = a.pro_stat.acc != nullptr;
-    if (src_acc && (a.pro_stat.nslot < 1 || a.pro_stat.nslot > CIN_ACC_MAX_SLOTS || a.pro_stat.C != a.cin ||
+    // (nslot <= 8 and C <= 128: the kernel's split affine form, CinAffineSplit<512, 2>, covers the accumulators)
+    if (src_acc && (a.pro_stat.nslot < 1 || a.pro_stat.nslot > 8 || a.pro_stat.C != a.cin || a.cin > XN ||
                     a.pro_stat.batch != a.batch || a.pro_stat.style == nullptr || a.pro_mode == PRO_NONE))
         return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);

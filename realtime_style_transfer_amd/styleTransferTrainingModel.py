@@ -644,13 +644,22 @@ class _SharedInference(StyleTransferInference):
         return self._models.style_predictor
 
     def _restore_tensors(self, tensors):
-        st = self._models.training._restore_tensors(tensors)
-        self._models.refresh()
-        return st
+        return _restore_weights_only(self._models, tensors)
 
     def _checkpoint_tensors(self):
         from .tf_checkpoint import parts_tensors
         return parts_tensors(self._models.training._checkpoint_parts())
+
+
+def _restore_weights_only(models, tensors):
+    """A restore through the inference view (``Checkpoint(models.inference).restore``, train_network.py:112-113;
+    ``inference.load_weights``): as in TF, the optimizer is not reachable from the inference model, so only the
+    predictor and transfer weights are bound — the RMSprop slots, ``iter`` and the hyperparameters stay untouched and
+    are reported unused (``assert_consumed()`` fails on a training checkpoint, as TF's does)."""
+    from .tf_checkpoint import restore_parts
+    st = restore_parts(models.training._checkpoint_parts(), tensors)
+    models.refresh()
+    return st
 
 
 class _SharedTransfer:
@@ -666,9 +675,7 @@ class _SharedTransfer:
         return self._models.transfer.predict(inputs)
 
     def _restore_tensors(self, tensors):
-        st = self._models.training._restore_tensors(tensors)
-        self._models.refresh()
-        return st
+        return _restore_weights_only(self._models, tensors)
 
     def _checkpoint_tensors(self):
         from .tf_checkpoint import parts_tensors

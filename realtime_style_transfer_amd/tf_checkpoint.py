@@ -731,20 +731,58 @@ class Checkpoint:
 
 class CheckpointManager:
     """``tf.train.CheckpointManager`` as tracing/checkpoint.py:22-34 uses it: numbered saves
-    ``<directory>/<checkpoint_name>-<n>``, the ``checkpoint`` state file, at most ``max_to_keep`` kept."""
+    ``<directory>/<checkpoint_name>-<n>``, the ``checkpoint`` state file, at most ``max_to_keep`` kept.
+
+    As TF's: an existing state file in ``directory`` is read at construction (its checkpoints become the managed list,
+    subject to ``max_to_keep``, and ``latest_checkpoint`` names its latest); with ``checkpoint_interval`` (requires
+    ``step_counter``: an int, a callable or an object with ``numpy()``/``value``) ``save(check_interval=True)`` writes
+    only when the step counter has advanced by at least the interval since the last save — the reference's cadence
+    manager (``cadence=10``, train_network.py:70) keeps every 10th epoch, not the last five."""
 
     def __init__(self, checkpoint: Checkpoint, directory, max_to_keep: Optional[int] = 5,
                  checkpoint_name: str = "ckpt", checkpoint_interval=None, step_counter=None):
+        if checkpoint_interval is not None and step_counter is None:
+            raise ValueError("`step_counter` should be passed if `checkpoint_interval` is not None.")
         self.checkpoint, self.directory = checkpoint, Path(directory)
         self.max_to_keep, self.checkpoint_name = max_to_keep, checkpoint_name
+        self.checkpoint_interval, self._step_counter = checkpoint_interval, step_counter
+        self._last_checkpoint_step = None
         self.checkpoints: List[str] = []
         self.directory.mkdir(parents=True, exist_ok=True)
+        self._latest = None
+        state = self.directory / "checkpoint"
+        if state.exists():   # recover the previous run's checkpoints (tf: get_checkpoint_state + _maybe_delete)
+            text = state.read_text()
+            m = re.search(r'^model_checkpoint_path:\s*"([^"]+)"', text, re.M)
+            olds = re.findall(r'^all_model_checkpoint_paths:\s*"([^"]+)"', text, re.M)
+            resolve = lambda q: str(Path(q) if Path(q).is_absolute() else self.directory / q)
+            self.checkpoints = [resolve(q) for q in olds]
+            if m:
+                self._latest = resolve(m.group(1))
+                if self._latest not in self.checkpoints:
+                    self.checkpoints.append(self._latest)
 
     @property
     def latest_checkpoint(self) -> Optional[str]:
-        return self.checkpoints[-1] if self.checkpoints else None
+        return self.checkpoints[-1] if self.checkpoints else self._latest
 
-    def save(self, checkpoint_number=None, check_interval: bool = True) -> str:
+    def _step(self) -> int:
+        c = self._step_counter
+        if callable(c):
+            c = c()
+        if hasattr(c, "numpy"):
+            c = c.numpy()
+        elif hasattr(c, "value") and not isinstance(c, (int, np.integer)):
+            c = c.value() if callable(c.value) else c.value
+        return int(c)
+
+    def save(self, checkpoint_number=None, check_interval: bool = True) -> Optional[str]:
+        if self.checkpoint_interval is not None and check_interval:
+            step = self._step()
+            if self._last_checkpoint_step is not None and (
+                    step == self._last_checkpoint_step or step < self._last_checkpoint_step + self.checkpoint_interval):
+                return None
+            self._last_checkpoint_step = step
         n = int(checkpoint_number) if checkpoint_number is not None else self.checkpoint.save_counter + 1
         prefix = self.directory / f"{self.checkpoint_name}-{n}"
         self.checkpoint.save_counter = n
@@ -754,7 +792,7 @@ class CheckpointManager:
             old = self.checkpoints.pop(0)
             for f in Path(old).parent.glob(Path(old).name + ".*"):
                 f.unlink()
-        names = [Path(c).name for c in self.checkpoints]
+        names = [Path(c).name if Path(c).parent == self.directory else c for c in self.checkpoints]
         (self.directory / "checkpoint").write_text(
             f'model_checkpoint_path: "{names[-1]}"\n' + ''.join(f'all_model_checkpoint_paths: "{n}"\n' for n in names))
         return str(prefix)

@@ -266,6 +266,34 @@ def test_checkpoint_manager_and_save_counter(tmp_path):
     assert int(keys["save_counter" + ck.VAR_SUFFIX]) == 1
 
 
+def test_checkpoint_manager_interval_and_recovery(tmp_path):
+    """the reference's cadence manager (tracing/checkpoint.py:22-27, checkpoint_interval=cadence with the
+    epoch as step_counter; train_network.py:70 cadence=10) keeps every 10th epoch; a new manager over an existing
+    directory recovers its checkpoints (latest_checkpoint, max_to_keep cleanup), as tf.train.CheckpointManager."""
+    a = _HostModel(_inference_layout())
+    step = [0]
+    d = tmp_path / "checkpoints"
+    with pytest.raises(ValueError):
+        ck.CheckpointManager(ck.Checkpoint(a), d, checkpoint_interval=10)
+    mgr = ck.CheckpointManager(ck.Checkpoint(a), d, checkpoint_name="ckpt", max_to_keep=5, checkpoint_interval=10,
+                               step_counter=lambda: step[0])
+    saved = []
+    for epoch in range(35):
+        step[0] = epoch
+        if mgr.save(epoch, check_interval=True) is not None:
+            saved.append(epoch)
+    assert saved == [0, 10, 20, 30]
+    step[0] = 31
+    assert mgr.save(31, check_interval=False).endswith("ckpt-31")   # check_interval=False always writes
+    # a second manager over the same directory: recovers the list and the latest, and cleans up under max_to_keep
+    mgr2 = ck.CheckpointManager(ck.Checkpoint(a), d, checkpoint_name="ckpt", max_to_keep=2)
+    assert mgr2.latest_checkpoint.endswith("ckpt-31")
+    assert ck.latest_checkpoint(d) == mgr2.latest_checkpoint
+    mgr2.save(40)
+    names = sorted(p.name for p in d.iterdir() if p.name.endswith(".index"))
+    assert names == ["ckpt-31.index", "ckpt-40.index"]
+
+
 def test_object_graph_slot_variables():
     """Optimizer slots: <variable>/.OPTIMIZER_SLOT/optimizer/rms keys become slot-variable nodes that the optimizer
     node references (original variable node, slot name, slot node)."""

@@ -200,10 +200,18 @@ def test_training_checkpoint_restore_continues_bitwise(tmp_path):
     assert chk.save_counter == 7
     assert all(np.array_equal(u, v) for u, v in zip(a.training.get_weights(), c.training.get_weights()))
     d = _training_models(33, 32)
-    d.inference.load_weights(mgr.latest_checkpoint).assert_nontrivial_match()
+    st = d.inference.load_weights(mgr.latest_checkpoint)
+    st.assert_nontrivial_match()
     a.refresh()
     assert torch.equal(a.inference(xi), d.inference(xi))
     assert all(np.array_equal(u, v) for u, v in zip(a.training.get_weights(), d.training.get_weights()))
+    # the inference view binds the weights only (TF: the optimizer is not reachable from it) — the
+    # RMSprop state stays at its initial value and the optimizer keys are reported unused
+    assert d.training.iterations == 0
+    assert all(not np.any(s) for s in d.training.optimizer_slots())
+    assert all(not np.any(s) for s in d.training.style_predictor.optimizer_slots())
+    with pytest.raises(AssertionError):
+        st.assert_consumed()
 
 
 def test_failed_step_between_targets_and_gradients_recovers():

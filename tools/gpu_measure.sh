@@ -13,7 +13,8 @@
 #   sq[=frame|train] the SQ counter passes (tools/pmc_sq.sh)              -> sq_<TAG>_<what>_{A,B}/
 #   ab=ENV_A@ENV_B@N alternating headline runs with env A then env B, N pairs ("-" = no env, ':' separates vars)
 #   trainab=ENV_A@ENV_B@N the same for the config-4 training step
-#   x6bench=ARGS     tools/wino_x6_bench ARGS (',' for ' ')               -> x6bench_<TAG>.log
+#   x6bench=ARGS     tools/wino_x6_bench ARGS (',' for ' ')               -> x6bench_<TAG>.log (appended)
+#   x6prof=ARGS      tools/wino_x6_bench_prof ARGS (X6_PROF timeline)     -> x6prof_<TAG>.log
 #   w9bench=ARGS     tools/wino9_x6_bench ARGS                            -> w9bench_<TAG>.log
 #   litebench=ARGS   tools/lite_bench_x6 ARGS                             -> litebench_<TAG>.log
 set -o pipefail
@@ -85,10 +86,13 @@ for step in "$@"; do
                 fi
             done
         done ;;
-    x6bench|w9bench|litebench)
-        case $name in x6bench) b=tools/wino_x6_bench ;; w9bench) b=tools/wino9_x6_bench ;; litebench) b=tools/lite_bench_x6 ;; esac
-        timeout -k 10 300 $b ${arg//,/ } > $O/${name}_$TAG.log 2>&1 || { tail -30 $O/${name}_$TAG.log; exit 1; }
-        tail -15 $O/${name}_$TAG.log ;;
+    x6bench|x6prof|w9bench|w9prof|litebench)
+        case $name in x6bench) b=tools/wino_x6_bench ;; x6prof) b=tools/wino_x6_bench_prof ;; w9bench) b=tools/wino9_x6_bench ;;
+                      w9prof) b=tools/wino9_x6_bench_prof ;; litebench) b=tools/lite_bench_x6 ;; esac
+        # several runs of one tool under one TAG append to its log
+        echo "== $b ${arg//,/ }" >> $O/${name}_$TAG.log
+        timeout -k 10 300 $b ${arg//,/ } >> $O/${name}_$TAG.log 2>&1 || { tail -30 $O/${name}_$TAG.log; exit 1; }
+        tail -6 $O/${name}_$TAG.log ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -119,16 +119,53 @@ int main(int argc, char** argv) {
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         printf("finalize alone: %.2f us/launch\n", ms * 1e3 / 200);
     }
-    cin_word* acc = nullptr;
+    // accumulator modes: the consumer side reads seeded accumulators (acc_in: slot 0 holds the fixed-point limbs of the
+    // input's own per-(image, channel) sums, the others zero), the producer side adds into acc_out (timing only); the f32
+    // kernel's prologue affine is the host restatement of cin_affine_table on the same sums, so the outputs compare
+    cin_word* acc_in = nullptr;
+    cin_word* acc_out = nullptr;
     float* sty = nullptr;
-    if (accm) {   // [8 slots][B][2][CIN_LIMBS][128] fixed-point limbs (kernels.h): S ~ 1e2, Q ~ 2e4 in the 2^-8 limb
-        const size_t n_acc = (size_t)8 * B * 2 * CIN_LIMBS * 128;
-        CK(hipMalloc(&acc, n_acc * sizeof(cin_word)));
+    if (accm) {
+        const size_t n_acc = (size_t)8 * B * 2 * CIN_LIMBS * C;
+        CK(hipMalloc(&acc_out, n_acc * sizeof(cin_word)));
+        CK(hipMemset(acc_out, 0, n_acc * sizeof(cin_word)));
         std::vector<cin_word> ha(n_acc, 0);
-        for (size_t i = 0; i < ha.size(); ++i)
-            if ((i / 128) % CIN_LIMBS == 1) ha[i] = (cin_word)(((i / (128 * CIN_LIMBS)) % 2 ? 2.0e4 : 1.0e2) * 256.0);
-        CK(hipMemcpy(acc, ha.data(), n_acc * sizeof(cin_word), hipMemcpyHostToDevice));
-        sty = dev(host_rand((size_t)B * 2 * C, 0.5f, 1.f, 9));
+        const auto hsty = host_rand((size_t)B * 2 * C, 0.5f, 1.f, 9);
+        sty = dev(hsty);
+        auto split = [](double v, cin_word* l) {   // kernels.h cin_fixed_split
+            const double m = std::fabs(v), h = std::floor(m * 0x1p-32), r = m - h * 0x1p32, q = std::floor(r * 0x1p8);
+            const double r2 = r - q * 0x1p-8;
+            const cin_word k[3] = {(cin_word)std::floor(r2 * 0x1p48), (cin_word)q, (cin_word)h};
+            for (int i = 0; i < 3; ++i) l[i] = v < 0 ? -k[i] : k[i];
+        };
+        for (int b = 0; b < B; ++b)
+            for (int c = 0; c < C; ++c) {
+                double S = 0, Q = 0;
+                for (size_t p = 0; p < (size_t)H * W; ++p) {
+                    const double x = hin[((size_t)b * H * W + p) * C + c];
+                    S += x;
+                    Q += x * x;
+                }
+                cin_word l[3];
+                double v[2];
+                for (int w = 0; w < 2; ++w) {
+                    split(w ? Q : S, l);
+                    for (int i = 0; i < 3; ++i) ha[((size_t)(b * 2 + w) * CIN_LIMBS + i) * C + c] = l[i];   // slot 0
+                    // the value the device merges back (kernels.h cin_fixed_value of one canonical copy)
+                    const double mag = (double)std::llabs(l[2]) * 0x1p32 +
+                                       ((double)std::llabs(l[1]) * 0x1p-8 + (double)std::llabs(l[0]) * 0x1p-48);
+                    v[w] = (w ? Q : S) < 0 ? -mag : mag;
+                }
+                S = v[0];
+                Q = v[1];
+                // the affine as cin_affine_table forms it (from the limbs' exact sums: S, Q truncated at 2^-48)
+                const double N = (double)H * W, mean = S / N, var = std::fmax(Q - S * mean, 0.0) / N;
+                const float rstd = (float)(1.0 / std::sqrt(var + (double)1e-5f)), g = hsty[b * 2 * C + c], be = hsty[b * 2 * C + C + c];
+                hab[((size_t)b * C + c) * 2] = g * rstd;
+                hab[((size_t)b * C + c) * 2 + 1] = be - (float)mean * (g * rstd);
+            }
+        acc_in = dev(ha);
+        CK(hipMemcpy(ab, hab.data(), hab.size() * 4, hipMemcpyHostToDevice));
     }
     const int iters = 200;
     const char* names[2] = {"wino   ", "wino_x6"};
@@ -137,11 +174,11 @@ int main(int argc, char** argv) {
         x.U = v ? U6 : U32; x.out = outs[v]; x.mat = nomat ? nullptr : mats[v]; x.part = parts[v];
         if (v && (accm == 1 || accm == 2)) {
             x.part = nullptr;
-            x.stat.acc = acc;
+            x.stat.acc = acc_out;
             x.stat.nslot = 8;
         }
         if (v && (accm == 1 || accm == 3) && pro != PRO_NONE) {
-            x.pro_stat.acc = acc;
+            x.pro_stat.acc = acc_in;
             x.pro_stat.nslot = 8;
             x.pro_stat.C = C;
             x.pro_stat.batch = B;
@@ -194,7 +231,10 @@ int main(int argc, char** argv) {
     // materialised block input (the same prologue arithmetic in both kernels: bitwise), statistics partials
     const auto m0 = host(mats[0], n_mat), m1 = host(mats[1], n_mat);
     size_t mdiff = 0;
-    for (size_t i = 0; i < n_mat; ++i) mdiff += m0[i] != m1[i];
+    // (accumulator consumer modes: the device forms the affine itself; its last bit may differ from the host's)
+    const bool cons_acc = (accm == 1 || accm == 3) && pro != PRO_NONE;
+    for (size_t i = 0; i < n_mat; ++i)
+        mdiff += cons_acc ? std::fabs(m0[i] - m1[i]) > 2e-6f * std::fmax(1.f, std::fabs(m0[i])) : m0[i] != m1[i];
     const auto p0 = host(parts[0], n_part), p1 = host(parts[1], n_part);
     double ds = 0, dm = 0, sc = 0, mc = 0;
     size_t dn = 0;
@@ -207,8 +247,10 @@ int main(int argc, char** argv) {
     }
     printf("x6 vs f32: materialised input differs in %zu of %zu; partial sums rel %.3e, M2 rel %.3e, counts differ %zu\n",
            mdiff, n_mat, ds / sc, dm / mc, dn);
-    // accumulator modes: the x6 launch reads its prologue affine from the accumulators and writes no partials, so
-    // the comparison with the f32 kernel is not meaningful (timing only)
-    const bool ok = accm != 0 || (md / mx < 1e-5 && bad == 0 && mdiff == 0 && ds / sc < 1e-5 && dm / mc < 1e-5 && dn == 0);
+    // accumulator modes: the outputs compare (the f32 kernel's affine restates the seeded accumulators' one); the
+    // statistics go to acc_out instead of partials (producer modes 1, 2), so the partials are not compared there
+    const bool prod_acc = accm == 1 || accm == 2;
+    const bool ok = md / mx < 1e-5 && bad == 0 && mdiff == 0 && (prod_acc || (ds / sc < 1e-5 && dm / mc < 1e-5 && dn == 0));
+    printf("correctness gate: %s\n", ok ? "pass" : "FAIL");
     return ok ? 0 : 2;
 }
