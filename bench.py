@@ -68,6 +68,7 @@ KERNEL_NAMES = {
     307: "conv_lite<3x3 s2 Cin16 Cout32 split-bf16 x6 32x32x16 MFMA>",
     308: "conv_lite<3x3 s2 transposed Cin32 Cout16 split-bf16 x6 16x16x32 MFMA>",
     203: "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 16x16 N32 split-bf16 x6 MFMA persistent>",
+    205: "wino9f3<9x9 as 9 x F(3x3,3x3) on one tile grid, 24x24 N32 split-bf16 x6 MFMA persistent>",
 }
 
 
@@ -81,8 +82,9 @@ DTYPE_DESC = {
     "bf16x3": "fp32 via 2-piece split bf16 (3 product terms, 16 significant bits per operand), fp32 accumulate, "
               "on the residual convs; other layers fp32 MFMA",
     "bf16": "bf16 operands (8 significant bits), fp32 accumulate, on the residual convs; other layers fp32 MFMA",
-    "winograd_bf16x6": "fp32-level: the residual convs and the 9x9 start conv (nine 3x3 sub-kernels) as fused Winograd "
-                       "F(2x2,3x3) whose transform-domain products are exact 3-piece split-bf16 MFMA terms (each "
+    "winograd_bf16x6": "fp32-level: the residual convs as fused Winograd F(2x2,3x3) and the 9x9 start conv as nine 3x3 "
+                       "sub-kernels on one F(3x3,3x3) tile grid, whose transform-domain products are exact 3-piece "
+                       "split-bf16 MFMA terms (each "
                        "fp32 operand = 3 bf16 pieces holding all 24 significant bits, 6 product terms, dropped "
                        "terms <= 2^-25 of each product, fp32 accumulate); the final 9x9 transposed conv as a GEMM "
                        "over (kx, co) columns and the narrow stride-2 (transposed) convs with the same exact "
@@ -110,6 +112,12 @@ def executed_mfma(model, plan, i: int, B: int):
         return 6 * 2.0 * tiles * 16 * l.cin * l.cout, BF16_MFMA_PEAK_TFLOPS
     if kid == 203:   # 9 sub-kernels x 16 channels + the gathered channel-16 K-step (16 wide), 6 terms
         return 6 * 2.0 * tiles * 16 * (9 * 16 + 16) * l.cout, BF16_MFMA_PEAK_TFLOPS
+    if kid == 205:   # 24x24 blocks of 64 F(3x3) tiles, 25 points: points 0..23 on 32x32x16 K-steps (5 per 8-channel chunk,
+        # one for channel 16), point 24 on 16x16x32 K-steps (3 per chunk, one for channel 16); 6 terms, padded K issued
+        blocks = B * (-(-Ho // 24)) * (-(-Wo // 24))
+        ks = 5 + (5 if l.cin > 8 else 0) + (1 if l.cin > 16 else 0)
+        k24 = 3 + (3 if l.cin > 8 else 0) + (1 if l.cin > 16 else 0)
+        return 6 * 2.0 * blocks * 64 * l.cout * (24 * 16 * ks + 32 * k24), BF16_MFMA_PEAK_TFLOPS
     if kid == 204:   # per output row and 88-column strip: 3 x' tiles of 32, N = 32 columns (27 used), K = 9 x 16
         return 6 * 2.0 * B * Ho * (-(-Wo // 88)) * 3 * 32 * 32 * 144, BF16_MFMA_PEAK_TFLOPS
     if kid in (305, 308):   # 9 (phase, tap) slots x Cin x Cout per input pixel, 6 bf16 terms, tiles of 4 x Cout

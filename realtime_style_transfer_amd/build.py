@@ -21,7 +21,7 @@ OBJ = PKG / "_build"
 SOURCES = ["conv_mfma.hip", "conv_small.hip", "norm.hip", "gram.hip", "loss.hip", "rst_api.hip", "loss_api.hip",
            "train.hip", "train_api.hip", "wgrad.hip",
            "conv_bf3.hip", "predictor.hip", "predictor_api.hip",
-           "predictor_train.hip", "predictor_train_api.hip", "wino.hip", "wino_x6.hip", "wino9.hip", "wino9_x6.hip", "conv_lite.hip", "conv_last.hip", "ingest.hip", "ingest_api.hip", "crc32c.hip"]
+           "predictor_train.hip", "predictor_train_api.hip", "wino.hip", "wino_x6.hip", "wino9.hip", "wino9_x6.hip", "wino9f3.hip", "conv_lite.hip", "conv_last.hip", "ingest.hip", "ingest_api.hip", "crc32c.hip"]
 ARCH = os.environ.get("RST_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", str(ROOT / "include"), "-I", str(CSRC),

@@ -749,22 +749,26 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // accumulators (no finalize ran). One image: the accumulator loads go out first (fill_issue, CinAffineSplit) and
     // are merged after the first tiles' input loads are issued (fill_table), so their wait excludes those loads'
     // latency (vmcnt retires in issue order); more images: cin_affine_table after the input loads
-    const bool split_aff = PRO != PRO_NONE && a.pro_stat.acc != nullptr && a.batch == 1 &&
+    // (not the x6 single-chunk layers, whose weights live in VGPRs: the split form's 24 registers held across the
+    // first input loads took expand_1 from 2 waves per SIMD to 1, 21.2 -> 28.3 us in the frame, profiles/r05)
+    constexpr bool SPLIT_OK = !C::WIN_REGS;
+    const bool split_aff = SPLIT_OK && PRO != PRO_NONE && a.pro_stat.acc != nullptr && a.batch == 1 &&
                            CinAffineSplit<256, 2>::usable(a.pro_stat);
     CinAffineSplit<256, 2> aff;
     auto fill_issue = [&]() __attribute__((always_inline)) {
         if constexpr (PRO != PRO_NONE)
-            if (split_aff) aff.issue(a.pro_stat, 0, BLEND);
+            if constexpr (SPLIT_OK)
+                if (split_aff) aff.issue(a.pro_stat, 0, BLEND);
     };
     auto fill_table = [&]() __attribute__((always_inline)) {
     if constexpr (PRO != PRO_NONE) {
         const CinSrc& ps = a.pro_stat;
         if (ps.acc != nullptr) {
             const bool store = blockIdx.x == 0;   // the host-visible copy (rst_copy_activation)
-            if (split_aff)
+            if (SPLIT_OK && split_aff)
                 aff.finish(ps, tab, BLEND ? tab + CIN : nullptr, store ? ps.ab_out : nullptr, store ? ps.ab1_out : nullptr);
             else
-                cin_affine_table<256>(ps, 0, a.batch, tab, BLEND ? tab + a.batch * CIN : nullptr,
+                cin_affine_table<256, SPLIT_OK ? 8 : 1>(ps, 0, a.batch, tab, BLEND ? tab + a.batch * CIN : nullptr,
                                       store ? ps.ab_out : nullptr, store ? ps.ab1_out : nullptr);
         } else {
             for (int i = tid; i < a.batch * CIN; i += 256) {

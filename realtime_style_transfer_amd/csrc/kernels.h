@@ -278,10 +278,12 @@ __device__ __forceinline__ void cin_affine_pass(const CinSrc& s, int b0, int n, 
 // host-visible copies, same indexing). L lanes per (image, channel) (a power of two, L * nb * C <= NT where
 // possible) each read K / L of the K = nslot (rounded up to a power of two) accumulator copies, all loads
 // issued together with the style-parameter loads, and reduce by DPP / xor shuffles: one memory latency per pass.
-template <int NT>
+template <int NT, int RMAX = 8>
 __device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb, float2* tab, float2* tab1,
                                                  float2* out, float2* out1) {
-    constexpr int RMAX = 8;   // copies per lane (each 2 x CIN_LIMBS words)
+    // RMAX: copies per lane (each 2 x CIN_LIMBS words in flight). Every instantiated pass width is register-allocated
+    // for the whole kernel, so a register-tight caller passes RMAX = 1 (one copy per lane, more lanes per item)
+    static_assert(RMAX == 1 || RMAX == 2 || RMAX == 4 || RMAX == 8, "RMAX");
     int K = 1;
     while (K < s.nslot) K <<= 1;
     const int items = nb * s.C;
@@ -289,11 +291,13 @@ __device__ __forceinline__ void cin_affine_table(const CinSrc& s, int b0, int nb
     // more lanes while one pass still covers every item, up to a quad (the lanes of an item merge by DPP: VALU only)
     while (L < K && L < 4 && 2 * L * items <= NT) L <<= 1;
     const int R = K / L, n = items * L;
-    switch (R) {   // uniform
-        case 1: cin_affine_pass<NT, 1>(s, b0, n, L, tab, tab1, out, out1); break;
-        case 2: cin_affine_pass<NT, 2>(s, b0, n, L, tab, tab1, out, out1); break;
-        case 4: cin_affine_pass<NT, 4>(s, b0, n, L, tab, tab1, out, out1); break;
-        default: cin_affine_pass<NT, RMAX>(s, b0, n, L, tab, tab1, out, out1); break;
+    if (RMAX == 1 || R == 1) cin_affine_pass<NT, 1>(s, b0, n, L, tab, tab1, out, out1);   // R is uniform
+    else if constexpr (RMAX >= 2) {
+        if (R == 2) cin_affine_pass<NT, 2>(s, b0, n, L, tab, tab1, out, out1);
+        else if constexpr (RMAX >= 4) {
+            if (R == 4) cin_affine_pass<NT, 4>(s, b0, n, L, tab, tab1, out, out1);
+            else if constexpr (RMAX >= 8) cin_affine_pass<NT, 8>(s, b0, n, L, tab, tab1, out, out1);
+        }
     }
 }
 
@@ -526,6 +530,13 @@ size_t wino9_x6_weight_floats();
 int wino9_x6_tiles_y(int H);   // 16 x 16-pixel workgroup blocks
 int wino9_x6_tiles_x(int W);
 hipError_t wino9_x6_launch(const Wino9Args& a, hipStream_t st);
+// The same layer for inference as nine 3x3 sub-kernels on Winograd F(3x3, 3x3) tiles sharing one input-transform grid
+// (wino9f3.hip; 24 x 24-pixel blocks, exact split-bf16 x6 products); U = wino9f3_pack_weights.
+std::vector<float> wino9f3_pack_weights(const float* kern, int cin);
+hipError_t wino9f3_prepare();
+int wino9f3_tiles_y(int H);
+int wino9f3_tiles_x(int W);
+hipError_t wino9f3_launch(const Wino9Args& a, hipStream_t st);
 int wino_tiles_y(int H);
 int wino_tiles_x(int W);
 std::vector<float> wino_pack_weights(const float* kern, int cin);

@@ -15,7 +15,7 @@ namespace rst {
 const int CONTRACT_FILTERS[4] = {16, 32, 32, 32};                // styleTransfer.py:218-223
 const int EXPAND_FILTERS[8] = {32, 16, 8, 4, 3, 3, 3, 3};        // styleTransfer.py:247-256
 
-enum LayerKind { K_CONV = 0, K_CONVT2 = 1, K_SMALL = 2, K_WINO = 3, K_WINO9 = 4, K_WINOX6 = 5, K_WINO9X6 = 6, K_LITE = 7, K_LASTX6 = 8 };
+enum LayerKind { K_CONV = 0, K_CONVT2 = 1, K_SMALL = 2, K_WINO = 3, K_WINO9 = 4, K_WINOX6 = 5, K_WINO9X6 = 6, K_LITE = 7, K_LASTX6 = 8, K_WINO9F3 = 9 };
 enum Norm { N_BN = 0, N_CIN = 1 };
 enum Post { P_RELU = 0, P_NONE = 1, P_SIGMOID = 2 };
 
@@ -64,7 +64,7 @@ size_t layer_weight_count(const LayerSpec& s);
 int build_plan(const rst_shape* sh, std::vector<LayerSpec>& L, int* P);
 int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const float* bias, std::vector<float>& packed,
                   std::vector<float>& bias_n, int precision = RST_PRECISION_FP32,
-                  bool allow_lite = false);
+                  bool allow_lite = false, bool inference = false);
 
 template <typename T>
 int upload(T** dst, const void* src, size_t bytes) {

@@ -200,7 +200,7 @@ namespace rst {
 // point at the layer's Keras weights; passing an array of (index + 1) values instead yields the
 // gather map from canonical weights to the packed image (training re-packs after each update).
 int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const float* bias, std::vector<float>& packed,
-                  std::vector<float>& bias_n, int precision, bool allow_lite) {
+                  std::vector<float>& bias_n, int precision, bool allow_lite, bool inference) {
     const size_t kcount = (size_t)s.k * s.k * s.cin * s.cout;
     (void)kcount;
     if (s.keras_kind == 1 && s.k == 9 && s.stride == 1) {
@@ -237,15 +237,18 @@ int prepare_layer(LayerExec& e, const LayerSpec& s, const float* kern, const flo
         // ---- first layer (9x9 conv + ReLU + BN + ReLU) as composite Winograd: f32 MFMA (wino9.hip) or
         // exact split-bf16 MFMA products (wino9_x6.hip)
         const bool x6 = precision == RST_PRECISION_WINOGRAD_BF16X6;
-        e.kind = x6 ? K_WINO9X6 : K_WINO9;
-        packed = x6 ? wino9_x6_pack_weights(kern, s.cin) : wino9_pack_weights(kern, s.cin);
+        // inference: the F(3x3, 3x3) form (wino9f3.hip; RST_START_F3=0 keeps wino9_x6 for A/B runs)
+        static const bool f3_on = [] { const char* v = getenv("RST_START_F3"); return !(v != nullptr && v[0] == '0'); }();
+        const bool f3 = x6 && inference && f3_on;
+        e.kind = f3 ? K_WINO9F3 : x6 ? K_WINO9X6 : K_WINO9;
+        packed = f3 ? wino9f3_pack_weights(kern, s.cin) : x6 ? wino9_x6_pack_weights(kern, s.cin) : wino9_pack_weights(kern, s.cin);
         bias_n.assign(bias, bias + s.cout);
         e.ntot = s.cout;
         e.pad_t = e.pad_l = 4;
         e.gHo = s.Ho;
         e.gWo = s.Wo;
-        e.tiles_y = x6 ? wino9_x6_tiles_y(s.Ho) : wino9_tiles_y(s.Ho);
-        e.tiles_x = x6 ? wino9_x6_tiles_x(s.Wo) : wino9_tiles_x(s.Wo);
+        e.tiles_y = f3 ? wino9f3_tiles_y(s.Ho) : x6 ? wino9_x6_tiles_y(s.Ho) : wino9_tiles_y(s.Ho);
+        e.tiles_x = f3 ? wino9f3_tiles_x(s.Wo) : x6 ? wino9_x6_tiles_x(s.Wo) : wino9_tiles_x(s.Wo);
         e.n_part = 0;
     } else if ((precision == RST_PRECISION_FP32_WINOGRAD && wino_supported(s.k, s.stride, s.cin, s.cout) ||
                 precision == RST_PRECISION_WINOGRAD_BF16X6 && wino_x6_supported(s.k, s.stride, s.cin, s.cout)) &&
@@ -419,7 +422,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         // does not (its layers keep the direct kernel)
         const bool blend_in = shape->num_styles == 2 && li > 0 && specs[li - 1].norm == N_CIN;
         const int lp = (blend_in && precision == RST_PRECISION_FP32_WINOGRAD) ? RST_PRECISION_FP32 : precision;
-        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, shape->max_batch <= LITE_MAX_BATCH)) != RST_OK) {
+        if ((st = prepare_layer(e, s, kern, bias, packed, bias_n, lp, shape->max_batch <= LITE_MAX_BATCH, true)) != RST_OK) {
             delete h;
             return st;
         }
@@ -554,6 +557,7 @@ int rst_create_ex(const rst_shape* shape, const float* weights_host, size_t num_
         hipError_t pe = e.kind == K_WINO      ? wino_prepare()
                         : e.kind == K_WINOX6  ? wino_x6_prepare()
                         : e.kind == K_WINO9X6 ? wino9_x6_prepare()
+                        : e.kind == K_WINO9F3 ? wino9f3_prepare()
                         : e.kind == K_LITE    ? conv_lite_prepare(e.lite)
                                               : conv_prepare(e.tile);
         if (pe != hipSuccess) {
@@ -682,7 +686,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         if (e.pro != PRO_AFF_RELU && e.pro != PRO_NONE)
             return fail(RST_ERR_UNSUPPORTED, "last layer prologue must be CIN+ReLU");
         HIP_TRY(small_conv_launch(a, st));
-    } else if (e.kind == K_WINO9 || e.kind == K_WINO9X6) {
+    } else if (e.kind == K_WINO9 || e.kind == K_WINO9X6 || e.kind == K_WINO9F3) {
         if (e.pro != PRO_NONE) return fail(RST_ERR_UNSUPPORTED, "9x9 Winograd conv reads the network input only");
         Wino9Args a{};
         a.in = in;
@@ -696,14 +700,14 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         a.cin = e.s.cin;
         a.tiles_y = e.tiles_y;
         a.tiles_x = e.tiles_x;
-        if (e.kind == K_WINO9X6 && li == 0 && h->d_acc_all != nullptr) {   // it zeroes the frame's accumulators
+        if ((e.kind == K_WINO9X6 || e.kind == K_WINO9F3) && li == 0 && h->d_acc_all != nullptr) {   // it zeroes the frame's accumulators
             a.zero = h->d_acc_all;
             a.zero_n2 = (long)(h->acc_per_image * B / 2);
         }
-        if (e.kind == K_WINO9X6) next_weights(h, li, &a.w_next, &a.w_next_bytes);
+        if (e.kind == K_WINO9X6 || e.kind == K_WINO9F3) next_weights(h, li, &a.w_next, &a.w_next_bytes);
         if (e.kind == K_WINO9X6 && h->w9_queue) a.queue = h->d_w9_queue;
         a.wt_stores = wt_bits(h, e, B, 4);
-        HIP_TRY(e.kind == K_WINO9X6 ? wino9_x6_launch(a, st) : wino9_launch(a, st));
+        HIP_TRY(e.kind == K_WINO9F3 ? wino9f3_launch(a, st) : e.kind == K_WINO9X6 ? wino9_x6_launch(a, st) : wino9_launch(a, st));
     } else if (e.kind == K_WINO || e.kind == K_WINOX6) {
         WinoArgs a{};
         a.in = in;
@@ -832,7 +836,7 @@ int rst_forward(rst_handle* h, const float* content, const float* style_params, 
         return fail(RST_ERR_INVALID, "rst_forward: num_styles == 2 needs style_weights (B, out_h, out_w, 1)");
     hipStream_t st = static_cast<hipStream_t>(stream);
     // the CIN accumulators start at zero: cleared by the first layer's kernel when that is wino9_x6
-    if (h->d_acc_all != nullptr && h->layers[0].kind != K_WINO9X6)
+    if (h->d_acc_all != nullptr && h->layers[0].kind != K_WINO9X6 && h->layers[0].kind != K_WINO9F3)
         HIP_TRY(hipMemsetAsync(h->d_acc_all, 0, h->acc_per_image * batch * sizeof(cin_word), st));
     for (size_t k = 1; k < h->d_mip.size(); ++k)
         HIP_TRY(avgpool2_1ch_launch(mip_ptr(h, (int)k - 1, style_weights), h->d_mip[k], batch, h->mip_h[k - 1],
@@ -898,6 +902,7 @@ int rst_layer_kernel_id(const rst_handle* h, int idx) {
         case K_WINO9: return 201;
         case K_WINOX6: return 202;
         case K_WINO9X6: return 203;
+        case K_WINO9F3: return 205;
         case K_LITE: return 300 + e.lite.id;   // 305: the x6 expand_0 form
         case K_LASTX6: return 204;
         default: return e.tile.id;

@@ -426,3 +426,83 @@ def test_full_size_bf16_training_step_properties(transfer, joint):
     assert l0 == l1 and np.array_equal(w0, w1) and np.array_equal(p0, p1), "training is not bitwise deterministic"
     assert np.array_equal(q0, q1), "predictor training is not bitwise deterministic"
     assert l0[2] < l0[1] < l0[0], l0
+
+
+def _grad_report(plan, tr, grads, ref, B):
+    """Relative L2 error per trainable transfer tensor (zero-gradient biases before an instance norm and the BN moving
+    statistics reported apart) and per layer output gradient."""
+    layer_of = []
+    for layer in plan.layers:
+        layer_of += [layer] * len(layer.weight_shapes)
+    rows, zero_bias = [], []
+    for i, (g, r) in enumerate(zip(grads, ref['grads'])):
+        layer = layer_of[i]
+        first = sum(len(l.weight_shapes) for l in plan.layers[:plan.layers.index(layer)])
+        kscale = float(np.abs(ref['grads'][first]).max())
+        scale = float(np.linalg.norm(r))
+        # a bias feeding an instance norm through a ReLU that never clips: zero up to round-off, which the float32
+        # oracle leaves at ~1e-7 of the kernel gradient's scale (the float64 small tests: 1e-9)
+        if i == first + 1 and layer.norm == 'cin' and np.abs(r).max() <= 1e-4 * kscale:
+            zero_bias.append((layer.name, float(np.abs(g).max() / kscale), float(np.abs(r).max() / kscale)))
+        elif scale > 0.0:
+            rows.append((f"{layer.name}/{i - first}", float(np.linalg.norm(g - r)) / scale))
+    og = []
+    for li in range(len(plan.layers)):
+        r = ref['output_grads'][li]
+        g = tr.output_gradient(li, B).cpu().numpy()
+        og.append((plan.layers[li].name, float(np.linalg.norm(g - r) / np.linalg.norm(r))))
+    return rows, zero_bias, og
+
+
+@pytest.mark.parametrize("size,precision,transfer", [
+    ("full", "fp32", "winograd_bf16x6"),     # BASELINE config 4's transfer arithmetic at 480x960 (bench.py's trainer)
+    ("quarter", "bf16", "winograd_bf16x6"),  # the bench's bf16 VGG16 line against its bf16 simulation, 128x256
+], ids=["config4_480x960_fp32_vgg", "config4_128x256_bf16_vgg"])
+def test_training_step_at_scale_matches_f32_oracle(size, precision, transfer):
+    """Config 4 (train_network.py:61,102,128-138) past the small parity shapes: one training step of the benchmarked
+    trainer (winograd_bf16x6 transfer convs, its default split-bf16 start-conv weight gradient, style parameters as
+    input) against oracle/torch_train.py run in float32 autograd on the host (the float64 oracle would take minutes at
+    this size; the reference's own arithmetic is float32), max-pool / ReLU routing from the GPU as in the small tests.
+    ``full``: 480x960 (rst-960-120-128-17), B=1, VGG16 in fp32. ``quarter``: 128x256 (bottleneck 32 x 128; VGG16's four pools need multiples of 16), B=1, VGG16
+    in plain bf16 against the oracle's _Bf16Conv / _Bf16Gram simulation of it.
+    Bounds (float32-level GPU vs float32 host, both rounding): prediction max-abs 5e-5, per-image loss terms rel 5e-4,
+    style-parameter gradient and every transfer gradient tensor rel L2 5e-3 (bf16 VGG: 0.05 / loss 5e-3, the
+    small-shape bf16 bounds: bf16 rounding flips between two different float32 forwards)."""
+    _need_gpu()
+    from oracle import torch_train as T
+    if size == "full":
+        from realtime_style_transfer_amd.shape_config import ShapeConfig
+        sc = ShapeConfig.from_spec("rst-960-120-128-17")
+        cfg = dict(input_shape=sc.input_shape['content'], output_shape=sc.output_shape,
+                   bottleneck_res_y=sc.bottleneck_res_y, bottleneck_num_filters=sc.bottleneck_num_filters)
+    else:
+        cfg = dict(input_shape=(128, 256, 17), output_shape=(128, 256, 3), bottleneck_res_y=32,
+                   bottleneck_num_filters=128)
+    B = 1
+    plan, w, vgg, content, sp, gtc, gts = _case(cfg, B, seed=9)
+    tr = _trainer(cfg, w, vgg, B, precision, transfer)
+    c, s, gc, gs = _cuda(content, sp, gtc, gts)
+    pred, losses, grad, gsp = tr.compute_gradients(c, s, gc, gs)
+    torch.cuda.synchronize()
+    pool, relu = _pool_route(tr, B), _relu_route(tr, B)
+    ref = T.training_step(w, vgg, content, sp, gtc, gts, pool_route=pool, relu_route=relu, vgg_bf16=precision == "bf16",
+                          dtype=torch.float32, **cfg)
+    del pool, relu
+    perr = float(np.abs(pred.cpu().numpy() - ref['prediction']).max())
+    lrel = float((np.abs(losses.cpu().numpy() - ref['losses']) / np.abs(ref['losses'])).max())
+    gerr = float(np.linalg.norm(gsp.cpu().numpy() - ref['grad_style_params']) /
+                 np.linalg.norm(ref['grad_style_params']))
+    rows, zero_bias, og = _grad_report(plan, tr, tr._unflatten(grad.cpu().numpy()), ref, B)
+    report = dict(size=size, precision=precision, transfer=transfer, prediction_max_abs=perr, loss_rel=lrel,
+                  style_grad_rel=gerr, grad_rel=rows, zero_bias_rel_to_kernel_scale=zero_bias, output_grad_rel=og)
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f'train_parity_scale_{size}_{precision}_{transfer}.json'), 'w') as f:
+        json.dump(report, f, indent=1, default=float)
+    gtol, ltol, ptol = (0.05, 5e-3, 5e-4) if precision == "bf16" else (5e-3, 5e-4, 5e-5)
+    assert perr < ptol, perr
+    assert lrel < ltol, lrel
+    assert gerr < gtol, gerr
+    bad = [r for r in rows if not r[1] <= gtol]
+    assert not bad, bad
+    # biases feeding an instance norm: mathematically zero gradient, round-off only on both sides
+    assert all(g <= 1e-4 for _, g, _r in zero_bias), zero_bias

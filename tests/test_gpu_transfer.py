@@ -327,7 +327,7 @@ def test_split_bf16_precision_modes(precision, tol):
     assert err < tol, err   # bf16x3: the float64 simulation of the split gives ~2e-5 here; fp32 gives ~2e-6
 
 
-WINO_MODES = {"fp32_winograd": (201, 200), "winograd_bf16x6": (203, 202)}   # (start conv, residual) kernel ids
+WINO_MODES = {"fp32_winograd": (201, 200), "winograd_bf16x6": (205, 202)}   # (start conv, residual) kernel ids
 
 
 @pytest.mark.parametrize("precision", list(WINO_MODES))
@@ -367,6 +367,33 @@ def test_winograd_residual_convs_match_oracle(precision):
         assert len(got) == len(ref_blocks) == 5
         for g, r in zip(got, ref_blocks):
             assert np.abs(g - r).max() / max(1.0, np.abs(r).max()) < 1e-4
+
+
+@pytest.mark.parametrize("cin", [3, 12, 17])
+def test_start_conv_f3_channel_chunks_match_oracle(cin):
+    """wino9f3 (the inference start conv on F(3x3, 3x3) tiles) with 1, 2 and 3 input-channel chunks (cin <= 8: chunk A
+    only; <= 16: A and B; 17: A, B and the channel-16 K-step) at sizes that leave partial 24 x 24 blocks, against the
+    float64 oracle (ReLU -> BN -> ReLU output, 1e-5 of the output range), deterministic."""
+    _need_gpu()
+    from oracle import numpy_ref as R
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    ins, outs, br, bf = (52, 100, cin), (52, 100, 3), 13, 128
+    plan = network_plan(ins, outs, br, bf)
+    w = init_weights(plan, seed=4)
+    sp = synthetic_style_params(2, 1, plan.num_style_params, plan, seed=2)
+    x = np.random.default_rng(7).random((2,) + ins).astype(np.float32)
+    _, inter = R.transfer_forward(x, sp, w, ins, outs, br, bf, return_intermediates=True)
+    r0 = list(inter.values())[0]
+    m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=2, precision="winograd_bf16x6")
+    assert m.layer_kernel_id(0) == 205
+    inp = {'content': torch.from_numpy(x).cuda(), 'style_params': torch.from_numpy(sp).cuda()}
+    m(inp)
+    g0 = m.layer_output(0, 2).cpu().numpy()
+    rel = float(np.abs(g0 - r0).max() / max(1.0, np.abs(r0).max()))
+    assert g0.shape == r0.shape and rel < 1e-5, rel
+    m(inp)
+    assert np.array_equal(g0, m.layer_output(0, 2).cpu().numpy()), "start conv is not deterministic"
 
 
 @pytest.mark.parametrize("precision", list(WINO_MODES))
