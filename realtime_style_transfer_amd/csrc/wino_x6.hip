@@ -99,7 +99,7 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 #ifdef X6_PROF
 // timeline per (workgroup, wave < 8) on the constant 100 MHz clock: 0 start, 8 first loads issued, 4 affine formed,
 // 5 chunk 0 staged, 1 pipeline filled, 2 chunk loop done, 6 epilogue image written, 7 outputs stored, 3 end
-__device__ unsigned long long x6_tl[X6_PROF][8][9];
+__device__ unsigned long long x6_tl[X6_PROF][8][12];
 #define XTL(k) \
     if (blockIdx.x < X6_PROF && lane == 0) x6_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -109,16 +109,19 @@ __device__ unsigned long long x6_tl[X6_PROF][8][9];
 #ifdef X6_PROF
 // timeline summary of the most recent launch (tools/wino_x6_bench)
 void x6_timeline_print(int nwg, int nwave) {
-    std::vector<unsigned long long> tl((size_t)X6_PROF * 72);
+    std::vector<unsigned long long> tl((size_t)X6_PROF * 96);
     if (hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(x6_tl), tl.size() * 8) != hipSuccess) return;
     if (nwg > X6_PROF) nwg = X6_PROF;
     unsigned long long t0 = ~0ull, tend = 0, slast = 0;
     // phases in time order: 0 -> 8 -> 4 -> 5 -> 1 -> 2 -> 6 -> 7 -> 3
     const int ord[9] = {0, 8, 4, 5, 1, 2, 6, 7, 3};
-    double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pre[3] = {0, 0, 0};
     for (int g = 0; g < nwg; ++g)
         for (int w = 0; w < nwave; ++w) {
-            const unsigned long long* q = &tl[((size_t)g * 8 + w) * 9];
+            const unsigned long long* q = &tl[((size_t)g * 8 + w) * 12];
+            pre[0] += (double)(q[9] - q[0]);
+            pre[1] += (double)(q[10] - q[9]);
+            pre[2] += (double)(q[11] - q[10]);
             t0 = q[0] < t0 ? q[0] : t0;
             tend = q[3] > tend ? q[3] : tend;
             slast = q[0] > slast ? q[0] : slast;
@@ -129,6 +132,8 @@ void x6_timeline_print(int nwg, int nwave) {
            "stage0 %.2f, transform0+stage1 %.2f, loop %.2f, epilogue image %.2f, stores %.2f, statistics %.2f\n",
            (tend - t0) * 0.01, (slast - t0) * 0.01, ph[0] / nw, ph[1] / nw, ph[2] / nw, ph[3] / nw, ph[4] / nw,
            ph[5] / nw, ph[6] / nw, ph[7] / nw);
+    printf("  issue split (us): descriptors %.2f, accumulator loads issued %.2f, staging loads issued %.2f\n", pre[0] / nw,
+           pre[1] / nw, pre[2] / nw);
 }
 #endif
 
@@ -164,6 +169,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int li = lane & 31, lh = lane >> 5;
     const int g = wave & 3, h = wave >> 2;   // output channel group, transform-point half
     XTL(0);
+// (Kernel arguments forced into one batch of scalar loads at the start measured neutral in the frame, round 5.)
     int bid = xcd_tile_order(blockIdx.x, gridDim.x);
     const int tx = bid % a.tiles_x;
     bid /= a.tiles_x;
@@ -212,6 +218,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const bool interior = it < XPF4 && inside && iy >= y0 && iy < y0 + XTH && ix >= x0 && ix < x0 + XTW;
         sg_moff[k] = interior ? (int)(((img + (size_t)iy * W + ix) * Cin + 4 * q) * 4) : 0x7F000000;
     }
+    XTL(9);
     const __amdgpu_buffer_rsrc_t msrd = __builtin_amdgcn_make_buffer_rsrc(
         a.mat, 0, a.mat != nullptr ? (int)((size_t)a.batch * H * W * Cin * 4) : 0, 0x00020000);
     f32x4 xr[YST], rr[YST];
@@ -374,8 +381,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     // ---- pipeline fill: V(0) in V[0], patch(1) in patch[1], patch(2) loads and U(0, 0..R-1) in flight ----
     if (split_aff) aff.issue(a.pro_stat, b, BLEND);
+    XTL(10);
     sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload(decltype(K)::value, 0); });
     if (nchunks > 1) sfor<0, YST>([&](auto K) __attribute__((always_inline)) { gload1(decltype(K)::value); });
+    XTL(11);
     sfor<0, YRING>([&](auto X) __attribute__((always_inline)) {
         sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
             load_u1(0, decltype(X)::value, decltype(X)::value, decltype(Pc)::value);
