@@ -34,6 +34,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -135,6 +136,8 @@ void x6_timeline_print(int nwg, int nwave) {
     printf("  issue split (us): descriptors %.2f, accumulator loads issued %.2f, staging loads issued %.2f\n", pre[0] / nw,
            pre[1] / nw, pre[2] / nw);
 }
+// profiling builds of the library only (tools/build_prof_lib.sh): the timeline of the frame's last residual conv
+extern "C" void rst_debug_x6_timeline(int nwg, int nwave) { x6_timeline_print(nwg, nwave); }
 #endif
 
 #ifndef X6W_RING
@@ -154,6 +157,46 @@ constexpr size_t YLDS_BLEND_BYTES = YLDS_BYTES + XMAX_CIN * sizeof(float2);   //
 static_assert(YLDS_BLEND_BYTES <= 160 * 1024, "LDS");
 static_assert(8 % YRING == 0, "ring must divide the points per wave");
 
+// Input prefetch by the workgroups past the tiles (wino_x6_launch adds them at B = 1, where 225 tiles leave 31 of the 256
+// CUs idle). In the chunk loop the staging loads of chunk c + 3 and the U ring's L2 loads share the in-order vmcnt
+// counter, so the U loads issued after a staging load wait out its HBM latency when they are consumed two points later.
+// With the input already in the XCD's L2 that wait is an L2 latency. A prefetch workgroup with blockIdx % 8 = r (one XCD
+// under the round-robin dispatch, speed only) reads one dword of every 128-B line of the input patches of the tiles
+// xcd_tile_order gives the compute workgroups of residue r (and of the residual source), chunk pairs 1.. in order
+// (chunks 0 and 1 the compute workgroups load at their start), split over the prefetch workgroups of residue r.
+__device__ __forceinline__ unsigned x6_prefetch_input(const WinoArgs& a, int n_units, bool res) {
+    const int r = (int)(blockIdx.x & 7);
+    const int nk = (n_units - r + 7) >> 3;   // compute workgroups (tiles) of residue r
+    if (nk <= 0) return 0u;
+    const int base = n_units >> 3, rem = n_units & 7;
+    const int t0 = r * base + min(r, rem);   // xcd_tile_order: their tiles are t0 .. t0 + nk - 1
+    const int first = n_units + ((r - (n_units & 7)) & 7);   // first prefetch workgroup of residue r
+    const int np = ((int)gridDim.x - first + 7) >> 3, j = ((int)blockIdx.x - first) >> 3;
+    const int nq = a.cin >> 5;               // 128-B lines (32 channels) per pixel
+    if (np <= 0 || nq < 2) return 0u;
+    const int H = a.H, W = a.W;
+    const int per_line = nk * XNP;           // lines of one chunk pair over the XCD's tiles
+    const int n_items = (nq - 1) * per_line;
+    const __amdgpu_buffer_rsrc_t isrd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.in), 0, (int)((size_t)a.batch * H * W * a.cin * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(res ? a.res : a.in), 0, (int)((size_t)a.batch * H * W * a.cin * 4), 0x00020000);
+    unsigned f = 0u;
+    for (int it = j * YT + (int)threadIdx.x; it < n_items; it += np * YT) {
+        const int q = 1 + it / per_line, rr = it - (q - 1) * per_line;
+        const int tl = rr / XNP, px = rr - tl * XNP;
+        int t = t0 + tl;
+        const int tx = t % a.tiles_x;
+        t /= a.tiles_x;
+        const int ty = t % a.tiles_y, b = t / a.tiles_y;
+        const int iy = min(max(ty * XTH - 1 + px / XPW, 0), H - 1), ix = min(max(tx * XTW - 1 + px % XPW, 0), W - 1);
+        const int off = (int)((((size_t)b * H + iy) * W + ix) * a.cin * 4) + q * 128;
+        f ^= __builtin_amdgcn_raw_buffer_load_b32(isrd, off, 0, 0);
+        if (res) f ^= __builtin_amdgcn_raw_buffer_load_b32(rsrd, off, 0, 0);
+    }
+    return f;   // (l2_touch_keep keeps the loads)
+}
+
 // BLEND: two styles — the prologue blends the two CIN affines per pixel (pro_ab1, pro_w)
 template <int PRO, bool BLEND = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void wino_x6_kernel(WinoArgs a) {
@@ -169,8 +212,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int li = lane & 31, lh = lane >> 5;
     const int g = wave & 3, h = wave >> 2;   // output channel group, transform-point half
     XTL(0);
-// (Kernel arguments forced into one batch of scalar loads at the start measured neutral in the frame, round 5.)
-    int bid = xcd_tile_order(blockIdx.x, gridDim.x);
+    const int n_units = a.batch * a.tiles_y * a.tiles_x;
+    if ((int)blockIdx.x >= n_units) {   // a CU the tiles leave idle (B = 1): this XCD's later input chunks into its L2
+        const unsigned f = x6_prefetch_input(a, n_units, PRO == PRO_AFF_RES);
+        const l2_touch_t u = l2_touch_xcd_slice<YT, 2>(a.u_next, a.u_next_bytes);
+        l2_touch_keep(l2_touch_t{f ^ u.x, u.y}, a.batch < 0, smem);
+        return;
+    }
+    int bid = xcd_tile_order(blockIdx.x, n_units);
     const int tx = bid % a.tiles_x;
     bid /= a.tiles_x;
     const int ty = bid % a.tiles_y;
@@ -772,7 +821,18 @@ hipError_t wino_x6_launch(const WinoArgs& a, hipStream_t st) {
     if (src_acc && (a.pro_stat.nslot < 1 || a.pro_stat.nslot > 8 || a.pro_stat.C != a.cin || a.cin > XN ||
                     a.pro_stat.batch != a.batch || a.pro_stat.style == nullptr || a.pro_mode == PRO_NONE))
         return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
+    unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
+    {   // B = 1: the CUs the tiles leave idle prefetch the later input chunks into their XCD's L2 (x6_prefetch_input)
+        static int n_cu = 0, pf = -1;
+        if (pf < 0) {
+            const char* e = getenv("RST_X6_PREFETCH");
+            pf = e != nullptr ? atoi(e) : 1;
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                n_cu = 0;
+        }
+        if (pf && a.cin >= 64 && (int)grid < n_cu && (int)grid + 8 <= n_cu) grid = (unsigned)n_cu;
+    }
     if (a.pro_w != nullptr) {   // two styles: the affines from pro_ab/pro_ab1, or both formed from pro_stat
         if (src_acc ? a.pro_stat.style1_offset < 0 : (a.pro_ab1 == nullptr || a.pro_ab == nullptr))
             return hipErrorInvalidValue;
