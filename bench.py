@@ -518,7 +518,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-budget-s", type=float, default=20.0, help="bounded CPU-baseline sample (seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="headline from eager launches instead of hipGraph replay")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "traffic_r05.json"),
+                    help="per-launch HBM bytes of the dominant kernel (tools/pmc_traffic.py on this build's FETCH/WRITE passes)")
     ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--train-modes", default="bf16,bf16x3,bf16x6,fp32",
