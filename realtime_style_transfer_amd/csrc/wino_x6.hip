@@ -459,9 +459,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     lds_barrier();
 
     XTL(1);
-#ifdef X6_SETPRIO
-    if (h == 1) __builtin_amdgcn_s_setprio(1);   // experiment: static priority for the second-dispatched half
-#endif
     const int varow = li * XVROW + 16 * (lh ^ ((li >> 3) & 1)) + 8 * h * 32 * XVROW;
     unsigned qa0 = 0, qa1 = 0, qb0 = 0, qb1 = 0;
     f32x4 sp01 = f32x4{0.f, 0.f, 0.f, 0.f}, sp23 = sp01, sv = sp01;
