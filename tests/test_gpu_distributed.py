@@ -6,6 +6,8 @@ needs one GPU per rank; the driver's 8-GPU run exercises RCCL itself).
   and the BatchNorm moving statistics averaged — and the averaged moving mean equals the mean of the
   per-rank updates (TF MirroredStrategy's MEAN aggregation);
 * `bench.py --gpus 2` end to end (real kernels) prints one line with n_gpus 2.
+* RCCL itself with one rank (`test_rccl_step_exchange_one_rank`): the step exchange's all-reduce on the
+  "nccl" backend leaves bucket and weights bitwise unchanged; a 6 MB SUM of a known pattern is exact.
 """
 import json
 import os
@@ -120,3 +122,69 @@ def test_bench_two_ranks_on_one_gpu():
     tr = line["training"]                           # config 5's training side: both ranks, one all-reduce per step
     assert tr["batch_per_gpu"] == 2 and tr["ms_per_step"] > 0 and np.isfinite(tr["last_loss_mean"])
     assert tr["frames_per_s"] > 0 and "one all-reduce per step" in tr["workload"]
+
+
+def _rccl_worker(rank, world, port, tmp):
+    import time
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    try:
+        import realtime_style_transfer_amd.styleTransferTrainingModel as stm
+        from realtime_style_transfer_amd.plan import init_weights, network_plan
+        from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG, init_vgg16_weights
+        ins, outs, br, bf = (32, 64, 17), (32, 64, 3), 8, 8
+        plan = network_plan(ins, outs, br, bf)
+        lm = StyleLossModelVGG(outs, weights=init_vgg16_weights(seed=3), max_batch=2)
+        tr = stm.StyleTransferTrainingModel(ins, outs, br, bf, loss_model=lm, weights=init_weights(plan, seed=2),
+                                            max_batch=2)
+        rng = np.random.default_rng(7)
+        x = {'content': torch.from_numpy(rng.random((2,) + ins, dtype=np.float32)).cuda(),
+             'style_params': torch.from_numpy(rng.random((2, plan.num_style_params), dtype=np.float32)).cuda()}
+        y = {'content': torch.from_numpy(rng.random((2,) + outs, dtype=np.float32)).cuda(),
+             'style': torch.from_numpy(rng.random((2, 1) + outs, dtype=np.float32)).cuda()}
+        tr.train_step(x, y)
+        torch.cuda.synchronize()
+        w_before = np.concatenate([a.reshape(-1) for a in tr.get_weights()])
+        # the step exchange's collective, run on RCCL in HBM: [gradients | moving statistics] SUM over one rank,
+        # the statistics divided by the world size and written back into the weights
+        tr._get_moving_statistics()
+        before = tr._bucket.clone()
+        stm._all_reduce_sum(tr._bucket, tr.process_group)
+        tr._set_moving_statistics(dist.get_world_size())
+        torch.cuda.synchronize()
+        w_after = np.concatenate([a.reshape(-1) for a in tr.get_weights()])
+        # a full-size bucket (rst-960-120-128-17's ~5.9 MB gradient): SUM of a known pattern, timed
+        big = torch.arange(1_500_000, dtype=torch.float32, device="cuda") * 0.5
+        ref = big.clone()
+        for _ in range(3):
+            dist.all_reduce(big, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            dist.all_reduce(big, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / 20 * 1e3
+        np.save(os.path.join(tmp, "rccl.npy"), np.array([
+            float(torch.equal(before, tr._bucket)), float(np.array_equal(w_before, w_after)),
+            float(torch.equal(big, ref)), ms]))
+        with open(os.path.join(tmp, "backend.txt"), "w") as f:
+            f.write(dist.get_backend())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_step_exchange_one_rank(tmp_path):
+    """BASELINE config 5's collective on RCCL (backend "nccl" on ROCm) — the one GPU of this box holds one rank, so
+    the SUM is an identity: the step exchange's bucket and the weights it writes back come out bitwise unchanged,
+    and a 6 MB all-reduce of a known pattern is exact. The 8-GPU curve is the driver's run."""
+    _need_gpu()
+    import torch.multiprocessing as mp
+    from realtime_style_transfer_amd.frames import free_port
+    mp.spawn(_rccl_worker, args=(1, free_port(), str(tmp_path)), nprocs=1, join=True)
+    assert (tmp_path / "backend.txt").read_text() == "nccl"
+    same_bucket, same_w, exact, ms = np.load(tmp_path / "rccl.npy")
+    assert same_bucket == 1.0 and same_w == 1.0 and exact == 1.0
+    print(f"RCCL all-reduce of 6 MB, one rank: {ms:.3f} ms")
