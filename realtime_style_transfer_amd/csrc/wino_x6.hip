@@ -93,16 +93,25 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 
 // Experiment knobs (tools/wino_x6_bench only; never set in the library build): X6_SKIP bit0 = no U reloads
 // in the loop, bit1 = no transform of the next chunk, bit2 = no staging / patch loads in the loop, bit3 = no
-// barrier at the end of a chunk (results wrong: timing only).
+// barrier at the end of a chunk, bit4 = no materialised block output stores (results wrong: timing only).
 #ifndef X6_SKIP
 #define X6_SKIP 0
+#endif
+// In the chunk loop a store issued before a U load makes that load's vmcnt wait include the store (vmcnt retires in
+// order): X6_MAT_LATE issues a chunk's materialised-output stores after the chunk's last U and staging loads.
+#ifndef X6_MAT_LATE
+#define X6_MAT_LATE 1
 #endif
 #ifdef X6_PROF
 // timeline per (workgroup, wave < 8) on the constant 100 MHz clock: 0 start, 8 first loads issued, 4 affine formed,
 // 5 chunk 0 staged, 1 pipeline filled, 2 chunk loop done, 6 epilogue image written, 7 outputs stored, 3 end
 __device__ unsigned long long x6_tl[X6_PROF][8][12];
+#ifndef X6_PROF_PRO
+#define X6_PROF_PRO -1   // -1: every launch stamps; else only the launches of that prologue form
+#endif
 #define XTL(k) \
-    if (blockIdx.x < X6_PROF && lane == 0) x6_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
+    if ((X6_PROF_PRO < 0 || PRO == X6_PROF_PRO) && blockIdx.x < X6_PROF && lane == 0) \
+        x6_tl[blockIdx.x][wave][(k)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define XTL(k)
 #endif
@@ -291,8 +300,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         xr1[k] = *reinterpret_cast<const f32x4*>(a.in + gi);
         if constexpr (pro == PRO_AFF_RES) rr1[k] = *reinterpret_cast<const f32x4*>(res_src + gi);
     };
-    // prologue of the staged value (affine [+ ReLU | + residual]) and the materialised block output
-    auto stage_math = [&](int k, int chunk, f32x4 p01, f32x4 p23) __attribute__((always_inline)) {
+    // the materialised block output of staging item k of a chunk
+    auto mat_store = [&](int k, int chunk, f32x4 v) __attribute__((always_inline)) {
+        if (!(X6_SKIP & 16) && a.mat != nullptr) {
+            if (a.wt_stores & 2)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd, sg_moff[k] + chunk * XCK * 4, 0, 16);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd, sg_moff[k] + chunk * XCK * 4, 0, 0);
+        }
+    };
+    // prologue of the staged value (affine [+ ReLU | + residual]) and (store) the materialised block output
+    auto stage_math = [&](int k, int chunk, f32x4 p01, f32x4 p23, bool store = true) __attribute__((always_inline)) {
         f32x4 v = xr[k];
         if constexpr (pro != PRO_NONE) {
             const f32x4 r = rr[k];
@@ -310,14 +328,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 v.z = pro_apply(pro, v.z, float2{p23.x, p23.y}, r.z);
                 v.w = pro_apply(pro, v.w, float2{p23.z, p23.w}, r.w);
             }
-            if (a.mat != nullptr) {
-                if (a.wt_stores & 2)
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd,
-                                                           sg_moff[k] + chunk * XCK * 4, 0, 16);
-                else
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd,
-                                                           sg_moff[k] + chunk * XCK * 4, 0, 0);
-            }
+            if (store) mat_store(k, chunk, v);
         }
         return v;
     };
@@ -461,7 +472,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     XTL(1);
     const int varow = li * XVROW + 16 * (lh ^ ((li >> 3) & 1)) + 8 * h * 32 * XVROW;
     unsigned qa0 = 0, qa1 = 0, qb0 = 0, qb1 = 0;
-    f32x4 sp01 = f32x4{0.f, 0.f, 0.f, 0.f}, sp23 = sp01, sv = sp01;
+    f32x4 sp01 = f32x4{0.f, 0.f, 0.f, 0.f}, sp23 = sp01, sv = sp01, sv0 = sp01;
+    static_assert(YST == 2, "the late materialised stores hold the chunk's two staging items");
 
     for (int c = 0; c < nchunks; ++c) {
         const int P = c & 1;
@@ -516,9 +528,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                         sp01 = *reinterpret_cast<const f32x4*>(pab + c2 * XCK + cq4);
                         sp23 = *reinterpret_cast<const f32x4*>(pab + c2 * XCK + cq4 + 2);
                     }
-                    if constexpr (k == 2) sv = stage_math(ks, c2, sp01, sp23);
+                    if constexpr (k == 2) sv = stage_math(ks, c2, sp01, sp23, !X6_MAT_LATE);
                     if constexpr (k == 4) stage_write(ks, pstage, sv);
+                    if constexpr (X6_MAT_LATE && k == 4 && ks == 0) sv0 = sv;
                     if constexpr (k == 5) gload(ks, c3);
+                    // X6_MAT_LATE: the chunk's materialised stores after all of its U and staging loads (below)
+                    if constexpr (X6_MAT_LATE && pro != PRO_NONE && k == 5 && ks == YST - 1) {
+                        mat_store(0, c2, sv0);
+                        mat_store(1, c2, sv);
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
             });

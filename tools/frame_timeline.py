@@ -34,5 +34,5 @@ for _ in range(n):
     g.replay()
 torch.cuda.synchronize()
 lib = ctypes.CDLL(os.environ["RST_LIB"])
-print(f"frame's last wino_x6 launch after {n} graph replays:", flush=True)
+print(f"frame's last wino_x6 launch (of the profiled prologue form) after {n} graph replays:", flush=True)
 lib.rst_debug_x6_timeline(225, 8)
