@@ -205,6 +205,13 @@ int rst_trainer_compute_targets(rst_trainer* t, const float* gt_content, const f
 /* Drop pending targets (the caller's step failed between compute_targets and compute_gradients): joins the side
  * stream into `stream`. No-op when none are pending. */
 int rst_trainer_cancel_targets(rst_trainer* t, void* stream);
+// Makes `stream` wait until grad_style_params of the most recent rst_trainer_compute_gradients is final — recorded
+// after the backward's last conditional-instance-norm layer, before the contract layers' backward and the start
+// conv's weight gradient — so the style predictor's backward (rst_predictor_trainer_backward) can run on `stream`
+// beside the rest of the transfer network's backward. The caller joins `stream` back before using either gradient.
+// Replaces the serial predictor backward after compute_gradients (reference: train_network.py:102 fits predictor and
+// transfer network in one tape, styleTransferTrainingModel.py:26-33).
+int rst_trainer_wait_style_gradient(rst_trainer* t, void* stream);
 /* RMSprop on the device-resident weights with gradient grad (num_weights), then re-pack them
  * into the kernels' weight images. Keras defaults: lr 1e-3, rho 0.9, epsilon 1e-7. */
 int rst_trainer_apply_gradients(rst_trainer* t, const float* grad, float learning_rate, float rho, float epsilon,

@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = [
     "rst_trainer_create", "rst_trainer_create_ex", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
     "rst_trainer_compute_gradients", "rst_trainer_compute_targets", "rst_trainer_apply_gradients",
     "rst_trainer_copy_weights",
-    "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_set_slots", "rst_trainer_cancel_targets",
+    "rst_trainer_copy_slots", "rst_trainer_set_weights", "rst_trainer_set_slots", "rst_trainer_cancel_targets", "rst_trainer_wait_style_gradient",
     "rst_trainer_copy_output_gradient",
     "rst_trainer_debug_vgg_gradient", "rst_trainer_loss", "rst_trainer_num_moving_statistics",
     "rst_trainer_get_moving_statistics", "rst_trainer_set_moving_statistics",
@@ -174,6 +174,8 @@ def load() -> ctypes.CDLL:
     lib.rst_trainer_apply_gradients.restype = i
     lib.rst_trainer_cancel_targets.argtypes = [vp, vp]
     lib.rst_trainer_cancel_targets.restype = i
+    lib.rst_trainer_wait_style_gradient.argtypes = [vp, vp]
+    lib.rst_trainer_wait_style_gradient.restype = i
     for name in ("rst_trainer_copy_weights", "rst_trainer_copy_slots", "rst_trainer_set_weights",
                  "rst_trainer_set_slots"):
         getattr(lib, name).argtypes = [vp, vp, sz, vp]

@@ -164,6 +164,11 @@ struct rst_trainer {
     // forward: fork after the caller's stream, join before the prediction's VGG16 pass (same VGG16 buffers)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // recorded in backward() right after the last CIN layer's norm backward: from there on grad_style_params is final
+    // and the rest of the backward (the contract layers, the start conv's weight gradient) no longer touches it, so the
+    // style predictor's backward can run beside it (rst_trainer_wait_style_gradient)
+    hipEvent_t ev_gstyle = nullptr;
+    bool gstyle_recorded = false;
     bool targets_pending = false;
     bool serial_targets = false;  // RST_SERIAL_TARGETS=1 at creation: targets on the caller's stream (A/B runs)
     int wt_stores = 5;            // RST_TRAIN_WT at creation: bit0 Winograd conv outputs, bit1 the residual convs'
@@ -179,6 +184,7 @@ struct rst_trainer {
         }
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
+        if (ev_gstyle) (void)hipEventDestroy(ev_gstyle);
         if (loss) rst_loss_destroy(loss);
         for (void* p : allocs) (void)hipFree(p);
     }
@@ -468,6 +474,10 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
 // ---- transfer-network backward ------------------------------------------------------------
 int backward(rst_trainer* t, const float* content, int B, float* grad, float* gstyle, hipStream_t st) {
     const int n = (int)t->L.size();
+    int first_cin = -1;   // the last CIN layer the backward reaches
+    for (int li = n - 1; li >= 0; --li)
+        if (t->L[li].e.s.norm == N_CIN) first_cin = li;
+    if (first_cin < 0) RST_HIP_TRY(hipEventRecord(t->ev_gstyle, st));
     for (int li = n - 1; li >= 0; --li) {
         TLayer& T = t->L[li];
         const LayerExec& e = T.e;
@@ -499,6 +509,7 @@ int backward(rst_trainer* t, const float* content, int B, float* grad, float* gs
         nb.conv_relu = s.conv_relu ? 1 : 0;
         nb.dconv_bias = grad + T.boff;
         RST_HIP_TRY(norm_bwd_launch(nb, st));
+        if (li == first_cin) RST_HIP_TRY(hipEventRecord(t->ev_gstyle, st));   // grad_style_params final
         WgradArgs w = wgrad_geometry(s, e, B);
         w.X = li == 0 ? content : T.d_x;
         w.D = t->d_dz;
@@ -598,7 +609,8 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
     rst_trainer* t = new rst_trainer();
     if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_gstyle, hipEventDisableTiming) != hipSuccess)
         return fail_delete(t, set_error(RST_ERR_HIP, "rst_trainer_create_ex: stream / event creation failed"));
     {
         const char* ser = getenv("RST_SERIAL_TARGETS");
@@ -915,7 +927,18 @@ int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const fl
     RST_HIP_TRY(hipMemsetAsync(grad, 0, t->nw * 4, st));
     float* gs = grad_style_params ? grad_style_params : t->d_gstyle;
     RST_HIP_TRY(hipMemsetAsync(gs, 0, (size_t)B * t->P * 4, st));
-    return backward(t, content, B, grad, gs, st);
+    t->gstyle_recorded = false;
+    if ((r = backward(t, content, B, grad, gs, st)) != RST_OK) return r;
+    t->gstyle_recorded = true;
+    return RST_OK;
+}
+
+int rst_trainer_wait_style_gradient(rst_trainer* t, void* stream) {
+    if (!t) return set_error(RST_ERR_INVALID, "rst_trainer_wait_style_gradient: null handle");
+    if (!t->gstyle_recorded)
+        return set_error(RST_ERR_INVALID, "rst_trainer_wait_style_gradient: no completed rst_trainer_compute_gradients");
+    RST_HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), t->ev_gstyle, 0));
+    return RST_OK;
 }
 
 int rst_trainer_apply_gradients(rst_trainer* t, const float* grad, float learning_rate, float rho, float epsilon,

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -129,6 +130,9 @@ class StyleTransferTrainingModel:
         self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
         self.optimizer = optimizer or RMSprop()
         self.process_group = process_group
+        # the style predictor's backward beside the transfer network's tail of the backward (_predictor_backward)
+        self._overlap_pbwd = os.environ.get("RST_SERIAL_PREDICTOR_BWD", "0") != "1"
+        self._pbwd_stream = None
         self.loss_model = loss_model or StyleLossModelVGG(self.output_shape, max_batch=self.max_batch,
                                                           device=self.device)
         if tuple(self.loss_model.input_shape) != self.output_shape:
@@ -533,6 +537,25 @@ class StyleTransferTrainingModel:
     def reset_metrics(self):
         self.style_losses = {}
 
+    def _predictor_backward(self, pr, gsp: torch.Tensor):
+        """The style predictor's backward from d loss / d style_params. On the GPU it runs on a side stream that starts
+        where the transfer network's backward has made gsp final (after its last conditional instance norm,
+        rst_trainer_wait_style_gradient) and so overlaps the rest of that backward — the contract layers and the start
+        conv's weight gradient — instead of following it; the caller's stream joins it before either gradient is used.
+        Same kernels on the same inputs: the gradients are bitwise those of the serial order (RST_SERIAL_PREDICTOR_BWD=1)."""
+        if not (gsp.is_cuda and getattr(self, "_overlap_pbwd", True)):
+            pr.backward(gsp, grad=self._pgrad)
+            return
+        main = torch.cuda.current_stream(gsp.device)
+        if getattr(self, "_pbwd_stream", None) is None:
+            self._pbwd_stream = torch.cuda.Stream(device=gsp.device)
+        side = self._pbwd_stream
+        _lib.check(_lib.load().rst_trainer_wait_style_gradient(self._handle, _lib.stream_ptr(side)))
+        gsp.record_stream(side)       # the allocator must not hand gsp's memory to the caller's stream before the join
+        with torch.cuda.stream(side):
+            pr.backward(gsp, grad=self._pgrad)
+        main.wait_stream(side)
+
     def train_step(self, x: Dict[str, torch.Tensor], y: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         """One Keras fit step. With a style predictor: x = {'content', 'style' (B,1,H,W,3)}; without:
         x = {'content', 'style_params'}. y = {'content', 'style'}."""
@@ -554,7 +577,7 @@ class StyleTransferTrainingModel:
             sp = x['style_params']
         pred, losses, grad, gsp = self.compute_gradients(x['content'], sp, y['content'], y['style'])
         if pr is not None:
-            pr.backward(gsp, grad=self._pgrad)
+            self._predictor_backward(pr, gsp)
         self.exchange()                       # one collective: gradients + BN moving statistics
         self.apply_gradients(grad)
         if pr is not None:

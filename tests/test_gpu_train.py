@@ -345,6 +345,43 @@ def test_joint_training_with_style_predictor_matches_oracle():
                    'grad_style_params_rel': gerr, 'predictor_grad_worst_rel': worst}, f, indent=1)
 
 
+def test_predictor_backward_beside_the_transfer_backward_is_bitwise_serial():
+    """train_step runs the style predictor's backward on a side stream from the point where the transfer network's
+    backward has made d loss / d style_params final (rst_trainer_wait_style_gradient, after its last conditional
+    instance norm), beside the contract layers' backward: two joint steps give bitwise the weights (both networks)
+    and losses of the serial order."""
+    _need_gpu()
+    from realtime_style_transfer_amd.stylePrediction import (StylePredictionTrainer, init_predictor_weights,
+                                                             predictor_weight_spec)
+    from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
+    cfg = CONFIGS['B']
+    B = 2
+    plan, w, vgg, content, _, gtc, gts = _case(cfg, B)
+    P = plan.num_style_params
+    sins = cfg['output_shape']
+    pw = init_predictor_weights(predictor_weight_spec(sins, 'MOBILE_NET', P), seed=3, perturb=True)
+    style = np.random.default_rng(12).random((B, 1) + sins).astype(np.float32)
+    c, gc, gs, st = _cuda(content, gtc, gts, style)
+    from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
+    runs = []
+    for overlap in (False, True):
+        lm = StyleLossModelVGG(cfg['output_shape'], weights=vgg, max_batch=B)
+        pr = StylePredictionTrainer(sins, 'MOBILE_NET', P, weights=pw, max_batch=B)
+        tr = StyleTransferTrainingModel(cfg['input_shape'], cfg['output_shape'], cfg['bottleneck_res_y'],
+                                        cfg['bottleneck_num_filters'], loss_model=lm, weights=w, max_batch=B,
+                                        style_predictor=pr)
+        tr._overlap_pbwd = overlap
+        losses = []
+        for _ in range(2):
+            tr.train_step({'content': c, 'style': st}, {'content': gc, 'style': gs})
+            losses.append(tr.style_losses['loss'].cpu().numpy())
+        torch.cuda.synchronize()
+        runs.append((np.concatenate([x.reshape(-1) for x in tr.get_weights()]),
+                     np.concatenate([x.reshape(-1) for x in pr.get_weights()]), np.stack(losses)))
+    for a, b in zip(runs[0], runs[1]):
+        assert np.array_equal(a, b)
+
+
 def test_training_model_reference_geometry_with_dummy_predictor():
     """styleTransferTrainingModelTest.py:15-58: 240x480x3 -> 480x960x3, bottleneck 30 rows x 4 filters,
     DUMMY predictor, a fit over two zero samples in one batch of 2 (the VGG loss stands in for
