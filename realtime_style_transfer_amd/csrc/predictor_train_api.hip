@@ -11,6 +11,7 @@
 // In training mode every BatchNormalization normalises with the batch statistics over (B, H, W)
 // and updates its moving statistics (Keras mobilenet_v3: momentum 0.999, eps 1e-3).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <algorithm>
 #include <cmath>
@@ -50,7 +51,14 @@ struct rst_predictor_trainer {
     float* feat_part = nullptr;
     int feat_nparts = 0;
     float *gap = nullptr, *hidden = nullptr, *dhid = nullptr, *dfeat = nullptr;
-    float* dz = nullptr;                    // norm-backward output (largest unit)
+    float* dz = nullptr;                    // norm-backward output (largest unit); ring slot 0
+    // the weight gradients (and the SE / head outer products) run on `wside` beside the input-gradient chain; the
+    // norm-backward outputs go round a ring of DZR buffers, each released by the weight gradient that reads it
+    static constexpr int DZR = 3;
+    float* dzr[DZR] = {};
+    hipStream_t wside = nullptr;
+    hipEvent_t ev_dz[DZR] = {}, ev_wg[DZR] = {}, ev_chain = nullptr, ev_done = nullptr;
+    bool serial_wgrad = false;              // RST_SERIAL_PREDICTOR_WGRAD=1 at creation: everything on the caller's stream
     float4* bn_part = nullptr;
     float2* consts = nullptr;
     float* slab = nullptr;
@@ -59,6 +67,16 @@ struct rst_predictor_trainer {
     size_t n_stat = 0;
     std::vector<void*> allocs;
     ~rst_predictor_trainer() {
+        if (wside) {
+            (void)hipStreamSynchronize(wside);
+            (void)hipStreamDestroy(wside);
+        }
+        for (int k = 0; k < DZR; ++k) {
+            if (ev_dz[k]) (void)hipEventDestroy(ev_dz[k]);
+            if (ev_wg[k]) (void)hipEventDestroy(ev_wg[k]);
+        }
+        if (ev_chain) (void)hipEventDestroy(ev_chain);
+        if (ev_done) (void)hipEventDestroy(ev_done);
         for (void* p : allocs) (void)hipFree(p);
     }
     template <typename T>
@@ -212,6 +230,22 @@ int rst_predictor_trainer_create(const rst_predictor_shape* shape, const float* 
     TRY(t->alloc(&t->consts, 1024 * 8));
     TRY(t->alloc(&t->slab, std::max<size_t>(max_slab, 1) * 4));
     TRY(t->alloc(&t->wt, std::max<size_t>(max_wt, 1) * 4));
+    t->dzr[0] = t->dz;
+    for (int k = 1; k < rst_predictor_trainer::DZR; ++k) TRY(t->alloc(&t->dzr[k], max_act * 4));
+    {
+        const char* sw = getenv("RST_SERIAL_PREDICTOR_WGRAD");
+        t->serial_wgrad = sw != nullptr && sw[0] == '1';
+        bool ok = hipStreamCreateWithFlags(&t->wside, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreateWithFlags(&t->ev_chain, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&t->ev_done, hipEventDisableTiming) == hipSuccess;
+        for (int k = 0; ok && k < rst_predictor_trainer::DZR; ++k)
+            ok = hipEventCreateWithFlags(&t->ev_dz[k], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&t->ev_wg[k], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            delete t;
+            return set_error(RST_ERR_HIP, "rst_predictor_trainer_create: stream / event creation failed");
+        }
+    }
 #undef TRY
     *out = t;
     return RST_OK;
@@ -279,17 +313,32 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
     const PPlan& P = t->plan;
     const int B = t->batch, NS = t->shape.num_style_parameters, NP = t->shape.num_top_parameters;
     const float* w = t->d_wc;
+    // Off the input-gradient chain (weight gradients, the SE / head outer products) on t->wside when par: every such
+    // launch follows a fork (ev_chain recorded on the chain, waited on wside) placed after the chain's last write of
+    // its operands; the chain's norm-backward outputs round a ring of DZR buffers released by ev_wg; joined at the end.
+    // Same kernels on the same operands: bitwise the serial order.
+    const bool par = !t->serial_wgrad;
+    hipStream_t ws = par ? t->wside : st;
+    auto fork = [&]() -> hipError_t {
+        if (!par) return hipSuccess;
+        hipError_t e = hipEventRecord(t->ev_chain, st);
+        return e != hipSuccess ? e : hipStreamWaitEvent(ws, t->ev_chain, 0);
+    };
     RST_HIP_TRY(hipMemsetAsync(grad, 0, P.total * sizeof(float), st));
     // heads (stylePrediction.py:60-71): P = W2^T h + b2, h = W1^T gap + b1
     RST_HIP_TRY(rowdot_launch(d_style_params, B, NP, w + P.head_w2, NS, 1.f, t->dhid, st));
-    RST_HIP_TRY(outer_launch(t->hidden, NS, d_style_params, NP, B, 0, grad + P.head_w2, grad + P.head_b2, st));
+    RST_HIP_TRY(fork());
+    RST_HIP_TRY(outer_launch(t->hidden, NS, d_style_params, NP, B, 0, grad + P.head_w2, grad + P.head_b2, ws));
     const PUnit& fu = P.units[P.feat_unit];
     // gradient of the pooled features; spread over the feature map as dgap / HW (DUMMY: dgap itself)
     RST_HIP_TRY(rowdot_launch(t->dhid, B, NS, w + P.head_w1, P.feat_c, fu.kind == PU_DUMMY ? 1.f : 1.f / P.feat_hw,
                               t->dfeat, st));
-    RST_HIP_TRY(outer_launch(t->gap, P.feat_c, t->dhid, NS, B, 0, grad + P.head_w1, grad + P.head_b1, st));
-    for (int i = (int)P.units.size() - 1; i >= 0; --i) {
+    RST_HIP_TRY(outer_launch(t->gap, P.feat_c, t->dhid, NS, B, 0, grad + P.head_w1, grad + P.head_b1, ws));
+    int j = 0;
+    for (int i = (int)P.units.size() - 1; i >= 0; --i, ++j) {
         const PUnit& u = P.units[i];
+        const int slot = j % rst_predictor_trainer::DZR;
+        float* const dz = par ? t->dzr[slot] : t->dz;
         const float* in = u.in < 0 ? t->style : t->y[u.in];
         if (u.kind == PU_DUMMY) {
             RST_HIP_TRY(dummy_wgrad_launch(t->style, t->dfeat, B, u.H, u.W, u.cin, u.Ho, u.Wo, u.pad_t, u.pad_l,
@@ -307,27 +356,32 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
         a.mr = t->mr[i];
         a.consts = t->consts;
         a.part = t->bn_part;
-        a.dz = t->dz;
+        a.dz = dz;
         a.dgamma = grad + u.goff;
         a.B = B;
         a.HW = u.Ho * u.Wo;
         a.C = u.cout;
         a.act = u.act;
+        if (par && j >= rst_predictor_trainer::DZR) RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_wg[slot], 0));
         RST_HIP_TRY(bn_backward_launch(a, st));
+        if (par) {
+            RST_HIP_TRY(hipEventRecord(t->ev_dz[slot], st));
+            RST_HIP_TRY(hipStreamWaitEvent(ws, t->ev_dz[slot], 0));
+        }
         if (u.res >= 0)   // y = BN(z) + shortcut: the shortcut's consumer adds this in its dgrad
             RST_HIP_TRY(hipMemcpyAsync(t->dres[u.res], t->dyb[i], (size_t)B * u.Ho * u.Wo * u.cout * sizeof(float),
                                        hipMemcpyDeviceToDevice, st));
         switch (u.kind) {
             case PU_STEM:
-                RST_HIP_TRY(stem_wgrad_launch(t->style, t->dz, B, u.H, u.W, u.Ho, u.Wo, u.pad_t, u.pad_l, t->slab,
-                                              grad + u.woff, st));
+                RST_HIP_TRY(stem_wgrad_launch(t->style, dz, B, u.H, u.W, u.Ho, u.Wo, u.pad_t, u.pad_l, t->slab,
+                                              grad + u.woff, ws));
                 break;
             case PU_PW: {
                 const float* se = u.se >= 0 ? t->se_val[u.se] : nullptr;
-                RST_HIP_TRY(pw_wgrad_launch(in, se, t->dz, B, u.H * u.W, u.cin, u.cout, t->slab, grad + u.woff, st));
+                RST_HIP_TRY(pw_wgrad_launch(in, se, dz, B, u.H * u.W, u.cin, u.cout, t->slab, grad + u.woff, ws));
                 // dgrad: the 1x1 conv with the transposed kernel; the shortcut gradient rides on its residual input
                 RST_HIP_TRY(transpose_launch(w + u.woff, u.cin, u.cout, t->wt, st));
-                RST_HIP_TRY(pw_launch(t->dz, nullptr, t->wt, t->d_ones, t->d_zeros,
+                RST_HIP_TRY(pw_launch(dz, nullptr, t->wt, t->d_ones, t->d_zeros,
                                       t->res_consumer[u.in] ? t->dres[u.in] : nullptr, t->dyb[u.in], nullptr, B,
                                       u.H * u.W, u.cout, u.cin, ACT_NONE, st));
                 if (u.se >= 0) {   // dyb[in] is d/d(u * se): SE backward (the dw unit applies mul/bcast)
@@ -338,20 +392,26 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
                     RST_HIP_TRY(se_bwd_launch(t->se_dpart[u.se], np, B, s.C, s.R, s.Ho * s.Wo, w + s.w1, w + s.w2,
                                               t->se_s1[u.se], t->se_s2[u.se], t->se_ds1[u.se], t->se_ds2[u.se],
                                               t->se_dgb[u.se], st));
+                    RST_HIP_TRY(fork());
                     RST_HIP_TRY(outer_launch(t->se_g[u.se], s.C, t->se_ds1[u.se], s.R, B, 0, grad + s.w1, grad + s.b1,
-                                             st));
+                                             ws));
                     RST_HIP_TRY(outer_launch(t->se_s1[u.se], s.R, t->se_ds2[u.se], s.C, B, 1, grad + s.w2, grad + s.b2,
-                                             st));
+                                             ws));
                 }
                 break;
             }
             case PU_DW:
-                RST_HIP_TRY(dw_wgrad_launch(in, t->dz, B, u.H, u.W, u.cout, u.Ho, u.Wo, u.k, u.stride, u.pad_t, u.pad_l,
-                                            t->slab, grad + u.woff, st));
-                RST_HIP_TRY(dw_dgrad_launch(t->dz, w + u.woff, t->dyb[u.in], B, u.H, u.W, u.cout, u.Ho, u.Wo, u.k,
+                RST_HIP_TRY(dw_wgrad_launch(in, dz, B, u.H, u.W, u.cout, u.Ho, u.Wo, u.k, u.stride, u.pad_t, u.pad_l,
+                                            t->slab, grad + u.woff, ws));
+                RST_HIP_TRY(dw_dgrad_launch(dz, w + u.woff, t->dyb[u.in], B, u.H, u.W, u.cout, u.Ho, u.Wo, u.k,
                                             u.stride, u.pad_t, u.pad_l, st));
                 break;
         }
+        if (par) RST_HIP_TRY(hipEventRecord(t->ev_wg[slot], ws));
+    }
+    if (par) {   // join: every gradient is in `grad` when the caller's stream goes on
+        RST_HIP_TRY(hipEventRecord(t->ev_done, ws));
+        RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_done, 0));
     }
     return RST_OK;
 }

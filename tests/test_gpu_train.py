@@ -348,8 +348,9 @@ def test_joint_training_with_style_predictor_matches_oracle():
 def test_predictor_backward_beside_the_transfer_backward_is_bitwise_serial():
     """train_step runs the style predictor's backward on a side stream from the point where the transfer network's
     backward has made d loss / d style_params final (rst_trainer_wait_style_gradient, after its last conditional
-    instance norm), beside the contract layers' backward: two joint steps give bitwise the weights (both networks)
-    and losses of the serial order."""
+    instance norm), beside the contract layers' backward, and inside it the weight gradients and SE / head outer
+    products run on a third stream beside its input-gradient chain: two joint steps give bitwise the weights (both
+    networks) and losses of the fully serial order."""
     _need_gpu()
     from realtime_style_transfer_amd.stylePrediction import (StylePredictionTrainer, init_predictor_weights,
                                                              predictor_weight_spec)
@@ -366,7 +367,12 @@ def test_predictor_backward_beside_the_transfer_backward_is_bitwise_serial():
     runs = []
     for overlap in (False, True):
         lm = StyleLossModelVGG(cfg['output_shape'], weights=vgg, max_batch=B)
-        pr = StylePredictionTrainer(sins, 'MOBILE_NET', P, weights=pw, max_batch=B)
+        # the serial reference also keeps the predictor's weight gradients on its backward's stream
+        os.environ["RST_SERIAL_PREDICTOR_WGRAD"] = "0" if overlap else "1"
+        try:
+            pr = StylePredictionTrainer(sins, 'MOBILE_NET', P, weights=pw, max_batch=B)
+        finally:
+            del os.environ["RST_SERIAL_PREDICTOR_WGRAD"]
         tr = StyleTransferTrainingModel(cfg['input_shape'], cfg['output_shape'], cfg['bottleneck_res_y'],
                                         cfg['bottleneck_num_filters'], loss_model=lm, weights=w, max_batch=B,
                                         style_predictor=pr)
