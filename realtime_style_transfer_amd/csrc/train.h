@@ -58,6 +58,16 @@ hipError_t gram_bwd_weights_launch(const float* gp, const float* gs, const int* 
 hipError_t preprocess_bwd_launch(const float* gpre, float* gx, size_t pixels, int accumulate, hipStream_t st);
 hipError_t rmsprop_launch(float* w, float* ms, const float* g, size_t n, float lr, float rho, float eps, hipStream_t st);
 hipError_t gather_launch(const float* src, const int* map, float* dst, size_t n, hipStream_t st);
+// batched gathers dst_j[i] = src[map_j[i]] (0 where map_j[i] < 0), one launch; gather_batch_launch resets jobs.n
+constexpr int GATHER_MAX_JOBS = 48;
+struct GatherJobs {
+    const int* map[GATHER_MAX_JOBS];
+    float* dst[GATHER_MAX_JOBS];
+    size_t count[GATHER_MAX_JOBS];
+    int first[GATHER_MAX_JOBS + 1];
+    int n;
+};
+hipError_t gather_batch_launch(const float* src, GatherJobs& jobs, hipStream_t st);
 hipError_t scatter_div_launch(const float* src, const int* index, float* dst, size_t n, float divisor, hipStream_t st);
 
 }  // namespace rst

@@ -567,4 +567,34 @@ hipError_t gather_launch(const float* src, const int* map, float* dst, size_t n,
     return hipGetLastError();
 }
 
+// Many gathers from one source in one launch (the trainer's re-pack after every update: ~40 index maps of 10^2 -
+// 10^6 entries, which as separate launches spent more time between kernels than in them). Job j owns blocks
+// [first[j], first[j + 1]); inside a job the same element loop as gather_kernel.
+__global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restrict__ src, GatherJobs jobs) {
+    int j = 0;
+    while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+    const int nb = jobs.first[j + 1] - jobs.first[j];
+    const int* __restrict__ map = jobs.map[j];
+    float* __restrict__ dst = jobs.dst[j];
+    const size_t n = jobs.count[j];
+    for (size_t i = (size_t)((int)blockIdx.x - jobs.first[j]) * 256 + threadIdx.x; i < n; i += (size_t)nb * 256) {
+        const int m = map[i];
+        dst[i] = m < 0 ? 0.f : src[m];
+    }
+}
+
+hipError_t gather_batch_launch(const float* src, GatherJobs& jobs, hipStream_t st) {
+    if (jobs.n == 0) return hipSuccess;
+    int blocks = 0;
+    for (int j = 0; j < jobs.n; ++j) {
+        jobs.first[j] = blocks;
+        long b = (long)((jobs.count[j] + 255) / 256);
+        blocks += (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+    }
+    jobs.first[jobs.n] = blocks;
+    hipLaunchKernelGGL(gather_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, jobs);
+    jobs.n = 0;
+    return hipGetLastError();
+}
+
 }  // namespace rst

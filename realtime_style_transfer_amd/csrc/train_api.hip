@@ -201,10 +201,24 @@ struct rst_trainer {
 namespace {
 
 int repack(rst_trainer* t, hipStream_t st) {
-    // the x6 transforms of every layer go into batched launches after the gathers that feed them
+    // the x6 transforms of every layer go into batched launches after the gathers that feed them; the gathers go into
+    // batched launches too (flushed before anything that reads their outputs)
+    GatherJobs gj{};
+    auto gather = [&](const int* map, float* dst, size_t n) -> hipError_t {
+        if (gj.n == GATHER_MAX_JOBS) {
+            const hipError_t e = gather_batch_launch(t->d_wc, gj, st);
+            if (e != hipSuccess) return e;
+        }
+        gj.map[gj.n] = map;
+        gj.dst[gj.n] = dst;
+        gj.count[gj.n] = n;
+        ++gj.n;
+        return hipSuccess;
+    };
     X6TransformJobs jobs{};
     auto add_job = [&](const float* kern, int cin, float* U) -> int {
         if (jobs.n == X6_MAX_JOBS) {
+            RST_HIP_TRY(gather_batch_launch(t->d_wc, gj, st));   // (a job may read a gathered d_kflip)
             RST_HIP_TRY(wino_x6_transform_batch_launch(jobs, st));
             jobs.n = 0;
         }
@@ -220,20 +234,22 @@ int repack(rst_trainer* t, hipStream_t st) {
         else if (T.e.kind == K_WINO9X6) RST_HIP_TRY(wino9_x6_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
         else if (T.e.kind == K_WINOX6) r = add_job(t->d_wc + T.woff, T.e.s.cin, T.e.d_w);
         else if (T.wino_fwd) RST_HIP_TRY(wino_transform_launch(t->d_wc + T.woff, T.e.s.cin, T.e.d_w, st));
-        else RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_w, T.e.d_w, T.n_w, st));
+        else RST_HIP_TRY(gather(T.d_map_w, T.e.d_w, T.n_w));
         if (r != RST_OK) return r;
-        RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_b, T.e.d_bias, T.n_b, st));
+        RST_HIP_TRY(gather(T.d_map_b, T.e.d_bias, T.n_b));
         if (T.has_dgrad && T.wino_dg) {
-            RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_dg, T.d_kflip, T.n_dg, st));
+            RST_HIP_TRY(gather(T.d_map_dg, T.d_kflip, T.n_dg));
             if (T.dg.kind == K_WINOX6) {
                 if ((r = add_job(T.d_kflip, T.dg.s.cin, T.d_wdg)) != RST_OK) return r;
             } else {
+                RST_HIP_TRY(gather_batch_launch(t->d_wc, gj, st));
                 RST_HIP_TRY(wino_transform_launch(T.d_kflip, T.dg.s.cin, T.d_wdg, st));
             }
         } else if (T.has_dgrad) {
-            RST_HIP_TRY(gather_launch(t->d_wc, T.d_map_dg, T.d_wdg, T.n_dg, st));
+            RST_HIP_TRY(gather(T.d_map_dg, T.d_wdg, T.n_dg));
         }
     }
+    RST_HIP_TRY(gather_batch_launch(t->d_wc, gj, st));
     RST_HIP_TRY(wino_x6_transform_batch_launch(jobs, st));
     return RST_OK;
 }
