@@ -111,6 +111,17 @@ int rst_copy_activation(rst_handle* h, int idx, float* dst, size_t count, int ba
  * summed conv-kernel time and conv+CIN-finalize time (ms) over the recorded steps. */
 int rst_profile_begin(rst_handle* h, int max_steps);
 int rst_profile_end(rst_handle* h, float* conv_ms, float* layer_ms, int* steps);
+
+/* In-graph kernel timeline (measurement; no reference counterpart). rst_timeline_begin (outside graph capture)
+ * allocates a per-layer stamp buffer that the forwards issued afterwards (eager or captured into a hipGraph) pass to
+ * the residual convs (wino_x6) and the narrow convs (conv_lite): every wave stores the 100-MHz realtime counter as it
+ * ends. rst_timeline_read synchronises the device and returns, per layer (n = number of layers), the latest end
+ * stamp of the most recent forward in microseconds after the first stamped layer's, or -1 for layers whose kernel
+ * does not stamp; end[k] - end[k - 1] is layer k's share of a back-to-back graph replay (what rocprofv3's kernel
+ * trace reports as its duration there). rst_timeline_end frees the buffer (after any graph holding it is gone). */
+int rst_timeline_begin(rst_handle* h);
+int rst_timeline_read(rst_handle* h, double* end_us, int n);
+int rst_timeline_end(rst_handle* h);
 /* Which compiled kernel configuration runs layer idx (100 = VALU 9x9 Cout=3 kernel). */
 int rst_layer_kernel_id(const rst_handle* h, int idx);
 

@@ -280,7 +280,9 @@ def vgg16_features(images01, vgg_weights: Dict[str, Tuple[np.ndarray, np.ndarray
     """StyleLossModelVGG.call (styleLoss.py:106-109): x*255, RGB->BGR, -mean, VGG16 trunk.
     ``operand_round`` (bf16_round) is applied to the input and kernel of every conv — the device's plain-bf16
     loss runs all thirteen on bf16 operands (block1_conv1 on vgg_conv0_bf16, the preprocessed image rounded),
-    as Keras mixed_bfloat16 does — to simulate that mode."""
+    as Keras mixed_bfloat16 does — and to every conv's output: the layer outputs are stored in bf16 (a
+    mixed_bfloat16 layer emits its compute dtype), which the content loss and the feature maps see directly
+    (the next conv's input rounding is then exact, and a max pool of rounded values is the rounded max)."""
     x = np.asarray(images01, np.float64) * 255.0
     x = x[..., ::-1] - VGG_MEAN_BGR                                   # vgg16.preprocess_input ('caffe')
     feats = {}
@@ -293,6 +295,8 @@ def vgg16_features(images01, vgg_weights: Dict[str, Tuple[np.ndarray, np.ndarray
         if operand_round is not None:
             x, w = operand_round(x), operand_round(w)
         x = relu(conv2d_same(x, w, b, 1))
+        if operand_round is not None:
+            x = operand_round(x)
         if name in STYLE_LAYERS or name in CONTENT_LAYERS:
             feats[name] = x
         if name == CONTENT_LAYERS[0]:

@@ -181,13 +181,26 @@ class _Bf16FwdConv(torch.autograd.Function):
         return gx, None, None
 
 
+class _Bf16Store(torch.autograd.Function):
+    """A mixed_bfloat16 layer output: the value rounded to bf16 (the device stores every VGG16 layer output as bf16
+    bits in the plain-bf16 loss); the cast's gradient passes through unchanged, as TF's Cast gradient does."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return _bf16(x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return gy
+
+
 def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None,
                  bf16: bool = False, relu_route=None) -> Dict[str, torch.Tensor]:
     """StyleLossModelVGG.call (styleLoss.py:106-109) on NCHW float64 images in [0, 1].
     ``taps``: list receiving every conv output (retain_grad) when the input requires grad.
     ``route``: {conv index: NCHW activations} whose window maxima route the max-pool backward.
     ``bf16``: every conv in bf16 arithmetic (_Bf16Conv; the first, whose input gradient stays f32 on the
-    device, _Bf16FwdConv).
+    device, _Bf16FwdConv) and every layer output stored in bf16 (_Bf16Store).
     ``relu_route``: {conv index: NCHW post-ReLU activations} whose positive units set the ReLU backward mask."""
     x = images01 * 255.0
     mean = torch.tensor(VGG_MEAN_BGR, dtype=x.dtype).view(1, 3, 1, 1)
@@ -209,6 +222,8 @@ def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None,
         else:
             x = conv2d_same(x, vgg[2 * i], vgg[2 * i + 1], 1)
         x = _RoutedRelu.apply(x, relu_route[i]) if relu_route is not None and i in relu_route else F.relu(x)
+        if bf16:
+            x = _Bf16Store.apply(x)
         i += 1
         if taps is not None and x.requires_grad:
             x.retain_grad()

@@ -25,7 +25,8 @@ EXPORTED_SYMBOLS = [
     "rst_create", "rst_create_ex", "rst_precision", "rst_destroy", "rst_num_style_params", "rst_num_weights_for_shape", "rst_forward",
     "rst_num_layers", "rst_layer_output_shape", "rst_copy_activation", "rst_gram_workspace_size", "rst_gram",
     "rst_instance_norm_workspace_size", "rst_instance_norm", "rst_style_param_map", "rst_last_error", "rst_version",
-    "rst_profile_begin", "rst_profile_end", "rst_layer_kernel_id",
+    "rst_profile_begin", "rst_profile_end", "rst_timeline_begin", "rst_timeline_read", "rst_timeline_end",
+    "rst_layer_kernel_id",
     "rst_loss_num_weights", "rst_loss_create", "rst_loss_destroy", "rst_loss_forward", "rst_loss_copy_feature",
     "rst_trainer_create", "rst_trainer_create_ex", "rst_trainer_destroy", "rst_trainer_num_style_params", "rst_trainer_num_weights",
     "rst_trainer_compute_gradients", "rst_trainer_compute_targets", "rst_trainer_apply_gradients",
@@ -142,6 +143,12 @@ def load() -> ctypes.CDLL:
     lib.rst_profile_begin.restype = i
     lib.rst_profile_end.argtypes = [vp, ctypes.POINTER(fp), ctypes.POINTER(fp), ctypes.POINTER(i)]
     lib.rst_profile_end.restype = i
+    lib.rst_timeline_begin.argtypes = [vp]
+    lib.rst_timeline_begin.restype = i
+    lib.rst_timeline_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i]
+    lib.rst_timeline_read.restype = i
+    lib.rst_timeline_end.argtypes = [vp]
+    lib.rst_timeline_end.restype = i
     lib.rst_layer_kernel_id.argtypes = [vp, i]
     lib.rst_layer_kernel_id.restype = i
     lib.rst_loss_num_weights.argtypes = []

@@ -201,8 +201,20 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
             f32x4 v = {0.f, 0.f, 0.f, 0.f}, r = {0.f, 0.f, 0.f, 0.f};
             if ((HITEMS % 256 == 0 || it < HITEMS) && halo_item(it, chunk, hp, q, iy, ix, c)) {
                 const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
-                v = *reinterpret_cast<const f32x4*>(a.in + gi);
-                if (need_r) r = *reinterpret_cast<const f32x4*>(a.res + gi);
+                if (a.act_bf16 & 1) {   // bf16 activations (8-B loads; the NP = 1 split below is then exact)
+                    const float4 u = ld_bf16x4(a.in, gi);
+                    v = f32x4{u.x, u.y, u.z, u.w};
+                } else {
+                    v = *reinterpret_cast<const f32x4*>(a.in + gi);
+                }
+                if (need_r) {
+                    if (a.act_bf16 & 4) {
+                        const float4 u = ld_bf16x4(a.res, gi);
+                        r = f32x4{u.x, u.y, u.z, u.w};
+                    } else {
+                        r = *reinterpret_cast<const f32x4*>(a.res + gi);
+                    }
+                }
             }
             pv[k] = v;
             pr[k] = r;
@@ -381,12 +393,15 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                     const int oy = y0 + p / TW, ox = x0 + p % TW;
                     const float4 v = *reinterpret_cast<const float4*>(ep + px * 64 + c4);
                     if (oy < a.Ho && ox < a.Wo) {
-                        float* const po = a.out + (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ngb + c4;
-                        if (a.wt_stores)   // write-through (sc1): no dirty lines left for the end-of-kernel write-back
-                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), osrd,
-                                                                   (int)((po - a.out) * 4), 0, 16);
-                        else
-                            *reinterpret_cast<float4*>(po) = v;
+                        const size_t oi = (((size_t)b * a.Ho + oy) * a.Wo + ox) * a.ntot + ngb + c4;
+                        if (a.act_bf16 & 2) {   // bf16 layer output (mixed_bfloat16): 8 B per lane, 512 B per wave
+                            *reinterpret_cast<uint2*>(reinterpret_cast<unsigned short*>(a.out) + oi) =
+                                pack_bf16x4(v.x, v.y, v.z, v.w);
+                        } else if (a.wt_stores) {   // write-through (sc1): no dirty lines left for the end-of-kernel write-back
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), osrd, (int)(oi * 4), 0, 16);
+                        } else {
+                            *reinterpret_cast<float4*>(a.out + oi) = v;
+                        }
                     }
                 }
                 if constexpr (TW == 16 && TH % 2 == 0) {
@@ -409,12 +424,15 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                             m.w = fmaxf(fmaxf(a0.w, a1.w), fmaxf(a2.w, a3.w));
                             const int py = (y0 >> 1) + mt, qx = (x0 >> 1) + j;
                             if (py < Hp && qx < Wp) {
-                                float* const pp = a.pool + (((size_t)b * Hp + py) * Wp + qx) * a.ntot + ngb + c4;
-                                if (a.wt_stores)
-                                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, m), psrd,
-                                                                           (int)((pp - a.pool) * 4), 0, 16);
+                                const size_t pi = (((size_t)b * Hp + py) * Wp + qx) * a.ntot + ngb + c4;
+                                if (a.act_bf16 & 2)   // max of the rounded values = the rounded max (RNE is monotone)
+                                    *reinterpret_cast<uint2*>(reinterpret_cast<unsigned short*>(a.pool) + pi) =
+                                        pack_bf16x4(m.x, m.y, m.z, m.w);
+                                else if (a.wt_stores)
+                                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, m), psrd, (int)(pi * 4),
+                                                                           0, 16);
                                 else
-                                    *reinterpret_cast<float4*>(pp) = m;
+                                    *reinterpret_cast<float4*>(a.pool + pi) = m;
                             }
                         }
                     }
@@ -569,6 +587,8 @@ hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a_in, hipStream_t 
         using C = Bf3Cfg<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>;                            \
         if ((a.cin & 3) != 0) return hipErrorInvalidValue;                                       \
         if (a.pool != nullptr && !conv_bf3_fuses_pool(t, a)) return hipErrorInvalidValue;        \
+        if ((a.act_bf16 & 2) && !conv_bf3_fuses_pool(t, a)) return hipErrorInvalidValue;        \
+        if ((a.act_bf16 & 5) && NP != 1) return hipErrorInvalidValue;                             \
         if (a.pro_w != nullptr && a.cin > C::MAX_CIN) return hipErrorInvalidValue;               \
         const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x * a.n_blocks);          \
         hipLaunchKernelGGL((conv_bf3_kernel<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>), dim3(grid), \
@@ -629,7 +649,7 @@ constexpr int TH = 8, TW = 32, PH = TH + 2, PW = TW + 2, PC = 4;   // patch [row
 __global__ __launch_bounds__(256) void vgg_conv0_bf16_kernel(const float* __restrict__ img, const float2* __restrict__ pre,
                                                              const unsigned short* __restrict__ wpk,
                                                              const float* __restrict__ bias, float* __restrict__ out,
-                                                             int H, int W, int tiles_x) {
+                                                             int H, int W, int tiles_x, int out_bf16) {
     using namespace vgg0;
     __shared__ __attribute__((aligned(16))) unsigned short patch[PH * PW * PC];
     __shared__ __attribute__((aligned(16))) float epi[4 * 32 * 64];   // per-wave epilogue images
@@ -702,7 +722,13 @@ __global__ __launch_bounds__(256) void vgg_conv0_bf16_kernel(const float* __rest
         for (int it = 0; it < 8; ++it) {
             const int px = 4 * it + (lane >> 4), c4 = 4 * (lane & 15), ox = x0 + px;
             const float4 v = *reinterpret_cast<const float4*>(ep + px * 64 + c4);
-            if (oy < H && ox < W) *reinterpret_cast<float4*>(out + (((size_t)b * H + oy) * W + ox) * 64 + c4) = v;
+            if (oy < H && ox < W) {
+                const size_t oi = (((size_t)b * H + oy) * W + ox) * 64 + c4;
+                if (out_bf16)   // bf16 layer output (mixed_bfloat16)
+                    *reinterpret_cast<uint2*>(reinterpret_cast<unsigned short*>(out) + oi) = pack_bf16x4(v.x, v.y, v.z, v.w);
+                else
+                    *reinterpret_cast<float4*>(out + oi) = v;
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
         __builtin_amdgcn_wave_barrier();
@@ -729,11 +755,11 @@ std::vector<unsigned short> vgg_conv0_bf16_pack(const float* wflip) {
 }
 
 hipError_t vgg_conv0_bf16_launch(const float* img, const float2* pre, const unsigned short* wpk, const float* bias,
-                                 float* out, int batch, int H, int W, hipStream_t st) {
+                                 float* out, int batch, int H, int W, hipStream_t st, bool out_bf16) {
     using namespace vgg0;
     const int tiles_y = (H + TH - 1) / TH, tiles_x = (W + TW - 1) / TW;
     hipLaunchKernelGGL(vgg_conv0_bf16_kernel, dim3((unsigned)(tiles_y * tiles_x), (unsigned)batch), dim3(256), 0, st,
-                       img, pre, wpk, bias, out, H, W, tiles_x);
+                       img, pre, wpk, bias, out, H, W, tiles_x, out_bf16 ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -865,6 +865,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     if (to_acc) acc_flush();
     LT0(1);
     l2_touch_keep(l2f, a.batch < 0, smem);
+    tl_stamp_end(a.tl);
 }
 
 // ------------------------------------------------------------------------------------------------

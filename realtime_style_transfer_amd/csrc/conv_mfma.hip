@@ -255,7 +255,8 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
                     v = *reinterpret_cast<const float4*>(a.in + gi);
                     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (pro == PRO_AFF_RES || pro == PRO_MASK) r = *reinterpret_cast<const float4*>(a.res + gi);
+                    if (pro == PRO_MASK && (a.act_bf16 & 4)) r = ld_bf16x4(a.res, gi);   // bf16 forward activations
+                    else if (pro == PRO_AFF_RES || pro == PRO_MASK) r = *reinterpret_cast<const float4*>(a.res + gi);
                     v = transform4(v, r, c, gi, iy, ix);
                 }
                 write_halo4(hbuf, hp, q, v);
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
                     v = a.in[gi];
                     if (pro == PRO_MASK) {
-                        v = a.res[gi] > 0.f ? v : 0.f;
+                        v = ((a.act_bf16 & 4) ? ld_bf16(a.res, gi) : a.res[gi]) > 0.f ? v : 0.f;
                     } else if (pro != PRO_NONE) {
                         const float r = pro == PRO_AFF_RES ? a.res[gi] : 0.f;
                         v = blend ? apply_pro_blend(pro, v, pab[c], pab1[c],
@@ -566,6 +567,10 @@ bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
 
 hipError_t conv_launch(const ConvTile& t, const ConvArgs& a_in, hipStream_t st) {
     if (t.bf3) return conv_bf3_launch(t, a_in, st);
+    // bf16 activations on the f32 kernel: only the ReLU-mask source of a synchronously staged halo (the VGG16 conv0
+    // input gradient's 1x1 conv in the plain-bf16 loss)
+    if ((a_in.act_bf16 & 3) || ((a_in.act_bf16 & 4) && (a_in.pro_mode != PRO_MASK || t.hb != 1)))
+        return hipErrorInvalidValue;
     const ConvArgs a = conv_wt_checked(a_in);
     switch (t.id) {
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, HB) \

@@ -111,6 +111,9 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restri
 namespace gramb {
 constexpr int KP = 64, TILE = 64, RS = KP + 8;   // pixels per chunk, channels per slice, LDS row (bf16)
 }
+// FEAT_BF16: the features are stored as bf16 bits (the plain-bf16 VGG16's layer outputs): 2-B loads (a wave's 64
+// channels are 128 B) and no rounding (the packed pieces are the stored bits)
+template <bool FEAT_BF16>
 __global__ __launch_bounds__(256) void gram_partial_bf16_kernel(const float* __restrict__ feat, float* __restrict__ slab,
                                                                 int hw, int C, int nsplit, int span) {
     using namespace gramb;
@@ -153,8 +156,14 @@ __global__ __launch_bounds__(256) void gram_partial_bf16_kernel(const float* __r
         for (int j = 0; j < 16; ++j) {
             const int p = p0 + 16 * sg + j;
             const bool ok = p < p_end;
-            va[j] = ok ? fb[(size_t)p * C + c0 + sc] : 0.f;
-            vb[j] = ok ? fb[(size_t)p * C + d0 + sc] : 0.f;
+            if constexpr (FEAT_BF16) {
+                const unsigned short* fh = reinterpret_cast<const unsigned short*>(feat) + (size_t)b * hw * C;
+                va[j] = ok ? __uint_as_float((unsigned)fh[(size_t)p * C + c0 + sc] << 16) : 0.f;
+                vb[j] = ok ? __uint_as_float((unsigned)fh[(size_t)p * C + d0 + sc] << 16) : 0.f;
+            } else {
+                va[j] = ok ? fb[(size_t)p * C + c0 + sc] : 0.f;
+                vb[j] = ok ? fb[(size_t)p * C + d0 + sc] : 0.f;
+            }
         }
         __syncthreads();   // the previous chunk's operand reads are done
 #pragma unroll
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
 }
 
 hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st,
-                       bool bf16) {
+                       bool bf16, bool feat_bf16) {
     if (channels % gram::TILE != 0) return hipErrorInvalidValue;
     const int ns = gram_splits(batch, hw, channels);
     int span = (hw + ns - 1) / ns;
@@ -230,8 +239,11 @@ hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float
     const int ntile = channels / gram::TILE;
     const unsigned grid = (unsigned)(batch * (ntile * (ntile + 1) / 2) * ns);
     float* slab = static_cast<float*>(ws);
-    if (bf16)
-        hipLaunchKernelGGL(gram_partial_bf16_kernel, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns, span);
+    if (feat_bf16)
+        hipLaunchKernelGGL(gram_partial_bf16_kernel<true>, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns, span);
+    else if (bf16)
+        hipLaunchKernelGGL(gram_partial_bf16_kernel<false>, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns,
+                           span);
     else
         hipLaunchKernelGGL(gram_partial_kernel, dim3(grid), dim3(256), 0, st, feat, slab, hw, channels, ns, span);
     hipError_t e = hipGetLastError();

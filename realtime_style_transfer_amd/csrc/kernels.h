@@ -42,6 +42,33 @@ __device__ __forceinline__ unsigned bf16_last_piece(float x, float y) {
     return __builtin_bit_cast(unsigned, __builtin_convertvector((rst_f32x2){x, y}, rst_bf16x2));
 }
 
+// bf16 activation storage (the plain-bf16 VGG16: Keras mixed_bfloat16 layer outputs are bf16). Four consecutive
+// bf16 values at element index i of `base` widened to f32 (exact), and four f32 values rounded to bf16 (RNE, as
+// every bf16 operand rounding here) and packed for one 8-byte store.
+__device__ __forceinline__ float4 ld_bf16x4(const void* base, size_t i) {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(base) + i);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xFFFF0000u));
+}
+__device__ __forceinline__ float ld_bf16(const void* base, size_t i) {
+    return __uint_as_float((unsigned)reinterpret_cast<const unsigned short*>(base)[i] << 16);
+}
+__device__ __forceinline__ uint2 pack_bf16x4(float x, float y, float z, float w) {
+    return make_uint2(bf16_last_piece(x, y), bf16_last_piece(z, w));
+}
+
+// In-graph kernel timeline (rst_timeline_begin / rst_timeline_read): every wave of a launch stores the 100-MHz
+// realtime counter as it ends into its slot of the layer's buffer (TL_SLOTS entries); the host takes the latest
+// stamp per layer, so end(k) - end(k - 1) is layer k's share of a graph replay. Measurement only: a null tl (the
+// default) stores nothing. The store is a vector store (global_store_dwordx2 from lane 0).
+constexpr int TL_SLOTS = 16384;   // >= waves of any stamped launch (wino_x6 at B = 8: 1800 x 8)
+__device__ __forceinline__ void tl_stamp_end(unsigned long long* tl) {
+    if (tl != nullptr && (threadIdx.x & 63) == 0) {
+        const unsigned idx = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        if (idx < (unsigned)TL_SLOTS) tl[idx] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // x + x[lane ^ O] for O = 16 / 32 on the VALU (v_permlane16/32_swap, gfx950) instead of ds_bpermute (__shfl_xor,
 // an LDS round trip per value): the swap hands each lane the partner's value, the add is commutative, so the result
 // is bitwise __shfl_xor's
@@ -417,6 +444,9 @@ struct ConvArgs {
     const void* w_next;     // conv_lite inference: the next layer's weight image into L2 (l2_touch_xcd_slice)
     int w_next_bytes;
     int wt_stores;          // nonzero: output stored write-through (sc1), as WinoArgs::wt_stores
+    unsigned long long* tl; // conv_lite: in-graph timeline stamps (tl_stamp_end) or null
+    int act_bf16;           // conv_bf3 / conv_mfma, the plain-bf16 VGG16 (Keras mixed_bfloat16 layer outputs): bit 0 `in`,
+                            // bit 1 `out` and `pool`, bit 2 `res` (PRO_MASK) hold bf16 bits (unsigned short), not f32
 };
 
 // Write-through stores address the output with 32-bit buffer offsets: the byte extent of what the kernel indexes
@@ -450,8 +480,9 @@ hipError_t conv_bf3_prepare(const ConvTile& t);
 bool conv_bf3_fuses_pool(const ConvTile& t, const ConvArgs& a);
 // VGG16 block1_conv1 (3 -> 64, preprocess fused) on bf16 operands: the plain-bf16 loss (conv_bf3.hip)
 std::vector<unsigned short> vgg_conv0_bf16_pack(const float* wflip);
+// out_bf16: the output is stored as bf16 bits (the plain-bf16 VGG16's layer outputs)
 hipError_t vgg_conv0_bf16_launch(const float* img, const float2* pre, const unsigned short* wpk, const float* bias,
-                                 float* out, int batch, int H, int W, hipStream_t st);
+                                 float* out, int batch, int H, int W, hipStream_t st, bool out_bf16 = false);
 
 // Residual-block conv (3x3 s1 SAME, 128 output channels) as fused Winograd F(2x2,3x3) on f32 MFMA
 // (wino.hip). Epilogue: bias + ReLU + store + per-(workgroup, channel) {sum, M2, n}, n_part =
@@ -475,6 +506,7 @@ struct WinoArgs {
     int u_next_bytes;       // epilogue (l2_touch_xcd_slice: its first loads then hit L2), or null
     int wt_stores;          // wino_x6: bit0 output, bit1 materialised input stored write-through (sc1): no dirty
                             // lines left in L2 for the end-of-kernel write-back
+    unsigned long long* tl; // wino_x6: in-graph timeline stamps (tl_stamp_end) or null
 };
 bool wino_supported(int kh, int stride, int cin, int cout);
 
@@ -657,14 +689,18 @@ hipError_t tile_stats_launch(const float* x, float4* part, int batch, long hw, i
 // Gram matrices (gram.hip)
 size_t gram_workspace_bytes(int batch, int hw, int channels);
 // bf16: features rounded to bf16, bf16 MFMA (RST_PRECISION_BF16 loss; the mixed_bfloat16 einsum)
+// feat_bf16: the features are stored as bf16 bits (the plain-bf16 VGG16's layer outputs; implies bf16)
 hipError_t gram_launch(const float* feat, int batch, int hw, int channels, float* out, void* ws, hipStream_t st,
-                       bool bf16 = false);
+                       bool bf16 = false, bool feat_bf16 = false);
 
 // Loss kernels (loss.hip)
 hipError_t maxpool2_launch(const float* x, float* y, int B, int H, int W, int C, hipStream_t st);
 int loss_partial_blocks(long n);
+// in_bf16: a and c hold bf16 bits (the plain-bf16 VGG16's block5_conv3 features)
 hipError_t sqdiff_loss_launch(const float* a, const float* c, int B, long n, float* partial, double scale, float* out,
-                              int out_stride, int out_col, int accumulate, hipStream_t st);
+                              int out_stride, int out_col, int accumulate, hipStream_t st, bool in_bf16 = false);
+// bf16 bits -> f32 (rst_loss_copy_feature of the plain-bf16 VGG16's stored layer outputs)
+hipError_t bf16_to_f32_launch(const void* x, float* y, size_t n, hipStream_t st);
 hipError_t tv_loss_launch(const float* x, int B, int H, int W, int C, float* partial, double scale, float* out,
                           int out_stride, int out_col, hipStream_t st);
 hipError_t loss_combine_launch(float* table, int B, hipStream_t st);

@@ -56,17 +56,18 @@ __device__ __forceinline__ float block_sum_f(float v, float* scratch) {
 }
 
 // partial[b * nblk + blk] = sum over this block's slice of image b of (a - b)^2
+// (BF16: a and c hold bf16 bits — the plain-bf16 VGG16's stored features — widened exactly to f32)
+template <bool BF16>
 __global__ __launch_bounds__(256) void sqdiff_partial_kernel(const float* __restrict__ a, const float* __restrict__ c,
                                                              float* __restrict__ partial, long n, int nblk) {
     __shared__ float scratch[4];
     const int blk = blockIdx.x, b = blockIdx.y;
     const long per = (n + nblk - 1) / nblk;
     const long s = (long)blk * per, e = (s + per < n) ? s + per : n;
-    const float* pa = a + (size_t)b * n;
-    const float* pc = c + (size_t)b * n;
     float acc = 0.f;
     for (long i = s + threadIdx.x; i < e; i += 256) {
-        const float d = pa[i] - pc[i];
+        const size_t k = (size_t)b * n + i;
+        const float d = BF16 ? ld_bf16(a, k) - ld_bf16(c, k) : a[k] - c[k];
         acc = fmaf(d, d, acc);
     }
     acc = block_sum_f(acc, scratch);
@@ -118,9 +119,12 @@ int loss_partial_blocks(long n) {
 }
 
 hipError_t sqdiff_loss_launch(const float* a, const float* c, int B, long n, float* partial, double scale, float* out,
-                              int out_stride, int out_col, int accumulate, hipStream_t st) {
+                              int out_stride, int out_col, int accumulate, hipStream_t st, bool in_bf16) {
     const int nblk = loss_partial_blocks(n);
-    hipLaunchKernelGGL(sqdiff_partial_kernel, dim3(nblk, B), dim3(256), 0, st, a, c, partial, n, nblk);
+    if (in_bf16)
+        hipLaunchKernelGGL(sqdiff_partial_kernel<true>, dim3(nblk, B), dim3(256), 0, st, a, c, partial, n, nblk);
+    else
+        hipLaunchKernelGGL(sqdiff_partial_kernel<false>, dim3(nblk, B), dim3(256), 0, st, a, c, partial, n, nblk);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(B), dim3(64), 0, st, partial, nblk, scale, out, out_stride, out_col,
@@ -136,6 +140,19 @@ hipError_t tv_loss_launch(const float* x, int B, int H, int W, int C, float* par
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(B), dim3(64), 0, st, partial, nblk, scale, out, out_stride, out_col,
                        0);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void bf16_to_f32_kernel(const unsigned short* __restrict__ x, float* __restrict__ y,
+                                                          size_t n) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        y[i] = __uint_as_float((unsigned)x[i] << 16);
+}
+
+hipError_t bf16_to_f32_launch(const void* x, float* y, size_t n, hipStream_t st) {
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(blocks), dim3(256), 0, st, static_cast<const unsigned short*>(x), y, n);
     return hipGetLastError();
 }
 

@@ -34,7 +34,7 @@ int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t s
     for (int i = 0; i <= last; ++i) {
         VggConv& c = h->convs[i];
         if (c.d_w0bf != nullptr) {   // plain-bf16 loss: block1_conv1 on bf16 operands, preprocess fused
-            RST_HIP_TRY(vgg_conv0_bf16_launch(in, h->d_pre, c.d_w0bf, c.d_b, c.d_out, B, c.H, c.W, st));
+            RST_HIP_TRY(vgg_conv0_bf16_launch(in, h->d_pre, c.d_w0bf, c.d_b, c.d_out, B, c.H, c.W, st, h->act_bf16));
             in = c.d_out;
             continue;
         }
@@ -67,9 +67,13 @@ int vgg_run(rst_loss_handle* h, const float* img, int B, int last, hipStream_t s
         if (fused) a.pool = c.d_pool;
         // write-through output stores (sc1, the VGG epilogue of conv_bf3) where the offsets fit 32 bits
         a.wt_stores = h->wt_stores && c.tile.bf3 && (size_t)B * c.H * c.W * c.cout * 4 < (size_t)0x7FFFFFF0 ? 1 : 0;
+        // bf16 layer outputs: this conv reads its input (the previous conv's or pool's bf16 output; conv 0 here only in
+        // the f32 modes) and stores its output and fused pool as bf16
+        if (h->act_bf16) a.act_bf16 = (i > 0 ? 1 : 0) | 2;
         RST_HIP_TRY(conv_launch(c.tile, a, st));
         in = c.d_out;
         if (pool) {
+            if (!fused && h->act_bf16) return set_error(RST_ERR_UNSUPPORTED, "bf16 VGG16 activations need the fused pool");
             if (!fused) RST_HIP_TRY(maxpool2_launch(c.d_out, c.d_pool, B, c.H, c.W, c.cout, st));
             in = c.d_pool;
         }
@@ -85,13 +89,15 @@ int loss_targets(rst_loss_handle* h, const float* gt_content, const float* gt_st
     if ((r = vgg_run(h, gt_style, B, STYLE_IDX[3], st)) != RST_OK) return r;
     for (int k = 0; k < 4; ++k) {
         const VggConv& c = h->convs[STYLE_IDX[k]];
-        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_style[k], h->d_gram_ws, st, gram_bf16));
+        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_style[k], h->d_gram_ws, st, gram_bf16,
+                                h->act_bf16));
     }
     // ground-truth content: block5_conv3 features
     if ((r = vgg_run(h, gt_content, B, CONTENT_IDX, st)) != RST_OK) return r;
     const VggConv& c5 = h->convs[CONTENT_IDX];
     const size_t f5 = (size_t)c5.H * c5.W * c5.cout;
-    RST_HIP_TRY(hipMemcpyAsync(h->d_content_feat, c5.d_out, (size_t)B * f5 * 4, hipMemcpyDeviceToDevice, st));
+    RST_HIP_TRY(hipMemcpyAsync(h->d_content_feat, c5.d_out, (size_t)B * f5 * (h->act_bf16 ? 2 : 4),
+                               hipMemcpyDeviceToDevice, st));
     return RST_OK;
 }
 
@@ -102,10 +108,11 @@ int loss_prediction(rst_loss_handle* h, const float* prediction, int B, float* l
     const size_t f5 = (size_t)c5.H * c5.W * c5.cout;
     if ((r = vgg_run(h, prediction, B, CONTENT_IDX, st)) != RST_OK) return r;
     RST_HIP_TRY(sqdiff_loss_launch(c5.d_out, h->d_content_feat, B, (long)f5, h->d_partial,
-                                   0.5 / (double)f5 * h->shape.content_factor, losses, 4, 1, 0, st));
+                                   0.5 / (double)f5 * h->shape.content_factor, losses, 4, 1, 0, st, h->act_bf16));
     for (int k = 0; k < 4; ++k) {
         const VggConv& c = h->convs[STYLE_IDX[k]];
-        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_pred[k], h->d_gram_ws, st, gram_bf16));
+        RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_pred[k], h->d_gram_ws, st, gram_bf16,
+                                h->act_bf16));
         const long n = (long)c.cout * c.cout;
         RST_HIP_TRY(sqdiff_loss_launch(h->d_gram_pred[k], h->d_gram_style[k], B, n, h->d_partial,
                                        0.5 / (double)n / 4.0 * h->shape.style_factor, losses, 4, 2, k > 0, st));
@@ -147,7 +154,10 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
     {
         const char* wt = getenv("RST_LOSS_WT");
         h->wt_stores = wt != nullptr && wt[0] == '1' ? 1 : 0;
+        const char* af = getenv("RST_VGG_ACT_F32");
+        h->act_bf16 = shape->precision == RST_PRECISION_BF16 && !(af != nullptr && af[0] == '1');
     }
+    const size_t es = h->act_bf16 ? 2 : 4;   // bytes per stored VGG16 activation
     h->shape = *shape;
     h->host_w.assign(vgg_weights_host, vgg_weights_host + num_weights);
     const int B = shape->max_batch;
@@ -189,9 +199,9 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
             if ((st = h->alloc(&c.d_w0bf, w0.size() * 2, w0.data())) != RST_OK) { delete h; return st; }
         }
         if ((st = h->alloc(&c.d_b, (size_t)c.cout * 4, bias)) != RST_OK) { delete h; return st; }
-        if ((st = h->alloc(&c.d_out, (size_t)B * H * W * c.cout * 4)) != RST_OK) { delete h; return st; }
+        if ((st = h->alloc(&c.d_out, (size_t)B * H * W * c.cout * es)) != RST_OK) { delete h; return st; }
         if (c.pool_after)
-            if ((st = h->alloc(&c.d_pool, (size_t)B * (H / 2) * (W / 2) * c.cout * 4)) != RST_OK) { delete h; return st; }
+            if ((st = h->alloc(&c.d_pool, (size_t)B * (H / 2) * (W / 2) * c.cout * es)) != RST_OK) { delete h; return st; }
         hipError_t pe = conv_prepare(c.tile);
         if (pe != hipSuccess) { delete h; return set_error(RST_ERR_HIP, hipGetErrorString(pe)); }
         h->convs.push_back(c);
@@ -204,7 +214,7 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
         for (int c = 0; c < 3; ++c) pre[(size_t)b * 3 + c] = make_float2(255.f, (float)(-VGG_MEAN_BGR[2 - c]));
     if ((st = h->alloc(&h->d_pre, pre.size() * sizeof(float2), pre.data())) != RST_OK) { delete h; return st; }
     const VggConv& c5 = h->convs[CONTENT_IDX];
-    if ((st = h->alloc(&h->d_content_feat, (size_t)B * c5.H * c5.W * c5.cout * 4)) != RST_OK) { delete h; return st; }
+    if ((st = h->alloc(&h->d_content_feat, (size_t)B * c5.H * c5.W * c5.cout * es)) != RST_OK) { delete h; return st; }
     size_t ws = 0;
     for (int k = 0; k < 4; ++k) {
         const VggConv& c = h->convs[STYLE_IDX[k]];
@@ -238,7 +248,10 @@ int rst_loss_copy_feature(rst_loss_handle* h, int layer, float* dst, size_t coun
     const VggConv& c = h->convs[layer];
     const size_t n = (size_t)batch * c.H * c.W * c.cout;
     if (count != n) return set_error(RST_ERR_INVALID, "rst_loss_copy_feature: count mismatch");
-    RST_HIP_TRY(hipMemcpyAsync(dst, c.d_out, n * 4, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    if (h->act_bf16)   // the stored bf16 layer output, widened (exactly) to f32
+        RST_HIP_TRY(bf16_to_f32_launch(c.d_out, dst, n, static_cast<hipStream_t>(stream)));
+    else
+        RST_HIP_TRY(hipMemcpyAsync(dst, c.d_out, n * 4, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
     return RST_OK;
 }
 

@@ -41,6 +41,9 @@ struct rst_loss_handle {
     float* d_partial = nullptr;
     size_t gram_ws_bytes = 0;
     int wt_stores = 0;                    // RST_LOSS_WT at creation: VGG conv outputs stored write-through (sc1)
+    bool act_bf16 = false;                // plain-bf16 loss: every VGG16 layer output (conv, pool, the content
+                                          // target) stored as bf16 bits, as Keras mixed_bfloat16 layers emit them
+                                          // (RST_VGG_ACT_F32=1 at creation: f32 storage, for A/B runs)
     std::vector<float> host_w;            // VGG16 weights as given (Keras order), for the backward packing
     ~rst_loss_handle() {
         for (void* p : allocs) (void)hipFree(p);

@@ -100,6 +100,11 @@ struct rst_handle {
     int wt_stores = 15;               // RST_WT_STORES at creation: write-through output stores (1 wino_x6 output, 2 its
                                       // materialised input, 4 wino9_x6 output, 8 conv_lite output)
     bool no_u_prefetch = false;       // RST_NO_U_PREFETCH=1 at creation: no next-layer U prefetch (A/B runs)
+    unsigned long long* d_tl = nullptr;   // rst_timeline_begin: [layers][TL_SLOTS] wave end stamps (wino_x6, conv_lite)
+    void tl_free() {
+        if (d_tl) (void)hipFree(d_tl);
+        d_tl = nullptr;
+    }
     void prof_free() {
         for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
         prof_events.clear();
@@ -108,6 +113,7 @@ struct rst_handle {
     }
     ~rst_handle() {
         prof_free();
+        tl_free();
         for (void* p : allocs) (void)hipFree(p);
     }
     template <typename T>

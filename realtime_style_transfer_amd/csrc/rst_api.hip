@@ -17,6 +17,7 @@
 //   last:      VALU 9x9 conv (CIN-apply+ReLU prologue) + stats -> finalize -> sigmoid(CIN) (:269-276)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -742,6 +743,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
         }
         if (e.kind == K_WINOX6) next_weights(h, li, &a.u_next, &a.u_next_bytes);   // into L2 during the epilogue
         a.wt_stores = wt_bits(h, e, B, 3);
+        if (h->d_tl && e.kind == K_WINOX6) a.tl = h->d_tl + li * (size_t)TL_SLOTS;
         if (ext_ev) wino_x6_set_timing_events(ev[0], ev[1]);
         HIP_TRY(e.kind == K_WINOX6 ? wino_x6_launch(a, st) : wino_launch(a, st));
     } else {
@@ -788,6 +790,7 @@ static int launch_layer(rst_handle* h, size_t li, const float* content, const fl
             }
             next_weights(h, li, &a.w_next, &a.w_next_bytes);
             a.wt_stores = wt_bits(h, e, B, 8);
+            if (h->d_tl) a.tl = h->d_tl + li * (size_t)TL_SLOTS;
             HIP_TRY(conv_lite_launch(e.lite, a, st));   // two styles: its blend prologue (pro_ab1, pro_w)
         } else {
             HIP_TRY(conv_launch(e.tile, a, st));
@@ -888,6 +891,42 @@ int rst_profile_end(rst_handle* h, float* conv_ms, float* layer_ms, int* steps) 
             layer_ms[i] += b;
         }
     h->prof_free();
+    return RST_OK;
+}
+
+int rst_timeline_begin(rst_handle* h) {
+    if (h == nullptr) return fail(RST_ERR_INVALID, "rst_timeline_begin: null handle");
+    h->tl_free();
+    const size_t bytes = h->layers.size() * (size_t)TL_SLOTS * sizeof(unsigned long long);
+    HIP_TRY(hipMalloc(&h->d_tl, bytes));
+    HIP_TRY(hipMemset(h->d_tl, 0, bytes));
+    HIP_TRY(hipDeviceSynchronize());
+    return RST_OK;
+}
+
+int rst_timeline_read(rst_handle* h, double* end_us, int n) {
+    if (h == nullptr || end_us == nullptr || n != (int)h->layers.size())
+        return fail(RST_ERR_INVALID, "rst_timeline_read: bad argument");
+    if (h->d_tl == nullptr) return fail(RST_ERR_INVALID, "rst_timeline_read: no rst_timeline_begin");
+    std::vector<unsigned long long> tl((size_t)n * TL_SLOTS);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(tl.data(), h->d_tl, tl.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long t0 = 0;
+    for (int i = 0; i < n; ++i) {
+        unsigned long long m = 0;
+        for (int k = 0; k < TL_SLOTS; ++k) m = std::max(m, tl[(size_t)i * TL_SLOTS + k]);
+        end_us[i] = m ? (double)m : -1.0;
+        if (m && !t0) t0 = m;
+    }
+    for (int i = 0; i < n; ++i)   // 100-MHz ticks -> us after the first stamped layer's end
+        if (end_us[i] >= 0.0) end_us[i] = (end_us[i] - (double)t0) * 0.01;
+    return RST_OK;
+}
+
+int rst_timeline_end(rst_handle* h) {
+    if (h == nullptr) return fail(RST_ERR_INVALID, "rst_timeline_end: null handle");
+    HIP_TRY(hipDeviceSynchronize());
+    h->tl_free();
     return RST_OK;
 }
 

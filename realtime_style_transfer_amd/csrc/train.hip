@@ -296,6 +296,8 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restri
 // Even H, W and C % 4 == 0 (every VGG16 pool here): one thread per (pooled pixel, channel quad) reads the
 // window's four pixels and the pooled gradient as 16-B vectors once and writes the four gradient pixels
 // (the element-per-thread form above re-read each window four times through 64-bit index math: 2.3 TB/s).
+// XBF16: the forward activations x are stored as bf16 bits (the plain-bf16 VGG16): four 8-B window loads
+template <bool XBF16>
 __global__ __launch_bounds__(256) void maxpool2_bwd4_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                                                             float* __restrict__ gx, int B, int H, int W, int C,
                                                             int accumulate) {
@@ -310,8 +312,19 @@ __global__ __launch_bounds__(256) void maxpool2_bwd4_kernel(const float* __restr
         const int oy = p % Ho;
         const int b = p / Ho;
         const size_t r0 = (((size_t)b * H + 2 * oy) * W + 2 * ox) * C + 4 * c4, r1 = r0 + (size_t)W * C;
-        const f4 v0 = *reinterpret_cast<const f4*>(x + r0), v1 = *reinterpret_cast<const f4*>(x + r0 + C);
-        const f4 v2 = *reinterpret_cast<const f4*>(x + r1), v3 = *reinterpret_cast<const f4*>(x + r1 + C);
+        f4 v0, v1, v2, v3;
+        if constexpr (XBF16) {
+            const float4 u0 = ld_bf16x4(x, r0), u1 = ld_bf16x4(x, r0 + C), u2 = ld_bf16x4(x, r1), u3 = ld_bf16x4(x, r1 + C);
+            v0 = f4{u0.x, u0.y, u0.z, u0.w};
+            v1 = f4{u1.x, u1.y, u1.z, u1.w};
+            v2 = f4{u2.x, u2.y, u2.z, u2.w};
+            v3 = f4{u3.x, u3.y, u3.z, u3.w};
+        } else {
+            v0 = *reinterpret_cast<const f4*>(x + r0);
+            v1 = *reinterpret_cast<const f4*>(x + r0 + C);
+            v2 = *reinterpret_cast<const f4*>(x + r1);
+            v3 = *reinterpret_cast<const f4*>(x + r1 + C);
+        }
         const f4 g = *reinterpret_cast<const f4*>(gy + (size_t)i * 4);
         f4 o0, o1, o2, o3;
 #pragma unroll
@@ -341,14 +354,19 @@ __global__ __launch_bounds__(256) void maxpool2_bwd4_kernel(const float* __restr
 }
 
 hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, int accumulate,
-                               hipStream_t st) {
+                               hipStream_t st, bool x_bf16) {
     if (H % 2 == 0 && W % 2 == 0 && C % 4 == 0 && (size_t)B * H * W * C < ((size_t)1 << 31)) {
         const size_t n = (size_t)B * (H / 2) * (W / 2) * (C / 4);
         unsigned blocks = (unsigned)((n + 255) / 256);
         if (blocks > 32768) blocks = 32768;
-        hipLaunchKernelGGL(maxpool2_bwd4_kernel, dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C, accumulate);
+        if (x_bf16)
+            hipLaunchKernelGGL(maxpool2_bwd4_kernel<true>, dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C, accumulate);
+        else
+            hipLaunchKernelGGL(maxpool2_bwd4_kernel<false>, dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C,
+                               accumulate);
         return hipGetLastError();
     }
+    if (x_bf16) return hipErrorInvalidValue;   // the bf16 VGG16 pools are all even-sized, C % 4 == 0
     const size_t n = (size_t)B * H * W * C;
     unsigned blocks = (unsigned)((n + 255) / 256);
     if (blocks > 16384) blocks = 16384;
@@ -356,20 +374,24 @@ hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B
     return hipGetLastError();
 }
 
-// g (+)= scale * (a - b)   (feature-loss gradient; accumulate into an existing gradient)
+// g (+)= scale * (a - b)   (feature-loss gradient; accumulate into an existing gradient; BF16: a, b bf16 bits)
+template <bool BF16>
 __global__ __launch_bounds__(256) void scaled_diff_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                           float scale, float* __restrict__ g, size_t n, int accumulate) {
     for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        const float v = scale * (a[i] - b[i]);
+        const float v = scale * (BF16 ? ld_bf16(a, i) - ld_bf16(b, i) : a[i] - b[i]);
         g[i] = accumulate ? g[i] + v : v;
     }
 }
 
 hipError_t scaled_diff_launch(const float* a, const float* b, float scale, float* g, size_t n, int accumulate,
-                              hipStream_t st) {
+                              hipStream_t st, bool in_bf16) {
     unsigned blocks = (unsigned)((n + 255) / 256);
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(scaled_diff_kernel, dim3(blocks), dim3(256), 0, st, a, b, scale, g, n, accumulate);
+    if (in_bf16)
+        hipLaunchKernelGGL(scaled_diff_kernel<true>, dim3(blocks), dim3(256), 0, st, a, b, scale, g, n, accumulate);
+    else
+        hipLaunchKernelGGL(scaled_diff_kernel<false>, dim3(blocks), dim3(256), 0, st, a, b, scale, g, n, accumulate);
     return hipGetLastError();
 }
 

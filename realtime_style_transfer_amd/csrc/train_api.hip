@@ -372,8 +372,9 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
     const size_t f5 = (size_t)c5.H * c5.W * c5.cout;
     int which = 0;
     float* g = t->d_vg[0];
+    const bool act = h->act_bf16;   // the forward activations (ReLU masks, pool routing, features) are bf16 bits
     RST_HIP_TRY(scaled_diff_launch(c5.d_out, h->d_content_feat, (float)(ls.content_factor / (double)f5), g, B * f5, 0,
-                                   st));
+                                   st, act));
     for (int i = CONTENT_IDX; i >= 0; --i) {
         const VggConv& c = h->convs[i];
         const ConvBwd& vb = t->vgg[i];
@@ -405,6 +406,7 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
             a.nchunks = pb.nchunks;
             a.pro_mode = PRO_MASK;
             a.epi_mode = EPI_NONE;
+            a.act_bf16 = act ? 4 : 0;
             RST_HIP_TRY(conv_launch(pb.tile, a, st));
             RST_HIP_TRY(tap3_sum_launch(pbuf, gimg, B, c.H, c.W, st));
             break;
@@ -432,6 +434,7 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
         a.pro_mode = PRO_MASK;
         a.epi_mode = EPI_NONE;
         a.wt_stores = train_wt(t, (size_t)B * c.H * c.W * c.cin, 8);
+        a.act_bf16 = act ? 4 : 0;
         RST_HIP_TRY(conv_launch(vb.tile, a, st));
         if (i == 0) break;
         const int p = i - 1;
@@ -456,7 +459,10 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
                                                     scale, t->d_gram_packed, B, st));
             for (int b = 0; b < B; ++b) {
                 ConvArgs m{};
-                m.in = cp.d_out + (size_t)b * hw * C;
+                m.in = act ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(cp.d_out) +
+                                                            (size_t)b * hw * C)
+                           : cp.d_out + (size_t)b * hw * C;
+                m.act_bf16 = act ? 1 : 0;
                 m.wpk = gbf16 ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(t->d_gram_packed) +
                                                                (size_t)b * gb.n_packed)
                               : t->d_gram_packed + (size_t)b * gb.n_packed;
@@ -479,7 +485,8 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
                 RST_HIP_TRY(conv_launch(gb.tile, m, st));
             }
         }
-        if (pooled) RST_HIP_TRY(maxpool2_bwd_launch(cp.d_out, t->d_vpool, gprev, B, cp.H, cp.W, cp.cout, k >= 0, st));
+        if (pooled)
+            RST_HIP_TRY(maxpool2_bwd_launch(cp.d_out, t->d_vpool, gprev, B, cp.H, cp.W, cp.cout, k >= 0, st, act));
         which ^= 1;
         g = gprev;
     }
@@ -739,6 +746,7 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
         }
         // same geometry as the launch (the split count and slab size depend on every field)
         WgradArgs w = wgrad_geometry(s, T.e, B);
+        w.x6 = T.e.kind == K_WINOX6 || T.e.kind == K_WINO9X6 ? 1 : 0;   // as backward() sets it before choosing
         w.nsplit = wgrad_choose_splits(w);
         slab = std::max(slab, wgrad_slab_bytes(w));
     }
@@ -923,6 +931,7 @@ int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const fl
                                   float* losses, float* grad, float* grad_style_params, void* stream) {
     if (!t || !content || !style_params || !gt_content || !gt_style || !prediction || !losses || !grad)
         return set_error(RST_ERR_INVALID, "rst_trainer_compute_gradients: null argument");
+    t->gstyle_recorded = false;   // a failure on any path below leaves no stale event for wait_style_gradient
     if (batch <= 0 || batch > t->shape.max_batch)
         return set_error(RST_ERR_INVALID, "rst_trainer_compute_gradients: batch outside [1, max_batch]");
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -943,7 +952,6 @@ int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const fl
     RST_HIP_TRY(hipMemsetAsync(grad, 0, t->nw * 4, st));
     float* gs = grad_style_params ? grad_style_params : t->d_gstyle;
     RST_HIP_TRY(hipMemsetAsync(gs, 0, (size_t)B * t->P * 4, st));
-    t->gstyle_recorded = false;
     if ((r = backward(t, content, B, grad, gs, st)) != RST_OK) return r;
     t->gstyle_recorded = true;
     return RST_OK;

@@ -226,6 +226,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const unsigned f = x6_prefetch_input(a, n_units, PRO == PRO_AFF_RES);
         const l2_touch_t u = l2_touch_xcd_slice<YT, 2>(a.u_next, a.u_next_bytes);
         l2_touch_keep(l2_touch_t{f ^ u.x, u.y}, a.batch < 0, smem);
+        tl_stamp_end(a.tl);
         return;
     }
     int bid = xcd_tile_order(blockIdx.x, n_units);
@@ -681,6 +682,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     XTL(3);
     l2_touch_keep(upf, a.batch < 0, smem);
+    tl_stamp_end(a.tl);
 }
 
 bool wino_x6_supported(int kh, int stride, int cin, int cout) {

@@ -202,6 +202,24 @@ class StyleTransferModel:
         _lib.check(lib.rst_profile_end(self._handle, conv, lay, ctypes.byref(steps)))
         return list(conv), list(lay), steps.value
 
+    def timeline_begin(self):
+        """Per-layer kernel end stamps for the forwards issued afterwards, eager or captured into a hipGraph
+        (rst_timeline_begin: the residual convs and the narrow convs stamp; a measurement aid)."""
+        _lib.check(_lib.load().rst_timeline_begin(self._handle))
+
+    def timeline_read(self) -> np.ndarray:
+        """-> end[L] in us after the first stamped layer's end (NaN where the layer's kernel does not stamp) of the
+        most recent forward; end[k] - end[k-1] is layer k's share of a back-to-back graph replay."""
+        L = self.num_layers()
+        buf = (ctypes.c_double * L)()
+        _lib.check(_lib.load().rst_timeline_read(self._handle, buf, L))
+        a = np.array(list(buf))
+        a[a < 0] = np.nan
+        return a
+
+    def timeline_end(self):
+        _lib.check(_lib.load().rst_timeline_end(self._handle))
+
     def layer_kernel_id(self, idx: int) -> int:
         return _lib.load().rst_layer_kernel_id(self._handle, idx)
 

@@ -777,11 +777,16 @@ class CheckpointManager:
         return int(c)
 
     def save(self, checkpoint_number=None, check_interval: bool = True) -> Optional[str]:
-        if self.checkpoint_interval is not None and check_interval:
+        # tf.train.CheckpointManager.save: with an interval, a save at the last saved step is always skipped, the
+        # interval test applies only when check_interval is set, and every save records its step (a forced save at
+        # step 31 moves the next cadence save to >= 31 + interval)
+        if self.checkpoint_interval is not None:
             step = self._step()
-            if self._last_checkpoint_step is not None and (
-                    step == self._last_checkpoint_step or step < self._last_checkpoint_step + self.checkpoint_interval):
-                return None
+            if self._last_checkpoint_step is not None:
+                if step == self._last_checkpoint_step:
+                    return None
+                if check_interval and step < self._last_checkpoint_step + self.checkpoint_interval:
+                    return None
             self._last_checkpoint_step = step
         n = int(checkpoint_number) if checkpoint_number is not None else self.checkpoint.save_counter + 1
         prefix = self.directory / f"{self.checkpoint_name}-{n}"

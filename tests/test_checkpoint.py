@@ -292,6 +292,17 @@ def test_checkpoint_manager_interval_and_recovery(tmp_path):
     mgr2.save(40)
     names = sorted(p.name for p in d.iterdir() if p.name.endswith(".index"))
     assert names == ["ckpt-31.index", "ckpt-40.index"]
+    # as tf.train.CheckpointManager, a forced save records its step (the next cadence save is due at
+    # >= 31 + 10) and a second save at the same step is skipped even when forced
+    m3 = ck.CheckpointManager(ck.Checkpoint(a), tmp_path / "c3", max_to_keep=None, checkpoint_interval=10,
+                              step_counter=lambda: step[0])
+    got = []
+    for s_ in [0, 5, 10, 31, 31, 40, 41, 50, 51]:
+        step[0] = s_
+        forced = s_ == 31
+        if m3.save(s_, check_interval=not forced) is not None:
+            got.append(s_)
+    assert got == [0, 10, 31, 41, 51]
 
 
 def test_object_graph_slot_variables():

@@ -76,3 +76,40 @@ def test_style_loss_matches_oracle(precision, rtol, ftol):
     with pytest.raises(ValueError):
         compute_loss(torch.zeros(B, H, W, 3, device='cuda'), {'content': torch.zeros(B, H, W, 3, device='cuda'),
                                                               'style': torch.zeros(B, 2, H, W, 3, device='cuda')})
+
+
+def test_bf16_activation_storage_equals_rounded_f32_storage():
+    """The plain-bf16 loss stores every VGG16 layer output as bf16 (Keras mixed_bfloat16 layer outputs). Its convs
+    already round their inputs to bf16 and a max pool commutes with the (monotone) rounding, so every stored feature
+    map must equal the bf16 rounding of the f32-stored one (RST_VGG_ACT_F32=1) bit for bit, and the style loss (Grams
+    of bf16-rounded features either way) must be bitwise equal; only the content term sees the rounded block5_conv3."""
+    _need_gpu()
+    import os
+    from oracle import numpy_ref as R
+    from realtime_style_transfer_amd.styleLoss import (VGG16_LAYER_NAMES, StyleLossModelVGG, init_vgg16_weights,
+                                                       make_style_loss_function)
+    H, W, B = 48, 64, 2
+    ws = init_vgg16_weights(seed=3)
+    rng = np.random.default_rng(21)
+    pred, content = rng.random((B, H, W, 3)).astype(np.float32), rng.random((B, H, W, 3)).astype(np.float32)
+    style = rng.random((B, 1, H, W, 3)).astype(np.float32)
+    runs = []
+    for f32_store in (False, True):
+        if f32_store:
+            os.environ["RST_VGG_ACT_F32"] = "1"
+        try:
+            model = StyleLossModelVGG((H, W, 3), weights=ws, max_batch=B, precision="bf16")
+        finally:
+            os.environ.pop("RST_VGG_ACT_F32", None)
+        compute_loss, _ = make_style_loss_function(model, (H, W, 3), 1, with_depth_loss=False)
+        out = compute_loss(torch.from_numpy(pred).cuda(), {'content': torch.from_numpy(content).cuda(),
+                                                           'style': torch.from_numpy(style).cuda()})
+        feats = [model.feature(n, B).cpu().numpy() for n in VGG16_LAYER_NAMES]   # the prediction's, run last
+        runs.append(({k: v.cpu().numpy() for k, v in out.items()}, feats))
+    (lb, fb), (lf, ff) = runs
+    for i in range(13):
+        assert np.array_equal(fb[i], R.bf16_round(ff[i]).astype(np.float32)), i
+    assert np.array_equal(lb['style_loss'], lf['style_loss'])
+    assert np.array_equal(lb['total_variation_loss'], lf['total_variation_loss'])
+    rel = np.abs(lb['feature_loss'] - lf['feature_loss']) / np.abs(lf['feature_loss'])
+    assert rel.max() < 2e-2   # the content term on bf16-rounded block5_conv3 features

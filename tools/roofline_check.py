@@ -1,13 +1,18 @@
 #!/usr/bin/env python3
-"""Recompute bench.py's `roofline.frac` from a committed rocprofv3 kernel-stats summary.
+"""Recompute bench.py's `roofline.frac` from a committed rocprofv3 kernel summary.
 
-bench.py times the dominant kernel with HIP events on the forward's stream; rocprofv3 --kernel-trace
---stats times every launch on the device. This script takes the executed FLOPs per launch that bench
-reports for the dominant kernel, divides by rocprof's average duration of the same kernel (all template
-instantiations that share bench's short name, launch-weighted) and compares the resulting fraction of
-the pipe's peak with bench's own.
+bench.py times the dominant kernel inside the headline's hipGraph frame replay (bench.graph_layer_ms: in-kernel end
+stamps, a layer's share = its end minus its predecessor's end); rocprofv3 --kernel-trace times every launch on the
+device. This script takes the executed FLOPs per launch that bench reports for the dominant kernel, divides by
+rocprof's average duration of the same kernel (all template instantiations that share bench's short name,
+launch-weighted) and compares the resulting fraction of the pipe's peak with bench's own.
 
-Usage: python tools/roofline_check.py <bench_json_line_file> <kernel_stats.csv> [tolerance=0.05]
+With a kernel TRACE (run_kernel_trace.csv) only the graph-replayed frames count: the dispatches are grouped into
+frames at each launch of the frame's first kernel (the start conv), and a frame is a graph
+replay when its kernels ran back to back (span - sum of durations < 5 us; eager frames have host launch gaps). With a
+kernel STATS file every launch counts (graph and eager alike).
+
+Usage: python tools/roofline_check.py <bench_json_line_file> <kernel_trace.csv | kernel_stats.csv> [tolerance=0.02]
 Exit status 1 when the two fractions differ by more than the tolerance (relative).
 """
 import csv
@@ -36,18 +41,46 @@ def rocprof_avg_ns(path, name):
     return (total / calls if calls else None), calls
 
 
+def trace_graph_avg_ns(path, name, frame_start="wino9f3_kernel<false>"):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    frames, cur = [], None
+    for r in rows:
+        if frame_start in r["Kernel_Name"]:
+            cur = []
+            frames.append(cur)
+        if cur is not None:
+            cur.append(r)
+    dur = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])   # noqa: E731
+    calls, total, nframes = 0, 0.0, 0
+    for fr in frames:
+        span = int(fr[-1]["End_Timestamp"]) - int(fr[0]["Start_Timestamp"])
+        if span - sum(dur(r) for r in fr) >= 5000:
+            continue   # an eager frame (host launch gaps between its kernels)
+        nframes += 1
+        for r in fr:
+            if short_name(r["Kernel_Name"]) == name:
+                calls += 1
+                total += dur(r)
+    return (total / calls if calls else None), calls, nframes
+
+
 def main():
     b = bench_line(sys.argv[1])
-    tol = float(sys.argv[3]) if len(sys.argv) > 3 else 0.05
+    tol = float(sys.argv[3]) if len(sys.argv) > 3 else 0.02
     rf = b["roofline"]
-    avg_ns, calls = rocprof_avg_ns(sys.argv[2], rf["kernel"])
+    frames = None
+    if "Start_Timestamp" in open(sys.argv[2]).readline():
+        avg_ns, calls, frames = trace_graph_avg_ns(sys.argv[2], rf["kernel"])
+    else:
+        avg_ns, calls = rocprof_avg_ns(sys.argv[2], rf["kernel"])
     if avg_ns is None:
         raise SystemExit(f"kernel {rf['kernel']!r} not in {sys.argv[2]}")
     achieved = rf["exec_flops_per_launch"] / (avg_ns * 1e-9) / 1e12
     frac = achieved / rf["peak"]
     rel = abs(frac - rf["frac"]) / rf["frac"]
     print(json.dumps({"kernel": rf["kernel"], "bench_avg_ms": rf["avg_launch_ms"], "rocprof_avg_ms": avg_ns * 1e-6,
-                      "rocprof_calls": calls, "bench_frac": rf["frac"], "rocprof_frac": round(frac, 4),
+                      "rocprof_calls": calls, "rocprof_graph_frames": frames, "bench_timing": rf.get("timing"),
+                      "bench_frac": rf["frac"], "rocprof_frac": round(frac, 4),
                       "rel_diff": round(rel, 4), "within_tolerance": rel <= tol}))
     return 0 if rel <= tol else 1
 
