@@ -29,9 +29,6 @@
 
 #include "kernels.h"
 
-#ifndef LAST_SKIP
-#define LAST_SKIP 0   // tools/last_bench knobs: 1 no MFMAs, 2 no input loads, 8 no epilogue, 16 no ring refill
-#endif
 #ifdef LAST_PROF
 // s_memrealtime (100 MHz) per (workgroup < 256, wave): start, staged, MFMAs done, end
 __device__ unsigned long long last_tl[256][4][4];
@@ -184,11 +181,7 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
             constexpr int k = decltype(Kk)::value;
             const int it = tid + 256 * k, r = it / ROW_F4, xp = (it % ROW_F4) >> 2;
             const int iy = min(max(y0 - PAD + r0 + r, 0), H - 1), ix = min(max(x0 - PAD + xp, 0), W - 1);
-#if LAST_SKIP & 2
-            pre[k] = f32x4{(float)iy, (float)ix, 0.f, 0.f};
-#else
             pre[k] = *reinterpret_cast<const f32x4*>(a.in + (((size_t)b * H + iy) * W + ix) * CIN + 4 * q);
-#endif
             if constexpr (BLEND) prw[k] = a.pro_w[((size_t)b * H + iy) * W + ix];
         });
     };
@@ -248,34 +241,33 @@ __global__ __launch_bounds__(256, 1) void last_x6_kernel(LastArgs a) {
         for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
-        if constexpr ((LAST_SKIP & 1) == 0) {
-            // MFMA step s = (tile t, ky): A pieces of input row 4k + wave + ky, read one step ahead
-            auto read = [&](int s, short8 (&A)[3]) __attribute__((always_inline)) {
-                const unsigned char* p = abase + ((4 * k + wave + s % K) % RING) * SLOT_B + 32 * (s / K) * 16;
-                A[0] = *reinterpret_cast<const short8*>(p);
-                A[1] = *reinterpret_cast<const short8*>(p + 2 * XW * 16);
-                A[2] = *reinterpret_cast<const short8*>(p + 4 * XW * 16);
-            };
-            short8 A0[3], A1[3];
-            read(0, A0);
-            sfor<0, NT * K>([&](auto S) __attribute__((always_inline)) {
-                constexpr int s = decltype(S)::value, t = s / K, ky = s % K;
-                if constexpr (s + 1 < NT * K) {
-                    if constexpr ((s & 1) == 0) read(s + 1, A1);
-                    else read(s + 1, A0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                constexpr int ap[6] = {0, 0, 1, 0, 1, 2}, bp[6] = {0, 1, 0, 2, 1, 0};
-                sfor<0, 6>([&](auto M) __attribute__((always_inline)) {
-                    constexpr int mm = decltype(M)::value;
-                    if constexpr ((s & 1) == 0)
-                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0[ap[mm]], bw[ky][bp[mm]], acc[t], 0, 0, 0);
-                    else
-                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[ap[mm]], bw[ky][bp[mm]], acc[t], 0, 0, 0);
-                });
-                __builtin_amdgcn_sched_barrier(0);
+        // MFMA step s = (tile t, ky): A pieces of input row 4k + wave + ky, read one step ahead
+        auto read = [&](int s, short8 (&A)[3]) __attribute__((always_inline)) {
+            const unsigned char* p = abase + ((4 * k + wave + s % K) % RING) * SLOT_B + 32 * (s / K) * 16;
+            A[0] = *reinterpret_cast<const short8*>(p);
+            A[1] = *reinterpret_cast<const short8*>(p + 2 * XW * 16);
+            A[2] = *reinterpret_cast<const short8*>(p + 4 * XW * 16);
+        };
+        short8 A0[3], A1[3];
+        read(0, A0);
+        sfor<0, NT * K>([&](auto S) __attribute__((always_inline)) {
+            constexpr int s = decltype(S)::value, t = s / K, ky = s % K;
+            if constexpr (s + 1 < NT * K) {
+                if constexpr ((s & 1) == 0) read(s + 1, A1);
+                else read(s + 1, A0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            constexpr int ap[6] = {0, 0, 1, 0, 1, 2}, bp[6] = {0, 1, 0, 2, 1, 0};
+            sfor<0, 6>([&](auto M) __attribute__((always_inline)) {
+                constexpr int mm = decltype(M)::value;
+                if constexpr ((s & 1) == 0)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0[ap[mm]], bw[ky][bp[mm]], acc[t], 0, 0, 0);
+                else
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[ap[mm]], bw[ky][bp[mm]], acc[t], 0, 0, 0);
             });
-        }
+            __builtin_amdgcn_sched_barrier(0);
+        });
+
         LSST(k, 1);
         // ---- diagonal sum over kx through the wave's transposed P buffer [28 n][x'] -----------------------
         if (n < 28)

@@ -41,10 +41,6 @@
 #define LITE_OSTAGE0 1   // the same for the x6 strided convs
 #endif
 
-#ifndef LITE_SKIP
-#define LITE_SKIP 0   // tools/lite_bench knobs: 1 no halo loads, 2 no MFMAs, 8 no output stores, 32 no statistics
-#endif
-
 namespace rst {
 
 #ifdef LITE_PROF
@@ -239,12 +235,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             constexpr int k = decltype(K)::value;
             const int hy = k < NMAIN ? min(rsub + RPP * k, HR - 1) : ehy;
             const int gi = ((rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)) * CIN + co + 4 * q;
-#if LITE_SKIP & 1
-            hreg[st][k] = f32x4{(float)gi, 0.f, 0.f, 0.f};
-#else
             hreg[st][k] = *reinterpret_cast<const f32x4*>(a.in + gi);
             if constexpr (PRO == PRO_AFF_RES) rreg[st][k] = *reinterpret_cast<const f32x4*>(a.res + gi);
-#endif
             if constexpr (BLEND) bw[st][k] = a.pro_w[(rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)];
         });
         if constexpr (NCH > 1) load_w(ch);
@@ -495,8 +487,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     };
     auto compute = [&]() __attribute__((always_inline)) {
         if constexpr (X6) {
-            if constexpr ((LITE_SKIP & 2) == 0) compute_x6();
-        } else if constexpr ((LITE_SKIP & 2) == 0) {
+            compute_x6();
+        } else {
             f32x4 A0[NA], B0[NB], A1[NA], B1[NB];
             read_step(std::integral_constant<int, 0>{}, A0, B0);
             sfor<0, NSTEP>([&](auto U) __attribute__((always_inline)) {
@@ -615,7 +607,6 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         s += acc[ph][j];
                     }
                 cnt = 4.f * C::NACC;
-#if (LITE_SKIP & 8) == 0
                 lds_barrier();   // every wave's MFMA operand reads are done
                 float* const ob = smem + wave * OST_FL;
 #pragma unroll
@@ -638,7 +629,6 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                             *reinterpret_cast<f32x4*>(a.out + obase + e) = v;
                     }
                 }
-#endif
             } else if (full) {
 #pragma unroll
                 for (int ph = 0; ph < 4; ++ph)
@@ -647,14 +637,12 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         const int qq = T.x0 + M::row(j, lane);
                         const float v = acc[ph][j] + bias;
                         acc[ph][j] = v;
-#if (LITE_SKIP & 8) == 0
                         if (a.wt_stores)
                             __builtin_amdgcn_raw_buffer_store_b32(
                                 __builtin_bit_cast(unsigned, v), osrd,
                                 (int)((orow + ((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC - a.out) * 4), 0, 16);
                         else
                             orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
-#endif
                         s += v;
                     }
                 cnt = 4.f * C::NACC;
@@ -673,7 +661,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         }
                     }
             }
-            if (to_acc && (LITE_SKIP & 32) == 0) {   // per-wave two-pass partials (see acc_flush)
+            if (to_acc) {   // per-wave two-pass partials (see acc_flush)
                 if constexpr (MS == 16) {
                     s = lane_xor_sum<16>(s);
                     cnt = lane_xor_sum<16>(cnt);
@@ -701,7 +689,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                     accS += dS;
                     if (cnt > 0.f) accQ += (double)m2 + dS * dS / (double)cnt;
                 }
-            } else if (a.part != nullptr && (LITE_SKIP & 32) == 0) {
+            } else if (a.part != nullptr) {
                 // lanes n, n + MS, ... hold column n: reduce over them, then over the 4 waves (fixed order)
                 if constexpr (MS == 16) {
                     s = lane_xor_sum<16>(s);

@@ -182,7 +182,8 @@ int rst_loss_create(const rst_loss_shape* shape, const float* vgg_weights_host, 
         const float* bias = wp + kc;
         wp += kc + c.cout;
         const int planes = bf16_planes(shape->precision);
-        const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cin, c.cout, planes, (long long)B * H * W, &c.tile);
+        const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cin, c.cout, planes, (long long)B * H * W, &c.tile,
+                                                       h->act_bf16 && i > 0);
         if (!bf3 && !conv_select(3, 1, cin, c.cout, &c.tile)) {
             delete h;
             return set_error(RST_ERR_UNSUPPORTED, "no conv tile configuration for VGG layer " + std::to_string(i));

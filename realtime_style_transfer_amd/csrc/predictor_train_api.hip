@@ -57,7 +57,11 @@ struct rst_predictor_trainer {
     static constexpr int DZR = 3;
     float* dzr[DZR] = {};
     hipStream_t wside = nullptr;
-    hipEvent_t ev_dz[DZR] = {}, ev_wg[DZR] = {}, ev_chain = nullptr, ev_done = nullptr;
+    // every fork / join of one backward records a fresh event (evs[ev_next++]): no event is recorded twice within a
+    // call, so a hipGraph capture of the step sees each dependency once (re-recording the ring's events within one
+    // capture crashed the capture's end on this stack, tools/train_graph_check.py, profiles/r06)
+    std::vector<hipEvent_t> evs;
+    size_t ev_next = 0;
     bool serial_wgrad = false;              // RST_SERIAL_PREDICTOR_WGRAD=1 at creation: everything on the caller's stream
     float4* bn_part = nullptr;
     float2* consts = nullptr;
@@ -71,12 +75,7 @@ struct rst_predictor_trainer {
             (void)hipStreamSynchronize(wside);
             (void)hipStreamDestroy(wside);
         }
-        for (int k = 0; k < DZR; ++k) {
-            if (ev_dz[k]) (void)hipEventDestroy(ev_dz[k]);
-            if (ev_wg[k]) (void)hipEventDestroy(ev_wg[k]);
-        }
-        if (ev_chain) (void)hipEventDestroy(ev_chain);
-        if (ev_done) (void)hipEventDestroy(ev_done);
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
         for (void* p : allocs) (void)hipFree(p);
     }
     template <typename T>
@@ -235,12 +234,11 @@ int rst_predictor_trainer_create(const rst_predictor_shape* shape, const float* 
     {
         const char* sw = getenv("RST_SERIAL_PREDICTOR_WGRAD");
         t->serial_wgrad = sw != nullptr && sw[0] == '1';
-        bool ok = hipStreamCreateWithFlags(&t->wside, hipStreamNonBlocking) == hipSuccess &&
-                  hipEventCreateWithFlags(&t->ev_chain, hipEventDisableTiming) == hipSuccess &&
-                  hipEventCreateWithFlags(&t->ev_done, hipEventDisableTiming) == hipSuccess;
-        for (int k = 0; ok && k < rst_predictor_trainer::DZR; ++k)
-            ok = hipEventCreateWithFlags(&t->ev_dz[k], hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&t->ev_wg[k], hipEventDisableTiming) == hipSuccess;
+        bool ok = hipStreamCreateWithFlags(&t->wside, hipStreamNonBlocking) == hipSuccess;
+        // forks: the heads' and one per SE unit; two per unit (norm-backward output handed over, released); the join
+        t->evs.assign(2 * t->plan.units.size() + t->plan.ses.size() + 4, nullptr);
+        for (size_t k = 0; ok && k < t->evs.size(); ++k)
+            ok = hipEventCreateWithFlags(&t->evs[k], hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             delete t;
             return set_error(RST_ERR_HIP, "rst_predictor_trainer_create: stream / event creation failed");
@@ -319,11 +317,20 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
     // Same kernels on the same operands: bitwise the serial order.
     const bool par = !t->serial_wgrad;
     hipStream_t ws = par ? t->wside : st;
+    t->ev_next = 0;
+    auto next_ev = [&](hipEvent_t* ev) -> hipError_t {
+        if (t->ev_next >= t->evs.size()) return hipErrorInvalidValue;
+        *ev = t->evs[t->ev_next++];
+        return hipSuccess;
+    };
     auto fork = [&]() -> hipError_t {
         if (!par) return hipSuccess;
-        hipError_t e = hipEventRecord(t->ev_chain, st);
-        return e != hipSuccess ? e : hipStreamWaitEvent(ws, t->ev_chain, 0);
+        hipEvent_t ev;
+        hipError_t e = next_ev(&ev);
+        if (e == hipSuccess) e = hipEventRecord(ev, st);
+        return e != hipSuccess ? e : hipStreamWaitEvent(ws, ev, 0);
     };
+    hipEvent_t ev_wg[rst_predictor_trainer::DZR] = {};   // the weight gradient that last read ring slot k
     RST_HIP_TRY(hipMemsetAsync(grad, 0, P.total * sizeof(float), st));
     // heads (stylePrediction.py:60-71): P = W2^T h + b2, h = W1^T gap + b1
     RST_HIP_TRY(rowdot_launch(d_style_params, B, NP, w + P.head_w2, NS, 1.f, t->dhid, st));
@@ -362,11 +369,13 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
         a.HW = u.Ho * u.Wo;
         a.C = u.cout;
         a.act = u.act;
-        if (par && j >= rst_predictor_trainer::DZR) RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_wg[slot], 0));
+        if (par && ev_wg[slot] != nullptr) RST_HIP_TRY(hipStreamWaitEvent(st, ev_wg[slot], 0));
         RST_HIP_TRY(bn_backward_launch(a, st));
         if (par) {
-            RST_HIP_TRY(hipEventRecord(t->ev_dz[slot], st));
-            RST_HIP_TRY(hipStreamWaitEvent(ws, t->ev_dz[slot], 0));
+            hipEvent_t ev_dz;
+            RST_HIP_TRY(next_ev(&ev_dz));
+            RST_HIP_TRY(hipEventRecord(ev_dz, st));
+            RST_HIP_TRY(hipStreamWaitEvent(ws, ev_dz, 0));
         }
         if (u.res >= 0)   // y = BN(z) + shortcut: the shortcut's consumer adds this in its dgrad
             RST_HIP_TRY(hipMemcpyAsync(t->dres[u.res], t->dyb[i], (size_t)B * u.Ho * u.Wo * u.cout * sizeof(float),
@@ -407,11 +416,16 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
                                             u.stride, u.pad_t, u.pad_l, st));
                 break;
         }
-        if (par) RST_HIP_TRY(hipEventRecord(t->ev_wg[slot], ws));
+        if (par) {
+            RST_HIP_TRY(next_ev(&ev_wg[slot]));
+            RST_HIP_TRY(hipEventRecord(ev_wg[slot], ws));
+        }
     }
     if (par) {   // join: every gradient is in `grad` when the caller's stream goes on
-        RST_HIP_TRY(hipEventRecord(t->ev_done, ws));
-        RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_done, 0));
+        hipEvent_t ev_done;
+        RST_HIP_TRY(next_ev(&ev_done));
+        RST_HIP_TRY(hipEventRecord(ev_done, ws));
+        RST_HIP_TRY(hipStreamWaitEvent(st, ev_done, 0));
     }
     return RST_OK;
 }

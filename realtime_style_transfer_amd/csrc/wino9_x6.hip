@@ -93,12 +93,8 @@ __device__ __forceinline__ void split8(const float (&v)[8], short8 (&A)[3]) {
 
 }  // namespace
 
-// Experiment knobs (tools/wino9_x6_bench only; never set in the library build): W9_SKIP bit0 = no U loads
-// in the loop, bit1 = no transform (patch reads), bit2 = no MFMAs, bit3 = no split, bit4 = no global loads of the
-// next tile's patch (the LDS stores stay)
-#ifndef W9_SKIP
-#define W9_SKIP 0
-#endif
+// (The knock-out measurements of DESIGN.md §3 were built from this file as of commit 94f9b44; the product kernel
+// carries no such switches.)
 // (Measured and removed, round 4: a software-pipelined unit loop with the next unit's operand preparation beside
 // the MFMAs, and an s_sleep stagger of the qh = 1 waves at each tile start — both slower,
 // profiles/r04/w9_stagger_pipe_slp.log.)
@@ -138,23 +134,16 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
     short8 ub[2][2][3];   // [buffer][q of the pair][piece]
     auto load_u = [&](auto BUF, int ab) __attribute__((always_inline)) {   // ab == 9: the channel-16 K-step
         constexpr int buf = decltype(BUF)::value;
-        if constexpr (!(W9_SKIP & 1)) {
-            sfor<0, 2>([&](auto Q) __attribute__((always_inline)) {
-                constexpr int q = decltype(Q)::value;
-                sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
-                    constexpr int pc = decltype(Pc)::value;
-                    ub[buf][q][pc] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
-                        usrd, uvoff, ((ab * NXI + 4 * p + 2 * qh + q) * 3 + pc) * UBLK, 0));
-                });
+        sfor<0, 2>([&](auto Q) __attribute__((always_inline)) {
+            constexpr int q = decltype(Q)::value;
+            sfor<0, 3>([&](auto Pc) __attribute__((always_inline)) {
+                constexpr int pc = decltype(Pc)::value;
+                ub[buf][q][pc] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
+                    usrd, uvoff, ((ab * NXI + 4 * p + 2 * qh + q) * 3 + pc) * UBLK, 0));
             });
-        }
+        });
+
     };
-    if constexpr (W9_SKIP & 1) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) ub[0][q][pc] = ub[1][q][pc] = short8{};
-    }
     load_u(std::integral_constant<int, 0>{}, 0);
 
     // ---- persistent tile loop: workgroup g takes tiles g, g + G, ... The next tile's patch is staged into
@@ -193,8 +182,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
             constexpr int r = hf * NH + decltype(K)::value;
             const int gy = min(max(y0 - 4 + r, 0), H - 1);
             const int soff = __builtin_amdgcn_readfirstlane((int)((img + (size_t)gy * W) * Cin * 4));
-            if constexpr (W9_SKIP & 16) pf[decltype(K)::value] = (float)(soff + voff);
-            else pf[decltype(K)::value] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(insrd, voff, soff, 0));
+            pf[decltype(K)::value] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(insrd, voff, soff, 0));
         });
     };
     auto store_half = [&](int t, float* pbuf, auto HALF) __attribute__((always_inline)) {   // zero outside
@@ -227,17 +215,13 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
     const int rY = p == 0 ? 0 : (p == 2 ? 2 : 1);
     const float sx = p == 1 ? 1.f : -1.f;
     auto mfma6 = [&](floatx16& C, const short8 (&A)[3], const short8 (&B)[3]) __attribute__((always_inline)) {
-        if constexpr (!(W9_SKIP & 4)) {
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], C, 0, 0, 0);   // a0 b0
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], C, 0, 0, 0);   // a0 b1
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], C, 0, 0, 0);   // a1 b0
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], C, 0, 0, 0);   // a0 b2
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], C, 0, 0, 0);   // a1 b1
-            C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], C, 0, 0, 0);   // a2 b0
-        } else {
-            C[0] += __builtin_bit_cast(float, (int)A[0][0] + (int)A[1][1] + (int)A[2][2] + (int)B[0][0] +
-                                                  (int)B[1][1] + (int)B[2][2]);
-        }
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], C, 0, 0, 0);   // a0 b0
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], C, 0, 0, 0);   // a0 b1
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], C, 0, 0, 0);   // a1 b0
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], C, 0, 0, 0);   // a0 b2
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], C, 0, 0, 0);   // a1 b1
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], C, 0, 0, 0);   // a2 b0
+
     };
     const int co = tid & 31, g = tid >> 5;   // epilogue thread: output channel co, tiles 2g, 2g + 1 of a block
     const float bias = a.bias[co];
@@ -315,30 +299,22 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
                     if constexpr (!(MASK & (1 << h))) return;   // half unit: the other M block only
                     const int tile = 32 * h + li;
                     float tv[3][8], t16[3];
-                    if constexpr (!(W9_SKIP & 2)) {
 #pragma unroll
-                        for (int cc = 0; cc < 3; ++cc) {
-                            // pixel (8h + 3sa, 3sb + QHC + cc) relative to the lane's tile origin (even x)
-                            const int off = (8 * h + 3 * sa) * RP + ((3 * sb + QHC + cc) & 1) * PLANE +
-                                            ((3 * sb + QHC + cc) >> 1) * PS;
-                            const f32x4 x0v = *reinterpret_cast<const f32x4*>(bx + off);
-                            const f32x4 x1v = *reinterpret_cast<const f32x4*>(bx + off + 4);
-                            const f32x4 y0v = *reinterpret_cast<const f32x4*>(by + off);
-                            const f32x4 y1v = *reinterpret_cast<const f32x4*>(by + off + 4);
-                            const float xv[8] = {x0v.x, x0v.y, x0v.z, x0v.w, x1v.x, x1v.y, x1v.z, x1v.w};
-                            const float yv[8] = {y0v.x, y0v.y, y0v.z, y0v.w, y1v.x, y1v.y, y1v.z, y1v.w};
+                    for (int cc = 0; cc < 3; ++cc) {
+                        // pixel (8h + 3sa, 3sb + QHC + cc) relative to the lane's tile origin (even x)
+                        const int off = (8 * h + 3 * sa) * RP + ((3 * sb + QHC + cc) & 1) * PLANE +
+                                        ((3 * sb + QHC + cc) >> 1) * PS;
+                        const f32x4 x0v = *reinterpret_cast<const f32x4*>(bx + off);
+                        const f32x4 x1v = *reinterpret_cast<const f32x4*>(bx + off + 4);
+                        const f32x4 y0v = *reinterpret_cast<const f32x4*>(by + off);
+                        const f32x4 y1v = *reinterpret_cast<const f32x4*>(by + off + 4);
+                        const float xv[8] = {x0v.x, x0v.y, x0v.z, x0v.w, x1v.x, x1v.y, x1v.z, x1v.w};
+                        const float yv[8] = {y0v.x, y0v.y, y0v.z, y0v.w, y1v.x, y1v.y, y1v.z, y1v.w};
 #pragma unroll
-                            for (int k = 0; k < 8; ++k) tv[cc][k] = fmaf(sx, xv[k], yv[k]);
-                            t16[cc] = fmaf(sx, bx16[off], by16[off]);   // channel 16 (the K-step gathered over ab)
-                        }
-                    } else {
-#pragma unroll
-                        for (int cc = 0; cc < 3; ++cc) {
-                            t16[cc] = bx[16 + cc];
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) tv[cc][k] = bx[k];
-                        }
+                        for (int k = 0; k < 8; ++k) tv[cc][k] = fmaf(sx, xv[k], yv[k]);
+                        t16[cc] = fmaf(sx, bx16[off], by16[off]);   // channel 16 (the K-step gathered over ab)
                     }
+
                     float v0[8], v1[8];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
@@ -352,16 +328,9 @@ __global__ __launch_bounds__(NTHR, 1) void wino9_x6_kernel(Wino9Args a, int n_un
                         v16s[((4 * p + 2 * QHC + lh) * 64 + tile) * V16S + ab] = lh ? w1 : w0;
                     }
                     short8 A0[3], A1[3];
-                    if constexpr (!(W9_SKIP & 8)) {
-                        split8(v0, A0);
-                        split8(v1, A1);
-                    } else {
-#pragma unroll
-                        for (int pc = 0; pc < 3; ++pc) {
-                            A0[pc] = __builtin_bit_cast(short8, (f32x4){v0[pc], v0[pc + 1], v0[pc + 2], v0[pc + 3]});
-                            A1[pc] = __builtin_bit_cast(short8, (f32x4){v1[pc], v1[pc + 1], v1[pc + 2], v1[pc + 3]});
-                        }
-                    }
+                    split8(v0, A0);
+                    split8(v1, A1);
+
                     mfma6(acc[0][h], A0, ub[cur][0]);
                     mfma6(acc[1][h], A1, ub[cur][1]);
                 });

@@ -32,6 +32,7 @@
 // (no U loads behind them there: vmcnt retires in order).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -108,11 +109,8 @@ __device__ __forceinline__ void split_pair(f32x2 v, unsigned& p0, unsigned& p1, 
 
 }  // namespace
 
-// Experiment knobs (tools/wino9f3_bench only; never set in the library build): F3_SKIP bit0 = no U loads in the MFMA
-// phases, bit1 = no input transforms, bit2 = no MFMAs, bit3 = no epilogue (results wrong: timing only)
-#ifndef F3_SKIP
-#define F3_SKIP 0
-#endif
+// (The knock-out measurements of DESIGN.md §3 — no U loads, transforms, MFMAs or epilogue — were built from this file
+// as of commit 94f9b44; the product kernel carries no such switches.)
 #ifdef W9F3_PROF
 // per (workgroup < W9F3_PROF, wave, unit iteration < 4) on the 100 MHz clock: 0 start, 1 staged, 2 transform A,
 // 3 MFMA A, 4 transform B, 5 MFMA B, 6 transform C, 7 MFMA C, 8 epilogue block 0, 9 epilogue block 1
@@ -125,8 +123,10 @@ __device__ unsigned long long f3_tl[W9F3_PROF][8][4][10];
 
 // HALF: the launch for the last partial round's blocks, each as two half units (one 12-row M block): unit u is M block
 // u & 1 of block blk0 + (u >> 1); the active block sits in accumulator slot 0 and its tile rows are an address offset
+// wg / ngrid: this workgroup's index among the ngrid workgroups that share the units (blockIdx.x / gridDim.x of a
+// launch of one kind; the fused launch below offsets its half-unit workgroups)
 template <bool HALF>
-__global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_units, int blk0) {
+__device__ __forceinline__ void wino9f3_body(const Wino9Args& a, int n_units, int blk0, int wg, int ngrid) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // LDS pointers, re-derived each unit from an opaque zero (the loop below): otherwise every LDS address of the unrolled
     // phases whose offset exceeds the 16-bit instruction offset is computed once before the persistent loop and kept
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
     };
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (a.zero != nullptr)   // the frame's CIN accumulators (no separate memset launch; no layer before this one)
-        for (long i = (long)blockIdx.x * NTHR + tid; i < a.zero_n2; i += (long)gridDim.x * NTHR)
+        for (long i = (long)wg * NTHR + tid; i < a.zero_n2; i += (long)ngrid * NTHR)
             reinterpret_cast<uint4*>(a.zero)[i] = make_uint4(0u, 0u, 0u, 0u);
     const int li = lane & 31, lh = lane >> 5;
     const int H = a.H, W = a.W, Cin = a.cin;
@@ -219,7 +219,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
     // ---- input transform of an 8-channel chunk: thread = (V tile vt, channel pair cp), vt < 100 (half units: the
     // six tile rows 4h .. 4h + 5 their M block reads)
     auto transform_ab = [&](int hmask) __attribute__((always_inline)) {
-        if constexpr (F3_SKIP & 2) return;
         const int r0 = hmask == 2 ? 4 : 0, nrow = hmask == 3 ? NV : 6;
         const int tt = otid();
         const int vt = (tt >> 2) + r0 * NV, cp = tt & 3;
@@ -256,7 +255,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
     // channel 16: one thread per V tile (threads 0..99: waves 0 and 1, two SIMDs), all 25 points (no per-lane
     // selection: a lane-dependent point row compiled to divergent branches); V16[xi][vt] = {p0 | p1 << 16, p2}
     auto transform_c = [&](int hmask) __attribute__((always_inline)) {
-        if constexpr (F3_SKIP & 2) return;
         const int r0 = hmask == 2 ? 4 : 0, nrow = hmask == 3 ? NV : 6;
         const int tt = otid();
         if (tt < nrow * NV) {
@@ -301,7 +299,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U), 0, U_BYTES, 0x00020000);
     const int uvoff = li * 32 + 16 * lh;
     auto load_u = [&](short8 (&u)[3], int slot, int xi) __attribute__((always_inline)) {
-        if constexpr (F3_SKIP & 1) return;
         sfor<0, 3>([&](auto P) __attribute__((always_inline)) {
             constexpr int p = decltype(P)::value;
             u[p] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(usrd, uvoff, ((slot * NXM + xi) * 3 + p) * UBLK, 0));
@@ -311,7 +308,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
     const int h24 = wave >> 2, mq = (wave >> 1) & 1, nh = wave & 1;
     const int u24off = l16 * 64 + kg * 16;
     auto load_u24 = [&](short8 (&u)[3], int slot24) __attribute__((always_inline)) {
-        if constexpr (F3_SKIP & 1) return;
         sfor<0, 3>([&](auto P) __attribute__((always_inline)) {
             constexpr int p = decltype(P)::value;
             u[p] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
@@ -323,10 +319,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
     // point 24: M row 16 mq + l16 of block h24 -> tile (row l16 & 3, column 4 mq + (l16 >> 2))
     const int vt24 = (4 * h24 + (l16 & 3)) * NV + 4 * mq + (l16 >> 2);
     auto mfma6 = [&](floatx16& C, const short8 (&A)[3], const short8 (&B)[3]) __attribute__((always_inline)) {
-        if constexpr (F3_SKIP & 4) {
-            C[0] += __builtin_bit_cast(float, (int)A[0][0] + (int)A[1][1] + (int)A[2][2] + (int)B[0][0] + (int)B[1][1] + (int)B[2][2]);
-            return;
-        }
         C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], C, 0, 0, 0);   // a0 b0
         C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], C, 0, 0, 0);   // a0 b1
         C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], C, 0, 0, 0);   // a1 b0
@@ -335,10 +327,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
         C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], C, 0, 0, 0);   // a2 b0
     };
     auto mfma6s = [&](floatx4& C, const short8 (&A)[3], const short8 (&B)[3]) __attribute__((always_inline)) {
-        if constexpr (F3_SKIP & 4) {
-            C[0] += __builtin_bit_cast(float, (int)A[0][0] + (int)A[1][1] + (int)A[2][2] + (int)B[0][0] + (int)B[1][1] + (int)B[2][2]);
-            return;
-        }
         C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[0], C, 0, 0, 0);
         C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[1], C, 0, 0, 0);
         C = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[0], C, 0, 0, 0);
@@ -380,10 +368,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
         constexpr int c = decltype(CH)::value, MASK = decltype(MK)::value;
         const bool do24 = MASK == 3 || ((MASK >> h24) & 1);
         short8 ub[3][3], u24[3];
-        if constexpr (F3_SKIP & 1) {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) u24[q] = ub[0][q] = ub[1][q] = ub[2][q] = short8{};
-        }
         load_u(ub[0], 5 * c, xi0);
         load_u(ub[1], 5 * c, xi0 + 8);
         sfor<0, 15>([&](auto SS) __attribute__((always_inline)) {
@@ -434,10 +418,6 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
     auto mfma_c = [&](auto MK) __attribute__((always_inline)) {
         constexpr int MASK = decltype(MK)::value;
         short8 ub[3][3], u24[3];
-        if constexpr (F3_SKIP & 1) {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) u24[q] = ub[0][q] = ub[1][q] = ub[2][q] = short8{};
-        }
         load_u(ub[0], 10, xi0);
         load_u(ub[1], 10, xi0 + 8);
         load_u(ub[2], 10, xi0 + 16);
@@ -559,10 +539,10 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
         reinterpret_cast<float*>(lds + PARAM_OFF)[tid] = a.bias[tid];
         reinterpret_cast<float2*>(lds + PARAM_OFF + NCO * 4)[tid] = a.bn_ab[tid];
     }
-    if ((int)blockIdx.x < n_units) load_patch(blockIdx.x);
-    for (int t = blockIdx.x; t < n_units; t += (int)gridDim.x, ++f3_it) {
+    if (wg < n_units) load_patch(wg);
+    for (int t = wg; t < n_units; t += ngrid, ++f3_it) {
         F3TL(0);
-        const int tn = t + (int)gridDim.x;
+        const int tn = t + ngrid;
         if (tn >= n_units) l2f = l2_touch_xcd_slice<NTHR, 1>(a.w_next, a.w_next_bytes).x;
         int y0, x0;
         size_t img;
@@ -623,15 +603,35 @@ __global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_uni
         // staging: its HBM latency hides behind the epilogue
         __builtin_amdgcn_sched_barrier(0);   // (the MFMA phase's operand registers are dead before these loads)
         if (tn < n_units) load_patch(tn);
-        if constexpr (!(F3_SKIP & 8)) {
-            epilogue(0, HALF ? hb : 0, y0, x0, img);
-            F3TL(8);
-            if (!HALF) epilogue(1, 1, y0, x0, img);
-        }
+        epilogue(0, HALF ? hb : 0, y0, x0, img);
+        F3TL(8);
+        if (!HALF) epilogue(1, 1, y0, x0, img);
+
         F3TL(9);
         lds_barrier();   // M image reads done before the next unit's staging
     }
     l2_touch_keep(l2_touch_t{l2f, 0u}, a.batch < 0, reinterpret_cast<float*>(lds));
+}
+
+template <bool HALF>
+__global__ __launch_bounds__(NTHR, 1) void wino9f3_kernel(Wino9Args a, int n_units, int blk0) {
+    wino9f3_body<HALF>(a, n_units, blk0, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// The last partial round inside the same launch: workgroups [0, n_main) walk the n_full whole blocks persistently, the
+// n_half workgroups after them take one half unit each. One workgroup fits a CU (LDS), and workgroups are dispatched in
+// index order as CUs free up, so the half units start on the first CUs whose persistent walk ends — while the other
+// walks finish — instead of after the whole launch (the second launch of wino9f3_launch's split form). Speed only: a
+// half unit's result does not depend on where or when it runs.
+__global__ __launch_bounds__(NTHR, 1) void wino9f3_fused_kernel(Wino9Args a, int n_full, int n_main) {
+    if ((int)blockIdx.x < n_main) {
+        wino9f3_body<false>(a, n_full, 0, (int)blockIdx.x, n_main);
+    } else {
+        Wino9Args b = a;
+        b.zero = nullptr;     // (cleared by the persistent workgroups)
+        b.w_next = nullptr;   // (touched by the persistent workgroups' last units)
+        wino9f3_body<true>(b, (int)gridDim.x - n_main, n_full, (int)blockIdx.x - n_main, (int)gridDim.x - n_main);
+    }
 }
 
 #ifdef W9F3_PROF
@@ -760,6 +760,8 @@ hipError_t wino9f3_prepare() {
     hipError_t e = hipFuncSetAttribute((const void*)wino9f3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)wino9f3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)wino9f3_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return e;
 }
 
@@ -784,6 +786,15 @@ hipError_t wino9f3_launch(const Wino9Args& a, hipStream_t st) {
     // 800 blocks on 256 CUs are 3 rounds and 32 blocks, i.e. 3.5 unit times instead of 4
     const int tail = n_blocks % (int)grid;
     const int n_full = (tail > 0 && 2 * tail <= (int)grid) ? n_blocks - tail : n_blocks;
+    static const bool fused = [] {   // RST_F3_FUSED_TAIL=0: the tail as a second launch (A/B runs)
+        const char* v = getenv("RST_F3_FUSED_TAIL");
+        return !(v != nullptr && v[0] == '0');
+    }();
+    if (n_full < n_blocks && fused) {
+        hipLaunchKernelGGL(wino9f3_fused_kernel, dim3(grid + (unsigned)(2 * tail)), dim3(NTHR), LDS_BYTES, st, a, n_full,
+                           (int)grid);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(wino9f3_kernel<false>, dim3(grid), dim3(NTHR), LDS_BYTES, st, a, n_full, 0);
     if (n_full < n_blocks) {
         Wino9Args b = a;

@@ -91,12 +91,8 @@ __device__ __forceinline__ float pro_apply_blend(int mode, float x, float2 ab, f
 
 }  // namespace
 
-// Experiment knobs (tools/wino_x6_bench only; never set in the library build): X6_SKIP bit0 = no U reloads
-// in the loop, bit1 = no transform of the next chunk, bit2 = no staging / patch loads in the loop, bit3 = no
-// barrier at the end of a chunk, bit4 = no materialised block output stores (results wrong: timing only).
-#ifndef X6_SKIP
-#define X6_SKIP 0
-#endif
+// (The knock-out measurements quoted in DESIGN.md §3 — no U reloads, no transform, no staging, no barrier, no
+// materialised stores — were built from this file as of commit 94f9b44; the product kernel carries no such switches.)
 // In the chunk loop a store issued before a U load makes that load's vmcnt wait include the store (vmcnt retires in
 // order): X6_MAT_LATE issues a chunk's materialised-output stores after the chunk's last U and staging loads.
 #ifndef X6_MAT_LATE
@@ -303,7 +299,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     };
     // the materialised block output of staging item k of a chunk
     auto mat_store = [&](int k, int chunk, f32x4 v) __attribute__((always_inline)) {
-        if (!(X6_SKIP & 16) && a.mat != nullptr) {
+        if (a.mat != nullptr) {
             if (a.wt_stores & 2)
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), msrd, sg_moff[k] + chunk * XCK * 4, 0, 16);
             else
@@ -503,14 +499,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                         av[(x + 1) & 1][p] = *reinterpret_cast<const short8*>(va + (p * XXI + x + 1) * 32 * XVROW);
                     });
                 }
-                if constexpr (!(X6_SKIP & 1) && k >= 3) {   // U ring refill (B2, B1, B0 last read by MFMAs 3, 4, 5)
+                if constexpr (k >= 3) {   // U ring refill (B2, B1, B0 last read by MFMAs 3, 4, 5)
                     constexpr int xn = (x + YRING) % YPT;
                     load_u1(x + YRING < YPT ? c : c1, xn, s, 5 - k);
                 }
                 // transform + split of chunk c+1 into V[1-P]
-                if constexpr (!(X6_SKIP & 2) && x == 0 && k < 4) tr_read_col(pnext, k);
-                if constexpr (!(X6_SKIP & 2) && x == 1 && k < 4) tr_rows_col(k);
-                if constexpr (!(X6_SKIP & 2) && x >= 2 && x < 6) {
+                if constexpr (x == 0 && k < 4) tr_read_col(pnext, k);
+                if constexpr (x == 1 && k < 4) tr_rows_col(k);
+                if constexpr (x >= 2 && x < 6) {
                     constexpr int rs = (x - 2) >> 1, q0 = ((x - 2) & 1) * 2, lx0 = 4 * rs + q0;
                     if constexpr (k == 0) cols(rs, q0);
                     if constexpr (k == 1) piece(w0x, w0y, qa0);
@@ -523,7 +519,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                     if constexpr (k == 5) vwrite(vnext, lx0 + 1, qb0, qb1, last_piece(w1x, w1y));
                 }
                 // staging of chunk c+2 into patch[P], then the loads of chunk c+3 into the freed registers
-                if constexpr (!(X6_SKIP & 4) && x >= 6) {
+                if constexpr (x >= 6) {
                     constexpr int ks = x - 6;
                     if constexpr (k == 0 && pro != PRO_NONE) {
                         sp01 = *reinterpret_cast<const f32x4*>(pab + c2 * XCK + cq4);
@@ -542,7 +538,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 __builtin_amdgcn_sched_barrier(0);
             });
         });
-        if constexpr (!(X6_SKIP & 8)) lds_barrier();
+        lds_barrier();
     }
 
     XTL(2);

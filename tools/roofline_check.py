@@ -16,6 +16,7 @@ Usage: python tools/roofline_check.py <bench_json_line_file> <kernel_trace.csv |
 Exit status 1 when the two fractions differ by more than the tolerance (relative).
 """
 import csv
+import gzip
 import json
 import os
 import sys
@@ -41,11 +42,15 @@ def rocprof_avg_ns(path, name):
     return (total / calls if calls else None), calls
 
 
-def trace_graph_avg_ns(path, name, frame_start="wino9f3_kernel<false>"):
-    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+def _open(path):
+    return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+
+
+def trace_graph_avg_ns(path, name, frame_start="wino9f3_"):
+    rows = sorted(csv.DictReader(_open(path)), key=lambda r: int(r["Start_Timestamp"]))
     frames, cur = [], None
     for r in rows:
-        if frame_start in r["Kernel_Name"]:
+        if frame_start in r["Kernel_Name"] and "<true>" not in r["Kernel_Name"]:
             cur = []
             frames.append(cur)
         if cur is not None:
@@ -69,7 +74,7 @@ def main():
     tol = float(sys.argv[3]) if len(sys.argv) > 3 else 0.02
     rf = b["roofline"]
     frames = None
-    if "Start_Timestamp" in open(sys.argv[2]).readline():
+    if "Start_Timestamp" in _open(sys.argv[2]).readline():
         avg_ns, calls, frames = trace_graph_avg_ns(sys.argv[2], rf["kernel"])
     else:
         avg_ns, calls = rocprof_avg_ns(sys.argv[2], rf["kernel"])

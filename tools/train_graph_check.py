@@ -1,7 +1,9 @@
 """Capture one full training step (bench.py's config-4 step: style predictor + transfer net + VGG16 loss,
 backward of both, RMSprop) into a hipGraph and check that a replay does exactly what an eager step does:
 two trainers with the same initial state, one eager step vs one graph replay -> bitwise-equal weights and
-losses. Prints eager vs replay ms/step.  Usage: python tools/train_graph_check.py [batch] [steps]"""
+losses. Prints eager vs replay ms/step.  Usage: python tools/train_graph_check.py [batch] [steps] [--small]
+(--small: a 32x64 frame, seconds). The step's stream overlaps (loss targets, the predictor's backward and its weight
+gradients) follow their RST_SERIAL_* switches at creation."""
 import os
 import sys
 import time
@@ -27,9 +29,13 @@ def make(cfg, plan, B, dev):
 
 
 def main():
-    B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    cfg = ShapeConfig.from_spec("rst-960-120-128-17")
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    B = int(args[0]) if len(args) > 0 else 4
+    steps = int(args[1]) if len(args) > 1 else 5
+    if "--small" in sys.argv:   # 32x64 frames, 8-row bottleneck of 32 filters: a seconds-long check
+        cfg = ShapeConfig.explicit((32, 64), (32, 64), num_channels=17, bottleneck_res_y=8, bottleneck_num_filters=32)
+    else:
+        cfg = ShapeConfig.from_spec("rst-960-120-128-17")
     ins, outs = cfg.input_shape['content'], cfg.output_shape
     sins = tuple(cfg.input_shape['style'][1:])
     plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
