@@ -565,7 +565,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-budget-s", type=float, default=20.0, help="bounded CPU-baseline sample (seconds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="headline from eager launches instead of hipGraph replay")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "traffic_r05.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06", "traffic_r06.json"),
                     help="per-launch HBM bytes of the dominant kernel (tools/pmc_traffic.py on this build's FETCH/WRITE passes)")
     ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
     ap.add_argument("--train-steps", type=int, default=5)

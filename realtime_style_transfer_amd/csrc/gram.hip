@@ -150,20 +150,51 @@ __global__ __launch_bounds__(256) void gram_partial_bf16_kernel(const float* __r
     auto pack = [](float x, float y) __attribute__((always_inline)) {
         return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
     };
+    // FEAT_BF16 staging: thread = (channel quad q4 = tid & 15, pixels 4 pg .. 4 pg + 3, pg = tid >> 4) loads the four
+    // pixels' 4-channel pieces of both slices (8-B loads: 128 B per pixel and 16 lanes) and writes them transposed,
+    // four pixels of one channel per 8-B LDS store
+    const int q4 = tid & 15, pg = tid >> 4;
+    const unsigned short* fh = reinterpret_cast<const unsigned short*>(feat) + (size_t)b * hw * C;
     for (int p0 = p_begin; p0 < p_end; p0 += KP) {
+        if constexpr (FEAT_BF16) {
+            uint2 ua[4], ub[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int p = p0 + 4 * pg + j;
+                const bool ok = p < p_end;
+                ua[j] = ok ? *reinterpret_cast<const uint2*>(fh + (size_t)p * C + c0 + 4 * q4) : make_uint2(0u, 0u);
+                ub[j] = ok ? *reinterpret_cast<const uint2*>(fh + (size_t)p * C + d0 + 4 * q4) : make_uint2(0u, 0u);
+            }
+            __syncthreads();   // the previous chunk's operand reads are done
+            // channel 4 q4 + k of pixel j: half (k & 1) of word (k >> 1) of u[j]
+            auto col = [](const uint2 (&u)[4], int k) __attribute__((always_inline)) {
+                const unsigned w0 = (k >> 1) ? u[0].y : u[0].x, w1 = (k >> 1) ? u[1].y : u[1].x;
+                const unsigned w2 = (k >> 1) ? u[2].y : u[2].x, w3 = (k >> 1) ? u[3].y : u[3].x;
+                // v_perm selectors: bytes 0-1 / 2-3 of each word (the low / high bf16)
+                const unsigned sel = (k & 1) ? 0x07060302u : 0x05040100u;
+                return make_uint2(__builtin_amdgcn_perm(w1, w0, sel), __builtin_amdgcn_perm(w3, w2, sel));
+            };
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                *reinterpret_cast<uint2*>(la + (4 * q4 + k) * RS + 4 * pg) = col(ua, k);
+                *reinterpret_cast<uint2*>(lb + (4 * q4 + k) * RS + 4 * pg) = col(ub, k);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < KP / 16; ++s) {   // K step: pixels 16 s + 8 lh .. + 7
+                const short8 av = *reinterpret_cast<const short8*>(la + (wi * 32 + li) * RS + 16 * s + 8 * lh);
+                const short8 bv = *reinterpret_cast<const short8*>(lb + (wj * 32 + li) * RS + 16 * s + 8 * lh);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+            }
+            continue;
+        }
         float va[16], vb[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int p = p0 + 16 * sg + j;
             const bool ok = p < p_end;
-            if constexpr (FEAT_BF16) {
-                const unsigned short* fh = reinterpret_cast<const unsigned short*>(feat) + (size_t)b * hw * C;
-                va[j] = ok ? __uint_as_float((unsigned)fh[(size_t)p * C + c0 + sc] << 16) : 0.f;
-                vb[j] = ok ? __uint_as_float((unsigned)fh[(size_t)p * C + d0 + sc] << 16) : 0.f;
-            } else {
-                va[j] = ok ? fb[(size_t)p * C + c0 + sc] : 0.f;
-                vb[j] = ok ? fb[(size_t)p * C + d0 + sc] : 0.f;
-            }
+            va[j] = ok ? fb[(size_t)p * C + c0 + sc] : 0.f;
+            vb[j] = ok ? fb[(size_t)p * C + d0 + sc] : 0.f;
         }
         __syncthreads();   // the previous chunk's operand reads are done
 #pragma unroll

@@ -543,7 +543,11 @@ class StyleTransferTrainingModel:
         rst_trainer_wait_style_gradient) and so overlaps the rest of that backward — the contract layers and the start
         conv's weight gradient — instead of following it; the caller's stream joins it before either gradient is used.
         Same kernels on the same inputs: the gradients are bitwise those of the serial order (RST_SERIAL_PREDICTOR_BWD=1)."""
-        if not (gsp.is_cuda and getattr(self, "_overlap_pbwd", True)):
+        # Under hipGraph capture the backward stays on the caller's stream: a capture whose fork is two levels deep
+        # (caller -> this side stream -> the predictor trainer's weight-gradient stream) segfaulted at capture end on
+        # this HIP runtime (tools/train_graph_check.py, profiles/r06/r06e); one level (the weight-gradient stream
+        # forked from the caller's) captures and replays bitwise. Same kernels, same bits either way.
+        if not (gsp.is_cuda and getattr(self, "_overlap_pbwd", True)) or torch.cuda.is_current_stream_capturing():
             pr.backward(gsp, grad=self._pgrad)
             return
         main = torch.cuda.current_stream(gsp.device)

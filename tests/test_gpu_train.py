@@ -388,6 +388,53 @@ def test_predictor_backward_beside_the_transfer_backward_is_bitwise_serial():
         assert np.array_equal(a, b)
 
 
+def test_joint_training_step_graph_replay_is_bitwise_eager():
+    """train_step forks onto the loss targets' side stream and the predictor trainer's weight-gradient stream
+    (and, eagerly, runs the predictor's backward on a third stream). A whole joint step captured into a hipGraph
+    (tools/train_graph_check.py at test size) replays exactly what an eager step does: two trainers from the same state,
+    eager steps vs replays -> bitwise weights (both networks) and losses, twice."""
+    _need_gpu()
+    from realtime_style_transfer_amd.styleLoss import StyleLossModelVGG
+    from realtime_style_transfer_amd.stylePrediction import (StylePredictionTrainer, init_predictor_weights,
+                                                             predictor_weight_spec)
+    from realtime_style_transfer_amd.styleTransferTrainingModel import StyleTransferTrainingModel
+    cfg = CONFIGS['A']
+    B = 2
+    plan, w, vgg, content, _, gtc, gts = _case(cfg, B)
+    P = plan.num_style_params
+    sins = cfg['output_shape']
+    pw = init_predictor_weights(predictor_weight_spec(sins, 'MOBILE_NET', P), seed=3, perturb=True)
+    style = np.random.default_rng(12).random((B, 1) + sins).astype(np.float32)
+    c, gc, gs, st = _cuda(content, gtc, gts, style)
+    x, y = {'content': c, 'style': st}, {'content': gc, 'style': gs}
+
+    def make():
+        lm = StyleLossModelVGG(cfg['output_shape'], weights=vgg, max_batch=B, precision="bf16")
+        pr = StylePredictionTrainer(sins, 'MOBILE_NET', P, weights=pw, max_batch=B)
+        return StyleTransferTrainingModel(cfg['input_shape'], cfg['output_shape'], cfg['bottleneck_res_y'],
+                                          cfg['bottleneck_num_filters'], loss_model=lm, weights=w, max_batch=B,
+                                          style_predictor=pr, precision="winograd_bf16x6")
+    a, b = make(), make()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        a.train_step(x, y)
+        b.train_step(x, y)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.train_step(x, y)
+    for _ in range(2):
+        a.train_step(x, y)
+        g.replay()
+        torch.cuda.synchronize()
+        wa = np.concatenate([q.ravel() for q in a.get_weights()] + [q.ravel() for q in a.style_predictor.get_weights()])
+        wb = np.concatenate([q.ravel() for q in b.get_weights()] + [q.ravel() for q in b.style_predictor.get_weights()])
+        assert np.array_equal(wa, wb)
+        assert np.array_equal(a.style_losses['loss'].cpu().numpy(), b.style_losses['loss'].cpu().numpy())
+
+
 def test_training_model_reference_geometry_with_dummy_predictor():
     """styleTransferTrainingModelTest.py:15-58: 240x480x3 -> 480x960x3, bottleneck 30 rows x 4 filters,
     DUMMY predictor, a fit over two zero samples in one batch of 2 (the VGG loss stands in for

@@ -5,11 +5,13 @@ Collected in two separate passes (MI355X_MICROARCH.md §rocprofv3 PMC slots: FET
 slots and WRITE_SIZE 2, they cannot share a pass):
     rocprofv3 --pmc FETCH_SIZE --output-format csv -d <dir_f> -o r01 -- python bench.py ...
     rocprofv3 --pmc WRITE_SIZE --output-format csv -d <dir_w> -o r01 -- python bench.py ...
-Units are KiB. gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports exactly half of
-the bytes of wide (16 B/lane) coalesced reads, which is how every conv kernel here stages its
-halo and weights, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B stores
-(our stores are 4-B/lane, 128-B contiguous per half-wave: treated as exact, uncalibrated).
-Infinity-Cache hits are counted too (the counters sit at the L2's memory side).
+Units are KiB. gfx950 correction, calibrated on this chip (tools/probe_r06.hip fetch,
+profiles/r06/r06a/fetch_calibration.json: 512 MiB per pattern): every read pattern the kernels issue — coalesced
+4-, 8- and 16-byte lanes and the one-dword-per-128-B-line L2 touch — reports FETCH_SIZE = exactly half its bytes
+(TCC_EA0_RDREQ = bytes / 128, TCC_BUBBLE = 0: each L2 miss is one 128-B request tallied at 64 B), so read bytes =
+2 x FETCH_SIZE x 1024 for every kernel here; WRITE_SIZE is exact for 4- and 16-byte stores.
+Infinity-Cache hits are counted too (the counters sit at the L2's memory side): these are L2 fill bytes, of which
+the HBM share is smaller when the 256 MB Infinity Cache holds the data (every frame's working set does).
 
 Usage: python tools/pmc_traffic.py <fetch_csv> <write_csv> <out_json>
 """
@@ -43,6 +45,8 @@ def short_name(k: str) -> str:
         return f"conv_lite<3x3 s2 {'transposed ' if mode else ''}Cin{cin} Cout{nc} f32 {shape} MFMA>"
     if "last_x6_kernel" in k:
         return "last_x6<9x9 transposed Cin16 Cout3 as N=(kx,co) split-bf16 x6 MFMA>"
+    if "wino9f3" in k:
+        return "wino9f3<9x9 as 9 x F(3x3,3x3) on one tile grid, 24x24 N32 split-bf16 x6 MFMA persistent>"
     if "wino9_x6_kernel" in k:
         return "wino9_x6_conv<9x9 as 9 x F(2x2,3x3) 16x16 N32 split-bf16 x6 MFMA persistent>"
     if "wino_x6_kernel" in k or "wino_x6w_kernel" in k:
@@ -69,7 +73,9 @@ def load(path, counter):
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
-    out = {"note": __doc__.split("\n\n")[1], "per_launch_bytes": {}, "raw": {}}
+    out = {"note": __doc__.split("\n\n")[1], "per_launch_bytes": {}, "raw": {},
+           "correction": "reads 2 x FETCH_SIZE (calibrated for 4/8/16-B lanes and the 128-B-line touch, "
+                         "profiles/r06/r06a/fetch_calibration.json); writes WRITE_SIZE (exact for 4- and 16-B stores)"}
     # instantiations that share a short name (e.g. the prologue-mode templates of one kernel) are
     # merged launch-weighted: per_launch_bytes is the mean over every launch of that kernel
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
