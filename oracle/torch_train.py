@@ -142,7 +142,8 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 class _Bf16Conv(torch.autograd.Function):
     """A VGG16 conv in the device's RST_PRECISION_BF16 arithmetic: forward on bf16-rounded input and
     kernel, input gradient from the bf16-rounded output gradient and kernel (products exact in
-    float64, as they are in the fp32 accumulators). The kernel is frozen (no weight gradient)."""
+    float64, as they are in the fp32 accumulators), rounded to bf16 as the device stores it. The kernel is frozen
+    (no weight gradient)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -157,7 +158,7 @@ class _Bf16Conv(torch.autograd.Function):
         with torch.enable_grad():
             y = conv2d_same(xd, _bf16(w), None, 1)
             (gx,) = torch.autograd.grad(y, xd, _bf16(gy))
-        return gx, None, None
+        return _bf16(gx), None, None   # the input gradient is stored as bf16 (a pool's input gradient routes it as is)
 
 
 class _Bf16FwdConv(torch.autograd.Function):
@@ -183,7 +184,8 @@ class _Bf16FwdConv(torch.autograd.Function):
 
 class _Bf16Store(torch.autograd.Function):
     """A mixed_bfloat16 layer output: the value rounded to bf16 (the device stores every VGG16 layer output as bf16
-    bits in the plain-bf16 loss); the cast's gradient passes through unchanged, as TF's Cast gradient does."""
+    bits in the plain-bf16 loss), and so is its gradient — the sum of what flows back into it (the next conv's or pool's
+    input gradient, the Gram's and the content term's), each contribution already bf16, rounded once."""
 
     @staticmethod
     def forward(ctx, x):
@@ -191,7 +193,7 @@ class _Bf16Store(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        return gy
+        return _bf16(gy)
 
 
 def vgg_features(images01, vgg: Sequence[torch.Tensor], taps=None, route=None,
@@ -258,7 +260,7 @@ class _Bf16Gram(torch.autograd.Function):
         B, C, H, W = f.shape
         f2 = _bf16(f.reshape(B, C, H * W))
         w = _bf16((gg + gg.transpose(1, 2)) / (H * W))
-        return torch.bmm(w, f2).reshape(B, C, H, W)
+        return torch.bmm(w, f2).reshape(B, C, H, W)   # f32 on the device; the sum with the pool's gradient is rounded once
 
 
 def _mean_l2(t):

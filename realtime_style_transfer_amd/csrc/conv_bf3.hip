@@ -196,7 +196,10 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
     // bf16 activations into one plane without a prologue (the plain-bf16 VGG16 forward): items of 8 channels (16-B
     // loads), stored to the halo image as they are (the bf16 bits are the operand), half the items of the f32 form
     constexpr int HQ8 = CK / 8, HITEMS8 = HP * HQ8;
-    constexpr bool in16 = (PF & 4) != 0;   // (conv_bf3_select(..., in_bf16): configs 144 / 145; launch-checked)
+    // (PF bit 3: the same for a bf16 gradient under a bf16 ReLU mask, PRO_MASK — the plain-bf16 VGG16's input-gradient
+    // convs: both 16-B items loaded, the mask applied on the bits)
+    constexpr bool in16 = (PF & 12) != 0;   // (conv_bf3_select(..., in_bf16 / mask_bf16): configs 144-147; launch-checked)
+    constexpr bool mask16 = (PF & 8) != 0;
     auto load_halo = [&](int chunk) __attribute__((always_inline)) {
         if constexpr (in16) {
             sfor<0, NPF>([&](auto K) __attribute__((always_inline)) {
@@ -206,12 +209,17 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                 f32x4 v = {0.f, 0.f, 0.f, 0.f};
                 const int hp = it / HQ8, q = it - hp * HQ8;
                 const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD, iy = iy0 + hy, ix = ix0 + hx, c = chunk * CK + q * 8;
+                f32x4 r = {0.f, 0.f, 0.f, 0.f};
                 if (it < HITEMS8 && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && c < Cin) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
                     v = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(
                                                       reinterpret_cast<const unsigned short*>(a.in) + gi));
+                    if constexpr (mask16)
+                        r = __builtin_bit_cast(f32x4, *reinterpret_cast<const u32x4*>(
+                                                          reinterpret_cast<const unsigned short*>(a.res) + gi));
                 }
                 pv[k] = v;
+                if constexpr (mask16) pr[k] = r;
             });
             return;
         }
@@ -249,7 +257,16 @@ __global__ __launch_bounds__(256) void conv_bf3_kernel(ConvArgs a) {
                 if constexpr (k * 256 >= HITEMS8) return;
                 if (it >= HITEMS8) return;
                 const int hp = it / HQ8, q = it - hp * HQ8;
-                *reinterpret_cast<u32x4*>(halo + hp * CSB + q * 8) = __builtin_bit_cast(u32x4, pv[k]);
+                u32x4 g = __builtin_bit_cast(u32x4, pv[k]);
+                if constexpr (mask16) {   // ReLU backward: keep a gradient where the forward output is > 0, i.e. its bf16
+                    const u32x4 m = __builtin_bit_cast(u32x4, pr[k]);   // bits are in [0x0001, 0x7FFF]
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const unsigned lo = m[w] & 0xFFFFu, hi = m[w] >> 16;
+                        g[w] &= (lo - 1u < 0x7FFFu ? 0x0000FFFFu : 0u) | (hi - 1u < 0x7FFFu ? 0xFFFF0000u : 0u);
+                    }
+                }
+                *reinterpret_cast<u32x4*>(halo + hp * CSB + q * 8) = g;
             });
             return;
         }
@@ -571,10 +588,13 @@ static ConvTile bf3_tile_of() {
     X(136, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 2)       \
     X(144, 3, 3, 1, 32, 64, 8, 16, 4, 1, 3, 1, 4)        \
     X(145, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 4)       \
+    X(146, 3, 3, 1, 32, 64, 8, 16, 4, 1, 3, 1, 8)        \
+    X(147, 3, 3, 1, 32, 128, 8, 16, 2, 2, 3, 1, 8)       \
     X(140, 1, 1, 1, 32, 64, 8, 16, 4, 1, 1, 1, 0)        \
     X(141, 1, 1, 1, 32, 128, 8, 16, 2, 2, 1, 1, 0)
 
-bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long long pixels, ConvTile* out, bool in_bf16) {
+bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long long pixels, ConvTile* out, bool in_bf16,
+                     bool mask_bf16) {
     if ((kh != 3 && kh != 1) || stride != 1 || cin % 32 != 0 || ntot % 64 != 0 || planes < 1 || planes > 3) return false;
     if (kh == 1 && planes != 1) return false;   // 1x1: the plain-bf16 Gram backward only
     // measured (tools/conv_bench, residual conv of rst-960-120-128-17): bf16x3 NT64 4x16 42.8 us at B=1;
@@ -605,6 +625,7 @@ bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long lon
     // bf16 activations without a prologue (the plain-bf16 VGG16 forward): the same tiles staging 8-channel 16-B items
     // straight into the halo image (PF bit 2)
     if (in_bf16 && kh == 3 && planes == 1 && cin % 8 == 0) want = want == 135 ? 145 : 144;
+    else if (mask_bf16 && kh == 3 && planes == 1 && cin % 8 == 0) want = want == 135 ? 147 : 146;
 #define X(ID, KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF)                  \
     if (ID == want) {                                                           \
         *out = bf3_tile_of<KH, KW, S, CK, NT, TH, TW, WM, WN, TPS, NP, PF>();   \
@@ -627,6 +648,8 @@ hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a_in, hipStream_t 
         if ((a.act_bf16 & 2) && !conv_bf3_fuses_pool(t, a)) return hipErrorInvalidValue;        \
         if ((a.act_bf16 & 5) && NP != 1) return hipErrorInvalidValue;                             \
         if ((PF & 4) && (!(a.act_bf16 & 1) || a.pro_mode != PRO_NONE || (a.cin & 7) != 0))        \
+            return hipErrorInvalidValue;                                                          \
+        if ((PF & 8) && ((a.act_bf16 & 5) != 5 || a.pro_mode != PRO_MASK || (a.cin & 7) != 0))    \
             return hipErrorInvalidValue;                                                          \
         if (a.pro_w != nullptr && a.cin > C::MAX_CIN) return hipErrorInvalidValue;               \
         const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x * a.n_blocks);          \

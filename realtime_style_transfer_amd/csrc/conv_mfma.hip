@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (pixel_of(hp, iy, ix) && c < Cin) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
-                    v = *reinterpret_cast<const float4*>(a.in + gi);
+                    v = (a.act_bf16 & 1) ? ld_bf16x4(a.in, gi) : *reinterpret_cast<const float4*>(a.in + gi);
                     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
                     if (pro == PRO_MASK && (a.act_bf16 & 4)) r = ld_bf16x4(a.res, gi);   // bf16 forward activations
                     else if (pro == PRO_AFF_RES || pro == PRO_MASK) r = *reinterpret_cast<const float4*>(a.res + gi);
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                 float v = 0.f;
                 if (pixel_of(hp, iy, ix) && c < Cin) {
                     const size_t gi = (img_base + (size_t)iy * a.W + ix) * Cin + c;
-                    v = a.in[gi];
+                    v = (a.act_bf16 & 1) ? ld_bf16(a.in, gi) : a.in[gi];
                     if (pro == PRO_MASK) {
                         v = ((a.act_bf16 & 4) ? ld_bf16(a.res, gi) : a.res[gi]) > 0.f ? v : 0.f;
                     } else if (pro != PRO_NONE) {
@@ -567,9 +567,9 @@ bool conv_select(int kh, int stride, int cin, int ntot, ConvTile* out) {
 
 hipError_t conv_launch(const ConvTile& t, const ConvArgs& a_in, hipStream_t st) {
     if (t.bf3) return conv_bf3_launch(t, a_in, st);
-    // bf16 activations on the f32 kernel: only the ReLU-mask source of a synchronously staged halo (the VGG16 conv0
-    // input gradient's 1x1 conv in the plain-bf16 loss)
-    if ((a_in.act_bf16 & 3) || ((a_in.act_bf16 & 4) && (a_in.pro_mode != PRO_MASK || t.hb != 1)))
+    // bf16 activations on the f32 kernel: only the input and the ReLU-mask source of a synchronously staged ReLU-mask
+    // halo (the VGG16 conv0 input gradient's 1x1 conv in the plain-bf16 loss); the output stays f32
+    if ((a_in.act_bf16 & 2) || ((a_in.act_bf16 & 5) && (a_in.pro_mode != PRO_MASK || t.hb != 1)))
         return hipErrorInvalidValue;
     const ConvArgs a = conv_wt_checked(a_in);
     switch (t.id) {

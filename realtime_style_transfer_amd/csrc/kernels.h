@@ -472,9 +472,10 @@ hipError_t conv_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st);
 // one-time per-configuration setup (dynamic LDS > 64 KB); call outside graph capture
 hipError_t conv_prepare(const ConvTile& t);
 // split-bf16 variant (conv_bf3.hip): 3x3 s1, Cin % 32 == 0; conv_launch/conv_prepare dispatch on t.bf3
-// in_bf16: the input is bf16 activations and the conv has no prologue (the plain-bf16 VGG16 forward after conv 0)
+// in_bf16: the input is bf16 activations and the conv has no prologue (the plain-bf16 VGG16 forward after conv 0);
+// mask_bf16: a bf16 gradient under a bf16 ReLU mask (PRO_MASK: the plain-bf16 VGG16's input-gradient convs)
 bool conv_bf3_select(int kh, int stride, int cin, int ntot, int planes, long long pixels, ConvTile* out,
-                     bool in_bf16 = false);
+                     bool in_bf16 = false, bool mask_bf16 = false);
 hipError_t conv_bf3_launch(const ConvTile& t, const ConvArgs& a, hipStream_t st);
 hipError_t conv_bf3_prepare(const ConvTile& t);
 // whether conv_bf3_launch can also write the 2x2 max-pooled output (ConvArgs.pool) for these arguments: the VGG16

@@ -27,6 +27,16 @@ struct BnBwdArgs {
 };
 hipError_t bn_backward_launch(BnBwdArgs a, hipStream_t st);
 
+// Every 1x1 kernel's transpose ([cin][cout] -> [cout][cin], the input-gradient conv's weights) in one launch: job j
+// reads rows x cols at w + src[j] and writes the transpose at wt + dst[j]; end[j] = cumulative element count.
+struct TransposeJobs {
+    static constexpr int MAX = 32;
+    int n = 0;
+    long long src[MAX], dst[MAX], end[MAX];
+    int rows[MAX], cols[MAX];
+};
+hipError_t transpose_batch_launch(const float* w, const TransposeJobs& jobs, float* wt, hipStream_t st);
+
 int pw_wgrad_splits(int B, int HW, int cin, int cout, int* pps);
 hipError_t pw_wgrad_launch(const float* x, const float* se, const float* dz, int B, int HW, int cin, int cout,
                            float* slab, float* dW, hipStream_t st);

@@ -385,6 +385,18 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
     }
 }
 
+__global__ __launch_bounds__(256) void transpose_batch_kernel(const float* __restrict__ w, TransposeJobs jobs,
+                                                              float* __restrict__ wt) {
+    const long long total = jobs.end[jobs.n - 1];
+    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        int j = 0;
+        while (i >= jobs.end[j]) ++j;
+        const long long e = i - (j ? jobs.end[j - 1] : 0);
+        const int cols = jobs.cols[j], r = (int)(e / cols), c = (int)(e - (long long)r * cols);
+        wt[jobs.dst[j] + (long long)c * jobs.rows[j] + r] = w[jobs.src[j] + e];
+    }
+}
+
 // -------------------------------------------------------------------------------- depthwise bwd
 // dx[b][iy][ix][c] = sum over taps (ky, kx) with oy = (iy + pad_t - ky) / S integral and in range of
 // w[ky][kx][c] dz[b][oy][ox][c]. One lane per (input pixel, channel quad), dw-style tiling over input
@@ -776,6 +788,12 @@ hipError_t pw_wgrad_launch(const float* x, const float* se, const float* dz, int
     if (e != hipSuccess) return e;
     const size_t n = (size_t)cin * cout;
     slab_sum_kernel<<<(unsigned)((n + 63) / 64), 256, 0, st>>>(slab, S, n, dW);
+    return hipGetLastError();
+}
+
+hipError_t transpose_batch_launch(const float* w, const TransposeJobs& jobs, float* wt, hipStream_t st) {
+    if (jobs.n <= 0 || jobs.n > TransposeJobs::MAX) return hipErrorInvalidValue;
+    transpose_batch_kernel<<<grid1d((size_t)jobs.end[jobs.n - 1], 1024), 256, 0, st>>>(w, jobs, wt);
     return hipGetLastError();
 }
 

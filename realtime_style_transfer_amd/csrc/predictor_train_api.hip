@@ -54,8 +54,9 @@ struct rst_predictor_trainer {
     float* dz = nullptr;                    // norm-backward output (largest unit); ring slot 0
     // the weight gradients (and the SE / head outer products) run on `wside` beside the input-gradient chain; the
     // norm-backward outputs go round a ring of DZR buffers, each released by the weight gradient that reads it
-    static constexpr int DZR = 3;
-    float* dzr[DZR] = {};
+    // (RST_PBWD_DZR at creation, default 3; at most one per unit)
+    int n_dzr = 3;
+    std::vector<float*> dzr;
     hipStream_t wside = nullptr;
     // every fork / join of one backward records a fresh event (evs[ev_next++]): no event is recorded twice within a
     // call, so a hipGraph capture of the step sees each dependency once (re-recording the ring's events within one
@@ -66,7 +67,9 @@ struct rst_predictor_trainer {
     float4* bn_part = nullptr;
     float2* consts = nullptr;
     float* slab = nullptr;
-    float* wt = nullptr;                    // transposed 1x1 weights (dgrad)
+    float* wt = nullptr;                    // transposed 1x1 weights (dgrad): every pointwise unit's at wt_off[unit]
+    std::vector<size_t> wt_off;
+    TransposeJobs wt_jobs;                  // all of them in one launch at the start of each backward
     int* stat_index = nullptr;              // weight index of every BN moving_mean / moving_variance entry
     size_t n_stat = 0;
     std::vector<void*> allocs;
@@ -180,7 +183,7 @@ int rst_predictor_trainer_create(const rst_predictor_shape* shape, const float* 
             int pps;
             const int S = pw_wgrad_splits((int)B, u.H * u.W, u.cin, u.cout, &pps);
             max_slab = std::max(max_slab, (size_t)S * u.cin * u.cout);
-            max_wt = std::max(max_wt, (size_t)u.cin * u.cout);
+            max_wt += (size_t)u.cin * u.cout;   // (the sum: one transposed image per pointwise unit)
         } else if (u.kind == PU_DW) {
             int pps, block, slots;
             const int S = dw_wgrad_splits((int)B, u.Ho * u.Wo, u.cout, &pps, &block, &slots);
@@ -229,8 +232,37 @@ int rst_predictor_trainer_create(const rst_predictor_shape* shape, const float* 
     TRY(t->alloc(&t->consts, 1024 * 8));
     TRY(t->alloc(&t->slab, std::max<size_t>(max_slab, 1) * 4));
     TRY(t->alloc(&t->wt, std::max<size_t>(max_wt, 1) * 4));
+    {
+        t->wt_off.assign(P.units.size(), 0);
+        size_t off = 0;
+        long long end = 0;
+        for (size_t i = 0; i < P.units.size(); ++i) {
+            const PUnit& u = P.units[i];
+            if (u.kind != PU_PW) continue;
+            TransposeJobs& J = t->wt_jobs;
+            if (J.n >= TransposeJobs::MAX) {
+                delete t;
+                return set_error(RST_ERR_UNSUPPORTED, "rst_predictor_trainer_create: too many pointwise units");
+            }
+            t->wt_off[i] = off;
+            end += (long long)u.cin * u.cout;
+            J.src[J.n] = (long long)u.woff;
+            J.dst[J.n] = (long long)off;
+            J.end[J.n] = end;
+            J.rows[J.n] = u.cin;
+            J.cols[J.n] = u.cout;
+            ++J.n;
+            off += (size_t)u.cin * u.cout;
+        }
+    }
+    {
+        const char* dv = getenv("RST_PBWD_DZR");
+        const int want = dv != nullptr ? atoi(dv) : 3, nu = (int)t->plan.units.size();
+        t->n_dzr = want < 1 ? 1 : (want > nu ? (nu > 0 ? nu : 1) : want);
+    }
+    t->dzr.assign((size_t)t->n_dzr, nullptr);
     t->dzr[0] = t->dz;
-    for (int k = 1; k < rst_predictor_trainer::DZR; ++k) TRY(t->alloc(&t->dzr[k], max_act * 4));
+    for (int k = 1; k < t->n_dzr; ++k) TRY(t->alloc(&t->dzr[k], max_act * 4));
     {
         const char* sw = getenv("RST_SERIAL_PREDICTOR_WGRAD");
         t->serial_wgrad = sw != nullptr && sw[0] == '1';
@@ -330,8 +362,11 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
         if (e == hipSuccess) e = hipEventRecord(ev, st);
         return e != hipSuccess ? e : hipStreamWaitEvent(ws, ev, 0);
     };
-    hipEvent_t ev_wg[rst_predictor_trainer::DZR] = {};   // the weight gradient that last read ring slot k
+    std::vector<hipEvent_t> ev_wg((size_t)t->n_dzr, nullptr);   // the weight gradient that last read ring slot k
     RST_HIP_TRY(hipMemsetAsync(grad, 0, P.total * sizeof(float), st));
+    // the input-gradient convs' transposed 1x1 weights, all in one launch (22 separate transposes on the chain were
+    // 1.1 ms of a config-4 step: each small launch waited for CUs beside the transfer network's backward)
+    if (t->wt_jobs.n > 0) RST_HIP_TRY(transpose_batch_launch(w, t->wt_jobs, t->wt, st));
     // heads (stylePrediction.py:60-71): P = W2^T h + b2, h = W1^T gap + b1
     RST_HIP_TRY(rowdot_launch(d_style_params, B, NP, w + P.head_w2, NS, 1.f, t->dhid, st));
     RST_HIP_TRY(fork());
@@ -344,7 +379,7 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
     int j = 0;
     for (int i = (int)P.units.size() - 1; i >= 0; --i, ++j) {
         const PUnit& u = P.units[i];
-        const int slot = j % rst_predictor_trainer::DZR;
+        const int slot = j % t->n_dzr;
         float* const dz = par ? t->dzr[slot] : t->dz;
         const float* in = u.in < 0 ? t->style : t->y[u.in];
         if (u.kind == PU_DUMMY) {
@@ -389,8 +424,7 @@ int rst_predictor_trainer_backward(rst_predictor_trainer* t, const float* d_styl
                 const float* se = u.se >= 0 ? t->se_val[u.se] : nullptr;
                 RST_HIP_TRY(pw_wgrad_launch(in, se, dz, B, u.H * u.W, u.cin, u.cout, t->slab, grad + u.woff, ws));
                 // dgrad: the 1x1 conv with the transposed kernel; the shortcut gradient rides on its residual input
-                RST_HIP_TRY(transpose_launch(w + u.woff, u.cin, u.cout, t->wt, st));
-                RST_HIP_TRY(pw_launch(dz, nullptr, t->wt, t->d_ones, t->d_zeros,
+                RST_HIP_TRY(pw_launch(dz, nullptr, t->wt + t->wt_off[i], t->d_ones, t->d_zeros,
                                       t->res_consumer[u.in] ? t->dres[u.in] : nullptr, t->dyb[u.in], nullptr, B,
                                       u.H * u.W, u.cout, u.cin, ACT_NONE, st));
                 if (u.se >= 0) {   // dyb[in] is d/d(u * se): SE backward (the dw unit applies mul/bcast)

@@ -45,12 +45,13 @@ int wgrad_choose_splits(const WgradArgs& a);
 size_t wgrad_slab_bytes(const WgradArgs& a);
 hipError_t wgrad_launch(WgradArgs a, hipStream_t st);
 
-// x_bf16: the pooled forward activations x are stored as bf16 bits (the plain-bf16 VGG16)
+// x_bf16: the pooled forward activations x are stored as bf16 bits (the plain-bf16 VGG16); g_bf16: gy and gx too,
+// with acc (f32, separate from gx) added before gx's one rounding instead of accumulate
 hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, int accumulate,
-                               hipStream_t st, bool x_bf16 = false);
-// in_bf16: a and b hold bf16 bits
+                               hipStream_t st, bool x_bf16 = false, bool g_bf16 = false, const float* acc = nullptr);
+// in_bf16: a and b hold bf16 bits; g_bf16: g is written as bf16 bits (needs in_bf16, no accumulate)
 hipError_t scaled_diff_launch(const float* a, const float* b, float scale, float* g, size_t n, int accumulate,
-                              hipStream_t st, bool in_bf16 = false);
+                              hipStream_t st, bool in_bf16 = false, bool g_bf16 = false);
 hipError_t tv_bwd_launch(const float* x, float factor, float* g, int B, int H, int W, int C, hipStream_t st);
 hipError_t tap3_sum_launch(const float* p, float* out, int B, int H, int W, hipStream_t st);
 hipError_t gram_bwd_weights_bf16_launch(const float* gp, const float* gs, const int* map, int n16, int C, float scale,

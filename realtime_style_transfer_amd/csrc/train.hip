@@ -296,11 +296,13 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restri
 // Even H, W and C % 4 == 0 (every VGG16 pool here): one thread per (pooled pixel, channel quad) reads the
 // window's four pixels and the pooled gradient as 16-B vectors once and writes the four gradient pixels
 // (the element-per-thread form above re-read each window four times through 64-bit index math: 2.3 TB/s).
-// XBF16: the forward activations x are stored as bf16 bits (the plain-bf16 VGG16): four 8-B window loads
-template <bool XBF16>
+// XBF16: the forward activations x are stored as bf16 bits (the plain-bf16 VGG16): four 8-B window loads.
+// GBF16: the gradients gy, gx are bf16 bits too (mixed_bfloat16 gradients); acc (optional, f32, not aliasing gx): the
+// Gram backward's f32 gradient of the same activations, added before the single rounding: gx = bf16(acc + routed gy)
+template <bool XBF16, bool GBF16>
 __global__ __launch_bounds__(256) void maxpool2_bwd4_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                                                             float* __restrict__ gx, int B, int H, int W, int C,
-                                                            int accumulate) {
+                                                            int accumulate, const float* __restrict__ acc) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
     const int total = B * Ho * Wo * C4;
@@ -325,7 +327,13 @@ __global__ __launch_bounds__(256) void maxpool2_bwd4_kernel(const float* __restr
             v2 = *reinterpret_cast<const f4*>(x + r1);
             v3 = *reinterpret_cast<const f4*>(x + r1 + C);
         }
-        const f4 g = *reinterpret_cast<const f4*>(gy + (size_t)i * 4);
+        f4 g;
+        if constexpr (GBF16) {
+            const float4 u = ld_bf16x4(gy, (size_t)i * 4);
+            g = f4{u.x, u.y, u.z, u.w};
+        } else {
+            g = *reinterpret_cast<const f4*>(gy + (size_t)i * 4);
+        }
         f4 o0, o1, o2, o3;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {   // gradient to the first maximum (TF MaxPoolGrad order), as above
@@ -335,6 +343,17 @@ __global__ __launch_bounds__(256) void maxpool2_bwd4_kernel(const float* __restr
             o1[k] = first == 1 ? g[k] : 0.f;
             o2[k] = first == 2 ? g[k] : 0.f;
             o3[k] = first == 3 ? g[k] : 0.f;
+        }
+        if constexpr (GBF16) {
+            const size_t r[4] = {r0, r0 + C, r1, r1 + C};
+            f4* const o[4] = {&o0, &o1, &o2, &o3};
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                f4 v = *o[w];
+                if (acc != nullptr) v += *reinterpret_cast<const f4*>(acc + r[w]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<unsigned short*>(gx) + r[w]) = pack_bf16x4(v[0], v[1], v[2], v[3]);
+            }
+            continue;
         }
         f4* d0 = reinterpret_cast<f4*>(gx + r0);
         f4* d1 = reinterpret_cast<f4*>(gx + r0 + C);
@@ -354,19 +373,26 @@ __global__ __launch_bounds__(256) void maxpool2_bwd4_kernel(const float* __restr
 }
 
 hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B, int H, int W, int C, int accumulate,
-                               hipStream_t st, bool x_bf16) {
+                               hipStream_t st, bool x_bf16, bool g_bf16, const float* acc) {
+    if (g_bf16 && accumulate) return hipErrorInvalidValue;   // (bf16 gradients sum through acc, rounded once)
     if (H % 2 == 0 && W % 2 == 0 && C % 4 == 0 && (size_t)B * H * W * C < ((size_t)1 << 31)) {
         const size_t n = (size_t)B * (H / 2) * (W / 2) * (C / 4);
         unsigned blocks = (unsigned)((n + 255) / 256);
         if (blocks > 32768) blocks = 32768;
-        if (x_bf16)
-            hipLaunchKernelGGL(maxpool2_bwd4_kernel<true>, dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C, accumulate);
+        if (x_bf16 && g_bf16)
+            hipLaunchKernelGGL((maxpool2_bwd4_kernel<true, true>), dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C,
+                               accumulate, acc);
+        else if (x_bf16 && acc == nullptr)
+            hipLaunchKernelGGL((maxpool2_bwd4_kernel<true, false>), dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C,
+                               accumulate, nullptr);
+        else if (!g_bf16 && acc == nullptr)
+            hipLaunchKernelGGL((maxpool2_bwd4_kernel<false, false>), dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C,
+                               accumulate, nullptr);
         else
-            hipLaunchKernelGGL(maxpool2_bwd4_kernel<false>, dim3(blocks), dim3(256), 0, st, x, gy, gx, B, H, W, C,
-                               accumulate);
+            return hipErrorInvalidValue;
         return hipGetLastError();
     }
-    if (x_bf16) return hipErrorInvalidValue;   // the bf16 VGG16 pools are all even-sized, C % 4 == 0
+    if (x_bf16 || g_bf16 || acc) return hipErrorInvalidValue;   // the bf16 VGG16 pools are all even-sized, C % 4 == 0
     const size_t n = (size_t)B * H * W * C;
     unsigned blocks = (unsigned)((n + 255) / 256);
     if (blocks > 16384) blocks = 16384;
@@ -375,20 +401,27 @@ hipError_t maxpool2_bwd_launch(const float* x, const float* gy, float* gx, int B
 }
 
 // g (+)= scale * (a - b)   (feature-loss gradient; accumulate into an existing gradient; BF16: a, b bf16 bits)
-template <bool BF16>
+// (GBF16: g is stored as bf16 bits, rounded once from the f32 value; no accumulate)
+template <bool BF16, bool GBF16 = false>
 __global__ __launch_bounds__(256) void scaled_diff_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                           float scale, float* __restrict__ g, size_t n, int accumulate) {
     for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         const float v = scale * (BF16 ? ld_bf16(a, i) - ld_bf16(b, i) : a[i] - b[i]);
-        g[i] = accumulate ? g[i] + v : v;
+        if constexpr (GBF16)
+            reinterpret_cast<unsigned short*>(g)[i] = (unsigned short)(bf16_last_piece(v, 0.f) & 0xFFFFu);
+        else
+            g[i] = accumulate ? g[i] + v : v;
     }
 }
 
 hipError_t scaled_diff_launch(const float* a, const float* b, float scale, float* g, size_t n, int accumulate,
-                              hipStream_t st, bool in_bf16) {
+                              hipStream_t st, bool in_bf16, bool g_bf16) {
     unsigned blocks = (unsigned)((n + 255) / 256);
     if (blocks > 16384) blocks = 16384;
-    if (in_bf16)
+    if (g_bf16 && (accumulate || !in_bf16)) return hipErrorInvalidValue;
+    if (g_bf16)
+        hipLaunchKernelGGL((scaled_diff_kernel<true, true>), dim3(blocks), dim3(256), 0, st, a, b, scale, g, n, accumulate);
+    else if (in_bf16)
         hipLaunchKernelGGL(scaled_diff_kernel<true>, dim3(blocks), dim3(256), 0, st, a, b, scale, g, n, accumulate);
     else
         hipLaunchKernelGGL(scaled_diff_kernel<false>, dim3(blocks), dim3(256), 0, st, a, b, scale, g, n, accumulate);

@@ -171,6 +171,7 @@ struct rst_trainer {
     bool gstyle_recorded = false;
     bool targets_pending = false;
     bool serial_targets = false;  // RST_SERIAL_TARGETS=1 at creation: targets on the caller's stream (A/B runs)
+    bool vgg_grad_f32 = false;    // RST_VGG_GRAD_F32=1 at creation: f32 VGG16 gradients beside bf16 activations (A/B)
     int wt_stores = 5;            // RST_TRAIN_WT at creation: bit0 Winograd conv outputs, bit1 the residual convs'
                                   // materialised inputs, bit2 the other transfer convs' outputs (forward and input
                                   // gradient), bit3 the VGG16 input gradients, stored write-through (sc1); default 5
@@ -372,15 +373,23 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
     const size_t f5 = (size_t)c5.H * c5.W * c5.cout;
     int which = 0;
     float* g = t->d_vg[0];
-    const bool act = h->act_bf16;   // the forward activations (ReLU masks, pool routing, features) are bf16 bits
+    // act: the forward activations (ReLU masks, pool routing, features) are bf16 bits, and so are the gradients of the
+    // VGG16 layer outputs (mixed_bfloat16: a bf16 layer's output gradient is bf16; every stored gradient is one rounding
+    // of an f32 value, sums of two bf16 gradients rounded once); the gradient reaching the prediction stays f32
+    const bool xa = h->act_bf16;                 // forward activations stored bf16
+    const bool act = xa && !t->vgg_grad_f32;     // ... and the gradients (RST_VGG_GRAD_F32=1 at creation: f32, A/B runs)
     RST_HIP_TRY(scaled_diff_launch(c5.d_out, h->d_content_feat, (float)(ls.content_factor / (double)f5), g, B * f5, 0,
-                                   st, act));
+                                   st, xa, act));
     for (int i = CONTENT_IDX; i >= 0; --i) {
         const VggConv& c = h->convs[i];
         const ConvBwd& vb = t->vgg[i];
-        if (t->d_vgg_dbg[i])
-            RST_HIP_TRY(hipMemcpyAsync(t->d_vgg_dbg[i], g, (size_t)B * c.H * c.W * c.cout * 4, hipMemcpyDeviceToDevice,
-                                       st));
+        if (t->d_vgg_dbg[i]) {
+            if (act)
+                RST_HIP_TRY(bf16_to_f32_launch(g, t->d_vgg_dbg[i], (size_t)B * c.H * c.W * c.cout, st));
+            else
+                RST_HIP_TRY(hipMemcpyAsync(t->d_vgg_dbg[i], g, (size_t)B * c.H * c.W * c.cout * 4, hipMemcpyDeviceToDevice,
+                                           st));
+        }
         const bool pooled = i > 0 && VGG_POOL[i - 1];
         if (i == 0) {   // 64 -> 3: 1x1 conv to the 27 (tap, c) columns (into the free gradient buffer), tap sum
             const ConvBwd& pb = t->vgg0p;
@@ -406,7 +415,7 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
             a.nchunks = pb.nchunks;
             a.pro_mode = PRO_MASK;
             a.epi_mode = EPI_NONE;
-            a.act_bf16 = act ? 4 : 0;
+            a.act_bf16 = (act ? 1 : 0) | (xa ? 4 : 0);   // bf16 gradient / mask in, f32 out (the f32 prediction's gradient)
             RST_HIP_TRY(conv_launch(pb.tile, a, st));
             RST_HIP_TRY(tap3_sum_launch(pbuf, gimg, B, c.H, c.W, st));
             break;
@@ -434,7 +443,7 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
         a.pro_mode = PRO_MASK;
         a.epi_mode = EPI_NONE;
         a.wt_stores = train_wt(t, (size_t)B * c.H * c.W * c.cin, 8);
-        a.act_bf16 = act ? 4 : 0;
+        a.act_bf16 = (act ? 1 | 2 : 0) | (xa ? 4 : 0);
         RST_HIP_TRY(conv_launch(vb.tile, a, st));
         if (i == 0) break;
         const int p = i - 1;
@@ -459,15 +468,15 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
                                                     scale, t->d_gram_packed, B, st));
             for (int b = 0; b < B; ++b) {
                 ConvArgs m{};
-                m.in = act ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(cp.d_out) +
-                                                            (size_t)b * hw * C)
-                           : cp.d_out + (size_t)b * hw * C;
-                m.act_bf16 = act ? 1 : 0;
+                m.in = xa ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(cp.d_out) +
+                                                           (size_t)b * hw * C)
+                          : cp.d_out + (size_t)b * hw * C;
+                m.act_bf16 = xa ? 1 : 0;
                 m.wpk = gbf16 ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(t->d_gram_packed) +
                                                                (size_t)b * gb.n_packed)
                               : t->d_gram_packed + (size_t)b * gb.n_packed;
                 m.bias = t->d_zero;
-                m.out = gprev + (size_t)b * hw * C;
+                m.out = gprev + (size_t)b * hw * C;   // f32 (the bf16 sum with the pool's gradient is rounded once)
                 m.batch = 1;
                 m.H = cp.H;
                 m.W = cp.W;
@@ -485,8 +494,16 @@ int vgg_backward(rst_trainer* t, const float* prediction, int B, float* gimg, hi
                 RST_HIP_TRY(conv_launch(gb.tile, m, st));
             }
         }
+        if (pooled && act && k >= 0) {
+            // bf16 gradients at a style layer: bf16(Gram gradient (f32, in gprev) + routed pool gradient) into the buffer
+            // of g (already consumed by the input-gradient conv above); `which` stays
+            float* gsum = t->d_vg[which];
+            RST_HIP_TRY(maxpool2_bwd_launch(cp.d_out, t->d_vpool, gsum, B, cp.H, cp.W, cp.cout, 0, st, xa, true, gprev));
+            g = gsum;
+            continue;
+        }
         if (pooled)
-            RST_HIP_TRY(maxpool2_bwd_launch(cp.d_out, t->d_vpool, gprev, B, cp.H, cp.W, cp.cout, k >= 0, st, act));
+            RST_HIP_TRY(maxpool2_bwd_launch(cp.d_out, t->d_vpool, gprev, B, cp.H, cp.W, cp.cout, k >= 0, st, xa, act));
         which ^= 1;
         g = gprev;
     }
@@ -630,7 +647,10 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
             return set_error(RST_ERR_UNSUPPORTED, "rst_trainer_create: odd size at stride-2 layer " + s.name +
                                                       " (its input gradient needs the even-size phase split)");
     rst_trainer* t = new rst_trainer();
-    if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
+    // (A CU-masked targets stream that left 16 / 32 / 64 CUs to the caller's stream ran the config-4 step at 41.5 / 38.7 /
+    // 38.9 ms against 20.7 ms unmasked, same box: profiles/r06/r06i. Not used.)
+    const hipError_t se = hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking);
+    if (se != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_gstyle, hipEventDisableTiming) != hipSuccess)
@@ -638,6 +658,8 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
     {
         const char* ser = getenv("RST_SERIAL_TARGETS");
         t->serial_targets = ser != nullptr && ser[0] == '1';
+        const char* vg = getenv("RST_VGG_GRAD_F32");
+        t->vgg_grad_f32 = vg != nullptr && vg[0] == '1';
         const char* twt = getenv("RST_TRAIN_WT");
         t->wt_stores = twt != nullptr ? atoi(twt) : 5;   // default: the transfer convs' outputs (-1.4 %, -0.4 % per step)
     }
@@ -800,7 +822,10 @@ int rst_trainer_create_ex(const rst_shape* shape, const float* weights_host, siz
             ConvBwd& vb = t->vgg[i];
             const int lp = loss->precision;
             const int planes = bf16_planes(lp);
-            const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cout, cin, planes, (long long)B * c.H * c.W, &vb.tile);
+            // bf16 gradients under bf16 ReLU masks (vgg_backward's `act`): the 16-B staging tiles
+            const bool gmask = t->loss->act_bf16 && !t->vgg_grad_f32 && i > 0;
+            const bool bf3 = planes > 0 && conv_bf3_select(3, 1, cout, cin, planes, (long long)B * c.H * c.W, &vb.tile,
+                                                           false, gmask);
             if (!bf3 && !conv_select(3, 1, cout, cin, &vb.tile))
                 return fail_delete(t, set_error(RST_ERR_UNSUPPORTED, "no tile for VGG dgrad " + std::to_string(i)));
             vb.tiles_y = (c.H + vb.tile.th - 1) / vb.tile.th;

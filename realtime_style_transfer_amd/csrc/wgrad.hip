@@ -836,7 +836,10 @@ int wgrad_choose_splits(const WgradArgs& a) {
         // one workgroup per CU (104 KB of LDS, launch_bounds(256, 1)): one round of persistent workgroups, never more
         // than the pixel tiles (each writes a slab the reduce then reads)
         const int ntiles = a.batch * ((a.Qh + w9x::TH - 1) / w9x::TH) * ((a.Qw + w9x::TW - 1) / w9x::TW);
-        const int n = wgrad_cu_count();
+        // RST_WGRAD9_FREE_CUS=k: k CUs fewer
+        static const int free_cus = [] { const char* v = getenv("RST_WGRAD9_FREE_CUS"); return v ? atoi(v) : 0; }();
+        int n = wgrad_cu_count() - free_cus;
+        if (n < 8) n = 8;
         return ntiles < n ? (ntiles < 1 ? 1 : ntiles) : n;
     }
     if (wgrad9_applies(a) || wgradT9_applies(a)) return W9_BLOCKS;

@@ -9,6 +9,7 @@
 #   short            bench.py headline only (no side legs)                -> bench_short_<TAG>.log
 #   prof             rocprofv3 --kernel-trace --stats of the short bench  -> prof_<TAG>/
 #   trainprof        rocprofv3 --kernel-trace --stats of the training step -> trainprof_<TAG>/
+#   trainhip         rocprofv3 --kernel-trace --hip-runtime-trace of the training step -> trainhip_<TAG>/
 #   pmc              FETCH_SIZE / WRITE_SIZE passes of the frame probe    -> pmc_{f,w}_<TAG>/
 #   sq[=frame|train] the SQ counter passes (tools/pmc_sq.sh)              -> sq_<TAG>_<what>_{A,B}/
 #   ab=ENV_A@ENV_B@N alternating headline runs with env A then env B, N pairs ("-" = no env, ':' separates vars)
@@ -62,6 +63,11 @@ for step in "$@"; do
         timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trainprof_$TAG -o run -- \
             python bench.py $TRAIN > $O/trainprof_$TAG.log 2>&1 || { tail -30 $O/trainprof_$TAG.log; exit 1; }
         echo "trainprof ok" ;;
+    trainhip)   # kernel + HIP runtime API trace of the training step (host issue vs device time)
+        rm -rf $O/trainhip_$TAG
+        timeout -k 10 400 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $O/trainhip_$TAG -o run -- \
+            python bench.py $TRAIN > $O/trainhip_$TAG.log 2>&1 || { tail -30 $O/trainhip_$TAG.log; exit 1; }
+        echo "trainhip ok" ;;
     pmc)
         rm -rf $O/pmc_f_$TAG $O/pmc_w_$TAG
         timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f_$TAG -o run -- \
