@@ -836,8 +836,13 @@ int wgrad_choose_splits(const WgradArgs& a) {
         // one workgroup per CU (104 KB of LDS, launch_bounds(256, 1)): one round of persistent workgroups, never more
         // than the pixel tiles (each writes a slab the reduce then reads)
         const int ntiles = a.batch * ((a.Qh + w9x::TH - 1) / w9x::TH) * ((a.Qw + w9x::TW - 1) / w9x::TW);
-        // RST_WGRAD9_FREE_CUS=k: k CUs fewer
-        static const int free_cus = [] { const char* v = getenv("RST_WGRAD9_FREE_CUS"); return v ? atoi(v) : 0; }();
+        // minus 3/8 of the CUs (RST_WGRAD9_FREE_CUS=k: k): the kernel runs beside the style predictor's backward, whose
+        // small launches found no CU while it held all of them (config-4 step, free 0 / 32 / 64 / 96 / 128 / 160 of
+        // 256: 20.9 / 20.8 / 20.7 / 20.3 / 20.3 / 21.2 ms, profiles/r06/r06k, r06n, r06q)
+        static const int free_cus = [] {
+            const char* v = getenv("RST_WGRAD9_FREE_CUS");
+            return v != nullptr ? atoi(v) : wgrad_cu_count() * 3 / 8;
+        }();
         int n = wgrad_cu_count() - free_cus;
         if (n < 8) n = 8;
         return ntiles < n ? (ntiles < 1 ? 1 : ntiles) : n;

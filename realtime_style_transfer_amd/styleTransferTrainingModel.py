@@ -571,17 +571,12 @@ class StyleTransferTrainingModel:
                 if style.shape[1] != 1:
                     raise ValueError("the training model takes one style (num_styles=1, styleTransferTrainingModel.py:46)")
                 style = style[:, 0]
-            late = os.environ.get("RST_TARGETS_AFTER_PFWD", "0") == "1"
-            if not late:
-                self.compute_targets(y['content'], y['style'])        # loss targets beside the predictor forward
+            self.compute_targets(y['content'], y['style'])            # loss targets beside the predictor forward
             try:
                 sp = pr.forward(style)                                 # styleTransferInferenceModel.py:23-28
             except BaseException:
-                if not late:
-                    self.cancel_targets()
+                self.cancel_targets()
                 raise
-            if late:
-                self.compute_targets(y['content'], y['style'])
         else:
             sp = x['style_params']
         pred, losses, grad, gsp = self.compute_gradients(x['content'], sp, y['content'], y['style'])
