@@ -855,7 +855,7 @@ def run(args, ctx):
             split[prec]["max_abs_delta_vs_oracle"] = float(np.abs(y3.cpu().numpy() - y_ref).max())
         if world == 1 and not args.no_cpu_baseline:
             n, tsum = 0, 0.0
-            while tsum < args.cpu_budget_s and n < 20:
+            while tsum < args.cpu_budget_s and n < 200:
                 ts = time.perf_counter()
                 ref(x0, sp_np[:1])
                 tsum += time.perf_counter() - ts

@@ -111,8 +111,8 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restri
 namespace gramb {
 constexpr int KP = 64, TILE = 64, RS = KP + 8;   // pixels per chunk, channels per slice, LDS row (bf16)
 }
-// FEAT_BF16: the features are stored as bf16 bits (the plain-bf16 VGG16's layer outputs): 2-B loads (a wave's 64
-// channels are 128 B) and no rounding (the packed pieces are the stored bits)
+// FEAT_BF16: the features are stored as bf16 bits (the plain-bf16 VGG16's layer outputs): 8-B loads of channel quads
+// (staging map below) and no rounding (the packed pieces are the stored bits)
 template <bool FEAT_BF16>
 __global__ __launch_bounds__(256) void gram_partial_bf16_kernel(const float* __restrict__ feat, float* __restrict__ slab,
                                                                 int hw, int C, int nsplit, int span) {
@@ -150,35 +150,46 @@ __global__ __launch_bounds__(256) void gram_partial_bf16_kernel(const float* __r
     auto pack = [](float x, float y) __attribute__((always_inline)) {
         return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x, y}, bf16x2));
     };
-    // FEAT_BF16 staging: thread = (channel quad q4 = tid & 15, pixels 4 pg .. 4 pg + 3, pg = tid >> 4) loads the four
-    // pixels' 4-channel pieces of both slices (8-B loads: 128 B per pixel and 16 lanes) and writes them transposed,
-    // four pixels of one channel per 8-B LDS store
-    const int q4 = tid & 15, pg = tid >> 4;
-    const unsigned short* fh = reinterpret_cast<const unsigned short*>(feat) + (size_t)b * hw * C;
+    // FEAT_BF16 staging: thread = (slice, channel quad q4, pixel octet pg8): eight 8-B loads (its quad of eight
+    // consecutive pixels; a wave's loads of one pixel cover 16 quads = one 128-B row piece), transposed with v_perm
+    // into four 16-B LDS stores (eight pixels of one channel). Lane bits: 0-1 q4 low, 2-3 pg8 low, 4-5 q4 high; wave
+    // bit 0 pg8 high, bit 1 the slice. A 16-lane store group then covers q4 = 4 consecutive rows (4 rows x 144 B apart
+    // = 64 B mod 256) x 4 octets (16 B apart): 16 distinct 16-B bank slots (the first form, lanes = 16 quads of 4 pixels
+    // with 8-B stores, put 4 lanes on each slot: SQ lds_conflict 0.78). The next chunk's loads are issued before this
+    // chunk's stores and MFMAs.
+    const int l64 = tid & 63;
+    const int q4 = (l64 & 3) | ((l64 >> 4) << 2), pg8 = ((l64 >> 2) & 3) | ((wave & 1) << 2);
+    const bool slice_b = (wave >> 1) != 0;
+    const unsigned short* fsrc =
+        reinterpret_cast<const unsigned short*>(feat) + (size_t)b * hw * C + (slice_b ? d0 : c0) + 4 * q4;
+    unsigned short* const ldst = (slice_b ? lb : la) + (4 * q4) * RS + 8 * pg8;
+    uint2 u8[8];
+    auto load8 = [&](int p0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int p = p0 + 8 * pg8 + j;
+            u8[j] = p < p_end ? *reinterpret_cast<const uint2*>(fsrc + (size_t)p * C) : make_uint2(0u, 0u);
+        }
+    };
+    if constexpr (FEAT_BF16) load8(p_begin);
     for (int p0 = p_begin; p0 < p_end; p0 += KP) {
         if constexpr (FEAT_BF16) {
-            uint2 ua[4], ub[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int p = p0 + 4 * pg + j;
-                const bool ok = p < p_end;
-                ua[j] = ok ? *reinterpret_cast<const uint2*>(fh + (size_t)p * C + c0 + 4 * q4) : make_uint2(0u, 0u);
-                ub[j] = ok ? *reinterpret_cast<const uint2*>(fh + (size_t)p * C + d0 + 4 * q4) : make_uint2(0u, 0u);
-            }
-            __syncthreads();   // the previous chunk's operand reads are done
-            // channel 4 q4 + k of pixel j: half (k & 1) of word (k >> 1) of u[j]
-            auto col = [](const uint2 (&u)[4], int k) __attribute__((always_inline)) {
-                const unsigned w0 = (k >> 1) ? u[0].y : u[0].x, w1 = (k >> 1) ? u[1].y : u[1].x;
-                const unsigned w2 = (k >> 1) ? u[2].y : u[2].x, w3 = (k >> 1) ? u[3].y : u[3].x;
-                // v_perm selectors: bytes 0-1 / 2-3 of each word (the low / high bf16)
-                const unsigned sel = (k & 1) ? 0x07060302u : 0x05040100u;
-                return make_uint2(__builtin_amdgcn_perm(w1, w0, sel), __builtin_amdgcn_perm(w3, w2, sel));
-            };
+            // channel 4 q4 + k of pixel j: half (k & 1) of word (k >> 1) of u8[j]; v_perm selectors pick the low /
+            // high bf16 of two words
+            uint4 rows[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                *reinterpret_cast<uint2*>(la + (4 * q4 + k) * RS + 4 * pg) = col(ua, k);
-                *reinterpret_cast<uint2*>(lb + (4 * q4 + k) * RS + 4 * pg) = col(ub, k);
+                const unsigned sel = (k & 1) ? 0x07060302u : 0x05040100u;
+                unsigned w[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) w[j] = (k >> 1) ? u8[j].y : u8[j].x;
+                rows[k] = make_uint4(__builtin_amdgcn_perm(w[1], w[0], sel), __builtin_amdgcn_perm(w[3], w[2], sel),
+                                     __builtin_amdgcn_perm(w[5], w[4], sel), __builtin_amdgcn_perm(w[7], w[6], sel));
             }
+            if (p0 + KP < p_end) load8(p0 + KP);
+            __syncthreads();   // the previous chunk's operand reads are done
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(ldst + k * RS) = rows[k];
             __syncthreads();
 #pragma unroll
             for (int s = 0; s < KP / 16; ++s) {   // K step: pixels 16 s + 8 lh .. + 7
