@@ -547,14 +547,16 @@ def _grad_report(plan, tr, grads, ref, B):
 @pytest.mark.parametrize("size,precision,transfer", [
     ("full", "fp32", "winograd_bf16x6"),     # BASELINE config 4's transfer arithmetic at 480x960 (bench.py's trainer)
     ("quarter", "bf16", "winograd_bf16x6"),  # the bench's bf16 VGG16 line against its bf16 simulation, 128x256
-], ids=["config4_480x960_fp32_vgg", "config4_128x256_bf16_vgg"])
+    ("full", "bf16", "winograd_bf16x6"),     # ... and at the bench's own 480x960
+], ids=["config4_480x960_fp32_vgg", "config4_128x256_bf16_vgg", "config4_480x960_bf16_vgg"])
 def test_training_step_at_scale_matches_f32_oracle(size, precision, transfer):
     """Config 4 (train_network.py:61,102,128-138) past the small parity shapes: one training step of the benchmarked
     trainer (winograd_bf16x6 transfer convs, its default split-bf16 start-conv weight gradient, style parameters as
     input) against oracle/torch_train.py run in float32 autograd on the host (the float64 oracle would take minutes at
     this size; the reference's own arithmetic is float32), max-pool / ReLU routing from the GPU as in the small tests.
-    ``full``: 480x960 (rst-960-120-128-17), B=1, VGG16 in fp32. ``quarter``: 128x256 (bottleneck 32 x 128; VGG16's four pools need multiples of 16), B=1, VGG16
-    in plain bf16 against the oracle's _Bf16Conv / _Bf16Gram simulation of it.
+    ``full``: 480x960 (rst-960-120-128-17), B=1, VGG16 in fp32 or in plain bf16. ``quarter``: 128x256 (bottleneck
+    32 x 128; VGG16's four pools need multiples of 16), B=1. Plain bf16 is checked against the oracle's _Bf16Conv /
+    _Bf16Store / _Bf16Gram simulation of it (bf16 operands, layer outputs and input gradients).
     Bounds (float32-level GPU vs float32 host, both rounding): prediction max-abs 5e-5, per-image loss terms rel 5e-4,
     style-parameter gradient and every transfer gradient tensor rel L2 5e-3 (bf16 VGG: 0.05 / loss 5e-3, the
     small-shape bf16 bounds: bf16 rounding flips between two different float32 forwards)."""
