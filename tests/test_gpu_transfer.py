@@ -131,6 +131,53 @@ def test_l2_weight_prefetch_is_numerically_neutral():
     assert np.array_equal(ys[0], ys[1]), np.abs(ys[0] - ys[1]).max()
 
 
+def test_timeline_stamps_are_neutral_and_ordered():
+    """rst_timeline_* (bench.graph_layer_ms's in-graph layer times): the stamping kernels' extra vector store per
+    wave leaves the frame bitwise unchanged, eager and replayed from a captured hipGraph; every residual conv and
+    narrow conv stamps, and the stamps of one frame's stamped layers are increasing (one stream, in layer order)."""
+    _need_gpu()
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    cfg = ShapeConfig.from_spec("rst-960-120-128-17")
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    m, _ = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                       weights=init_weights(plan, seed=2), max_batch=1, precision="winograd_bf16x6")
+    rng = np.random.default_rng(12)
+    x = torch.from_numpy(rng.random((1,) + ins).astype(np.float32)).cuda()
+    sp = torch.from_numpy(np.ascontiguousarray(synthetic_style_params(1, 1, plan.num_style_params, plan, seed=5))).cuda()
+    inp = {'content': x, 'style_params': sp}
+    y0 = m(inp).cpu().numpy()
+    m.timeline_begin()
+    try:
+        y1 = m(inp).cpu().numpy()
+        e_eager = m.timeline_read()
+        out = torch.empty_like(torch.from_numpy(y0)).cuda()
+        s = torch.cuda.Stream()   # bench.capture_graph's recipe: a warm-up launch on a side stream, then the capture
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            m(inp, out=out)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            m(inp, out=out)
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        y2 = out.cpu().numpy()
+        e_graph = m.timeline_read()
+        del g
+        torch.cuda.synchronize()
+    finally:
+        m.timeline_end()
+    assert np.array_equal(y0, y1) and np.array_equal(y0, y2)
+    for e in (e_eager, e_graph):
+        st = e[np.isfinite(e)]
+        assert st.size >= 14, e            # ten residual convs, four narrow convs
+        assert np.all(np.diff(st) > 0), e
+
+
 def test_full_size_repeated_calls_mixed_batch():
     """Full size, one handle: B=2, then B=1 on other content, then B=2 again all match the oracle and
     the repeated call is bitwise equal (no state — CIN partials, affines, workspaces — carries over
