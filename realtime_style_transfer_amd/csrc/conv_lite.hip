@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -46,8 +47,8 @@ namespace rst {
 #ifdef LITE_PROF
 // s_memtime per (workgroup < 64, wave, step < 16, point): 0 step top, 1 after staging + barrier,
 // 2 after the MFMAs, 3 after the epilogue (tools/lite_bench)
-__device__ unsigned long long lite_tl[64][4][16][4];
-__device__ unsigned long long lite_t0[64][4][2];   // kernel start, end of the last step
+__device__ unsigned long long lite_tl[64][8][16][4];
+__device__ unsigned long long lite_t0[64][8][2];   // kernel start, end of the last step
 #define LTL(st, pt) \
     if (blockIdx.x < 64 && lane == 0 && (st) < 16) lite_tl[blockIdx.x][wave][(st)][(pt)] = __builtin_amdgcn_s_memtime()
 #define LT0(k) \
@@ -72,7 +73,7 @@ __device__ __forceinline__ void split3(float x, float y, unsigned& p0, unsigned&
     p2 = bf16_last_piece(x, y);
 }
 
-template <int MODE, int CIN, int NC, int CKC, int X6 = 0>
+template <int MODE, int CIN, int NC, int CKC, int X6 = 0, int KSP = 1>
 struct Cfg {
     static constexpr int MS = NC;                           // MFMA M = N = Cout
     static constexpr int TW = MS, TH = 4;                   // GEMM-grid tile: 4 rows x MS pixels
@@ -94,16 +95,30 @@ struct Cfg {
     static constexpr int KS2 = X6 ? CKC / KSTEP : 1;        // K steps per chunk (x6)
     static constexpr int NPIXP = (NPIX + 15) / 16 * 16;
     static constexpr bool WIN_REGS = X6 && NCH == 1;        // x6 weights in registers
+    // K split (expand_0): waves w and w + 4 compute pixel row w & 3 over the even / odd K steps of every chunk, then
+    // trade accumulators so that each finishes one output row (two phases): two waves per SIMD hide each other's LDS
+    // operand latency and the staging work per thread halves (one workgroup per CU either way: 240 tiles, 256 CUs)
+    // The K split's weights come by LDS-DMA (global_load_lds, no staging registers: two waves per SIMD leave 256
+    // registers a wave) into two weight buffers, chunk c + 1's landing while chunk c's MFMAs read the other.
+    static constexpr int KSPLIT = KSP;
+    static_assert(KSP == 1 || (KSP == 2 && X6 && MODE == 1 && NCH > 1 && KS2 % 2 == 0), "K split: x6 multi-chunk transposed");
+    static constexpr bool WDMA = KSPLIT == 2;
+    static constexpr int NW = 4 * KSPLIT, NT = 64 * NW;     // waves, threads per workgroup
     static constexpr int HALO = X6 ? 3 * KS2 * G * NPIXP * 4 : NPIX * CS;   // floats per halo buffer
     static constexpr int WCH = WIN_REGS ? 0 : (X6 ? 9 * CKC * NC * 3 / 2 : 9 * CKC * NC);   // floats per chunk of weights in LDS
-    static constexpr int HITEMS = HR * HC * QC;             // float4 items per halo chunk
-    static constexpr int HREG = (HITEMS + 255) / 256;
+    static constexpr int WBUF = WDMA ? 2 : 1;               // weight buffers
     static constexpr int WITEMS = WCH / 4;
-    static constexpr int WREG = (WITEMS + 255) / 256;
+    static constexpr int WREG = (WITEMS + NT - 1) / NT;
+    static_assert(!WDMA || (WITEMS % 64 == 0 && NCH % 2 == 0), "LDS-DMA: whole wave instructions, chunk parity = buffer");
     static constexpr int NACC = MS == 16 ? 4 : 16;          // accumulator floats per MFMA tile and lane
     static constexpr int NPH = MODE == 0 ? 1 : 4;           // output phases
-    static constexpr int RED = MODE == 1 ? 16 * NC : 0;     // statistics scratch (floats): [16][NC]
-    static constexpr size_t LDS_BYTES = (size_t)(HALO + WCH) * 4 + RED * 4;
+    static constexpr int OST_FL = 4 * TW * NC;              // floats of one pixel row's output (4 phases)
+    static constexpr int XCH = KSPLIT == 2 ? NW * 2 * NACC * 64 : 0;   // K-split accumulator exchange (floats)
+    // LDS body: the halo + weight images; at the end of a tile the K split's exchange, then its output staging, in it
+    static constexpr int IMG = HALO + WBUF * WCH;
+    static constexpr int BODY = IMG > 4 * OST_FL && IMG > XCH ? IMG : (4 * OST_FL > XCH ? 4 * OST_FL : XCH);
+    static constexpr int RED = MODE == 1 ? 4 * NW * NC : 0; // statistics scratch (floats): [NW][NC] f64 pairs
+    static constexpr size_t LDS_BYTES = (size_t)BODY * 4 + RED * 4;
     static_assert(CIN % CKC == 0 && CKC % (4 * KS) == 0, "chunking");
     static_assert(MS == 16 || MS == 32, "MFMA shape");
     static_assert(((CS / 4) & 1) == 1, "odd 16-B slots per halo pixel");
@@ -142,6 +157,13 @@ __device__ __forceinline__ void sfor(F&& f) {
     }
 }
 
+// sum of N per-wave values p[0], p[stride], ... as a pairwise tree (fixed order; N = 4: (p0 + p1) + (p2 + p3))
+template <int N, typename T>
+__device__ __forceinline__ T wave_sum(const T* p, int stride) {
+    if constexpr (N == 1) return p[0];
+    else return wave_sum<N / 2>(p, stride) + wave_sum<N / 2>(p + (N / 2) * stride, stride);
+}
+
 // transposed-conv slots: (phase, operand position ty*2+tx); the kernel tap is ky = py + 2(1-ty), kx = px + 2(1-tx)
 __host__ __device__ constexpr int t_phase(int s) { return s < 4 ? 0 : (s < 6 ? 1 : (s < 8 ? 2 : 3)); }
 __host__ __device__ constexpr int t_pos(int s) {
@@ -153,27 +175,35 @@ __host__ __device__ constexpr int t_pos(int s) {
 // affines, styleTransfer.py:36-44, as conv_mfma.hip's prologue)
 constexpr int LITE_BLEND = 8;
 
-template <int MODE, int CIN, int NC, int CKC, int PROF, int X6>
-__global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles) {
+template <int MODE, int CIN, int NC, int CKC, int PROF, int X6, int KSP>
+__global__ __launch_bounds__((lite::Cfg<MODE, CIN, NC, CKC, X6, KSP>::NT)) void conv_lite_kernel(ConvArgs a, int n_tiles) {
     using namespace lite;
     constexpr int PRO = PROF & 7;
     constexpr bool BLEND = (PROF & LITE_BLEND) != 0;
-    using C = Cfg<MODE, CIN, NC, CKC, X6>;
+    using C = Cfg<MODE, CIN, NC, CKC, X6, KSP>;
     using M = Mfma<C::MS>;
     typedef typename M::acc_t acc_t;
     constexpr int MS = C::MS, TW = C::TW, TH = C::TH, KS = C::KS, CS = C::CS, HC = C::HC, HR = C::HR, R = C::R;
     constexpr int QC = C::QC, NCH = C::NCH;
 
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    // [HALO] one Cin chunk of the tile's input halo, then [WCH] its weights
-    float* const halo = smem;
-    float* const wts = smem + C::HALO;
-    // [16][NC] statistics: S, n, M2 per wave (partials path) / [4][NC][2] f64 (accumulator flush)
-    float* const red = smem + (C::HALO + C::WCH);
-    static_assert((C::HALO + C::WCH) % 2 == 0, "f64-aligned statistics scratch");
+    // [HALO] one Cin chunk of the tile's input halo, then [WCH] its weights. LDS-DMA weights (K split): [WCH] weight
+    // buffer 1, [HALO], [WCH] buffer 0 — chunk c uses buffer c & 1, so a tile's last chunk reads buffer 1 and the next
+    // tile's first chunk lands in buffer 0 while the epilogue's exchange / output staging use [0, 64 KB)
+    float* const halo = smem + (C::WDMA ? C::WCH : 0);
+    float* const wts = smem + C::HALO;   // (not LDS-DMA)
+    auto wbase = [&](int buf) __attribute__((always_inline)) {
+        return C::WDMA ? (buf == 0 ? smem + C::WCH + C::HALO : smem) : wts;
+    };
+    int wbuf = 0;   // LDS-DMA weights: the buffer the current step's MFMAs read
+    // [3][NW][NC] statistics: S, n, M2 per wave (partials path) / [NW][NC][2] f64 (accumulator flush)
+    float* const red = smem + C::BODY;
+    static_assert(C::BODY % 2 == 0, "f64-aligned statistics scratch");
+    constexpr int NT = C::NT, NW = C::NW;
     float2* const tab = reinterpret_cast<float2*>(red + C::RED);   // prologue affine [batch][CIN] (+ second style)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rw = wave & 3, kh = C::KSPLIT == 2 ? wave >> 2 : 0;   // pixel row of the tile, K half
     LT0(0);
     const int H = a.H, W = a.W;
     auto halo_off = [&](int hy, int hx) __attribute__((always_inline)) {
@@ -202,9 +232,9 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // Thread t stages channel quad q = t % QC of main column col = (t / QC) % (HC - 1) in rows
     // rsub + RPP k, and (t < HR QC) the last halo column in row t / QC: the global and LDS offsets
     // advance by a constant per row (a per-item (pixel, quad) decode cost as much VALU as the MFMAs).
-    constexpr int HCM = HC - 1, TPR = HCM * QC, RPP = 256 / TPR, NMAIN = (HR + RPP - 1) / RPP;
+    constexpr int HCM = HC - 1, TPR = HCM * QC, RPP = NT / TPR, NMAIN = (HR + RPP - 1) / RPP;
     constexpr int NEXTRA = HR * QC;
-    static_assert(256 % TPR == 0 && NEXTRA <= 256, "staging map");
+    static_assert(NT % TPR == 0 && NEXTRA <= NT, "staging map");
     const int q = tid % QC;
     const int col = (tid / QC) % HCM;
     const int rsub = tid / TPR;
@@ -215,18 +245,26 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // under load exceeds one tile's MFMAs); multi-chunk layers use set 0 only
     // (x6 single-chunk layers hold their weights in VGPRs instead: one set, two workgroups per CU cover the latency)
     constexpr int NSET = NCH == 1 && !C::WIN_REGS ? 2 : 1;
-    f32x4 hreg[NSET][NMAIN + 1], rreg[NSET][NMAIN + 1], wreg[NCH > 1 ? C::WREG : 1], pa01[NSET], pa23[NSET];
+    f32x4 hreg[NSET][NMAIN + 1], rreg[NSET][NMAIN + 1], wreg[NCH > 1 && !C::WDMA ? C::WREG : 1], pa01[NSET], pa23[NSET];
     f32x4 pb01[NSET], pb23[NSET];   // BLEND: the second style's affine of the thread's channel quad
     float bw[NSET][NMAIN + 1];      // BLEND: the second style's weight at each staged pixel
     // one chunk's weight image (multi-chunk layers, one register set)
-    auto load_w = [&](int ch) __attribute__((always_inline)) {
+    auto load_w = [&](int ch, int buf) __attribute__((always_inline)) {
         sfor<0, C::WREG>([&](auto K) __attribute__((always_inline)) {
             constexpr int k = decltype(K)::value;
-            const int it = min(tid + 256 * k, C::WITEMS - 1);
-            wreg[k] = reinterpret_cast<const f32x4*>(a.wpk)[(size_t)ch * C::WITEMS + it];
+            if constexpr (C::WDMA) {   // 1 KB per wave instruction into the lane-linear image (the packed order)
+                const int i0 = NT * k + wave * 64;   // wave-uniform
+                if (C::WITEMS % NT == 0 || i0 < C::WITEMS)
+                    __builtin_amdgcn_global_load_lds(
+                        (const void*)(reinterpret_cast<const f32x4*>(a.wpk) + (size_t)ch * C::WITEMS + i0 + lane),
+                        (__attribute__((address_space(3))) void*)(wbase(buf) + i0 * 4), 16, 0, 0);
+            } else {
+                const int it = min(tid + NT * k, C::WITEMS - 1);
+                wreg[k] = reinterpret_cast<const f32x4*>(a.wpk)[(size_t)ch * C::WITEMS + it];
+            }
         });
     };
-    auto load_in = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {
+    auto load_in = [&](const Tile& T, int ch, auto SET, int buf = 0) __attribute__((always_inline)) {
         constexpr int st = decltype(SET)::value;
         const int co = ch * CKC;
         const int ixm = min(max(T.ix0 + col, 0), W - 1), ixe = min(max(T.ix0 + HCM, 0), W - 1);
@@ -239,7 +277,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             if constexpr (PRO == PRO_AFF_RES) rreg[st][k] = *reinterpret_cast<const f32x4*>(a.res + gi);
             if constexpr (BLEND) bw[st][k] = a.pro_w[(rb + min(max(T.iy0 + hy, 0), H - 1)) * W + (k < NMAIN ? ixm : ixe)];
         });
-        if constexpr (NCH > 1) load_w(ch);
+        if constexpr (NCH > 1) load_w(ch, buf);
     };
     auto load_aff = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {   // from the LDS table
         constexpr int st = decltype(SET)::value;
@@ -255,8 +293,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
         }
     };
-    auto load_step = [&](const Tile& T, int ch, auto SET) __attribute__((always_inline)) {
-        load_in(T, ch, SET);
+    auto load_step = [&](const Tile& T, int ch, auto SET, int buf = 0) __attribute__((always_inline)) {
+        load_in(T, ch, SET, buf);
         load_aff(T, ch, SET);
     };
     auto xform = [&](f32x4 v, f32x4 r, const f32x4& p01, const f32x4& p23, float w, const f32x4& q01,
@@ -306,7 +344,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     };
     // staging of one chunk into LDS, as NSTORE items: the NMAIN main-column rows, the last halo column, then the WREG
     // weight float4s
-    constexpr int NSTORE = NMAIN + 1 + (NCH > 1 ? C::WREG : 0);
+    constexpr int NSTORE = NMAIN + 1 + (NCH > 1 && !C::WDMA ? C::WREG : 0);
     auto store_item = [&](const Tile& T, auto SET, auto IDX) __attribute__((always_inline)) {
         constexpr int st = decltype(SET)::value, idx = decltype(IDX)::value;
         auto row_ok = [&](int hy) __attribute__((always_inline)) { return T.iy0 + hy >= 0 && T.iy0 + hy < H; };
@@ -330,8 +368,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
         } else if constexpr (NCH > 1) {
             constexpr int k = idx - NMAIN - 1;
-            const int it = tid + 256 * k;
-            if (C::WITEMS % 256 == 0 || it < C::WITEMS) reinterpret_cast<f32x4*>(wts)[it] = wreg[k];
+            const int it = tid + NT * k;
+            if (C::WITEMS % NT == 0 || it < C::WITEMS) reinterpret_cast<f32x4*>(wts)[it] = wreg[k];
         }
     };
     auto store_step = [&](const Tile& T, auto SET) __attribute__((always_inline)) {
@@ -341,8 +379,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // ---- operands: A = pixel m of this wave's row, quad g + KS r; B = row (slot, r, g), column m ------
     const int m = lane % MS, g = lane / MS;
     auto a_off = [&](int pos) __attribute__((always_inline)) {   // pos: tap (MODE 0) / operand position (MODE 1)
-        if constexpr (MODE == 0) return halo_off(2 * wave + pos / 3, 2 * m + pos % 3);
-        else return halo_off(wave + (pos >> 1), m + (pos & 1));
+        if constexpr (MODE == 0) return halo_off(2 * rw + pos / 3, 2 * m + pos % 3);
+        else return halo_off(rw + (pos >> 1), m + (pos & 1));
     };
     // software pipeline: the operands of step u+1 are read before the MFMAs of step u issue. Steps:
     // MODE 0 one (r, kernel row) = 3 taps, 12 MFMAs into 3 accumulators (one per kx: no back-to-back
@@ -350,7 +388,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // accumulators (phase 0's four slots alternate between two).
     constexpr int NA = MODE == 0 ? 3 : 4, NB = MODE == 0 ? 3 : 9, NSTEP = MODE == 0 ? 3 * R : R;
     // (x6 strided conv with Cout 32: one 32x32x16 accumulator chain, which issues back to back, MI355X_MICROARCH.md)
-    constexpr int NACCS = MODE == 0 ? (X6 && MS == 32 ? 1 : 3) : 5;
+    // (K split: one accumulator per phase — two waves per SIMD interleave their MFMA chains — for the registers)
+    constexpr int NACCS = MODE == 0 ? (X6 && MS == 32 ? 1 : 3) : (C::KSPLIT == 2 ? 4 : 5);
     acc_t acc[NACCS];
     auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -426,7 +465,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     };
     auto compute_x6 = [&]() __attribute__((always_inline)) {
       if constexpr (X6) {   // discarded (not instantiated) for the f32 configurations
-        const unsigned char* wbytes = reinterpret_cast<const unsigned char*>(wts);
+        const unsigned char* wbytes = reinterpret_cast<const unsigned char*>(wbase(wbuf));
         const unsigned char* hbytes = hbytes_r();
         auto readB = [&](int sl, int ks, short8 (&Bv)[3]) __attribute__((always_inline)) {
             sfor<0, 3>([&](auto PC) __attribute__((always_inline)) {
@@ -440,14 +479,37 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 A[pc] = *reinterpret_cast<const short8*>(hbytes + pc * XPIECE + ((ks * C::G + kg) * C::NPIXP + pix) * 16);
             });
         };
-        sfor<0, C::KS2>([&](auto KSI) __attribute__((always_inline)) {
-            constexpr int ks = decltype(KSI)::value;
-            if constexpr (MODE == 1) {
+        sfor<0, C::KS2 / C::KSPLIT>([&](auto KSI) __attribute__((always_inline)) {
+            const int ks = decltype(KSI)::value * C::KSPLIT + kh;   // this wave's K steps
+            if constexpr (MODE == 1 && C::KSPLIT == 2) {
+                // each operand position read one or two slots before its first use and dead after its last (slot order
+                // 0 1 4 2 6 3 5 7 8: position 0 | 1 1 | 2 2 | 3 3 3 3): two positions live instead of four
+                constexpr int order[9] = {0, 1, 4, 2, 6, 3, 5, 7, 8};
+                short8 A[4][3];
+                auto rdA = [&](auto P) __attribute__((always_inline)) {
+                    constexpr int pos = decltype(P)::value;
+                    readA((rw + (pos >> 1)) * HC + m + (pos & 1), ks, A[pos]);
+                };
+                rdA(std::integral_constant<int, 0>{});
+                rdA(std::integral_constant<int, 1>{});
+                constexpr int BD = 2;   // B operand one slot ahead
+                short8 Bq[BD][3];
+                readB(order[0], ks, Bq[0]);
+                sfor<0, 9>([&](auto J) __attribute__((always_inline)) {
+                    constexpr int j = decltype(J)::value, sl = order[j];
+                    if constexpr (j == 1) rdA(std::integral_constant<int, 2>{});
+                    if constexpr (j == 3) rdA(std::integral_constant<int, 3>{});
+                    if constexpr (j + 1 < 9) readB(order[j + 1], ks, Bq[(j + 1) % BD]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mfma6(acc[t_phase(sl)], A[t_pos(sl)], Bq[j % BD]);
+                    __builtin_amdgcn_sched_barrier(0);
+                });
+            } else if constexpr (MODE == 1) {
                 constexpr int order[9] = {0, 4, 6, 8, 1, 5, 7, 2, 3};
                 short8 A[4][3];
                 sfor<0, 4>([&](auto P) __attribute__((always_inline)) {
                     constexpr int pos = decltype(P)::value;
-                    readA((wave + (pos >> 1)) * HC + m + (pos & 1), ks, A[pos]);
+                    readA((rw + (pos >> 1)) * HC + m + (pos & 1), ks, A[pos]);
                 });
                 constexpr int BD = 2;   // B operand one slot ahead
                 short8 Bq[BD][3];
@@ -467,13 +529,13 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             } else {   // taps t = 3 ky + kx into acc[kx]; A of tap t + 1 read while tap t's MFMAs run
                 static_assert(MODE != 0 || C::WIN_REGS, "x6 strided conv: single-chunk layers");
                 short8 A0[3], A1[3];
-                readA(hpix(2 * wave, 2 * m), ks, A0);
+                readA(hpix(2 * rw, 2 * m), ks, A0);
                 sfor<0, 9>([&](auto T) __attribute__((always_inline)) {
                     constexpr int t = decltype(T)::value, ky = t / 3, kx = t % 3;
                     if constexpr (t + 1 < 9) {
                         constexpr int ky1 = (t + 1) / 3, kx1 = (t + 1) % 3;
-                        if constexpr ((t & 1) == 0) readA(hpix(2 * wave + ky1, 2 * m + kx1), ks, A1);
-                        else readA(hpix(2 * wave + ky1, 2 * m + kx1), ks, A0);
+                        if constexpr ((t & 1) == 0) readA(hpix(2 * rw + ky1, 2 * m + kx1), ks, A1);
+                        else readA(hpix(2 * rw + ky1, 2 * m + kx1), ks, A0);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                     constexpr int ai = NACCS == 1 ? 0 : kx;
@@ -517,7 +579,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     const bool to_acc = a.stat.acc != nullptr;
     double accS = 0.0, accQ = 0.0;
     int acc_b = -1;
-    double* const red_d = reinterpret_cast<double*>(red);   // [4 waves][NC][2] at the flush
+    double* const red_d = reinterpret_cast<double*>(red);   // [NW waves][NC][2] at the flush
     auto acc_flush = [&]() __attribute__((always_inline)) {
         if (acc_b >= 0) {
             if (lane < MS) {
@@ -526,10 +588,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             }
             lds_barrier();   // (the next write of red_d comes after the next step's top barrier)
             if (tid < NC) {
-                const double S = (red_d[tid * 2] + red_d[(NC + tid) * 2]) +
-                                 (red_d[(2 * NC + tid) * 2] + red_d[(3 * NC + tid) * 2]);
-                const double Q = (red_d[tid * 2 + 1] + red_d[(NC + tid) * 2 + 1]) +
-                                 (red_d[(2 * NC + tid) * 2 + 1] + red_d[(3 * NC + tid) * 2 + 1]);
+                const double S = wave_sum<NW>(red_d + tid * 2, 2 * NC);
+                const double Q = wave_sum<NW>(red_d + tid * 2 + 1, 2 * NC);
                 cin_acc_add(a.stat, a.batch, NC, acc_b, tid, (int)blockIdx.x % a.stat.nslot, S, Q);
             }
         }
@@ -538,17 +598,17 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFF0, 0x00020000);
     // x6 transposed convs stage full tiles' output through LDS
     constexpr bool OSTAGE = X6 && MODE == 1 && LITE_OSTAGE;
-    constexpr int OST_FL = 4 * TW * NC;   // floats per wave
+    constexpr int OST_FL = C::OST_FL;   // floats per pixel row
     // x6 strided convs (contract_0 / _1, weights in VGPRs): the same for their one output row per wave
     constexpr bool OSTAGE0 = X6 && MODE == 0 && C::WIN_REGS && LITE_OSTAGE0;
     static_assert(!OSTAGE0 || 4 * TW * NC <= C::HALO, "output staging fits the halo image");
-    static_assert(!OSTAGE || 4 * OST_FL <= C::HALO + C::WCH, "output staging fits the halo + weight images");
+    static_assert(!OSTAGE || 4 * OST_FL <= C::BODY, "output staging fits the LDS body");
     auto epilogue = [&](const Tile& T) __attribute__((always_inline)) {
         if constexpr (MODE == 0) {   // bias + ReLU -> BatchNorm (inference affine) -> ReLU, NHWC store
             acc_t y;
             if constexpr (NACCS == 1) y = acc[0];
             else y = (acc[0] + acc[1]) + acc[2];
-            const int oy = T.y0 + wave;
+            const int oy = T.y0 + rw;
             const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
             float* const orow = a.out + ((size_t)(T.b * a.Ho + oy) * a.Wo) * NC + n;
             if (OSTAGE0 && full) {   // the wave's TW x NC output row segment through LDS, 16 B per lane
@@ -558,7 +618,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                     y[j] = fmaxf(fmaf(bn.x, v, bn.y), 0.f);
                 }
                 lds_barrier();   // every wave's MFMA operand reads are done
-                float* const ob = smem + wave * (TW * NC);
+                float* const ob = smem + rw * (TW * NC);
 #pragma unroll
                 for (int j = 0; j < C::NACC; ++j) ob[M::row(j, lane) * NC + n] = y[j];
                 const size_t obase = ((size_t)(T.b * a.Ho + oy) * a.Wo + T.x0) * NC;
@@ -588,35 +648,73 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 }
             }
         } else {   // bias, pixel-shuffle store, per-tile CIN statistics over the four phases
-            acc[0] = acc[0] + acc[4];
-            const int p = T.y0 + wave;
+            if constexpr (NACCS == 5) acc[0] = acc[0] + acc[4];
+            const int p = T.y0 + rw;
             const int Ho2 = 2 * a.Ho, Wo2 = 2 * a.Wo;
-            float s = 0.f, cnt = 0.f;
             // interior tiles (every pixel inside) store without per-element guards
             const bool full = T.y0 + TH <= a.Ho && T.x0 + TW <= a.Wo;
             float* const orow = a.out + ((size_t)(T.b * Ho2 + 2 * p) * Wo2) * NC + n;
+            // the phases [P0, P0 + NPHW) this wave finishes: all four, or (K split) output row py = kh's two
+            constexpr int NPHW = 4 / C::KSPLIT;
+            if constexpr (C::KSPLIT == 2) {
+                // the two K halves of a pixel row meet: wave (rw, kh) hands its partial sums of the partner's output row
+                // (phases 2 - 2 kh, 3 - 2 kh) to the partner through LDS (the halo / weight images are dead after the
+                // barrier) and adds the partner's partials of its own row, which it keeps in acc[0..1]; float adds
+                // commute, so both sides form the same sums. Selects on values, not on accumulator indices: a
+                // kh-dependent index would put the accumulators in scratch.
+                lds_barrier();   // every wave's MFMA operand reads are done
+                f32x4* const xw = reinterpret_cast<f32x4*>(smem) + (size_t)wave * (2 * C::NACC / 4) * 64 + lane;
+                const f32x4* const xr = reinterpret_cast<const f32x4*>(smem) + (size_t)(wave ^ 4) * (2 * C::NACC / 4) * 64 + lane;
+                const bool hi = kh != 0;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j4 = 0; j4 < C::NACC / 4; ++j4) {
+                        f32x4 v;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = hi ? acc[i][4 * j4 + e] : acc[2 + i][4 * j4 + e];
+                        xw[(i * (C::NACC / 4) + j4) * 64] = v;
+                    }
+                lds_barrier();
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j4 = 0; j4 < C::NACC / 4; ++j4) {
+                        const f32x4 v = xr[(i * (C::NACC / 4) + j4) * 64];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            acc[i][4 * j4 + e] = (hi ? acc[2 + i][4 * j4 + e] : acc[i][4 * j4 + e]) + v[e];
+                    }
+                lds_barrier();   // the output staging below reuses the exchange area
+            }
+            // output row (0 / 1 of the pixel row's two) of this wave's local phase ph: K split, all in row kh
+            auto prow = [&](int ph) __attribute__((always_inline)) { return C::KSPLIT == 2 ? kh : ph >> 1; };
+            auto finish = [&](auto PH0) __attribute__((always_inline)) {
+            constexpr int P0 = decltype(PH0)::value;
+            float s = 0.f, cnt = 0.f;
             if (full && OSTAGE) {
-                // x6: the wave's 2 output rows x 2 TW pixels x NC channels through LDS (the tile's halo / weight
+                // x6: the wave's output rows x 2 TW pixels x NC channels through LDS (the tile's halo / weight
                 // images are dead after the barrier), then stored as whole 128-B lines, 16 B per lane: 4x fewer
                 // store instructions than the per-accumulator dword stores, no half-line writes
 #pragma unroll
-                for (int ph = 0; ph < 4; ++ph)
+                for (int ph = P0; ph < P0 + NPHW; ++ph)
 #pragma unroll
                     for (int j = 0; j < C::NACC; ++j) {
                         acc[ph][j] += bias;
                         s += acc[ph][j];
                     }
-                cnt = 4.f * C::NACC;
-                lds_barrier();   // every wave's MFMA operand reads are done
-                float* const ob = smem + wave * OST_FL;
+                cnt = (float)NPHW * C::NACC;
+                if constexpr (C::KSPLIT == 1) lds_barrier();   // every wave's MFMA operand reads are done
+                float* const ob = smem + rw * OST_FL;
 #pragma unroll
-                for (int ph = 0; ph < 4; ++ph)
+                for (int ph = P0; ph < P0 + NPHW; ++ph)
 #pragma unroll
                     for (int j = 0; j < C::NACC; ++j)
-                        ob[((ph >> 1) * 2 * TW + 2 * M::row(j, lane) + (ph & 1)) * NC + n] = acc[ph][j];
+                        ob[(prow(ph) * 2 * TW + 2 * M::row(j, lane) + (ph & 1)) * NC + n] = acc[ph][j];
                 constexpr int ROWF = 2 * TW * NC;   // floats of one output row segment (contiguous in NHWC)
 #pragma unroll
-                for (int py = 0; py < 2; ++py) {
+                for (int pr = 0; pr < NPHW / 2; ++pr) {
+                    const int py = C::KSPLIT == 2 ? kh : pr;
                     const size_t obase = ((size_t)(T.b * Ho2 + 2 * p + py) * Wo2 + 2 * T.x0) * NC;
 #pragma unroll
                     for (int it = 0; it < ROWF / 256; ++it) {
@@ -631,7 +729,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 }
             } else if (full) {
 #pragma unroll
-                for (int ph = 0; ph < 4; ++ph)
+                for (int ph = P0; ph < P0 + NPHW; ++ph)
 #pragma unroll
                     for (int j = 0; j < C::NACC; ++j) {
                         const int qq = T.x0 + M::row(j, lane);
@@ -640,22 +738,22 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                         if (a.wt_stores)
                             __builtin_amdgcn_raw_buffer_store_b32(
                                 __builtin_bit_cast(unsigned, v), osrd,
-                                (int)((orow + ((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC - a.out) * 4), 0, 16);
+                                (int)((orow + ((size_t)prow(ph) * Wo2 + 2 * qq + (ph & 1)) * NC - a.out) * 4), 0, 16);
                         else
-                            orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
+                            orow[((size_t)prow(ph) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
                         s += v;
                     }
-                cnt = 4.f * C::NACC;
+                cnt = (float)NPHW * C::NACC;
             } else {
 #pragma unroll
-                for (int ph = 0; ph < 4; ++ph)
+                for (int ph = P0; ph < P0 + NPHW; ++ph)
 #pragma unroll
                     for (int j = 0; j < C::NACC; ++j) {
                         const int qq = T.x0 + M::row(j, lane);
                         const float v = acc[ph][j] + bias;
                         acc[ph][j] = v;
                         if (p < a.Ho && qq < a.Wo) {
-                            orow[((size_t)(ph >> 1) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
+                            orow[((size_t)prow(ph) * Wo2 + 2 * qq + (ph & 1)) * NC] = v;
                             s += v;
                             cnt += 1.f;
                         }
@@ -671,7 +769,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 const float mean = cnt > 0.f ? s / cnt : 0.f;
                 float m2 = 0.f;
 #pragma unroll
-                for (int ph = 0; ph < 4; ++ph)
+                for (int ph = P0; ph < P0 + NPHW; ++ph)
 #pragma unroll
                     for (int j = 0; j < C::NACC; ++j) {
                         const int qq = T.x0 + M::row(j, lane);
@@ -690,7 +788,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                     if (cnt > 0.f) accQ += (double)m2 + dS * dS / (double)cnt;
                 }
             } else if (a.part != nullptr) {
-                // lanes n, n + MS, ... hold column n: reduce over them, then over the 4 waves (fixed order)
+                // lanes n, n + MS, ... hold column n: reduce over them, then over the NW waves (fixed order)
                 if constexpr (MS == 16) {
                     s = lane_xor_sum<16>(s);
                     cnt = lane_xor_sum<16>(cnt);
@@ -699,15 +797,15 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                 cnt = lane_xor_sum<32>(cnt);
                 if (lane < MS) {
                     red[wave * NC + n] = s;
-                    red[4 * NC + wave * NC + n] = cnt;
+                    red[NW * NC + wave * NC + n] = cnt;
                 }
                 lds_barrier();
-                const float S = (red[n] + red[NC + n]) + (red[2 * NC + n] + red[3 * NC + n]);
-                const float N = (red[4 * NC + n] + red[5 * NC + n]) + (red[6 * NC + n] + red[7 * NC + n]);
+                const float S = wave_sum<NW>(red + n, NC);
+                const float N = wave_sum<NW>(red + NW * NC + n, NC);
                 const float mean = N > 0.f ? S / N : 0.f;
                 float m2 = 0.f;
 #pragma unroll
-                for (int ph = 0; ph < 4; ++ph)
+                for (int ph = P0; ph < P0 + NPHW; ++ph)
 #pragma unroll
                     for (int j = 0; j < C::NACC; ++j) {
                         const int qq = T.x0 + M::row(j, lane);
@@ -716,21 +814,23 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
                     }
                 if constexpr (MS == 16) m2 = lane_xor_sum<16>(m2);
                 m2 = lane_xor_sum<32>(m2);
-                if (lane < MS) red[8 * NC + wave * NC + n] = m2;   // its own rows: no barrier before the write
+                if (lane < MS) red[2 * NW * NC + wave * NC + n] = m2;   // its own rows: no barrier before the write
                 lds_barrier();
                 if (tid < NC) {   // lane tid < NC holds column tid
-                    const float M2 = (red[8 * NC + tid] + red[9 * NC + tid]) + (red[10 * NC + tid] + red[11 * NC + tid]);
+                    const float M2 = wave_sum<NW>(red + 2 * NW * NC + tid, NC);
                     const int n_part = a.tiles_y * a.tiles_x;
                     a.part[((size_t)T.b * NC + tid) * n_part + T.ty * a.tiles_x + T.tx] = make_float4(S, M2, N, 0.f);
                 }
             }
+            };
+            finish(std::integral_constant<int, 0>{});   // (K split: the wave's own phases sit in acc[0..1])
         }
     };
 
     // ---- main loop over (tile, chunk) steps: step s+1's global loads are in flight while step s
     // computes and (last chunk) stores its tile ---------------------------------------------------------
     if constexpr (NCH == 1 && !C::WIN_REGS) {   // one weight image for every tile: staged once
-        for (int it = tid; it < C::WITEMS; it += 256)
+        for (int it = tid; it < C::WITEMS; it += NT)
             reinterpret_cast<f32x4*>(wts)[it] = reinterpret_cast<const f32x4*>(a.wpk)[it];
     }
     // the prologue affine of every image into the LDS table: given, or formed from the producer's fixed-point
@@ -741,8 +841,8 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
     // first input loads took expand_1 from 2 waves per SIMD to 1, 21.2 -> 28.3 us in the frame, profiles/r05)
     constexpr bool SPLIT_OK = !C::WIN_REGS;
     const bool split_aff = SPLIT_OK && PRO != PRO_NONE && a.pro_stat.acc != nullptr && a.batch == 1 &&
-                           CinAffineSplit<256, 2>::usable(a.pro_stat);
-    CinAffineSplit<256, 2> aff;
+                           CinAffineSplit<NT, 2>::usable(a.pro_stat);
+    CinAffineSplit<NT, 2> aff;
     auto fill_issue = [&]() __attribute__((always_inline)) {
         if constexpr (PRO != PRO_NONE)
             if constexpr (SPLIT_OK)
@@ -756,10 +856,10 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
             if (SPLIT_OK && split_aff)
                 aff.finish(ps, tab, BLEND ? tab + CIN : nullptr, store ? ps.ab_out : nullptr, store ? ps.ab1_out : nullptr);
             else
-                cin_affine_table<256, SPLIT_OK ? 8 : 1>(ps, 0, a.batch, tab, BLEND ? tab + a.batch * CIN : nullptr,
+                cin_affine_table<NT, SPLIT_OK ? 8 : 1>(ps, 0, a.batch, tab, BLEND ? tab + a.batch * CIN : nullptr,
                                       store ? ps.ab_out : nullptr, store ? ps.ab1_out : nullptr);
         } else {
-            for (int i = tid; i < a.batch * CIN; i += 256) {
+            for (int i = tid; i < a.batch * CIN; i += NT) {
                 tab[i] = a.pro_ab[i];
                 if constexpr (BLEND) tab[a.batch * CIN + i] = a.pro_ab1[i];
             }
@@ -788,7 +888,7 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         if (my_tiles > 1) load_aff(T1, 0, S1{});
         for (int k = 0; k < my_tiles; k += 2) {
             LTL(k, 0);
-            if (k + 2 >= my_tiles) l2f = l2_touch_xcd_slice<256, 2>(a.w_next, a.w_next_bytes);
+            if (k + 2 >= my_tiles) l2f = l2_touch_xcd_slice<NT, 2>(a.w_next, a.w_next_bytes);
             if (k > 0) lds_barrier();
             store_step(T0, S0{});
             lds_barrier();
@@ -829,17 +929,19 @@ __global__ __launch_bounds__(256) void conv_lite_kernel(ConvArgs a, int n_tiles)
         for (int s = 0; s < n_steps; ++s) {
             const int ch = s % NCH;
             LTL(s, 0);
-            if (s == n_steps - NCH) l2f = l2_touch_xcd_slice<256, 2>(a.w_next, a.w_next_bytes);
+            if (s == n_steps - NCH) l2f = l2_touch_xcd_slice<NT, 2>(a.w_next, a.w_next_bytes);
             if (s > 0) lds_barrier();        // the previous step's operand reads are done
             store_step(cur, S0{});
+            if constexpr (C::WDMA) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this chunk's weights have landed
             lds_barrier();
             LTL(s, 1);
             Tile nxt = cur;
             if (s + 1 < n_steps) {
                 const int ch1 = (s + 1) % NCH;
                 if (ch1 == 0) nxt = tile_of((s + 1) / NCH);
-                load_step(nxt, ch1, S0{});
+                load_step(nxt, ch1, S0{}, ch1 & 1);
             }
+            wbuf = ch & 1;
             compute();
             LTL(s, 2);
             if (ch == NCH - 1) {
@@ -955,14 +1057,14 @@ std::vector<float> conv_lite_pack_weights(const LiteTile& t, const float* kern) 
 
 #ifdef LITE_PROF
 void lite_timeline_print(int nsteps) {
-    std::vector<unsigned long long> tl((size_t)64 * 4 * 16 * 4);
+    std::vector<unsigned long long> tl((size_t)64 * 8 * 16 * 4);
     if (hipMemcpyFromSymbol(tl.data(), HIP_SYMBOL(lite_tl), tl.size() * 8) != hipSuccess) return;
     double d[3] = {0, 0, 0}, gap = 0;
     int n = 0, ng = 0;
     for (int g = 0; g < 64; ++g)
-        for (int w = 0; w < 4; ++w)
+        for (int w = 0; w < 8; ++w)
             for (int st = 0; st < nsteps && st < 16; ++st) {
-                const unsigned long long* q = &tl[(((size_t)g * 4 + w) * 16 + st) * 4];
+                const unsigned long long* q = &tl[(((size_t)g * 8 + w) * 16 + st) * 4];
                 if (q[0] == 0 || q[3] < q[0]) continue;
                 for (int k = 0; k < 3; ++k) d[k] += (double)(q[k + 1] - q[k]);
                 ++n;
@@ -973,14 +1075,14 @@ void lite_timeline_print(int nsteps) {
             }
     if (n) printf("    per step (100 cycles): staging+barrier %.2f, MFMA %.2f, epilogue %.2f (n=%d)\n", d[0] / n * 0.01,
                   d[1] / n * 0.01, d[2] / n * 0.01, n);
-    std::vector<unsigned long long> t0((size_t)64 * 4 * 2);
+    std::vector<unsigned long long> t0((size_t)64 * 8 * 2);
     if (hipMemcpyFromSymbol(t0.data(), HIP_SYMBOL(lite_t0), t0.size() * 8) == hipSuccess) {
         double fill = 0, span = 0;
         int nw = 0;
         for (int g = 0; g < 64; ++g)
-            for (int w = 0; w < 4; ++w) {
-                const unsigned long long s0 = t0[(g * 4 + w) * 2], s1 = t0[(g * 4 + w) * 2 + 1];
-                const unsigned long long f = tl[(((size_t)g * 4 + w) * 16) * 4];
+            for (int w = 0; w < 8; ++w) {
+                const unsigned long long s0 = t0[(g * 8 + w) * 2], s1 = t0[(g * 8 + w) * 2 + 1];
+                const unsigned long long f = tl[(((size_t)g * 8 + w) * 16) * 4];
                 if (s0 == 0 || s1 < s0 || f < s0) continue;
                 fill += (double)(f - s0);
                 span += (double)(s1 - s0);
@@ -1014,13 +1116,13 @@ static size_t lite_tab_bytes(int pro, int cin, int batch) {
 }
 constexpr int LITE_MAX_TAB_BATCH = LITE_MAX_BATCH;
 
-template <int MODE, int CIN, int NC, int CKC, int PRO, int X6>
+template <int MODE, int CIN, int NC, int CKC, int PRO, int X6, int KSP>
 static int lite_slots() {
     static int slots = 0;
     if (slots == 0) {
-        using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
+        using C = lite::Cfg<MODE, CIN, NC, CKC, X6, KSP>;
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6>, 256,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6, KSP>, C::NT,
                                                          C::LDS_BYTES + lite_tab_bytes(PRO, CIN, 1)) != hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
@@ -1030,12 +1132,37 @@ static int lite_slots() {
     return slots;
 }
 
-template <int MODE, int CIN, int NC, int CKC, int PRO, int X6>
+template <int MODE, int CIN, int NC, int CKC, int PRO, int X6, int KSP>
 static void lite_launch_pro(const ConvArgs& a, int n_tiles, hipStream_t st) {
-    using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
-    const int grid = std::min(n_tiles, lite_slots<MODE, CIN, NC, CKC, PRO, X6>());
-    hipLaunchKernelGGL((conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6>), dim3(grid), dim3(256),
+    using C = lite::Cfg<MODE, CIN, NC, CKC, X6, KSP>;
+    const int grid = std::min(n_tiles, lite_slots<MODE, CIN, NC, CKC, PRO, X6, KSP>());
+    hipLaunchKernelGGL((conv_lite_kernel<MODE, CIN, NC, CKC, PRO, X6, KSP>), dim3(grid), dim3(C::NT),
                        C::LDS_BYTES + lite_tab_bytes(PRO, CIN, a.batch), st, a, n_tiles);
+}
+
+// the K-split form (x6 multi-chunk transposed convs) exists, and its LDS with the prologue table of `batch` images fits
+template <int MODE, int CIN, int NC, int CKC, int X6>
+static constexpr bool lite_ksplit_ok() {
+    return X6 && MODE == 1 && CIN / CKC > 1 && CIN / CKC % 2 == 0 && CKC % (2 * (NC == 32 ? 16 : 32)) == 0;
+}
+static bool lite_ksplit_env() {   // RST_LITE_KSPLIT=0: the four-wave form everywhere (A/B measurements)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("RST_LITE_KSPLIT");
+        v = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
+template <int MODE, int CIN, int NC, int CKC, int X6, int KSP>
+static void lite_launch_sel(const ConvArgs& a, int n_tiles, int pro, hipStream_t st) {
+    switch (pro) {
+        case PRO_NONE: lite_launch_pro<MODE, CIN, NC, CKC, PRO_NONE, X6, KSP>(a, n_tiles, st); break;
+        case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6, KSP>(a, n_tiles, st); break;
+        case PRO_AFF_RES: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES, X6, KSP>(a, n_tiles, st); break;
+        case PRO_AFF_RELU | LITE_BLEND: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6, KSP>(a, n_tiles, st); break;
+        case PRO_AFF_RES | LITE_BLEND: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6, KSP>(a, n_tiles, st); break;
+    }
 }
 
 template <int MODE, int CIN, int NC, int CKC, int X6>
@@ -1052,44 +1179,53 @@ static hipError_t lite_launch_cfg(const ConvArgs& a, hipStream_t st) {
                     a.pro_stat.batch != a.batch || a.pro_stat.style == nullptr || a.pro_mode == PRO_NONE))
         return hipErrorInvalidValue;
     const int n_tiles = a.batch * a.tiles_y * a.tiles_x;
+    int pro = a.pro_mode;
     if (a.pro_w != nullptr) {   // two styles
         if (src_acc ? a.pro_stat.style1_offset < 0 : (a.pro_ab1 == nullptr || a.pro_ab == nullptr))
             return hipErrorInvalidValue;
-        switch (a.pro_mode) {
-            case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6>(a, n_tiles, st); break;
-            case PRO_AFF_RES: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6>(a, n_tiles, st); break;
-            default: return hipErrorInvalidValue;
+        if (pro != PRO_AFF_RELU && pro != PRO_AFF_RES) return hipErrorInvalidValue;
+        pro |= LITE_BLEND;
+    } else if (pro != PRO_NONE && pro != PRO_AFF_RELU && pro != PRO_AFF_RES) {
+        return hipErrorInvalidValue;
+    }
+    if constexpr (lite_ksplit_ok<MODE, CIN, NC, CKC, X6>()) {
+        using K = lite::Cfg<MODE, CIN, NC, CKC, X6, 2>;
+        if (lite_ksplit_env() && K::LDS_BYTES + lite_tab_bytes(pro, CIN, a.batch) <= 160 * 1024) {
+            lite_launch_sel<MODE, CIN, NC, CKC, X6, 2>(a, n_tiles, pro, st);
+            return hipGetLastError();
         }
-        return hipGetLastError();
     }
-    switch (a.pro_mode) {
-        case PRO_NONE: lite_launch_pro<MODE, CIN, NC, CKC, PRO_NONE, X6>(a, n_tiles, st); break;
-        case PRO_AFF_RELU: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>(a, n_tiles, st); break;
-        case PRO_AFF_RES: lite_launch_pro<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>(a, n_tiles, st); break;
-        default: return hipErrorInvalidValue;
-    }
+    lite_launch_sel<MODE, CIN, NC, CKC, X6, 1>(a, n_tiles, pro, st);
     return hipGetLastError();
 }
 
-template <int MODE, int CIN, int NC, int CKC, int X6>
-static hipError_t lite_prepare_cfg() {
-    using C = lite::Cfg<MODE, CIN, NC, CKC, X6>;
-    for (const void* k : {(const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_NONE, X6>,
-                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>,
-                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>,
-                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6>,
-                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6>}) {
+template <int MODE, int CIN, int NC, int CKC, int X6, int KSP>
+static hipError_t lite_prepare_ksp() {
+    using C = lite::Cfg<MODE, CIN, NC, CKC, X6, KSP>;
+    for (const void* k : {(const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_NONE, X6, KSP>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6, KSP>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES, X6, KSP>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6, KSP>,
+                          (const void*)conv_lite_kernel<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6, KSP>}) {
         const size_t bytes = std::min<size_t>(C::LDS_BYTES + lite_tab_bytes(PRO_AFF_RELU | LITE_BLEND, CIN, LITE_MAX_TAB_BATCH),
                                               160 * 1024);
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return e;
     }
     // occupancy queries outside any graph capture
-    lite_slots<MODE, CIN, NC, CKC, PRO_NONE, X6>();
-    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6>();
-    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES, X6>();
-    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6>();
-    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_NONE, X6, KSP>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU, X6, KSP>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES, X6, KSP>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RELU | LITE_BLEND, X6, KSP>();
+    lite_slots<MODE, CIN, NC, CKC, PRO_AFF_RES | LITE_BLEND, X6, KSP>();
+    return hipSuccess;
+}
+
+template <int MODE, int CIN, int NC, int CKC, int X6>
+static hipError_t lite_prepare_cfg() {
+    const hipError_t e = lite_prepare_ksp<MODE, CIN, NC, CKC, X6, 1>();
+    if (e != hipSuccess) return e;
+    if constexpr (lite_ksplit_ok<MODE, CIN, NC, CKC, X6>()) return lite_prepare_ksp<MODE, CIN, NC, CKC, X6, 2>();
     return hipSuccess;
 }
 
