@@ -262,7 +262,18 @@ static int train_wt(const rst_trainer* t, size_t elems, int mask = 1) {
 
 // ---- forward (training mode) ------------------------------------------------------------------
 int forward(rst_trainer* t, const float* content, const float* style, int B, float* prediction, hipStream_t st) {
+    // The forward waits for the loss targets before its layer join_at (default 0: the targets never run beside the
+    // transfer network's forward; they still run beside the style predictor's forward, train_step). With the plain-bf16
+    // VGG16 targets running beside it, the forward's prediction was not repeatable (tools/pred_race_check.py: ~all
+    // pixels, up to 7e-2, from call to call, profiles/r06/r06am): joining before any of layers 0-13 made it bitwise
+    // repeatable, overlapping the targets with expand_0 .. expand_last did not. Root cause not identified (no shared
+    // buffer between the two); RST_TARGETS_JOIN_AT=k moves the join (-1: none) for diagnosis.
+    static const int join_at = [] {
+        const char* v = getenv("RST_TARGETS_JOIN_AT");
+        return v != nullptr ? atoi(v) : 0;
+    }();
     for (size_t li = 0; li < t->L.size(); ++li) {
+        if ((int)li == join_at && t->targets_pending) RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_join, 0));
         TLayer& T = t->L[li];
         LayerExec& e = T.e;
         const TLayer* Pv = li ? &t->L[li - 1] : nullptr;

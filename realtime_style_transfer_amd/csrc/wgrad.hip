@@ -370,6 +370,191 @@ __global__ __launch_bounds__(256, 2) void wgrad_x6_kernel(WgradArgs a) {
             }
 }
 
+// ---- residual convs, tap-row tiles (wgrad_x6r): one kernel row ky per workgroup ----------------------------
+// wgrad_x6_kernel's 128-row tiles are one tap each, so every tile re-reads the 32 stage pixels of both operands:
+// 9 x (X + dZ) per launch, 1.06 GB at B = 4 (120 x 240 x 128), which bounds it (~4 TB/s L2/MALL -> CU).
+// Here a workgroup owns the three taps (ky, 0..2) of one kernel row (384 rows = kx x 128 ci) x all 128 columns:
+// per stage of 32 pixels it loads the 34-pixel window of X row-shifted by ky - 1 once (17 KB contiguous) and the
+// 32 dZ pixels once, and forms the three column-shifted S images in LDS (masked where x + kx - 1 or y + ky - 1
+// leaves the image: SAME zero padding). 3 x (X + dZ) per launch. 8 waves (two per SIMD), wave (wr, wc) owns rows
+// 96 wr .. +95 (3 M tiles) x columns 64 wc .. +63 (2 N tiles): 72 MFMAs of 32x32x16 bf16 per stage, the same
+// six split terms as wgrad_x6_kernel. Stage k+1's loads are issued before stage k's MFMAs (register prefetch) and
+// split into bf16 pieces right after them; the masked / shifted pieces go to LDS behind the stage's barrier.
+namespace wx6r {
+constexpr int TAPS = 3, CI = 128, CO = 128, TR = TAPS * CI, KP = 32;
+constexpr int RSB = 80;                       // bytes per LDS row (32 bf16 + 16 B pad: conflict-free b128 reads)
+constexpr int SPLANE = TR * RSB, UPLANE = CO * RSB;
+constexpr size_t LDS_BYTES = (size_t)3 * SPLANE + 3 * UPLANE;   // 122880
+typedef short short8 __attribute__((ext_vector_type(8)));
+}  // namespace wx6r
+
+__global__ __launch_bounds__(512, 1) void wgrad_x6r_kernel(WgradArgs a) {
+    using namespace wx6r;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_x6r[];
+    unsigned char* const ls = lds_x6r;                   // [piece][384 rows (kx, ci)][80 B]
+    unsigned char* const lu = lds_x6r + 3 * SPLANE;      // [piece][128 rows co][80 B]
+    // blockIdx -> (split, ky): the three kernel rows of one pixel split on one XCD (xcd_tile_order: contiguous runs)
+    const int t3 = xcd_tile_order(blockIdx.x, gridDim.x);
+    const int ky = t3 % TAPS, split = t3 / TAPS;
+    const int H = a.Qh, W = a.Qw;
+    const long qhw = (long)H * W;
+    const long total = (long)a.batch * qhw;
+    const long q_begin = (long)split * a.span;
+    const long q_end = min(total, q_begin + a.span);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int li = lane & 31, lh = lane >> 5;
+    const int dy = ky - a.pad_t;
+
+    // staging: every thread builds both operands for (channel quad cq, pixel pair pp), pp fastest (a wave's b32 LDS
+    // writes of one channel cover 4 rows x 64 contiguous bytes: 64 distinct banks). S: the window pixels 2 pp .. 2 pp + 3
+    // (= stage pixels 2 pp - 1 .. 2 pp + 2) are split once into two bf16 pair words per channel and piece; tap kx of
+    // LDS pixels (2 pp, 2 pp + 1) is window pixels (kx, kx + 1): pair word A (kx 0), B (kx 2) or the v_perm of A's high
+    // and B's low half (kx 1), masked per pixel. U: stage pixels 2 pp, 2 pp + 1.
+    const int pp = tid & 15, cq = tid >> 4;
+    // the stage's first pixel of this thread's pair as (row, column), advanced by KP per stage
+    int py, px;
+    {
+        const long q0 = q_begin + 2 * pp;
+        const int rem = (int)(q0 % qhw);
+        py = rem / W;
+        px = rem - py * W;
+    }
+    auto advance = [&]() __attribute__((always_inline)) {
+        px += KP;
+        while (px >= W) {
+            px -= W;
+            if (++py == H) py = 0;
+        }
+    };
+    f32x4 sreg[4], ureg[2];
+    auto load_stage = [&](long q0) __attribute__((always_inline)) {
+        const long qt = q0 + 2 * pp;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // window pixel j <-> X linear index qt - 1 + j + dy W (clamped; masked later)
+            long xi = qt - 1 + j + (long)dy * W;
+            xi = xi < 0 ? 0 : (xi >= total ? total - 1 : xi);
+            sreg[j] = *reinterpret_cast<const f32x4*>(a.X + (size_t)xi * CI + 4 * cq);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const long q = qt + j;
+            ureg[j] = *reinterpret_cast<const f32x4*>(a.D + (size_t)(q < q_end ? q : q_begin) * CO + 4 * cq);
+        }
+    };
+    unsigned sw[4][3][2], uw[4][3];   // [channel][piece][pair A / B], [channel][piece]
+    auto split_stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float x0 = sreg[0][c], y0 = sreg[1][c], x1 = sreg[2][c], y1 = sreg[3][c], xu = ureg[0][c], yu = ureg[1][c];
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+                sw[c][pc][0] = bf16_piece(x0, y0);
+                sw[c][pc][1] = bf16_piece(x1, y1);
+                uw[c][pc] = bf16_piece(xu, yu);
+            }
+        }
+    };
+    auto write_stage = [&](long q0) __attribute__((always_inline)) {
+        // masks of the pair's two pixels (low / high bf16 half) per tap; U: inside the split
+        const long qt = q0 + 2 * pp;
+        int y1 = py, x1 = px + 1;
+        if (x1 == W) {
+            x1 = 0;
+            if (++y1 == H) y1 = 0;
+        }
+        const bool in0 = qt < q_end && py + dy >= 0 && py + dy < H, in1 = qt + 1 < q_end && y1 + dy >= 0 && y1 + dy < H;
+        unsigned ms[TAPS];
+#pragma unroll
+        for (int kx = 0; kx < TAPS; ++kx) {
+            const int d = kx - a.pad_l;
+            ms[kx] = (in0 && px + d >= 0 && px + d < W ? 0x0000FFFFu : 0u) | (in1 && x1 + d >= 0 && x1 + d < W ? 0xFFFF0000u : 0u);
+        }
+        const unsigned mu = (qt < q_end ? 0x0000FFFFu : 0u) | (qt + 1 < q_end ? 0xFFFF0000u : 0u);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+                const unsigned A = sw[c][pc][0], Bw = sw[c][pc][1];
+                unsigned char* dst = ls + pc * SPLANE + (4 * cq + c) * RSB + 4 * pp;
+                *reinterpret_cast<unsigned*>(dst) = A & ms[0];
+                *reinterpret_cast<unsigned*>(dst + CI * RSB) = __builtin_amdgcn_perm(Bw, A, 0x05040302u) & ms[1];
+                *reinterpret_cast<unsigned*>(dst + 2 * CI * RSB) = Bw & ms[2];
+                *reinterpret_cast<unsigned*>(lu + pc * UPLANE + (4 * cq + c) * RSB + 4 * pp) = uw[c][pc] & mu;
+            }
+    };
+
+    floatx16 acc[3][2];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
+    auto mfma_stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int ks = 0; ks < KP / 16; ++ks) {
+            short8 B[2][3];
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc)
+                    B[n][pc] = *reinterpret_cast<const short8*>(lu + pc * UPLANE + (wc * 64 + n * 32 + li) * RSB +
+                                                                (16 * ks + 8 * lh) * 2);
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                short8 A[3];
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc)
+                    A[pc] = *reinterpret_cast<const short8*>(ls + pc * SPLANE + (wr * 96 + m * 32 + li) * RSB +
+                                                             (16 * ks + 8 * lh) * 2);
+#pragma unroll
+                for (int n = 0; n < 2; ++n) {
+                    floatx16& C = acc[m][n];
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[n][0], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[n][1], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[n][0], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[n][2], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[n][1], C, 0, 0, 0);
+                    C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[n][0], C, 0, 0, 0);
+                }
+            }
+        }
+    };
+    const int nst = q_begin < q_end ? (int)((q_end - q_begin + KP - 1) / KP) : 0;
+    if (nst > 0) {
+        load_stage(q_begin);
+        split_stage();
+        write_stage(q_begin);
+        advance();
+        __syncthreads();
+    }
+    for (int k = 0; k < nst; ++k) {
+        const long qn = q_begin + (long)(k + 1) * KP;
+        if (k + 1 < nst) load_stage(qn);
+        mfma_stage();
+        if (k + 1 < nst) split_stage();   // VALU beside the other wave's MFMAs; LDS untouched until the barrier
+        __syncthreads();
+        if (k + 1 < nst) {
+            write_stage(qn);
+            advance();
+            __syncthreads();
+        }
+    }
+    // slab rows [ky * 384, +384) = taps (ky, 0..2) x ci, all 128 columns
+    float* out = a.slab + (size_t)split * (9 * CI) * CO;
+    const int r0 = ky * TR;
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = (i & 3) + 8 * (i >> 2) + 4 * lh;
+                out[(size_t)(r0 + wr * 96 + m * 32 + row) * CO + wc * 64 + n * 32 + li] = acc[m][n][i];
+            }
+}
+
 // ---- contract_start (9x9 s1 SAME, cin <= 17 -> 32): LDS-patch weight gradient --------------------------
 // The generic kernel above reads its S operand (the shifted input, R = 81 taps x 17 channels = 1377
 // rows) straight from global memory with 4-byte loads (17 channels: no 16-B vectors): every input
@@ -831,7 +1016,28 @@ static int wgrad_cu_count() {
     return n_cu;
 }
 
+// the tap-row kernel (wgrad_x6r_kernel): the residual convs of the split-bf16 trainer (3x3 s1 SAME, 128 -> 128);
+// RST_WGRAD_X6R=0: wgrad_x6_kernel
+static bool wgrad_x6r_applies(const WgradArgs& a) {
+    static const bool ok = [] {
+        const char* v = getenv("RST_WGRAD_X6R");
+        if (v != nullptr && v[0] == '0') return false;
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad_x6r_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)wx6r::LDS_BYTES) == hipSuccess;
+    }();
+    return ok && a.x6 && !a.transposed && a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad_t == 1 && a.pad_l == 1 &&
+           a.C1 == wx6r::CI && a.C2 == wx6r::CO && a.XH == a.Qh && a.XW == a.Qw;
+}
+
 int wgrad_choose_splits(const WgradArgs& a) {
+    if (wgrad_x6r_applies(a)) {
+        // one workgroup per CU: 3 kernel rows x splits, each split >= 8 stages
+        const long total = (long)a.batch * a.Qh * a.Qw;
+        long ns = wgrad_cu_count() / wx6r::TAPS;
+        const long max_ns = (total + 8 * wx6r::KP - 1) / (8 * wx6r::KP);
+        if (ns > max_ns) ns = max_ns;
+        return (int)(ns < 1 ? 1 : ns);
+    }
     if (wgrad9_applies(a) && a.x6 && wgrad9_x6_enabled()) {
         // one workgroup per CU (104 KB of LDS, launch_bounds(256, 1)): one round of persistent workgroups, never more
         // than the pixel tiles (each writes a slab the reduce then reads)
@@ -860,6 +1066,7 @@ int wgrad_choose_splits(const WgradArgs& a) {
 }
 
 size_t wgrad_slab_bytes(const WgradArgs& a) {
+    if (wgrad_x6r_applies(a)) return (size_t)a.nsplit * 9 * wx6r::CI * wx6r::CO * sizeof(float);
     if (wgrad9_applies(a)) return (size_t)a.nsplit * w9::NCOLP * 32 * sizeof(float);
     if (wgradT9_applies(a)) return (size_t)a.nsplit * wt9::RP * wt9::CP * sizeof(float);
     int R, Cu, Cs;
@@ -891,6 +1098,19 @@ hipError_t wgrad_launch(WgradArgs a, hipStream_t st) {
         if (e != hipSuccess) return e;
         const size_t n4 = (size_t)R * Cu / 4;
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, a, wt9::RP, wt9::CP);
+        return hipGetLastError();
+    }
+    if (wgrad_x6r_applies(a)) {
+        if (a.nsplit < 1) return hipErrorInvalidValue;
+        const long total = (long)a.batch * a.Qh * a.Qw;
+        long span = (total + a.nsplit - 1) / a.nsplit;
+        a.span = ((span + wx6r::KP - 1) / wx6r::KP) * wx6r::KP;
+        hipLaunchKernelGGL(wgrad_x6r_kernel, dim3((unsigned)(wx6r::TAPS * a.nsplit)), dim3(512), wx6r::LDS_BYTES, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const size_t n4 = (size_t)R * Cu / 4;
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, a, 9 * wx6r::CI,
+                           wx6r::CO);
         return hipGetLastError();
     }
     if (Cu % 4 != 0) return hipErrorInvalidValue;

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #include "kernels.h"
@@ -39,9 +40,16 @@ int main(int argc, char** argv) {
     a.Qh = H; a.Qw = W;
     a.kh = a.kw = 3; a.stride = 1; a.pad_t = a.pad_l = 1;
     a.transposed = 0;
-    a.nsplit = wgrad_choose_splits(a);
+    // each variant's own split count (x6 = 1: the tap-row kernel unless RST_WGRAD_X6R=0); one slab for the larger
+    size_t slab_bytes = 0;
+    for (int v = 0; v < 2; ++v) {
+        WgradArgs x = a;
+        x.x6 = v;
+        x.nsplit = wgrad_choose_splits(x);
+        slab_bytes = std::max(slab_bytes, wgrad_slab_bytes(x));
+    }
     float* slab;
-    CK(hipMalloc(&slab, wgrad_slab_bytes(a)));
+    CK(hipMalloc(&slab, slab_bytes));
     a.slab = slab;
     const size_t nw = (size_t)9 * C * C;
     float *dw0, *dw1;
@@ -54,6 +62,7 @@ int main(int argc, char** argv) {
     for (int v = 0; v < 2; ++v) {
         WgradArgs x = a;
         x.x6 = v;
+        x.nsplit = wgrad_choose_splits(x);
         x.dW = v ? dw1 : dw0;
         for (int i = 0; i < 3; ++i) CK(wgrad_launch(x, 0));
         CK(hipEventRecord(e0, 0));
@@ -64,7 +73,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = 1e3 * ms / iters, flops = 2.0 * B * H * W * 9.0 * C * C;
         printf("%s B=%d nsplit=%d: %.1f us (kernel + reduce), %.1f TFLOP/s algorithmic\n", v ? "wgrad_x6  " : "wgrad_mfma",
-               B, a.nsplit, us, flops / us * 1e-6);
+               B, x.nsplit, us, flops / us * 1e-6);
     }
     std::vector<float> h0(nw), h1(nw);
     CK(hipMemcpy(h0.data(), dw0, nw * 4, hipMemcpyDeviceToHost));
