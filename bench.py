@@ -381,7 +381,7 @@ def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"
          'style': torch.from_numpy(rng.random((TB, 1) + sins, dtype=np.float32)).to(dev)}
     y = {'content': torch.from_numpy(rng.random((TB,) + outs, dtype=np.float32)).to(dev),
          'style': torch.from_numpy(rng.random((TB, 1) + outs, dtype=np.float32)).to(dev)}
-    for _ in range(2):
+    for _ in range(args.train_warmup):   # untimed: allocations, first-use kernel attributes, clocks settle
         tr.train_step(x, y)
     torch.cuda.synchronize()
     el = ctx.timed(lambda: tr.train_step(x, y), args.train_steps)
@@ -396,7 +396,7 @@ def bench_training(args, ctx, cfg, ins, outs, plan, weights, P, precision="fp32"
     return {"workload": f"{SPEC} train_network.py step (BASELINE config 4): MobileNetV3Small style predictor + "
                         f"transfer net, training-mode forward, VGG16/Gram loss (no depth term), backward of both, " +
                         ("one all-reduce per step (SUM, one bucket: gradients + BN moving statistics, the latter then / world), "
-                         if ctx.world > 1 else "") + "RMSprop on both", "batch_per_gpu": TB, "steps": args.train_steps,
+                         if ctx.world > 1 else "") + "RMSprop on both", "batch_per_gpu": TB, "steps": args.train_steps, "warmup": args.train_warmup,
             "ms_per_step": round(ms, 3),
             "frames_per_s": round(ctx.world * TB * args.train_steps / el, 3),
             "dtype": {"fp32": "fp32 (f32 MFMA)",
@@ -568,7 +568,8 @@ def parse_args(argv=None):
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06", "traffic_r06.json"),
                     help="per-launch HBM bytes of the dominant kernel (tools/pmc_traffic.py on this build's FETCH/WRITE passes)")
     ap.add_argument("--train-batch", type=int, default=4, help="config 4 training step batch per GPU; 0 to skip")
-    ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--train-steps", type=int, default=10)
+    ap.add_argument("--train-warmup", type=int, default=5)
     ap.add_argument("--train-modes", default="bf16,bf16x3,bf16x6,fp32",
                     help="VGG16 precisions of the training line, comma-separated; the first is the headline")
     ap.add_argument("--precision", default=DEFAULT_PRECISION,
