@@ -533,7 +533,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_x6r_kernel(WgradArgs a) {
         const long qn = q_begin + (long)(k + 1) * KP;
         if (k + 1 < nst) load_stage(qn);
         mfma_stage();
-        if (k + 1 < nst) split_stage();   // VALU beside the other wave's MFMAs; LDS untouched until the barrier
+        split_stage();   // (after the last stage: on stale registers, never written)
+        // one MFMA, then three VALU, 72 times: the split's VALU issues between this wave's MFMAs (197 -> 192 us at
+        // B = 4, two VALU per MFMA the same, profiles/r06/r06ap)
+#pragma unroll
+        for (int i = 0; i < 72; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        }
         __syncthreads();
         if (k + 1 < nst) {
             write_stage(qn);
