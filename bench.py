@@ -790,6 +790,20 @@ def run(args, ctx):
                             "tflops_direct_equiv": round(flops[i] / (ms_i * 1e-3) / 1e12, 2) if ms_i > 0 else None,
                             "exec_frac": round(ex / (ms_i * 1e-3) / 1e12 / peak, 4) if ms_i > 0 else None})
 
+    # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
+    # measured right after the headline, before the side legs' models, graphs and trainers exist (they held memory
+    # and host state through a later training leg: 22.0 ms there against 20.4 ms alone on one box, profiles/r06/r06ar: 22.35 -> 21.65 ms, 2 alternating pairs)
+    train = None
+    if args.train_batch > 0:
+        # BASELINE config 4 trains in bf16: the headline training figure runs the VGG16 3x3 convs with bf16
+        # operands and fp32 accumulation; the split-bf16 (bf16x3, bf16x6) and fp32 runs are reported beside it
+        modes = [m for m in args.train_modes.split(",") if m]
+        train = bench_training(args, ctx, cfg, ins, outs, plan, weights, P, modes[0])
+        keep = ("ms_per_step", "frames_per_s", "algorithmic_tflops_per_gpu", "dtype", "roofline")
+        train["other_precisions"] = {p: {k: v for k, v in bench_training(args, ctx, cfg, ins, outs, plan, weights, P,
+                                                                          p).items() if k in keep}
+                                     for p in modes[1:]}
+
     # ---------------- config 3: batch-8 stream, hipGraph steady state (50 warm-up + 500 frames) ----------
     stream = None
     if args.stream_batch > 0:
@@ -822,18 +836,6 @@ def run(args, ctx):
     # ---------------- style predictor / inference model -----------------------
     predictor = None if args.no_predictor else bench_predictor(args, ctx, cfg, model, inputs, P)
     ingest = None if args.no_ingest else bench_ingest(args, ctx, cfg)
-
-    # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
-    train = None
-    if args.train_batch > 0:
-        # BASELINE config 4 trains in bf16: the headline training figure runs the VGG16 3x3 convs with bf16
-        # operands and fp32 accumulation; the split-bf16 (bf16x3, bf16x6) and fp32 runs are reported beside it
-        modes = [m for m in args.train_modes.split(",") if m]
-        train = bench_training(args, ctx, cfg, ins, outs, plan, weights, P, modes[0])
-        keep = ("ms_per_step", "frames_per_s", "algorithmic_tflops_per_gpu", "dtype", "roofline")
-        train["other_precisions"] = {p: {k: v for k, v in bench_training(args, ctx, cfg, ins, outs, plan, weights, P,
-                                                                          p).items() if k in keep}
-                                     for p in modes[1:]}
 
     # ---------------- parity + CPU baseline (rank 0 at N=1 only, bounded sample) ----------------
     max_abs = None

@@ -416,6 +416,36 @@ def test_winograd_residual_convs_match_oracle(precision):
             assert np.abs(g - r).max() / max(1.0, np.abs(r).max()) < 1e-4
 
 
+def test_expand0_ksplit_and_four_wave_forms_match_oracle():
+    """expand_0 (the 3x3 s2 transposed 128 -> 32 conv, conv_lite.hip) runs its K-split form (8 waves, LDS-DMA weights)
+    while its LDS with the prologue table of the batch fits, and the four-wave form above that (here B = 12). Both
+    against float64: the same two images repeated to B = 2 and B = 12 (instance norm is per image)."""
+    _need_gpu()
+    from oracle import numpy_ref as R
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    ins, outs, br, bf = (32, 64, 17), (32, 64, 3), 8, 128
+    plan = network_plan(ins, outs, br, bf)
+    w = init_weights(plan, seed=2)
+    sp = synthetic_style_params(2, 1, plan.num_style_params, plan, seed=1)
+    x = np.random.default_rng(0).random((2,) + ins).astype(np.float32)
+    ref, inter = R.transfer_forward(x, sp, w, ins, outs, br, bf, return_intermediates=True)
+    names = [l.name for l in plan.layers]
+    e0 = names.index('expand_0')
+    r_e0 = [v for k, v in inter.items() if k.endswith('_expand')][0]   # the first expand block's CIN + ReLU output
+    m, _ = create_style_transfer_model(ins, outs, br, bf, 1, weights=w, max_batch=12, precision="winograd_bf16x6")
+    for B in (2, 12):
+        k = B // 2
+        inp = {'content': torch.from_numpy(np.tile(x, (k, 1, 1, 1))).cuda(),
+               'style_params': torch.from_numpy(np.tile(sp, (k, 1, 1))).cuda()}
+        y = m(inp).cpu().numpy()
+        g = m.layer_output(e0, B).cpu().numpy()
+        for j in range(k):
+            assert np.abs(y[2 * j:2 * j + 2] - ref).max() < OUT_TOL, (B, j)
+            gj = g[2 * j:2 * j + 2]
+            assert gj.shape == r_e0.shape and np.abs(gj - r_e0).max() / max(1.0, np.abs(r_e0).max()) < 1e-4, (B, j)
+
+
 @pytest.mark.parametrize("cin", [3, 12, 17])
 def test_start_conv_f3_channel_chunks_match_oracle(cin):
     """wino9f3 (the inference start conv on F(3x3, 3x3) tiles) with 1, 2 and 3 input-channel chunks (cin <= 8: chunk A
