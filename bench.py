@@ -678,6 +678,21 @@ def run(args, ctx):
             graph.replay()
         torch.cuda.synchronize()
         elapsed = ctx.timed(graph.replay, args.steps)
+    # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
+    # measured right after the headline's timed region, before any side leg: the PCIe leg's copy stream alone cost the
+    # step 0.75 ms when it ran first (20.5 vs 19.7 ms, profiles/r06/r06as; GPU_MAX_HW_QUEUES = 4 hardware queues carry
+    # every stream of the process), and the later side legs another 0.7 ms (profiles/r06/r06ar)
+    train = None
+    if args.train_batch > 0:
+        # BASELINE config 4 trains in bf16: the headline training figure runs the VGG16 3x3 convs with bf16
+        # operands and fp32 accumulation; the split-bf16 (bf16x3, bf16x6) and fp32 runs are reported beside it
+        modes = [m for m in args.train_modes.split(",") if m]
+        train = bench_training(args, ctx, cfg, ins, outs, plan, weights, P, modes[0])
+        keep = ("ms_per_step", "frames_per_s", "algorithmic_tflops_per_gpu", "dtype", "roofline")
+        train["other_precisions"] = {p: {k: v for k, v in bench_training(args, ctx, cfg, ins, outs, plan, weights, P,
+                                                                          p).items() if k in keep}
+                                     for p in modes[1:]}
+
     # ---------------- PCIe-inclusive rate (reported beside the headline, never as `value`) ------
     # The C-ABI hands over device pointers; a host-resident frame loop adds H2D of the 31 MB
     # G-buffer and D2H of the 5.5 MB output per frame. "serial": upload -> graph -> download on one
@@ -789,20 +804,6 @@ def run(args, ctx):
                                          np.isfinite(graph_ms[i]) else None),
                             "tflops_direct_equiv": round(flops[i] / (ms_i * 1e-3) / 1e12, 2) if ms_i > 0 else None,
                             "exec_frac": round(ex / (ms_i * 1e-3) / 1e12 / peak, 4) if ms_i > 0 else None})
-
-    # ---------------- config 4: training step (fwd + VGG loss + bwd + [RCCL all-reduce] + RMSprop) --
-    # measured right after the headline, before the side legs' models, graphs and trainers exist (they held memory
-    # and host state through a later training leg: 22.0 ms there against 20.4 ms alone on one box, profiles/r06/r06ar: 22.35 -> 21.65 ms, 2 alternating pairs)
-    train = None
-    if args.train_batch > 0:
-        # BASELINE config 4 trains in bf16: the headline training figure runs the VGG16 3x3 convs with bf16
-        # operands and fp32 accumulation; the split-bf16 (bf16x3, bf16x6) and fp32 runs are reported beside it
-        modes = [m for m in args.train_modes.split(",") if m]
-        train = bench_training(args, ctx, cfg, ins, outs, plan, weights, P, modes[0])
-        keep = ("ms_per_step", "frames_per_s", "algorithmic_tflops_per_gpu", "dtype", "roofline")
-        train["other_precisions"] = {p: {k: v for k, v in bench_training(args, ctx, cfg, ins, outs, plan, weights, P,
-                                                                          p).items() if k in keep}
-                                     for p in modes[1:]}
 
     # ---------------- config 3: batch-8 stream, hipGraph steady state (50 warm-up + 500 frames) ----------
     stream = None
