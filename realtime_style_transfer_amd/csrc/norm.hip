@@ -172,15 +172,19 @@ __global__ __launch_bounds__(256) void fin_sigmoid3_kernel(CinSrc s, const float
                                                            float* __restrict__ y, int n4_img) {
     __shared__ float2 aff[3];
     const int b = blockIdx.y;
+    const float4* __restrict__ xi = reinterpret_cast<const float4*>(x) + (size_t)b * n4_img;
+    float4* __restrict__ yo = reinterpret_cast<float4*>(y) + (size_t)b * n4_img;
+    // the thread's first two float4 are loaded before the affine merge: their latency overlaps the accumulator loads'
+    // instead of following them (the merge's loads and these are independent)
+    const int i0 = blockIdx.x * 256 + threadIdx.x, i1 = i0 + gridDim.x * 256;
+    const float4 pre0 = xi[min(i0, n4_img - 1)], pre1 = xi[min(i1, n4_img - 1)];
     cin_affine_table<256>(s, b, 1, aff, nullptr, blockIdx.x == 0 && s.ab_out != nullptr ? s.ab_out + b * 3 : nullptr,
                           nullptr);
     __syncthreads();
     const float a0 = aff[0].x, b0 = aff[0].y, a1 = aff[1].x, b1 = aff[1].y, a2 = aff[2].x, b2 = aff[2].y;
-    const float4* __restrict__ xi = reinterpret_cast<const float4*>(x) + (size_t)b * n4_img;
-    float4* __restrict__ yo = reinterpret_cast<float4*>(y) + (size_t)b * n4_img;
     auto sig = [](float v) __attribute__((always_inline)) { return 1.f / (1.f + __expf(-v)); };
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n4_img; i += gridDim.x * 256) {
-        const float4 v = xi[i];
+    for (int i = i0; i < n4_img; i += gridDim.x * 256) {
+        const float4 v = i == i0 ? pre0 : (i == i1 ? pre1 : xi[i]);
         // element 4i + k has channel (4i + k) % 3: the float4 starts at channel (i % 3) ... (4i % 3 = i % 3)
         const int c0 = i % 3;
         const float aA = c0 == 0 ? a0 : (c0 == 1 ? a1 : a2), bA = c0 == 0 ? b0 : (c0 == 1 ? b1 : b2);
