@@ -1,5 +1,7 @@
 // common.h — host helpers shared by the C-ABI translation units of librst.
 #pragma once
+#include <hip/hip_runtime.h>
+
 #include <string>
 #include <vector>
 
@@ -23,6 +25,14 @@ std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int c
 std::vector<float> pack_conv_tiles_bf3(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t);
 // source index in Wg of every bf16 element of the one-plane pack_conv_tiles_bf3 image (-1: padding)
 std::vector<int> pack_conv_tiles_bf3_index(int taps, int cin, int ntot, const ConvTile& t);
+
+// Diagnostic guard bands (RST_ALLOC_PAD=<bytes>, default 0 = plain hipMalloc): the trainer's and the loss network's
+// buffers get a canary-filled band of that many bytes on both sides; guard_check reports every band a kernel wrote
+// (an out-of-bounds store) to stderr and returns their count. guard_free takes the pointer guard_malloc returned.
+size_t guard_pad();
+hipError_t guard_malloc(void** p, size_t bytes);
+void guard_free(void* p);
+int guard_check(const char* when);
 
 }  // namespace rst
 

@@ -85,19 +85,26 @@ int loss_targets(rst_loss_handle* h, const float* gt_content, const float* gt_st
     // plain-bf16 loss: the Gram matrices on bf16-rounded features as well (mixed_bfloat16 compute dtype)
     const bool gram_bf16 = h->shape.precision == RST_PRECISION_BF16;
     int r;
+    // diagnostic (race bisection): RST_TARGETS_PARTS bit 0 style VGG16, 1 its Grams, 2 content VGG16, 3 the content
+    // copy (default all); the losses are meaningless without all four
+    static const int parts = [] {
+        const char* v = getenv("RST_TARGETS_PARTS");
+        return v != nullptr ? atoi(v) : 15;
+    }();
     // style image: grams of the four style layers
-    if ((r = vgg_run(h, gt_style, B, STYLE_IDX[3], st)) != RST_OK) return r;
-    for (int k = 0; k < 4; ++k) {
+    if ((parts & 1) && (r = vgg_run(h, gt_style, B, STYLE_IDX[3], st)) != RST_OK) return r;
+    for (int k = 0; k < 4 && (parts & 2); ++k) {
         const VggConv& c = h->convs[STYLE_IDX[k]];
         RST_HIP_TRY(gram_launch(c.d_out, B, c.H * c.W, c.cout, h->d_gram_style[k], h->d_gram_ws, st, gram_bf16,
                                 h->act_bf16));
     }
     // ground-truth content: block5_conv3 features
-    if ((r = vgg_run(h, gt_content, B, CONTENT_IDX, st)) != RST_OK) return r;
+    if ((parts & 4) && (r = vgg_run(h, gt_content, B, CONTENT_IDX, st)) != RST_OK) return r;
     const VggConv& c5 = h->convs[CONTENT_IDX];
     const size_t f5 = (size_t)c5.H * c5.W * c5.cout;
-    RST_HIP_TRY(hipMemcpyAsync(h->d_content_feat, c5.d_out, (size_t)B * f5 * (h->act_bf16 ? 2 : 4),
-                               hipMemcpyDeviceToDevice, st));
+    if (parts & 8)
+        RST_HIP_TRY(hipMemcpyAsync(h->d_content_feat, c5.d_out, (size_t)B * f5 * (h->act_bf16 ? 2 : 4),
+                                   hipMemcpyDeviceToDevice, st));
     return RST_OK;
 }
 

@@ -46,11 +46,11 @@ struct rst_loss_handle {
                                           // (RST_VGG_ACT_F32=1 at creation: f32 storage, for A/B runs)
     std::vector<float> host_w;            // VGG16 weights as given (Keras order), for the backward packing
     ~rst_loss_handle() {
-        for (void* p : allocs) (void)hipFree(p);
+        for (void* p : allocs) rst::guard_free(p);
     }
     template <typename T>
     int alloc(T** p, size_t bytes, const void* src = nullptr) {
-        if (hipMalloc((void**)p, bytes) != hipSuccess) return rst::set_error(RST_ERR_ALLOC, "hipMalloc failed");
+        if (rst::guard_malloc((void**)p, bytes) != hipSuccess) return rst::set_error(RST_ERR_ALLOC, "hipMalloc failed");
         allocs.push_back((void*)*p);
         if (src && hipMemcpy(*p, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
             return rst::set_error(RST_ERR_HIP, "hipMemcpy failed");

@@ -106,6 +106,83 @@ std::vector<float> pack_tiles(const std::vector<float>& Wg, int taps, int cin, i
 
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 
+namespace {
+struct GuardRec {
+    char* base;
+    size_t bytes;
+};
+std::vector<GuardRec> g_guards;   // live guarded allocations (diagnostic runs only)
+const unsigned char GUARD_BYTE = 0xA5;
+}  // namespace
+
+size_t guard_pad() {
+    static const size_t pad = [] {
+        const char* v = getenv("RST_ALLOC_PAD");
+        return v != nullptr ? (size_t)(strtoull(v, nullptr, 0) + 255) / 256 * 256 : (size_t)0;
+    }();
+    return pad;
+}
+
+hipError_t guard_malloc(void** p, size_t bytes) {
+    const size_t pad = guard_pad();
+    if (pad == 0) return hipMalloc(p, bytes);
+    char* base = nullptr;
+    hipError_t e = hipMalloc((void**)&base, bytes + 2 * pad);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemset(base, GUARD_BYTE, pad)) != hipSuccess ||
+        (e = hipMemset(base + pad + bytes, GUARD_BYTE, pad)) != hipSuccess) {
+        (void)hipFree(base);
+        return e;
+    }
+    g_guards.push_back({base, bytes});
+    *p = base + pad;
+    return hipSuccess;
+}
+
+void guard_free(void* p) {
+    const size_t pad = guard_pad();
+    if (pad == 0) {
+        (void)hipFree(p);
+        return;
+    }
+    for (size_t i = 0; i < g_guards.size(); ++i)
+        if (g_guards[i].base + pad == p) {
+            (void)hipFree(g_guards[i].base);
+            g_guards.erase(g_guards.begin() + i);
+            return;
+        }
+    (void)hipFree(p);
+}
+
+int guard_check(const char* when) {
+    const size_t pad = guard_pad();
+    if (pad == 0) return 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    int bad = 0;
+    std::vector<unsigned char> h(pad);
+    for (size_t i = 0; i < g_guards.size(); ++i)
+        for (int side = 0; side < 2; ++side) {
+            const char* band = g_guards[i].base + (side ? pad + g_guards[i].bytes : 0);
+            if (hipMemcpy(h.data(), band, pad, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+            size_t first = pad, last = 0, n = 0;
+            for (size_t k = 0; k < pad; ++k)
+                if (h[k] != GUARD_BYTE) {
+                    first = std::min(first, k);
+                    last = k;
+                    ++n;
+                }
+            if (n == 0) continue;
+            ++bad;
+            fprintf(stderr, "RST_ALLOC_PAD %s: allocation %zu (%zu bytes at %p): %zu bytes written in the %s band, "
+                            "offsets %lld .. %lld from the buffer start\n",
+                    when, i, g_guards[i].bytes, (void*)(g_guards[i].base + pad), n, side ? "trailing" : "leading",
+                    side ? (long long)(g_guards[i].bytes + first) : -(long long)(pad - first),
+                    side ? (long long)(g_guards[i].bytes + last) : -(long long)(pad - last));
+            (void)hipMemset((void*)band, GUARD_BYTE, pad);   // re-armed: the next check reports new writes only
+        }
+    return bad;
+}
+
 std::vector<float> pack_conv_tiles(const std::vector<float>& Wg, int taps, int cin, int ntot, const ConvTile& t) {
     const int ck = t.ck, nt = t.nt, tps = t.tps, vec = t.vec;
     const int ksteps = ck / 2, sg_n = ksteps / vec;

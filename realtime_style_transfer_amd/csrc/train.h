@@ -72,5 +72,8 @@ struct GatherJobs {
 };
 hipError_t gather_batch_launch(const float* src, GatherJobs& jobs, hipStream_t st);
 hipError_t scatter_div_launch(const float* src, const int* index, float* dst, size_t n, float divisor, hipStream_t st);
+// Diagnostic (RST_LDS_POISON): fill the whole LDS of every CU with the bit pattern `bits`, so that the next kernel on
+// the stream finds that pattern wherever it reads LDS it did not write first
+hipError_t lds_poison_launch(unsigned bits, hipStream_t st);
 
 }  // namespace rst

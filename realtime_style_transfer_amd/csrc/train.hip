@@ -652,4 +652,33 @@ hipError_t gather_batch_launch(const float* src, GatherJobs& jobs, hipStream_t s
     return hipGetLastError();
 }
 
+
+namespace {
+constexpr int POISON_LDS_BYTES = 160 * 1024;
+__global__ __launch_bounds__(1024) void lds_poison_kernel(unsigned bits, unsigned* sink) {
+    extern __shared__ unsigned poison_lds[];
+    for (int i = threadIdx.x; i < POISON_LDS_BYTES / 4; i += 1024) poison_lds[i] = bits;
+    __syncthreads();
+    // a read the compiler cannot drop the stores for (sink is null: the condition never holds on a real pattern)
+    if (sink != nullptr && poison_lds[(threadIdx.x * 37) % (POISON_LDS_BYTES / 4)] == ~bits) sink[0] = 1u;
+}
+}  // namespace
+
+hipError_t lds_poison_launch(unsigned bits, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)lds_poison_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, POISON_LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    int dev = 0, cus = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    // one 160 KB workgroup fits a CU at a time: four rounds per CU cover every CU whatever the dispatch order
+    hipLaunchKernelGGL(lds_poison_kernel, dim3(4 * cus), dim3(1024), POISON_LDS_BYTES, st, bits, (unsigned*)nullptr);
+    return hipGetLastError();
+}
+
 }  // namespace rst

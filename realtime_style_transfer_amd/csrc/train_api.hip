@@ -187,11 +187,17 @@ struct rst_trainer {
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (ev_gstyle) (void)hipEventDestroy(ev_gstyle);
         if (loss) rst_loss_destroy(loss);
-        for (void* p : allocs) (void)hipFree(p);
+        for (void* p : allocs) rst::guard_free(p);
     }
     template <typename T>
     int alloc(T** p, size_t bytes, const void* src = nullptr) {
-        int st = rst::upload(p, src, bytes ? bytes : 4);
+        int st = RST_OK;
+        if (rst::guard_malloc((void**)p, bytes ? bytes : 4) != hipSuccess) {
+            *p = nullptr;
+            st = rst::set_error(RST_ERR_ALLOC, "hipMalloc failed");
+        } else if (src != nullptr && hipMemcpy(*p, src, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+            st = rst::set_error(RST_ERR_HIP, "hipMemcpy failed");
+        }
         if (*p) allocs.push_back((void*)*p);
         if (st == RST_OK && src == nullptr && hipMemset(*p, 0, bytes ? bytes : 4) != hipSuccess)
             return set_error(RST_ERR_HIP, "hipMemset failed");
@@ -272,8 +278,52 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
         const char* v = getenv("RST_TARGETS_JOIN_AT");
         return v != nullptr ? atoi(v) : 0;
     }();
-    for (size_t li = 0; li < t->L.size(); ++li) {
+    // diagnostic: RST_LDS_POISON=<bits> fills every CU's LDS with that pattern before each kernel of layer
+    // RST_LDS_POISON_LAYER (default -1: every layer; L.size(): the final sigmoid), so a read of LDS the kernel did not
+    // write shows in the prediction
+    static const long long poison_bits = [] {
+        const char* v = getenv("RST_LDS_POISON");
+        return v != nullptr ? (long long)strtoull(v, nullptr, 0) : -1LL;
+    }();
+    static const int poison_layer = [] {
+        const char* v = getenv("RST_LDS_POISON_LAYER");
+        return v != nullptr ? atoi(v) : -1;
+    }();
+    // diagnostic: RST_TARGETS_JOIN_KERNEL=k joins the loss targets before the forward's k-th kernel instead (counting
+    // every conv, materialisation, finalize and the final sigmoid in launch order)
+    static const int join_kernel = [] {
+        const char* v = getenv("RST_TARGETS_JOIN_KERNEL");
+        return v != nullptr ? atoi(v) : -1;
+    }();
+    // diagnostic: RST_FENCE_KERNEL=k puts a cross-stream dependency (an event recorded on an idle stream) before the
+    // forward's k-th kernel: a barrier packet with its cache fences, without waiting for the targets
+    static const int fence_kernel = [] {
+        const char* v = getenv("RST_FENCE_KERNEL");
+        return v != nullptr ? atoi(v) : -1;
+    }();
+    static hipStream_t fence_stream = nullptr;
+    static hipEvent_t fence_event = nullptr;
+    size_t li = 0;
+    int kernel_idx = 0;
+    auto poison = [&]() -> hipError_t {
+        if (kernel_idx == fence_kernel) {
+            hipError_t e = hipSuccess;
+            if (fence_stream == nullptr) e = hipStreamCreateWithFlags(&fence_stream, hipStreamNonBlocking);
+            if (e == hipSuccess && fence_event == nullptr) e = hipEventCreateWithFlags(&fence_event, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(fence_event, fence_stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(st, fence_event, 0);
+            if (e != hipSuccess) return e;
+        }
+        if (kernel_idx++ == join_kernel && t->targets_pending) {
+            const hipError_t e = hipStreamWaitEvent(st, t->ev_join, 0);
+            if (e != hipSuccess) return e;
+        }
+        if (poison_bits < 0 || (poison_layer >= 0 && (size_t)poison_layer != li)) return hipSuccess;
+        return lds_poison_launch((unsigned)poison_bits, st);
+    };
+    for (li = 0; li < t->L.size(); ++li) {
         if ((int)li == join_at && t->targets_pending) RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_join, 0));
+        RST_HIP_TRY(poison());
         TLayer& T = t->L[li];
         LayerExec& e = T.e;
         const TLayer* Pv = li ? &t->L[li - 1] : nullptr;
@@ -294,6 +344,7 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             a.cin = e.s.cin;
             a.tiles_y = e.tiles_y;
             a.tiles_x = e.tiles_x;
+            RST_HIP_TRY(poison());
             RST_HIP_TRY(small_conv_launch(a, st));
         } else if (e.kind == K_WINO9 || e.kind == K_WINO9X6) {
             Wino9Args a{};
@@ -369,9 +420,11 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
             f.momentum = 0.99f;
             f.eps = 1e-3f;
         }
+        RST_HIP_TRY(poison());
         RST_HIP_TRY(finalize_launch(f, st));
     }
     const LayerExec& last = t->L.back().e;
+    RST_HIP_TRY(poison());
     RST_HIP_TRY(affine_act_launch(last.d_out, last.d_ab, nullptr, prediction, B, (long)last.s.Ho * last.s.Wo, 3, 2, st));
     return RST_OK;
 }
@@ -968,6 +1021,7 @@ int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const fl
     if (!t || !content || !style_params || !gt_content || !gt_style || !prediction || !losses || !grad)
         return set_error(RST_ERR_INVALID, "rst_trainer_compute_gradients: null argument");
     t->gstyle_recorded = false;   // a failure on any path below leaves no stale event for wait_style_gradient
+    if (rst::guard_pad() != 0) rst::guard_check("before compute_gradients");   // diagnostic runs only
     if (batch <= 0 || batch > t->shape.max_batch)
         return set_error(RST_ERR_INVALID, "rst_trainer_compute_gradients: batch outside [1, max_batch]");
     hipStream_t st = static_cast<hipStream_t>(stream);

@@ -2,7 +2,8 @@
 The config-4 480x960 trainer (winograd_bf16x6 transfer convs, VGG16 in plain bf16 or fp32) runs compute_gradients
 N times on the same inputs; every prediction must be bitwise the first one (the targets run on the trainer's side
 stream beside the forward). Prints the max |difference| per call and the differing pixel count.
-Usage: python tools/pred_race_check.py [bf16|fp32] [N] [B]"""
+Usage: python tools/pred_race_check.py [bf16|fp32] [N] [B] [save.npy]   (save.npy: call 0's prediction, for comparing
+runs under different environments, e.g. RST_LDS_POISON)"""
 import importlib.util
 import os
 import sys
@@ -35,6 +36,8 @@ def main():
         p = pred.cpu().numpy()
         if first is None:
             first = p
+            if len(sys.argv) > 4:
+                np.save(sys.argv[4], p)
             print(f"call 0: prediction range [{p.min():.4f}, {p.max():.4f}]", flush=True)
             continue
         d = np.abs(p - first)
