@@ -15,6 +15,8 @@
 //   * each 12-float input row segment (3 x ds_read_b128) feeds 108 FMAs.
 // The epilogue writes the raw conv output plus per-tile {sum, M2, n} for the final CIN.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include "kernels.h"
 
 namespace rst {
@@ -273,7 +275,23 @@ int small_conv_weight_stride() { return small::WS; }
 hipError_t small_conv_launch(const SmallConvArgs& a, hipStream_t st) {
     if (a.cin > 256 || ((RST_SMALL_OPT & 2) && a.cin > 16)) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)(a.batch * a.tiles_y * a.tiles_x);
-    hipLaunchKernelGGL(small_conv_kernel<RST_SMALL_OPT>, dim3(grid), dim3(256), 0, st, a, a.w, a.in);
+    // diagnostic (the targets race): RST_SMALL_EXCLUSIVE=1 pads the workgroup's LDS to the whole 160 KB, so
+    // no other workgroup (of this or another kernel) shares its CU
+    static const bool exclusive = [] {
+        const char* v = getenv("RST_SMALL_EXCLUSIVE");
+        return v != nullptr && atoi(v) != 0;
+    }();
+    size_t dyn = 0;
+    if (exclusive) {
+        hipFuncAttributes fa{};
+        hipError_t e = hipFuncGetAttributes(&fa, (const void*)small_conv_kernel<RST_SMALL_OPT>);
+        if (e != hipSuccess) return e;
+        dyn = 160 * 1024 - fa.sharedSizeBytes;
+        e = hipFuncSetAttribute((const void*)small_conv_kernel<RST_SMALL_OPT>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(small_conv_kernel<RST_SMALL_OPT>, dim3(grid), dim3(256), dyn, st, a, a.w, a.in);
     return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -1036,6 +1037,30 @@ int rst_trainer_compute_gradients(rst_trainer* t, const float* content, const fl
     r = forward(t, content, style_params, B, prediction, st);
     t->targets_pending = false;                            // joined on every path, failed forward included
     RST_HIP_TRY(hipStreamWaitEvent(st, t->ev_join, 0));
+    // diagnostic (race bisection): RST_RACE_DUMP=<prefix> writes the last layer's raw output, its statistics partials
+    // and its input to <prefix>_{out,part,in}_<call>.bin after every forward
+    static const char* dump = getenv("RST_RACE_DUMP");
+    static int dump_call = 0;
+    if (dump != nullptr && r == RST_OK) {
+        const TLayer& T = t->L.back();
+        const LayerExec& e = T.e;
+        const size_t n_out = (size_t)B * e.s.Ho * e.s.Wo * e.s.cout, n_in = (size_t)B * e.s.H * e.s.W * e.s.cin;
+        const size_t n_part = (size_t)B * e.ntot * e.n_part * 4;
+        RST_HIP_TRY(hipStreamSynchronize(st));
+        const struct { const char* tag; const float* p; size_t n; } items[3] = {
+            {"out", e.d_out, n_out}, {"part", reinterpret_cast<const float*>(e.d_part), n_part}, {"in", T.d_x, n_in}};
+        for (const auto& it : items) {
+            std::vector<float> h(it.n);
+            RST_HIP_TRY(hipMemcpy(h.data(), it.p, it.n * 4, hipMemcpyDeviceToHost));
+            const std::string fn = std::string(dump) + "_" + it.tag + "_" + std::to_string(dump_call) + ".bin";
+            FILE* f = fopen(fn.c_str(), "wb");
+            if (f != nullptr) {
+                fwrite(h.data(), 4, h.size(), f);
+                fclose(f);
+            }
+        }
+        ++dump_call;
+    }
     if (r != RST_OK) return r;
     if ((r = loss_prediction(t->loss, prediction, B, losses, st)) != RST_OK) return r;
     if ((r = vgg_backward(t, prediction, B, t->L.back().d_g, st)) != RST_OK) return r;

@@ -30,10 +30,16 @@ def main():
     tr = tgt._trainer(cfg, w, vgg, B, prec, "winograd_bf16x6")
     c, s, gc, gs = tgt._cuda(content, sp, gtc, gts)
     first = None
+    first_loss = None
     for i in range(n):
         pred, losses, grad, gsp = tr.compute_gradients(c, s, gc, gs)
         torch.cuda.synchronize()
         p = pred.cpu().numpy()
+        lo = losses.cpu().numpy()
+        if first_loss is None:
+            first_loss = lo
+        elif not np.array_equal(lo, first_loss):
+            print(f"call {i}: losses differ from call 0 ({lo.ravel()} vs {first_loss.ravel()})", flush=True)
         if first is None:
             first = p
             if len(sys.argv) > 4:
