@@ -18,4 +18,11 @@ for i in range(1, n):
             tiles = sorted({(int(y) // 32, int(x) // 32) for y, x in zip(ys, xs)})
             msg.append(f"(rows {ys.min()}..{ys.max()}, cols {xs.min()}..{xs.max()}, {len(tiles)} 32x32 tiles: "
                        f"{tiles[:8]}, max |diff| {np.abs(a - ref[k])[d].max():.3e})")
+            idx = np.flatnonzero(d)[:12]
+            for j in idx:   # the first differing values: flat index -> (b, y, x, c), call-0 value, this call's, bits
+                bb, rem = divmod(int(j), H * W * 3)
+                y, rem = divmod(rem, W * 3)
+                x, c = divmod(rem, 3)
+                msg.append(f"\n    ({bb},{y},{x},{c}) ref {ref[k][j]:+.6e} [{ref[k][j:j+1].view(np.uint32)[0]:08x}]"
+                           f" got {a[j]:+.6e} [{a[j:j+1].view(np.uint32)[0]:08x}]")
     print(" ".join(msg), flush=True)
