@@ -30,7 +30,9 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", str(ROOT
 
 # per-source extra flags: the split-bf16 Winograd kernel keeps its transform in scalar f32 ops (packed f32
 # VALU beside MFMAs costs more issue cycles than two scalar ops on gfx950)
-EXTRA = {"wino_x6.hip": ["-fno-slp-vectorize"], "wino9_x6.hip": ["-fno-slp-vectorize"]}
+EXTRA = {"wino_x6.hip": ["-fno-slp-vectorize"], "wino9_x6.hip": ["-fno-slp-vectorize"],
+         # the last conv's scalar FMAs must stay scalar (conv_small.hip: SLP would re-pack them into v_pk_fma_f32)
+         "conv_small.hip": ["-fno-slp-vectorize"]}
 
 
 def _digest() -> str:

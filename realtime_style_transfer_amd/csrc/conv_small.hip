@@ -175,7 +175,16 @@ __global__ __launch_bounds__(256, RST_SMALL_RX == 8 ? 1 : 2) void small_conv_ker
 #pragma unroll
                         for (int p = 0; p < RX / 2; ++p) {
                             const sf32x2 xv = (kx & 1) ? xo[p + kx / 2] : xe[p + kx / 2];
+#ifdef RST_SMALL_PK   // the packed form (v_pk_fma_f32): see below
                             acc2[p][co] = __builtin_elementwise_fma(xv, wp, acc2[p][co]);
+#else
+                            // two scalar FMAs, not v_pk_fma_f32: with the packed accumulate chains, a few 8-lane
+                            // groups of a workgroup took a wrong sum (one accumulator element) whenever bf16-VGG16
+                            // waves of another stream shared the CU (profiles/r06/r06bf-r06bj); the
+                            // scalar form is clean there and the training step is no slower (r06bk)
+                            acc2[p][co][0] = fmaf(xv[0], wp[0], acc2[p][co][0]);
+                            acc2[p][co][1] = fmaf(xv[1], wp[1], acc2[p][co][1]);
+#endif
                         }
                     }
                 }

@@ -10,7 +10,7 @@ mkdir -p $D
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I include -I realtime_style_transfer_amd/csrc -Wall -Wno-unused-function -Wno-unused-variable -munsafe-fp-atomics"
 excl=""
 for src in "$@"; do
-  extra=""; case $src in wino_x6.hip|wino9_x6.hip) extra="-fno-slp-vectorize" ;; esac
+  extra=""; case $src in wino_x6.hip|wino9_x6.hip|conv_small.hip) extra="-fno-slp-vectorize" ;; esac
   /opt/rocm/bin/hipcc $F $extra $VFLAGS -c realtime_style_transfer_amd/csrc/$src -o $D/${src%.hip}.o &
   excl="$excl|/${src%.hip}.o\$"
 done
