@@ -273,8 +273,9 @@ int forward(rst_trainer* t, const float* content, const float* style, int B, flo
     // transfer network's forward; they still run beside the style predictor's forward, train_step). With the plain-bf16
     // VGG16 targets running beside it, the forward's prediction was not repeatable (tools/pred_race_check.py: ~all
     // pixels, up to 7e-2, from call to call, profiles/r06/r06am): joining before any of layers 0-13 made it bitwise
-    // repeatable, overlapping the targets with expand_0 .. expand_last did not. Root cause not identified (no shared
-    // buffer between the two); RST_TARGETS_JOIN_AT=k moves the join (-1: none) for diagnosis.
+    // repeatable, overlapping the targets with expand_0 .. expand_last did not. Traced to the last conv's packed-FMA
+    // accumulate chains taking wrong sums when bf16-VGG16 waves shared its CU; that kernel now uses scalar
+    // FMAs and is clean without the join, which stays as a second fence. RST_TARGETS_JOIN_AT=k moves it (-1: none).
     static const int join_at = [] {
         const char* v = getenv("RST_TARGETS_JOIN_AT");
         return v != nullptr ? atoi(v) : 0;
