@@ -523,3 +523,40 @@ def test_bf16_inference_needs_explicit_opt_in():
     d, ws, ins, outs, bres, bf = _load_fixture("transfer_small.npz")
     with pytest.raises(ValueError, match="allow_reduced_precision"):
         create_style_transfer_model(ins, outs, bres, bf, 1, weights=ws, max_batch=2, precision="bf16")
+
+
+@pytest.mark.gpu
+def test_two_networks_on_two_streams_are_bitwise_their_lone_runs():
+    """Co-residency: two full-size networks (480x960x17, the headline precision) launched on two streams at
+    once give bitwise the outputs each gives alone (tools/concurrent_infer_check.py, profiles/r06/r06bo)."""
+    _need_gpu()
+    import bench
+    from realtime_style_transfer_amd.plan import init_weights, network_plan, synthetic_style_params
+    from realtime_style_transfer_amd.shape_config import ShapeConfig
+    from realtime_style_transfer_amd.styleTransfer import create_style_transfer_model
+    cfg = ShapeConfig.from_spec("rst-960-120-128-17")
+    ins, outs = cfg.input_shape['content'], cfg.output_shape
+    plan = network_plan(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters)
+    nets = []
+    for k in range(2):
+        model, P = create_style_transfer_model(ins, outs, cfg.bottleneck_res_y, cfg.bottleneck_num_filters, 1,
+                                               weights=init_weights(plan, seed=3 + k), max_batch=1,
+                                               precision=bench.DEFAULT_PRECISION)
+        rng = np.random.default_rng(100 + k)
+        inp = {'content': torch.from_numpy(rng.random((1,) + ins, dtype=np.float32)).cuda(),
+               'style_params': torch.from_numpy(synthetic_style_params(1, 1, P, plan, seed=7 + k)).cuda()}
+        nets.append((model, inp, torch.empty((1,) + outs, device='cuda')))
+    refs = []
+    for model, inp, out in nets:
+        model(inp, out=out)
+        torch.cuda.synchronize()
+        refs.append(out.clone())
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for _ in range(5):
+        for (model, inp, out), s in zip(nets, streams):
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                model(inp, out=out)
+        torch.cuda.synchronize()
+        for (_, _, out), ref in zip(nets, refs):
+            assert torch.equal(out, ref), "a network's output changed while another ran beside it"
